@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark of the rig_calibrator evaluator hot path on MI355X.
+
+Metric (BASELINE.json): residual+Jacobian evals/sec, 3-cam rig, 1M obs.
+Workload (configs[1], "c2"): 3-sensor rig, 100k landmarks / 1M observations,
+radial-tangential distortion (K=5), fp64, every block floating. A STEP is one
+full pass of the hot path over all observations with inputs resident in HBM:
+point gather + per-frame pose kernel (K0) + per-observation residual and
+analytic Jacobian kernel (K1), outputs written to HBM (materialised Ceres
+columns).
+
+Multi-GPU (one process per GPU, torchrun): observations are sharded by
+landmark range; each rank owns a c2-sized shard of a global
+problem with N x 100k landmarks over the same cameras. Evaluation has no
+data-path collective ("scaling": "weak"); value = all ranks' evals / max time.
+
+Also reported: "roofline" of the dominant kernel (K1, radtan) from HIP events on
+its launch stream, and "cpu_baseline" = the oracle's Ceres-1.14-style central
+differences (oracle/, a port of the reference evaluator) on a bounded sample,
+timed on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+CPU_THREADS = 16       # reference default --num_opt_threads (rig_calibrator.cc:256)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="residuals in the CPU sample (0 = auto)")
+    return ap.parse_args()
+
+
+def cpu_baseline(problem, sample: int, min_seconds: float = 10.0):
+    """Oracle (port of the reference evaluator: per-residual functor + Ceres
+    central differences) on the first `sample` residual blocks."""
+    from oracle import oracle_py
+
+    n = min(sample, problem.num_residuals) if sample else problem.num_residuals
+    oracle_py.load()
+    # warm-up on a small slice
+    oracle_py.evaluate_mt(problem, oracle_py.NUMDIFF, 0, min(n, 2000), threads=CPU_THREADS)
+    t0 = time.perf_counter()
+    done = 0
+    passes = 0
+    # whole passes over the sample until >= min_seconds of CPU work (bounded: <= 4 passes)
+    while True:
+        oracle_py.evaluate_mt(problem, oracle_py.NUMDIFF, 0, n, threads=CPU_THREADS)
+        done += n
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds or passes >= 4:
+            break
+    return {"value": done / dt, "unit": "evals/s", "cores": CPU_THREADS, "kind": "port",
+            "sample": f"{passes} pass(es) over {n} of {problem.num_residuals} residual blocks of the "
+                      f"same workload: oracle NUMDIFF = per-block functor + Ceres 1.14 central "
+                      f"differences (1 + 2*n_free calls per block), {CPU_THREADS} OpenMP threads, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from multiview_amd import _lib, rig
+    from multiview_amd.evaluator import Evaluator
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    cfg = dict(rig.CONFIGS[args.config])
+    npts = cfg["num_points"]
+    cfg["point_range"] = (rank * npts, (rank + 1) * npts)
+    t0 = time.perf_counter()
+    R = rig.make_rig(**cfg)
+    P = rig.build_problem(R)
+    t_gen = time.perf_counter() - t0
+
+    ev = Evaluator(P, device=dev)
+    ev.set_params()
+    n = ev.num_residuals
+    ld = ((n + 63) // 64) * 64
+    res = torch.empty((2, ld), dtype=torch.float64, device="cuda")
+    jac = torch.empty((ev.stride, ld), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def step(events=None):
+        if events is None:
+            ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh)
+        else:
+            events[0].record(stream)
+            ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh, phase=_lib.EVAL_PREP_ONLY)
+            events[1].record(stream)
+            ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh, phase=_lib.EVAL_SKIP_PREP)
+            events[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    ev.sync(sh)
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ev.sync(sh)  # raises on device-side errors (alpha out of range)
+
+    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    obs_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([float(n)], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    dt_max = float(t.item())
+    total_evals = float(tot.item()) * args.steps
+
+    bytes_eval = ev.eval_bytes(True)                 # algorithmic bytes of K1 per launch set
+    achieved = bytes_eval / (obs_ms * 1e-3) / 1e9    # GB/s
+    line = {
+        "metric": "residual+Jacobian evals/sec (3-cam rig, 1M obs)",
+        "value": total_evals / dt_max,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt_max / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic rig generator, multiview_amd/rig.py)",
+        "config": {
+            "workload": f"{args.config}: {cfg['num_sensors']}-sensor rig, "
+                        f"{npts} landmarks x {world} shard(s), {n} obs/GPU, "
+                        f"{cfg['models'][0]} distortion, all blocks floating, fp64",
+            "num_residuals_per_gpu": n,
+            "num_frames": ev.num_frames,
+            "num_points_per_gpu": ev.num_points,
+            "parallelism": f"landmark-range shards x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_obs<radtan> (K1)",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "bytes_per_launch": bytes_eval,
+            "kernel_ms": obs_ms,
+            "prep_ms": prep_ms,
+        },
+        "gen_s": t_gen,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(P, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ev.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

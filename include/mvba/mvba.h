@@ -1,0 +1,213 @@
+/*
+ * mvba.h — C ABI of the MI355X-native bundle-adjustment evaluator for
+ * MultiView's rig_calibrator hot path.
+ *
+ * What this replaces (reference, oleg-alexandrov/MultiView):
+ *   - dense_map::BracketedCamError::operator() / ::Create
+ *       rig_calibrator/bin/rig_calibrator.cc:419-514
+ *     wrapped in ceres::DynamicNumericDiffCostFunction<..., CENTRAL>
+ *       (Ceres 1.14 [ext]; rig_calibrator.cc:489-505)
+ *   - the per-observation pose math it calls:
+ *       calc_world_to_cam_trans      rig_calibrator.cc:362-390
+ *       calc_interp_world_to_ref     rig_calibrator.cc:322-353
+ *       array_to_rigid_transform     rig_calibrator/src/dense_map_utils.cc:171-178
+ *       linearInterp (slerp)         rig_calibrator/src/dense_map_utils.cc:315-329
+ *   - the camera model it calls:
+ *       CameraParameters::Convert<UNDISTORTED_C,DISTORTED>  camera_model/camera_params.cc:412-415
+ *       CameraParameters::DistortCentered                    camera_model/camera_params.cc:260-314
+ *       RPCLensDistortion::distort_centered / compute_rpc    camera_model/rpc_distortion.cc:116-160, 358-360
+ *   - the Ceres Evaluate path over all residual blocks
+ *       evalResiduals → Problem::Evaluate                    rig_calibrator.cc:1157-1180
+ *   - the Cauchy loss applied by Ceres (GetLossFunction)      rig_calibrator.cc:394-411
+ *
+ * The reference evaluates one heap-allocated functor per observation and
+ * obtains the Jacobian by central differences (1 + 2*n_free functor calls per
+ * observation). This library evaluates ALL residual blocks of a problem in one
+ * pass on the GPU, with the analytic Jacobian, writing results to HBM.
+ *
+ * Rules of the boundary
+ *   - extern "C", plain pointers and sizes, no exceptions cross it.
+ *   - Host memory is caller-owned; the library copies what it needs.
+ *   - Device buffers are library-owned unless passed in by the caller
+ *     (mvba_evaluate_into).
+ *   - A handle is NOT re-entrant: one evaluation at a time per handle
+ *     (ceres::EvaluationCallback guarantees this).
+ *   - Every entry point returns an mvba_status; on error the message is
+ *     available from mvba_last_error(handle) and mirrors the reference's
+ *     LOG(FATAL) text for the same condition.
+ */
+#ifndef MVBA_MVBA_H_
+#define MVBA_MVBA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVBA_ABI_VERSION 1
+
+/* Status codes. Non-zero codes mirror the reference's fatal checks. */
+typedef enum mvba_status {
+  MVBA_OK = 0,
+  /* "Out of bounds in interpolation." rig_calibrator.cc:346 */
+  MVBA_E_ALPHA_RANGE = 1,
+  /* "BracketedCamError: The block sizes were not set up properly." rig_calibrator.cc:433-440 */
+  MVBA_E_BLOCK_SIZES = 2,
+  /* "Recieved irregular distortion vector size." camera_params.cc:199-206 */
+  MVBA_E_BAD_DISTORTION = 3,
+  /* HIP runtime failure (allocation, launch, copy). */
+  MVBA_E_HIP = 4,
+  /* Invalid argument (null pointer, out-of-range index, ...). */
+  MVBA_E_INVALID = 5,
+  /* No usable GPU (the product path has no CPU fallback). */
+  MVBA_E_NO_DEVICE = 6,
+  /* "BracketedDepthError: The block sizes were not set up properly." rig_calibrator.cc:534-543 */
+  MVBA_E_DEPTH_BLOCK_SIZES = 7
+} mvba_status;
+
+/* Parameter-block order of one BracketedCamError residual block, exactly the
+ * AddResidualBlock argument order of rig_calibrator.cc:1695-1699. */
+enum {
+  MVBA_BLK_BEG = 0,        /* beg world_to_ref (7: tx ty tz qx qy qz qw) */
+  MVBA_BLK_END = 1,        /* end world_to_ref (7) */
+  MVBA_BLK_REF_TO_CAM = 2, /* ref_to_cam (7) */
+  MVBA_BLK_XYZ = 3,        /* triangulated point (3) */
+  MVBA_BLK_OFFSET = 4,     /* ref_to_cam timestamp offset (1) */
+  MVBA_BLK_FOCAL = 5,      /* focal length (1) */
+  MVBA_BLK_CENTER = 6,     /* optical center (2) */
+  MVBA_BLK_DIST = 7,       /* distortion (K = GetDistortion().size()) */
+  MVBA_NUM_CAM_BLOCKS = 8
+};
+
+/* Jacobian row layout of one residual block (2 residual rows), identical in
+ * the host Ceres layout and in the device column-plane layout:
+ * block b occupies rows [mvba_jac_row_base(b), +2*size_b), row-major 2 x size_b
+ * (Ceres convention: jacobians[b][r * size_b + c]). */
+#define MVBA_JAC_BASE_BEG 0
+#define MVBA_JAC_BASE_END 14
+#define MVBA_JAC_BASE_REF_TO_CAM 28
+#define MVBA_JAC_BASE_XYZ 42
+#define MVBA_JAC_BASE_OFFSET 48
+#define MVBA_JAC_BASE_FOCAL 50
+#define MVBA_JAC_BASE_CENTER 52
+#define MVBA_JAC_BASE_DIST 56 /* 2*K rows follow */
+
+/* Description of a problem made of BracketedCamError residual blocks.
+ * All arrays are caller-owned and only read during mvba_create(). */
+typedef struct mvba_problem_desc {
+  /* Parameter blocks, packed into one vector of doubles. */
+  int32_t num_blocks;
+  const int32_t* block_size;     /* [num_blocks] */
+  const int64_t* block_offset;   /* [num_blocks] offset into the packed vector */
+  const uint8_t* block_constant; /* [num_blocks] 1 = Problem::SetParameterBlockConstant */
+  int64_t num_param_doubles;
+
+  /* Camera models: the camera::CameraParameters copies captured by
+   * BracketedCamError::Create (rig_calibrator.cc:512). Only the distorted
+   * half size and the distortion length are used on the residual path. */
+  int32_t num_cameras;
+  const int32_t* camera_dist_size; /* [num_cameras] K = GetDistortion().size() */
+  const double* camera_half_size;  /* [2*num_cameras] GetDistortedHalfSize() */
+
+  /* Residual blocks, in AddResidualBlock order (= Problem::Evaluate order). */
+  int64_t num_residuals;
+  const int32_t* residual_blocks; /* [8*num_residuals] block ids, MVBA_BLK_* order */
+  const int32_t* residual_camera; /* [num_residuals] camera model index */
+  const double* residual_meas;    /* [2*num_residuals] meas_dist_pix */
+  const double* residual_stamps;  /* [3*num_residuals] left_ref, right_ref, cam stamp */
+} mvba_problem_desc;
+
+typedef struct mvba_options {
+  int32_t device;        /* HIP device ordinal */
+  int32_t reserved0;
+  double reserved1;
+} mvba_options;
+
+/* Evaluation flags. */
+#define MVBA_EVAL_RESIDUALS 0x1
+#define MVBA_EVAL_JACOBIAN 0x2
+/* Apply the Cauchy loss through the Ceres corrector (r*sqrt(rho'), J*sqrt(rho')).
+ * Without it residuals/Jacobians are raw, as a ceres::CostFunction returns them. */
+#define MVBA_EVAL_APPLY_LOSS 0x4
+/* Phase control of mvba_evaluate_device (for timing the kernels separately):
+ * PREP_ONLY runs only the point gather and the per-frame kernel (K0);
+ * SKIP_PREP runs only the per-observation kernels (K1), reusing the frame
+ * records of the previous evaluation (parameters must be unchanged since). */
+#define MVBA_EVAL_PREP_ONLY 0x8
+#define MVBA_EVAL_SKIP_PREP 0x10
+
+/* Device view of the last evaluation (device order = grouped by camera model,
+ * then by image frame; see DESIGN.md "HBM layout"). */
+typedef struct mvba_device_view {
+  int64_t num_residuals;
+  int64_t ld;              /* leading dimension (elements) of residual/Jacobian planes */
+  int32_t jac_rows;        /* 56 + 2*K_max rows per residual */
+  int32_t max_dist_size;   /* K_max */
+  double* residuals;       /* [2][ld]  plane 0 = x residual, plane 1 = y residual */
+  double* jacobian;        /* [jac_rows][ld] column planes */
+  const int64_t* order;    /* [num_residuals] device position -> AddResidualBlock index */
+  const uint8_t* row_written; /* [num_residuals] bit b set = block b written (non-constant) */
+} mvba_device_view;
+
+/* Library / device queries. */
+int mvba_abi_version(void);
+mvba_status mvba_device_count(int32_t* count);
+
+/* Create a handle: validates block sizes and distortion sizes (the reference's
+ * constructor checks), groups residual blocks into image frames and uploads
+ * the static topology to HBM. */
+mvba_status mvba_create(const mvba_problem_desc* desc, const mvba_options* opts,
+                        struct mvba_handle** out);
+void mvba_destroy(struct mvba_handle* h);
+const char* mvba_last_error(const struct mvba_handle* h);
+/* Error text of the last failed mvba_create (thread-local). */
+const char* mvba_create_error(void);
+
+/* Upload the packed parameter vector (num_param_doubles doubles, host). */
+mvba_status mvba_set_params(struct mvba_handle* h, const double* packed_params);
+/* Same, from device memory (e.g. a GPU-resident solver's state), on stream. */
+mvba_status mvba_set_params_device(struct mvba_handle* h, const double* d_packed_params,
+                                   void* hip_stream);
+
+/* Evaluate all residual blocks. Host outputs in AddResidualBlock order.
+ *   cost      : nullable; 0.5*sum(r^2), or sum 0.5*rho(|r|^2) with APPLY_LOSS
+ *   residuals : nullable; [2*num_residuals]
+ *   jacobian  : nullable; [num_residuals * jac_stride] Ceres layout
+ *               (MVBA_JAC_BASE_*), constant blocks zero-filled,
+ *               jac_stride = mvba_jacobian_stride(h).
+ * Blocks until the results are on the host. */
+mvba_status mvba_evaluate(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
+                          double* cost, double* residuals, double* jacobian);
+int32_t mvba_jacobian_stride(const struct mvba_handle* h);
+
+/* Device-resident evaluation (no host transfer). Outputs go to the library's
+ * buffers (see mvba_device_buffers) or, if d_residuals/d_jacobian are non-null,
+ * into caller-owned device memory with leading dimension ld (>= num_residuals).
+ * Asynchronous on hip_stream (NULL = default stream). Errors raised by the
+ * kernels (interpolation alpha out of range) are reported by mvba_sync_status(). */
+mvba_status mvba_evaluate_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                 double* d_residuals, double* d_jacobian, int64_t ld,
+                                 void* hip_stream);
+mvba_status mvba_device_buffers(struct mvba_handle* h, mvba_device_view* view);
+/* Host copy of the device order: out[p] = AddResidualBlock index of device
+ * position p (num_residuals int64). */
+mvba_status mvba_residual_order(const struct mvba_handle* h, int64_t* out);
+/* Wait for the stream and convert any device-side error word into a status. */
+mvba_status mvba_sync_status(struct mvba_handle* h, void* hip_stream);
+
+/* Counts for reporting. */
+int64_t mvba_num_residuals(const struct mvba_handle* h);
+int64_t mvba_num_frames(const struct mvba_handle* h);
+int64_t mvba_num_points(const struct mvba_handle* h);
+/* Algorithmic HBM bytes of one materialised evaluation (residual+Jacobian),
+ * per DESIGN.md: per residual 16 (meas) + 4 (point index) + 24 (point) +
+ * 16 (residual) + 16 * (written Jacobian columns). */
+double mvba_eval_bytes(const struct mvba_handle* h, int32_t flags);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MVBA_MVBA_H_ */

@@ -1,0 +1,137 @@
+"""ctypes binding of the C ABI in include/mvba/mvba.h (libmvba.so).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``python -m multiview_amd.build``). There is no CPU fallback: if the library or
+a GPU is missing, every computing call raises ``MvbaError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmvba.so")
+
+# Status codes (mvba_status).
+MVBA_OK = 0
+MVBA_E_ALPHA_RANGE = 1
+MVBA_E_BLOCK_SIZES = 2
+MVBA_E_BAD_DISTORTION = 3
+MVBA_E_HIP = 4
+MVBA_E_INVALID = 5
+MVBA_E_NO_DEVICE = 6
+MVBA_E_DEPTH_BLOCK_SIZES = 7
+
+STATUS_NAMES = {
+    0: "MVBA_OK", 1: "MVBA_E_ALPHA_RANGE", 2: "MVBA_E_BLOCK_SIZES",
+    3: "MVBA_E_BAD_DISTORTION", 4: "MVBA_E_HIP", 5: "MVBA_E_INVALID",
+    6: "MVBA_E_NO_DEVICE", 7: "MVBA_E_DEPTH_BLOCK_SIZES",
+}
+
+EVAL_RESIDUALS = 0x1
+EVAL_JACOBIAN = 0x2
+EVAL_APPLY_LOSS = 0x4
+EVAL_PREP_ONLY = 0x8
+EVAL_SKIP_PREP = 0x10
+
+# Jacobian row bases (MVBA_JAC_BASE_*), block order of rig_calibrator.cc:1695-1699.
+JAC_BASE = (0, 14, 28, 42, 48, 50, 52, 56)
+FIXED_BLOCK_SIZES = (7, 7, 7, 3, 1, 1, 2)
+
+
+class MvbaError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"{STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+        self.message = message
+
+
+class ProblemDesc(C.Structure):
+    _fields_ = [
+        ("num_blocks", C.c_int32),
+        ("block_size", C.c_void_p),
+        ("block_offset", C.c_void_p),
+        ("block_constant", C.c_void_p),
+        ("num_param_doubles", C.c_int64),
+        ("num_cameras", C.c_int32),
+        ("camera_dist_size", C.c_void_p),
+        ("camera_half_size", C.c_void_p),
+        ("num_residuals", C.c_int64),
+        ("residual_blocks", C.c_void_p),
+        ("residual_camera", C.c_void_p),
+        ("residual_meas", C.c_void_p),
+        ("residual_stamps", C.c_void_p),
+    ]
+
+
+class Options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32), ("reserved1", C.c_double)]
+
+
+class DeviceView(C.Structure):
+    _fields_ = [
+        ("num_residuals", C.c_int64),
+        ("ld", C.c_int64),
+        ("jac_rows", C.c_int32),
+        ("max_dist_size", C.c_int32),
+        ("residuals", C.c_void_p),
+        ("jacobian", C.c_void_p),
+        ("order", C.c_void_p),
+        ("row_written", C.c_void_p),
+    ]
+
+
+# Every symbol include/mvba/mvba.h declares, with (restype, argtypes).
+SIGNATURES = {
+    "mvba_abi_version": (C.c_int, []),
+    "mvba_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
+    "mvba_create": (C.c_int, [C.POINTER(ProblemDesc), C.POINTER(Options), C.POINTER(C.c_void_p)]),
+    "mvba_destroy": (None, [C.c_void_p]),
+    "mvba_last_error": (C.c_char_p, [C.c_void_p]),
+    "mvba_create_error": (C.c_char_p, []),
+    "mvba_set_params": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mvba_set_params_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_evaluate": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_jacobian_stride": (C.c_int32, [C.c_void_p]),
+    "mvba_evaluate_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
+                                       C.c_int64, C.c_void_p]),
+    "mvba_device_buffers": (C.c_int, [C.c_void_p, C.POINTER(DeviceView)]),
+    "mvba_sync_status": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mvba_residual_order": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mvba_num_residuals": (C.c_int64, [C.c_void_p]),
+    "mvba_num_frames": (C.c_int64, [C.c_void_p]),
+    "mvba_num_points": (C.c_int64, [C.c_void_p]),
+    "mvba_eval_bytes": (C.c_double, [C.c_void_p, C.c_int32]),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libmvba.so and bind every ABI symbol. Raises if the library is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise MvbaError(MVBA_E_NO_DEVICE,
+                        f"{path} not built — run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError = missing export: fail loudly
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, handle=None, create: bool = False):
+    if status == MVBA_OK:
+        return
+    lib = load()
+    if create:
+        msg = lib.mvba_create_error().decode()
+    elif handle is not None:
+        msg = lib.mvba_last_error(handle).decode()
+    else:
+        msg = ""
+    raise MvbaError(status, msg)

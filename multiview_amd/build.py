@@ -1,0 +1,42 @@
+"""Build libmvba.so (gfx950) in-tree with hipcc.
+
+    python -m multiview_amd.build
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libmvba.so")
+SOURCES = ["mvba_kernels.hip", "mvba_host.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wall",
+         "-Wno-unused-function"]
+
+
+def build(verbose: bool = False) -> str:
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
+        srcp = os.path.join(CSRC, src)
+        deps = [srcp] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
+            [os.path.join(HERE, "..", "include", "mvba", "mvba.h")]
+        if not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps):
+            cmd = [HIPCC] + FLAGS + ["-x", "hip" if src.endswith(".hip") else "hip", "-c", srcp, "-o", obj]
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.run(cmd, check=True)
+        objs.append(obj)
+    if not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fopenmp", "-o", OUT] + objs
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv))

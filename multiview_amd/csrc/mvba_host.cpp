@@ -1,0 +1,607 @@
+// mvba_host.cpp — C ABI implementation (include/mvba/mvba.h).
+//
+// mvba_create "compiles" a Ceres-style problem of BracketedCamError residual
+// blocks (rig_calibrator.cc:1614-1752 builds exactly this) into an HBM-resident
+// structure-of-arrays:
+//   * image frames: unique (beg, end, ref_to_cam, offset, focal, center, dist,
+//     camera, stamps) tuples — world_to_cam depends only on these
+//     (calc_world_to_cam_trans, rig_calibrator.cc:362-390);
+//   * points: unique xyz blocks;
+//   * residuals reordered into device order = (camera model, frame, insertion),
+//     cut into wavefront segments of <= 64 residuals of one frame.
+// The product path has no CPU fallback: without a GPU every entry point that
+// computes returns MVBA_E_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mvba/mvba.h"
+#include "mvba_types.h"
+
+using mvba::FrameDesc;
+using mvba::Segment;
+
+extern "C" {
+hipError_t mvba_launch_points(const double* params, const int64_t* pt_off, const uint8_t* pt_free,
+                              int64_t npts, double4* pts, hipStream_t s);
+hipError_t mvba_launch_frames(const FrameDesc* fd, int64_t nframes, const double* params,
+                              double* frec, int* err, hipStream_t s);
+hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
+                           const FrameDesc* fd, const double* frec, const double* params,
+                           const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                           double* res, double* J, int64_t ld, int32_t flags, double cauchy_c,
+                           hipStream_t s);
+}
+
+namespace {
+
+thread_local std::string g_create_error;
+
+constexpr int kFixedSize[7] = {7, 7, 7, 3, 1, 1, 2};
+
+int rpc_degree(int n) { return static_cast<int>(std::round(std::sqrt(2.0 * n + 5.0) / 2.0 - 1.5)); }
+int rpc_num_dist_params(int d) { return 2 * (d + 1) * (d + 2) - 2; }
+
+// camera_params.cc:169-208 / rpc_distortion.cc:53-57 size rules.
+// Returns model kind, or -1 if SetDistortion would LOG(FATAL).
+int model_of(int K, int* deg) {
+  *deg = 0;
+  if (K == 0) return mvba::kModelNone;
+  if (K == 1) return mvba::kModelFov;
+  if (K == 4 || K == 5) return mvba::kModelRadtan;
+  if (K % 2 != 0) return -1;
+  const int n = K / 2;
+  const int d = rpc_degree(n);
+  if (rpc_num_dist_params(d) != n || d <= 0) return -1;
+  *deg = d;
+  return mvba::kModelRpc;
+}
+
+struct Group {
+  int model = 0, deg = 0;
+  int32_t seg_begin = 0, seg_count = 0;
+  int64_t res_begin = 0, res_count = 0;
+};
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+}
+
+template <class T>
+hipError_t upload(T** p, const std::vector<T>& v) {
+  hipError_t e = dalloc(p, v.size());
+  if (e != hipSuccess) return e;
+  if (v.empty()) return hipSuccess;
+  return hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+}  // namespace
+
+struct mvba_handle {
+  int device = 0;
+  std::string err;
+  int64_t nres = 0, nframes = 0, npts = 0, nparams = 0;
+  int kmax = 0, jac_rows = 0;
+  std::vector<int64_t> order;        // device position -> insertion index
+  std::vector<uint8_t> row_written;  // device position -> block bitmask
+  std::vector<int16_t> pos_K;        // device position -> distortion length
+  std::vector<Group> groups;
+  double bytes_res = 0.0, bytes_jac = 0.0;
+
+  double* d_params = nullptr;
+  FrameDesc* d_fd = nullptr;
+  double* d_frec = nullptr;
+  int64_t* d_pt_off = nullptr;
+  uint8_t* d_pt_free = nullptr;
+  double4* d_pts = nullptr;
+  int32_t* d_obs_pid = nullptr;
+  double2* d_obs_meas = nullptr;
+  Segment* d_segs = nullptr;
+  int64_t* d_order = nullptr;
+  uint8_t* d_row_written = nullptr;
+  int* d_err = nullptr;
+  double* d_res = nullptr;  // library-owned outputs, allocated lazily
+  double* d_J = nullptr;
+  int64_t ld = 0;
+  bool params_set = false;
+  bool prep_done = false;
+
+  std::vector<double> h_res, h_J;  // host staging for mvba_evaluate
+
+  mvba_status fail(mvba_status st, const std::string& msg) {
+    err = msg;
+    return st;
+  }
+  mvba_status hip_fail(hipError_t e, const char* where) {
+    err = std::string("HIP error in ") + where + ": " + hipGetErrorString(e);
+    return MVBA_E_HIP;
+  }
+};
+
+static void free_all(mvba_handle* h) {
+  if (!h) return;
+  void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
+                  h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
+                  h->d_row_written, h->d_err, h->d_res, h->d_J};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+}
+
+extern "C" {
+
+int mvba_abi_version(void) { return MVBA_ABI_VERSION; }
+
+mvba_status mvba_device_count(int32_t* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  if (count) *count = n;
+  return n > 0 ? MVBA_OK : MVBA_E_NO_DEVICE;
+}
+
+const char* mvba_create_error(void) { return g_create_error.c_str(); }
+
+const char* mvba_last_error(const mvba_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+void mvba_destroy(mvba_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  free_all(h);
+  delete h;
+}
+
+mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mvba_handle** out) {
+  g_create_error.clear();
+  if (!out) return MVBA_E_INVALID;
+  *out = nullptr;
+  auto bad = [&](mvba_status st, const std::string& m) {
+    g_create_error = m;
+    return st;
+  };
+  if (!d) return bad(MVBA_E_INVALID, "null problem description");
+  if (d->num_residuals < 0 || d->num_blocks < 0 || d->num_cameras < 0)
+    return bad(MVBA_E_INVALID, "negative sizes in problem description");
+  if (d->num_residuals > std::numeric_limits<int32_t>::max() - 64)
+    return bad(MVBA_E_INVALID, "too many residual blocks for one handle (shard the problem)");
+  if (d->num_residuals > 0 && (!d->residual_blocks || !d->residual_camera || !d->residual_meas ||
+                               !d->residual_stamps || !d->block_size || !d->block_offset ||
+                               !d->block_constant || !d->camera_dist_size || !d->camera_half_size))
+    return bad(MVBA_E_INVALID, "null array in problem description");
+
+  // Camera models (SetDistortion validation, camera_params.cc:199-206).
+  std::vector<int> cam_model(d->num_cameras), cam_deg(d->num_cameras);
+  int kmax = 0;
+  for (int c = 0; c < d->num_cameras; c++) {
+    const int K = d->camera_dist_size[c];
+    cam_model[c] = model_of(K, &cam_deg[c]);
+    if (cam_model[c] < 0)
+      return bad(MVBA_E_BAD_DISTORTION, "Recieved irregular distortion vector size. Size = " +
+                                            std::to_string(K) +
+                                            "\nAdditional message: Incorrect number of RPC coefficients.");
+    if (cam_model[c] == mvba::kModelRpc && cam_deg[c] > mvba::kMaxRpcDegree)
+      return bad(MVBA_E_BAD_DISTORTION, "RPC degree " + std::to_string(cam_deg[c]) +
+                                            " exceeds the compiled maximum " +
+                                            std::to_string(mvba::kMaxRpcDegree));
+    kmax = std::max(kmax, K);
+  }
+
+  const int64_t N = d->num_residuals;
+  // Block-size checks of BracketedCamError's constructor (rig_calibrator.cc:433-443).
+  for (int64_t i = 0; i < N; i++) {
+    const int32_t* blk = d->residual_blocks + 8 * i;
+    const int cam = d->residual_camera[i];
+    if (cam < 0 || cam >= d->num_cameras) return bad(MVBA_E_INVALID, "residual camera index out of range");
+    for (int b = 0; b < 8; b++)
+      if (blk[b] < 0 || blk[b] >= d->num_blocks) return bad(MVBA_E_INVALID, "parameter block index out of range");
+    for (int b = 0; b < 7; b++)
+      if (d->block_size[blk[b]] != kFixedSize[b])
+        return bad(MVBA_E_BLOCK_SIZES, "BracketedCamError: The block sizes were not set up properly.");
+    const int K = d->camera_dist_size[cam];
+    if (K > 0 && d->block_size[blk[7]] != K)
+      return bad(MVBA_E_BLOCK_SIZES, "BracketedCamError: The block sizes were not set up properly.");
+  }
+  for (int b = 0; b < d->num_blocks; b++)
+    if (d->block_offset[b] < 0 || d->block_offset[b] + d->block_size[b] > d->num_param_doubles)
+      return bad(MVBA_E_INVALID, "parameter block outside the packed vector");
+
+  // The product path computes on the GPU only: no device, no handle.
+  int32_t ndev = 0;
+  if (mvba_device_count(&ndev) != MVBA_OK) return bad(MVBA_E_NO_DEVICE, "no HIP device available");
+  const int dev = opts ? opts->device : 0;
+  if (dev < 0 || dev >= ndev) return bad(MVBA_E_INVALID, "invalid device ordinal");
+  if (hipSetDevice(dev) != hipSuccess) return bad(MVBA_E_HIP, "hipSetDevice failed");
+
+  mvba_handle* h = new mvba_handle();
+  h->device = dev;
+  h->nres = N;
+  h->nparams = d->num_param_doubles;
+  h->kmax = kmax;
+  h->jac_rows = MVBA_JAC_BASE_DIST + 2 * kmax;
+
+  // ---- points: unique xyz blocks, in order of first use
+  std::unordered_map<int32_t, int32_t> pt_index;
+  std::vector<int64_t> pt_off;
+  std::vector<uint8_t> pt_free;
+  std::vector<int32_t> res_pt(N);
+  pt_index.reserve(N / 4 + 16);
+  for (int64_t i = 0; i < N; i++) {
+    const int32_t b = d->residual_blocks[8 * i + MVBA_BLK_XYZ];
+    auto it = pt_index.find(b);
+    if (it == pt_index.end()) {
+      const int32_t id = (int32_t)pt_off.size();
+      pt_index.emplace(b, id);
+      pt_off.push_back(d->block_offset[b]);
+      pt_free.push_back(d->block_constant[b] ? 0 : 1);
+      res_pt[i] = id;
+    } else {
+      res_pt[i] = it->second;
+    }
+  }
+  h->npts = (int64_t)pt_off.size();
+
+  // ---- frames: unique (blocks except xyz, camera, stamps)
+  struct Key {
+    int32_t b[7];
+    int32_t cam;
+    uint64_t s[3];
+    bool operator==(const Key& o) const {
+      return std::memcmp(b, o.b, sizeof(b)) == 0 && cam == o.cam && s[0] == o.s[0] &&
+             s[1] == o.s[1] && s[2] == o.s[2];
+    }
+  };
+  struct KeyHash {
+    size_t operator()(const Key& k) const {
+      uint64_t x = 1469598103934665603ull;
+      auto mix = [&](uint64_t v) { x = (x ^ v) * 1099511628211ull; };
+      for (int q = 0; q < 7; q++) mix((uint64_t)(uint32_t)k.b[q]);
+      mix((uint64_t)(uint32_t)k.cam);
+      mix(k.s[0]); mix(k.s[1]); mix(k.s[2]);
+      return (size_t)x;
+    }
+  };
+  std::unordered_map<Key, int32_t, KeyHash> frame_index;
+  frame_index.reserve(1024);
+  std::vector<FrameDesc> frames;
+  std::vector<int32_t> res_frame(N);
+  for (int64_t i = 0; i < N; i++) {
+    const int32_t* blk = d->residual_blocks + 8 * i;
+    Key k;
+    int q = 0;
+    for (int b = 0; b < 8; b++)
+      if (b != MVBA_BLK_XYZ) k.b[q++] = blk[b];
+    k.cam = d->residual_camera[i];
+    std::memcpy(&k.s[0], &d->residual_stamps[3 * i], 24);
+    auto it = frame_index.find(k);
+    if (it != frame_index.end()) {
+      res_frame[i] = it->second;
+      continue;
+    }
+    FrameDesc F;
+    std::memset(&F, 0, sizeof(F));
+    for (int b = 0; b < 8; b++) F.off[b] = d->block_offset[blk[b]];
+    F.sb = d->residual_stamps[3 * i];
+    F.se = d->residual_stamps[3 * i + 1];
+    F.sc = d->residual_stamps[3 * i + 2];
+    F.cam = k.cam;
+    F.h0 = d->camera_half_size[2 * k.cam];
+    F.h1 = d->camera_half_size[2 * k.cam + 1];
+    F.K = d->camera_dist_size[k.cam];
+    int mask = 0;
+    for (int b = 0; b < 8; b++)
+      if (b != MVBA_BLK_XYZ && !d->block_constant[blk[b]]) mask |= (1 << b);
+    if (F.K == 0) mask &= ~(1 << MVBA_BLK_DIST);
+    F.free_mask = mask;
+    const int32_t id = (int32_t)frames.size();
+    frames.push_back(F);
+    frame_index.emplace(k, id);
+    res_frame[i] = id;
+  }
+  h->nframes = (int64_t)frames.size();
+
+  // ---- groups by (model, degree), then device order
+  std::vector<int> gkey_of_cam(d->num_cameras);
+  std::vector<int> keys;
+  for (int c = 0; c < d->num_cameras; c++) {
+    gkey_of_cam[c] = cam_model[c] * 16 + cam_deg[c];
+    keys.push_back(gkey_of_cam[c]);
+  }
+  std::sort(keys.begin(), keys.end());
+  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+  std::vector<int> grank(d->num_cameras);
+  for (int c = 0; c < d->num_cameras; c++)
+    grank[c] = (int)(std::lower_bound(keys.begin(), keys.end(), gkey_of_cam[c]) - keys.begin());
+
+  std::vector<int64_t> idx(N);
+  for (int64_t i = 0; i < N; i++) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+    const int ga = grank[d->residual_camera[a]], gb = grank[d->residual_camera[b]];
+    if (ga != gb) return ga < gb;
+    return res_frame[a] < res_frame[b];
+  });
+
+  std::vector<int32_t> obs_pid(N);
+  std::vector<double2> obs_meas(N);
+  h->order.resize(N);
+  h->row_written.resize(N);
+  h->pos_K.resize(N);
+  std::vector<Segment> segs;
+  segs.reserve(N / 32 + keys.size() + 1);
+  h->groups.resize(keys.size());
+  double bytes_res = 0.0, bytes_jac = 0.0;
+  for (size_t g = 0; g < keys.size(); g++) {
+    h->groups[g].model = keys[g] / 16;
+    h->groups[g].deg = keys[g] % 16;
+  }
+  int cur_group = -1;
+  for (int64_t p = 0; p < N; p++) {
+    const int64_t i = idx[p];
+    const int g = grank[d->residual_camera[i]];
+    const int32_t fr = res_frame[i];
+    if (g != cur_group) {
+      if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
+      cur_group = g;
+      h->groups[g].seg_begin = (int32_t)segs.size();
+      h->groups[g].res_begin = p;
+    }
+    h->groups[g].res_count++;
+    if (segs.empty() || segs.back().frame != fr || segs.back().count == 64 ||
+        (int32_t)segs.size() == h->groups[g].seg_begin) {
+      Segment s;
+      s.begin = (int32_t)p;
+      s.count = 0;
+      s.frame = fr;
+      s.pad = 0;
+      segs.push_back(s);
+    }
+    segs.back().count++;
+    obs_pid[p] = res_pt[i];
+    obs_meas[p] = make_double2(d->residual_meas[2 * i], d->residual_meas[2 * i + 1]);
+    h->order[p] = i;
+    const int mask = frames[fr].free_mask | (pt_free[res_pt[i]] ? (1 << MVBA_BLK_XYZ) : 0);
+    h->row_written[p] = (uint8_t)mask;
+    h->pos_K[p] = (int16_t)frames[fr].K;
+    // Algorithmic bytes (DESIGN.md "Roofline"): meas 16 + point index 4 + point 24 + r 16.
+    bytes_res += 16.0 + 4.0 + 24.0 + 16.0;
+    int cols = 0;
+    for (int b = 0; b < 8; b++)
+      if (mask & (1 << b)) cols += (b == 7) ? frames[fr].K : kFixedSize[b];
+    bytes_jac += 16.0 * cols;
+  }
+  if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
+  h->bytes_res = bytes_res;
+  h->bytes_jac = bytes_jac;
+
+  // ---- upload
+  hipError_t e = hipSuccess;
+  auto chk = [&](hipError_t x) {
+    if (e == hipSuccess && x != hipSuccess) e = x;
+  };
+  chk(dalloc(&h->d_params, (size_t)std::max<int64_t>(d->num_param_doubles, 1)));
+  chk(upload(&h->d_fd, frames));
+  chk(dalloc(&h->d_frec, (size_t)h->nframes * mvba::kFrameRecDoubles));
+  chk(upload(&h->d_pt_off, pt_off));
+  chk(upload(&h->d_pt_free, pt_free));
+  chk(dalloc(&h->d_pts, (size_t)h->npts));
+  chk(upload(&h->d_obs_pid, obs_pid));
+  chk(upload(&h->d_obs_meas, obs_meas));
+  chk(upload(&h->d_segs, segs));
+  chk(upload(&h->d_order, h->order));
+  chk(upload(&h->d_row_written, h->row_written));
+  chk(dalloc(&h->d_err, 1));
+  if (e == hipSuccess) chk(hipMemset(h->d_err, 0, sizeof(int)));
+  if (e != hipSuccess) {
+    g_create_error = std::string("HIP error during mvba_create: ") + hipGetErrorString(e);
+    free_all(h);
+    delete h;
+    return MVBA_E_HIP;
+  }
+  *out = h;
+  return MVBA_OK;
+}
+
+mvba_status mvba_set_params(mvba_handle* h, const double* packed) {
+  if (!h || !packed) return MVBA_E_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  hipError_t e = hipMemcpy(h->d_params, packed, (size_t)h->nparams * sizeof(double), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_set_params");
+  h->params_set = true;
+  h->prep_done = false;
+  return MVBA_OK;
+}
+
+mvba_status mvba_set_params_device(mvba_handle* h, const double* dp, void* stream) {
+  if (!h || !dp) return MVBA_E_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  hipError_t e = hipMemcpyAsync(h->d_params, dp, (size_t)h->nparams * sizeof(double),
+                                hipMemcpyDeviceToDevice, (hipStream_t)stream);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_set_params_device");
+  h->params_set = true;
+  h->prep_done = false;
+  return MVBA_OK;
+}
+
+int32_t mvba_jacobian_stride(const mvba_handle* h) { return h ? h->jac_rows : 0; }
+
+mvba_status mvba_residual_order(const mvba_handle* h, int64_t* out) {
+  if (!h || !out) return MVBA_E_INVALID;
+  std::memcpy(out, h->order.data(), h->order.size() * sizeof(int64_t));
+  return MVBA_OK;
+}
+int64_t mvba_num_residuals(const mvba_handle* h) { return h ? h->nres : 0; }
+int64_t mvba_num_frames(const mvba_handle* h) { return h ? h->nframes : 0; }
+int64_t mvba_num_points(const mvba_handle* h) { return h ? h->npts : 0; }
+
+double mvba_eval_bytes(const mvba_handle* h, int32_t flags) {
+  if (!h) return 0.0;
+  return h->bytes_res + ((flags & MVBA_EVAL_JACOBIAN) ? h->bytes_jac : 0.0);
+}
+
+static mvba_status ensure_outputs(mvba_handle* h) {
+  if (h->d_res) return MVBA_OK;
+  h->ld = ((h->nres + 63) / 64) * 64;
+  if (h->ld == 0) h->ld = 64;
+  hipError_t e = dalloc(&h->d_res, (size_t)(2 * h->ld));
+  if (e == hipSuccess) e = dalloc(&h->d_J, (size_t)h->jac_rows * (size_t)h->ld);
+  if (e != hipSuccess) return h->hip_fail(e, "allocating evaluation outputs");
+  return MVBA_OK;
+}
+
+mvba_status mvba_evaluate_device(mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                 double* d_res, double* d_J, int64_t ld, void* stream) {
+  if (!h) return MVBA_E_INVALID;
+  if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  hipStream_t s = (hipStream_t)stream;
+  if (!d_res && !d_J) {
+    mvba_status st = ensure_outputs(h);
+    if (st != MVBA_OK) return st;
+    d_res = h->d_res;
+    d_J = (flags & MVBA_EVAL_JACOBIAN) ? h->d_J : nullptr;
+    ld = h->ld;
+  } else if (ld < h->nres) {
+    return h->fail(MVBA_E_INVALID, "leading dimension smaller than the number of residuals");
+  }
+  if ((flags & MVBA_EVAL_JACOBIAN) && !d_J)
+    return h->fail(MVBA_E_INVALID, "Jacobian requested without a Jacobian buffer");
+  if (!(flags & MVBA_EVAL_JACOBIAN)) d_J = nullptr;
+  double cauchy_c = 0.0;
+  if (flags & MVBA_EVAL_APPLY_LOSS) {
+    if (!(cauchy_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
+    cauchy_c = 1.0 / (cauchy_threshold * cauchy_threshold);
+  }
+  hipError_t e = hipSuccess;
+  if (!(flags & MVBA_EVAL_SKIP_PREP)) {
+    e = hipMemsetAsync(h->d_err, 0, sizeof(int), s);
+    if (e == hipSuccess) e = mvba_launch_points(h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts, s);
+    if (e == hipSuccess) e = mvba_launch_frames(h->d_fd, h->nframes, h->d_params, h->d_frec, h->d_err, s);
+    h->prep_done = true;
+  } else if (!h->prep_done) {
+    return h->fail(MVBA_E_INVALID, "MVBA_EVAL_SKIP_PREP before any full evaluation");
+  }
+  if (flags & MVBA_EVAL_PREP_ONLY) {
+    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
+    return MVBA_OK;
+  }
+  for (size_t g = 0; g < h->groups.size() && e == hipSuccess; g++) {
+    const Group& G = h->groups[g];
+    e = mvba_launch_obs(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->d_frec,
+                        h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags,
+                        cauchy_c, s);
+  }
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
+  return MVBA_OK;
+}
+
+mvba_status mvba_sync_status(mvba_handle* h, void* stream) {
+  if (!h) return MVBA_E_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_sync_status");
+  int err = 0;
+  e = hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_sync_status copy");
+  if (err & 1) return h->fail(MVBA_E_ALPHA_RANGE, "Out of bounds in interpolation.");
+  return MVBA_OK;
+}
+
+mvba_status mvba_device_buffers(mvba_handle* h, mvba_device_view* v) {
+  if (!h || !v) return MVBA_E_INVALID;
+  mvba_status st = ensure_outputs(h);
+  if (st != MVBA_OK) return st;
+  v->num_residuals = h->nres;
+  v->ld = h->ld;
+  v->jac_rows = h->jac_rows;
+  v->max_dist_size = h->kmax;
+  v->residuals = h->d_res;
+  v->jacobian = h->d_J;
+  v->order = h->d_order;
+  v->row_written = h->d_row_written;
+  return MVBA_OK;
+}
+
+mvba_status mvba_evaluate(mvba_handle* h, int32_t flags, double cauchy_threshold, double* cost,
+                          double* residuals, double* jacobian) {
+  if (!h) return MVBA_E_INVALID;
+  const bool want_jac = jacobian != nullptr && (flags & MVBA_EVAL_JACOBIAN);
+  const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
+  if (loss && !(cauchy_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
+  // Raw residuals/Jacobian on the device; the Ceres corrector is applied here
+  // so the cost can use the uncorrected squared norm.
+  const int32_t dflags = MVBA_EVAL_RESIDUALS | (want_jac ? MVBA_EVAL_JACOBIAN : 0);
+  mvba_status st = mvba_evaluate_device(h, dflags, 0.0, nullptr, nullptr, 0, nullptr);
+  if (st != MVBA_OK) return st;
+  st = mvba_sync_status(h, nullptr);
+  if (st != MVBA_OK) return st;
+  const int64_t N = h->nres, ld = h->ld;
+  h->h_res.resize((size_t)(2 * ld));
+  hipError_t e = hipMemcpy(h->h_res.data(), h->d_res, (size_t)(2 * ld) * sizeof(double), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate residual copy");
+  if (want_jac) {
+    h->h_J.resize((size_t)h->jac_rows * (size_t)ld);
+    e = hipMemcpy(h->h_J.data(), h->d_J, h->h_J.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate Jacobian copy");
+  }
+  const double b = cauchy_threshold * cauchy_threshold;
+  const double c = loss ? 1.0 / b : 0.0;
+  const int stride = h->jac_rows;
+  std::vector<double> scale(loss ? N : 0);
+  double total = 0.0;
+  // Cost is summed in AddResidualBlock order (Problem::Evaluate, num_threads = 1).
+  std::vector<double> cost_dev((size_t)N);
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < N; p++) {
+    const double r0 = h->h_res[p], r1 = h->h_res[ld + p];
+    const double s2 = r0 * r0 + r1 * r1;
+    double sr = 1.0, ci;
+    if (!loss) {
+      ci = 0.5 * s2;
+    } else {
+      const double sum = 1.0 + s2 * c;
+      const double inv = 1.0 / sum;
+      ci = 0.5 * (b * std::log(sum));
+      sr = std::sqrt(std::max(std::numeric_limits<double>::min(), inv));
+      scale[p] = sr;
+    }
+    cost_dev[p] = ci;
+    const int64_t i = h->order[p];
+    if (residuals) {
+      residuals[2 * i] = r0 * sr;
+      residuals[2 * i + 1] = r1 * sr;
+    }
+    if (want_jac) {
+      double* Jo = jacobian + i * stride;
+      const int mask = h->row_written[p];
+      for (int row = 0; row < stride; row++) Jo[row] = 0.0;
+      static const int base[8] = {MVBA_JAC_BASE_BEG, MVBA_JAC_BASE_END, MVBA_JAC_BASE_REF_TO_CAM,
+                                  MVBA_JAC_BASE_XYZ, MVBA_JAC_BASE_OFFSET, MVBA_JAC_BASE_FOCAL,
+                                  MVBA_JAC_BASE_CENTER, MVBA_JAC_BASE_DIST};
+      for (int bb = 0; bb < 8; bb++) {
+        if (!(mask & (1 << bb))) continue;
+        const int rows = (bb == 7) ? 2 * h->pos_K[p] : 2 * kFixedSize[bb];
+        for (int q = 0; q < rows; q++) {
+          const int row = base[bb] + q;
+          Jo[row] = h->h_J[(size_t)row * ld + p] * sr;
+        }
+      }
+    }
+  }
+  if (cost) {
+    std::vector<double> by_ins((size_t)N);
+    for (int64_t p = 0; p < N; p++) by_ins[h->order[p]] = cost_dev[p];
+    for (int64_t i = 0; i < N; i++) total += by_ins[i];
+    *cost = total;
+  }
+  return MVBA_OK;
+}
+
+}  // extern "C"

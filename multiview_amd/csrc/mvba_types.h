@@ -1,0 +1,52 @@
+// mvba_types.h — host/device shared records of the MI355X evaluator.
+// See DESIGN.md "HBM layout" for how these are laid out in device memory.
+#ifndef MVBA_TYPES_H_
+#define MVBA_TYPES_H_
+
+#include <stdint.h>
+
+namespace mvba {
+
+// Per image frame (one unique set of pose blocks, intrinsics blocks and stamps;
+// calc_world_to_cam_trans depends only on these, rig_calibrator.cc:362-390,
+// called per image at :1633-1651). 128 bytes, read with scalar loads.
+struct FrameDesc {
+  int64_t off[8];      // offsets of the 8 parameter blocks in the packed vector (off[3] unused)
+  double sb, se, sc;   // left_ref_stamp, right_ref_stamp, cam_stamp
+  double h0, h1;       // distorted half size (camera_params.cc:107-110)
+  int32_t cam;         // camera model index
+  int32_t K;           // distortion length
+  int32_t free_mask;   // bit b: block b is not constant (b != 3)
+  int32_t pad;
+};
+
+// K0 output per frame, in doubles:
+//   [0..8]   R_wc row-major      [9..11]  t_wc
+//   [12 + 6k .. 12 + 6k + 5] for pose column k (22 columns:
+//        beg tx ty tz qx qy qz qw | end (7) | ref_to_cam (7) | offset (1)):
+//        omega_k (3), v_k (3), with d(Xc)/dp_k = omega_k x Xc + v_k.
+constexpr int kFrameRecDoubles = 144;
+constexpr int kPoseCols = 22;
+
+// A segment = up to 64 consecutive device-order residuals of ONE frame,
+// processed by one wavefront (frame data is wave-uniform -> scalar loads).
+struct Segment {
+  int32_t begin;
+  int32_t count;
+  int32_t frame;
+  int32_t pad;
+};
+
+// Distortion model kinds (camera_params.cc:181-207 dispatch by size).
+enum ModelKind : int32_t {
+  kModelNone = 0,    // K = 0
+  kModelFov = 1,     // K = 1
+  kModelRadtan = 2,  // K = 4 or 5
+  kModelRpc = 3      // K = 2 * (2 (d+1)(d+2) - 2)
+};
+
+constexpr int kMaxRpcDegree = 6;
+
+}  // namespace mvba
+
+#endif  // MVBA_TYPES_H_

@@ -1,0 +1,111 @@
+"""Python handle over the C ABI (one ``mvba_handle``).
+
+This is a thin convenience layer used by tests and bench.py; the boundary a
+maintainer binds is include/mvba/mvba.h. Every computing
+call goes to libmvba.so on the GPU — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .problem import CamProblem
+
+
+class Evaluator:
+    """GPU evaluator for a CamProblem (BracketedCamError residual blocks)."""
+
+    def __init__(self, problem: CamProblem, device: int = 0):
+        self.lib = _lib.load()
+        self.problem = problem
+        self._desc = problem.desc()
+        opts = _lib.Options(device=device, reserved0=0, reserved1=0.0)
+        h = C.c_void_p()
+        st = self.lib.mvba_create(C.byref(self._desc), C.byref(opts), C.byref(h))
+        _lib.check(st, create=True)
+        self.h = h
+        self.stride = int(self.lib.mvba_jacobian_stride(self.h))
+        self.num_residuals = int(self.lib.mvba_num_residuals(self.h))
+        self.num_frames = int(self.lib.mvba_num_frames(self.h))
+        self.num_points = int(self.lib.mvba_num_points(self.h))
+
+    # ---------------------------------------------------------------- params
+    def set_params(self, params: np.ndarray | None = None):
+        p = self.problem.params if params is None else params
+        p = np.ascontiguousarray(p, dtype=np.float64)
+        if p.size != self.problem.params.size:
+            raise ValueError("packed parameter vector has the wrong size")
+        _lib.check(self.lib.mvba_set_params(self.h, p.ctypes.data), self.h)
+
+    def set_params_device(self, tensor, stream=None):
+        """tensor: torch float64 CUDA tensor with the packed parameters."""
+        _lib.check(self.lib.mvba_set_params_device(self.h, C.c_void_p(tensor.data_ptr()),
+                                                   C.c_void_p(stream or 0)), self.h)
+
+    # ------------------------------------------------------------ evaluation
+    def evaluate(self, jacobian: bool = True, apply_loss: bool = False,
+                 robust_threshold: float = 3.0):
+        """Host evaluation in AddResidualBlock order.
+
+        Returns (cost, residuals [N, 2], jacobian [N, stride] or None), the
+        Jacobian in the Ceres layout (MVBA_JAC_BASE_*), constant blocks zero."""
+        n = self.num_residuals
+        r = np.empty((n, 2), dtype=np.float64)
+        J = np.empty((n, self.stride), dtype=np.float64) if jacobian else None
+        cost = C.c_double(0.0)
+        flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0) | \
+            (_lib.EVAL_APPLY_LOSS if apply_loss else 0)
+        st = self.lib.mvba_evaluate(self.h, flags, float(robust_threshold), C.byref(cost),
+                                    r.ctypes.data, J.ctypes.data if J is not None else None)
+        _lib.check(st, self.h)
+        return cost.value, r, J
+
+    def evaluate_device(self, jacobian: bool = True, apply_loss: bool = False,
+                        robust_threshold: float = 3.0, residuals=None, jac=None, ld: int = 0,
+                        stream=None, phase: int = 0):
+        """Asynchronous device evaluation. residuals/jac: optional torch float64
+        CUDA tensors of shape [2, ld] / [stride, ld] (caller-owned outputs)."""
+        flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0) | \
+            (_lib.EVAL_APPLY_LOSS if apply_loss else 0) | phase
+        rp = C.c_void_p(residuals.data_ptr()) if residuals is not None else None
+        jp = C.c_void_p(jac.data_ptr()) if jac is not None else None
+        st = self.lib.mvba_evaluate_device(self.h, flags, float(robust_threshold), rp, jp,
+                                           int(ld), C.c_void_p(stream or 0))
+        _lib.check(st, self.h)
+
+    def sync(self, stream=None):
+        _lib.check(self.lib.mvba_sync_status(self.h, C.c_void_p(stream or 0)), self.h)
+
+    def device_view(self) -> _lib.DeviceView:
+        v = _lib.DeviceView()
+        _lib.check(self.lib.mvba_device_buffers(self.h, C.byref(v)), self.h)
+        return v
+
+    def order(self) -> np.ndarray:
+        """device position -> AddResidualBlock index."""
+        out = np.empty(self.num_residuals, dtype=np.int64)
+        _lib.check(self.lib.mvba_residual_order(self.h, out.ctypes.data), self.h)
+        return out
+
+    def eval_bytes(self, jacobian: bool = True) -> float:
+        flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0)
+        return float(self.lib.mvba_eval_bytes(self.h, flags))
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.mvba_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

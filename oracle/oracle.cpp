@@ -1,0 +1,670 @@
+// ============================================================================
+// oracle.cpp — CPU restatement of MultiView's rig_calibrator residual path.
+//
+// TEST INFRASTRUCTURE ONLY. This file is the parity checker for the HIP
+// product path (multiview_amd/csrc). Only tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg may load it. The product never links or calls it.
+//
+// PARITY STATUS: UNPINNED against the reference binary. The reference cannot be
+// built in this container (Eigen 3.4, Ceres 1.14, glog, OpenCV 3.2 absent — see
+// DESIGN.md "Oracle") and the reference ships no tests, fixtures or golden
+// vectors. This restatement is pinned instead by
+//   (1) known-answer tests (identity poses, RPC identity, structural zeros),
+//   (2) an independent 50-digit mpmath restatement (tests/golden/make_golden.py)
+//       whose vectors are committed under tests/golden/.
+//
+// What is restated, line by line (op order of the reference formulas):
+//   array_to_rigid_transform  dense_map_utils.cc:171-178
+//   linearInterp              dense_map_utils.cc:315-329   (Eigen 3.4 slerp [ext])
+//   calc_interp_world_to_ref  rig_calibrator.cc:322-353
+//   calc_world_to_cam_trans   rig_calibrator.cc:362-390
+//   BracketedCamError         rig_calibrator.cc:447-482
+//   BracketedDepthError       rig_calibrator.cc:547-583
+//   XYZError                  rig_calibrator.cc:721-727
+//   DistortCentered           camera_params.cc:260-314 (+ Convert :412-415)
+//   SetDistortion precalcs    camera_params.cc:169-208
+//   compute_rpc               rpc_distortion.cc:116-160 (rpc_degree :43-49)
+//   Ceres 1.14 [ext] DynamicNumericDiffCostFunction<CENTRAL> (numeric_diff.h):
+//       delta = max(sqrt(DBL_EPSILON), 1e-6*|x_j|),
+//       J_j = (f(x+delta e_j) - f(x-delta e_j)) * ((1/delta)/2)
+//   Ceres 1.14 [ext] CauchyLoss + Corrector (loss_function.cc, corrector.cc)
+//   calc_residuals_stats      rig_calibrator.cc:753-789
+//
+// Three evaluation modes over the same templated functor:
+//   ORACLE_RESIDUAL  : T = double
+//   ORACLE_NUMDIFF   : T = double, Ceres central differences (the reference's
+//                      own Jacobian)
+//   ORACLE_ANALYTIC  : T = Dual (forward-mode), one seeded column at a time —
+//                      exact derivative of the same formulas, independent of the
+//                      hand-derived chain rule used by the HIP kernels.
+// ============================================================================
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
+#include <map>
+#include <sstream>
+#include <iomanip>
+
+#include "../include/mvba/mvba.h"
+
+namespace oracle {
+
+// ---------------------------------------------------------------- dual number
+struct Dual {
+  double v, d;
+  Dual() : v(0), d(0) {}
+  Dual(double a) : v(a), d(0) {}  // NOLINT
+  Dual(double a, double b) : v(a), d(b) {}
+};
+inline Dual operator+(Dual a, Dual b) { return Dual(a.v + b.v, a.d + b.d); }
+inline Dual operator-(Dual a, Dual b) { return Dual(a.v - b.v, a.d - b.d); }
+inline Dual operator-(Dual a) { return Dual(-a.v, -a.d); }
+inline Dual operator*(Dual a, Dual b) { return Dual(a.v * b.v, a.d * b.v + a.v * b.d); }
+inline Dual operator/(Dual a, Dual b) {
+  double q = a.v / b.v;
+  return Dual(q, (a.d - q * b.d) / b.v);
+}
+inline Dual& operator+=(Dual& a, Dual b) { a = a + b; return a; }
+inline Dual& operator-=(Dual& a, Dual b) { a = a - b; return a; }
+inline Dual& operator*=(Dual& a, Dual b) { a = a * b; return a; }
+inline Dual& operator/=(Dual& a, Dual b) { a = a / b; return a; }
+inline double val(double a) { return a; }
+inline double val(const Dual& a) { return a.v; }
+inline double dsqrt(double a) { return std::sqrt(a); }
+inline Dual dsqrt(Dual a) { double s = std::sqrt(a.v); return Dual(s, a.d / (2.0 * s)); }
+inline double dsin(double a) { return std::sin(a); }
+inline Dual dsin(Dual a) { return Dual(std::sin(a.v), std::cos(a.v) * a.d); }
+inline double dcos(double a) { return std::cos(a); }
+inline Dual dcos(Dual a) { return Dual(std::cos(a.v), -std::sin(a.v) * a.d); }
+inline double dacos(double a) { return std::acos(a); }
+inline Dual dacos(Dual a) { return Dual(std::acos(a.v), -a.d / std::sqrt(1.0 - a.v * a.v)); }
+inline double datan(double a) { return std::atan(a); }
+inline Dual datan(Dual a) { return Dual(std::atan(a.v), a.d / (1.0 + a.v * a.v)); }
+inline double dtan(double a) { return std::tan(a); }
+inline Dual dtan(Dual a) { double t = std::tan(a.v); return Dual(t, (1.0 + t * t) * a.d); }
+inline double dabs(double a) { return std::fabs(a); }
+inline Dual dabs(Dual a) { return a.v < 0 ? -a : a; }
+
+// ------------------------------------------------------------------- affine
+template <class T>
+struct Aff {
+  T R[9];  // row-major linear part
+  T t[3];
+};
+
+// Eigen QuaternionBase::toRotationMatrix [ext Eigen 3.4], q = (x, y, z, w).
+// No normalisation happens here (the slerp result goes through it as is).
+template <class T>
+void quat_to_rot(T x, T y, T z, T w, T* R) {
+  const T tx = T(2) * x, ty = T(2) * y, tz = T(2) * z;
+  const T twx = tx * w, twy = ty * w, twz = tz * w;
+  const T txx = tx * x, txy = ty * x, txz = tz * x;
+  const T tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  R[0] = T(1) - (tyy + tzz); R[1] = txy - twz;           R[2] = txz + twy;
+  R[3] = txy + twz;          R[4] = T(1) - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy;          R[7] = tyz + twx;          R[8] = T(1) - (txx + tyy);
+}
+
+// Eigen Quaternion(const Matrix3d&) [ext Eigen 3.4, quaternionbase_assign_impl]:
+// Shepperd's method, q = (x, y, z, w).
+template <class T>
+void rot_to_quat(const T* m, T* q /* x y z w */) {
+  T t = m[0] + m[4] + m[8];
+  if (val(t) > 0.0) {
+    t = dsqrt(t + T(1.0));
+    q[3] = T(0.5) * t;
+    t = T(0.5) / t;
+    q[0] = (m[7] - m[5]) * t;
+    q[1] = (m[2] - m[6]) * t;
+    q[2] = (m[3] - m[1]) * t;
+  } else {
+    int i = 0;
+    if (val(m[4]) > val(m[0])) i = 1;
+    if (val(m[8]) > val(m[3 * i + i])) i = 2;
+    int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = dsqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + T(1.0));
+    q[i] = T(0.5) * t;
+    t = T(0.5) / t;
+    q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
+    q[j] = (m[3 * j + i] + m[3 * i + j]) * t;
+    q[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+  }
+}
+
+// dense_map_utils.cc:171-178 — array [tx ty tz qx qy qz qw] -> Affine3d,
+// Quaterniond(w=arr[6], x=arr[3], y=arr[4], z=arr[5]).normalize().
+template <class T>
+Aff<T> array_to_rigid_transform(const T* arr) {
+  T x = arr[3], y = arr[4], z = arr[5], w = arr[6];
+  T n2 = x * x + y * y + z * z + w * w;
+  if (val(n2) > 0.0) {
+    T n = dsqrt(n2);
+    x /= n; y /= n; z /= n; w /= n;
+  }
+  Aff<T> a;
+  quat_to_rot(x, y, z, w, a.R);
+  a.t[0] = arr[0]; a.t[1] = arr[1]; a.t[2] = arr[2];
+  return a;
+}
+
+// dense_map_utils.cc:195-208 — 12 numbers, row-major 3x4.
+template <class T>
+Aff<T> array_to_affine_transform(const T* arr) {
+  Aff<T> a;
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) a.R[3 * r + c] = arr[4 * r + c];
+    a.t[r] = arr[4 * r + 3];
+  }
+  return a;
+}
+
+// Affine3d product [ext]: linear = A.lin*B.lin, t = A.lin*B.t + A.t
+template <class T>
+Aff<T> compose(const Aff<T>& A, const Aff<T>& B) {
+  Aff<T> C;
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++)
+      C.R[3 * r + c] = A.R[3 * r + 0] * B.R[c] + A.R[3 * r + 1] * B.R[3 + c] + A.R[3 * r + 2] * B.R[6 + c];
+    C.t[r] = A.R[3 * r + 0] * B.t[0] + A.R[3 * r + 1] * B.t[1] + A.R[3 * r + 2] * B.t[2] + A.t[r];
+  }
+  return C;
+}
+
+template <class T>
+void apply(const Aff<T>& A, const T* X, T* Y) {
+  for (int r = 0; r < 3; r++)
+    Y[r] = A.R[3 * r + 0] * X[0] + A.R[3 * r + 1] * X[1] + A.R[3 * r + 2] * X[2] + A.t[r];
+}
+
+// Eigen Transform::inverse() with the default Affine hint [ext]: 3x3 inverse by
+// cofactors, t' = -L^{-1} t.
+template <class T>
+Aff<T> affine_inverse(const Aff<T>& A) {
+  const T* m = A.R;
+  T c00 = m[4] * m[8] - m[5] * m[7];
+  T c10 = m[5] * m[6] - m[3] * m[8];
+  T c20 = m[3] * m[7] - m[4] * m[6];
+  T det = c00 * m[0] + c10 * m[1] + c20 * m[2];
+  T inv = T(1) / det;
+  Aff<T> B;
+  B.R[0] = c00 * inv;
+  B.R[1] = (m[2] * m[7] - m[1] * m[8]) * inv;
+  B.R[2] = (m[1] * m[5] - m[2] * m[4]) * inv;
+  B.R[3] = c10 * inv;
+  B.R[4] = (m[0] * m[8] - m[2] * m[6]) * inv;
+  B.R[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
+  B.R[6] = c20 * inv;
+  B.R[7] = (m[1] * m[6] - m[0] * m[7]) * inv;
+  B.R[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
+  for (int r = 0; r < 3; r++)
+    B.t[r] = -(B.R[3 * r + 0] * A.t[0] + B.R[3 * r + 1] * A.t[1] + B.R[3 * r + 2] * A.t[2]);
+  return B;
+}
+
+// dense_map_utils.cc:315-329 with Eigen 3.4 QuaternionBase::slerp [ext].
+template <class T>
+Aff<T> linear_interp(T alpha, const Aff<T>& a0, const Aff<T>& a1) {
+  T q0[4], q1[4];
+  rot_to_quat(a0.R, q0);
+  rot_to_quat(a1.R, q1);
+  Aff<T> res;
+  for (int i = 0; i < 3; i++) res.t[i] = (T(1.0) - alpha) * a0.t[i] + alpha * a1.t[i];
+  const double one = 1.0 - DBL_EPSILON;  // NumTraits<double>::epsilon()
+  T d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
+  T absD = dabs(d);
+  T scale0, scale1;
+  if (val(absD) >= one) {
+    scale0 = T(1) - alpha;
+    scale1 = alpha;
+  } else {
+    T theta = dacos(absD);
+    T sinTheta = dsin(theta);
+    scale0 = dsin((T(1) - alpha) * theta) / sinTheta;
+    scale1 = dsin(alpha * theta) / sinTheta;
+  }
+  if (val(d) < 0.0) scale1 = -scale1;
+  T qi[4];
+  for (int i = 0; i < 4; i++) qi[i] = scale0 * q0[i] + scale1 * q1[i];
+  quat_to_rot(qi[0], qi[1], qi[2], qi[3], res.R);
+  return res;
+}
+
+// rig_calibrator.cc:322-353. Returns false for the LOG(FATAL) alpha check.
+template <class T>
+bool calc_interp_world_to_ref(const T* beg, const T* end, double beg_stamp, double end_stamp,
+                              T offset, double cam_stamp, Aff<T>* out) {
+  Aff<T> b = array_to_rigid_transform(beg);
+  Aff<T> e = array_to_rigid_transform(end);
+  if (end_stamp == beg_stamp) { *out = b; return true; }
+  // Subtract the big timestamps first (comment at :338-342).
+  T alpha = ((T(cam_stamp - beg_stamp)) - offset) / T(end_stamp - beg_stamp);
+  if (val(alpha) < 0.0 || val(alpha) > 1.0) return false;  // :346
+  *out = linear_interp(alpha, b, e);
+  return true;
+}
+
+// rig_calibrator.cc:362-390
+template <class T>
+bool calc_world_to_cam_trans(const T* beg, const T* end, const T* ref_to_cam, double beg_stamp,
+                             double end_stamp, T offset, double cam_stamp, Aff<T>* out) {
+  if (beg_stamp == end_stamp) {
+    *out = array_to_rigid_transform(beg);
+    return true;
+  }
+  Aff<T> r2c = array_to_rigid_transform(ref_to_cam);
+  Aff<T> w2r;
+  if (!calc_interp_world_to_ref(beg, end, beg_stamp, end_stamp, offset, cam_stamp, &w2r)) return false;
+  *out = compose(r2c, w2r);
+  return true;
+}
+
+// rpc_distortion.cc:43-49
+inline int rpc_degree(int n) { return static_cast<int>(std::round(std::sqrt(2.0 * n + 5.0) / 2.0 - 1.5)); }
+inline int rpc_num_dist_params(int d) { return 2 * (d + 1) * (d + 2) - 2; }
+inline bool rpc_valid(int n) {
+  int d = rpc_degree(n);
+  return !(rpc_num_dist_params(d) != n || d <= 0);
+}
+// camera_params.cc:169-208 — sizes accepted by SetDistortion.
+inline bool distortion_size_valid(int K) {
+  if (K == 0 || K == 1 || K == 4 || K == 5) return true;
+  if (K % 2 != 0) return false;
+  return rpc_valid(K / 2);
+}
+
+// rpc_distortion.cc:116-160 — coeffs [num_x | den_x | num_y | den_y]
+template <class T>
+void compute_rpc(T x, T y, const T* coeffs, int ncoeff, T* ox, T* oy) {
+  int deg = rpc_degree(ncoeff);
+  std::vector<T> powx(deg + 1), powy(deg + 1);
+  T valx = T(1.0), valy = T(1.0);
+  for (int k = 0; k <= deg; k++) {
+    powx[k] = valx; valx *= x;
+    powy[k] = valy; valy *= y;
+  }
+  int ci = 0;
+  T vals[4] = {T(0.0), T(1.0), T(0.0), T(1.0)};
+  for (int count = 0; count < 4; count++) {
+    int start = (count == 1 || count == 3) ? 1 : 0;
+    for (int dg = start; dg <= deg; dg++)
+      for (int i = 0; i <= dg; i++) {
+        vals[count] += coeffs[ci] * powx[dg - i] * powy[i];
+        ci++;
+      }
+  }
+  *ox = vals[0] / vals[1];
+  *oy = vals[2] / vals[3];
+}
+
+// camera_params.cc:260-314 then Convert<UNDISTORTED_C, DISTORTED> (:412-415).
+template <class T>
+void distort(T u0, T u1, T f, T c0, T c1, const T* k, int K, double h0, double h1, T* d0, T* d1) {
+  if (K == 0) {
+    *d0 = ((u0 + c0) - T(h0));
+    *d1 = ((u1 + c1) - T(h1));
+  } else if (K == 1) {
+    // SetDistortion precalcs (:185-190) recomputed from the parameter.
+    T pc1 = T(1) / k[0];
+    T pc2 = T(2) * dtan(k[0] / T(2));
+    T n0 = u0 / f, n1 = u1 / f;
+    T ru = dsqrt(n0 * n0 + n1 * n1);
+    T rd = datan(ru * pc2) * pc1;
+    T conv = (val(ru) > 1e-5) ? rd / ru : T(1);
+    *d0 = (c0 - T(h0)) + conv * (n0 * f);
+    *d1 = (c1 - T(h1)) + conv * (n1 * f);
+  } else if (K == 4 || K == 5) {
+    T k1 = k[0], k2 = k[1], p1 = k[2], p2 = k[3];
+    T k3 = (K == 5) ? k[4] : T(0);
+    T n0 = u0 / f, n1 = u1 / f;
+    T r2 = n0 * n0 + n1 * n1;
+    T radial = T(1) + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2;
+    T e0 = radial * n0, e1 = radial * n1;
+    e0 += T(2) * p1 * n0 * n1 + p2 * (r2 + T(2) * n0 * n0);
+    e1 += p1 * (r2 + T(2) * n1 * n1) + T(2) * p2 * n0 * n1;
+    *d0 = e0 * f + (c0 - T(h0));
+    *d1 = e1 * f + (c1 - T(h1));
+  } else {
+    // RPC: only the distortion half [0, K/2) enters; the optical centre is unused (:311).
+    compute_rpc(u0, u1, k, K / 2, d0, d1);
+  }
+  *d0 += T(h0);
+  *d1 += T(h1);
+}
+
+// rig_calibrator.cc:447-482. p = 8 parameter blocks.
+template <class T>
+bool cam_error(const T* const* p, int K, double h0, double h1, double m0, double m1, double sb,
+               double se, double sc, T* r) {
+  Aff<T> wc;
+  if (!calc_world_to_cam_trans(p[0], p[1], p[2], sb, se, p[4][0], sc, &wc)) return false;
+  T X[3] = {p[3][0], p[3][1], p[3][2]};
+  T Xc[3];
+  apply(wc, X, Xc);
+  T f = p[5][0];
+  T u0 = f * (Xc[0] / Xc[2]);
+  T u1 = f * (Xc[1] / Xc[2]);
+  T d0, d1;
+  distort(u0, u1, f, p[6][0], p[6][1], p[7], K, h0, h1, &d0, &d1);
+  r[0] = d0 - T(m0);
+  r[1] = d1 - T(m1);
+  return true;
+}
+
+// rig_calibrator.cc:547-583. p = [beg, end, ref_to_cam, depth_to_image(7|12),
+// scale, xyz, offset].
+template <class T>
+bool depth_error(const T* const* p, int dti_size, double weight, const double* meas, double sb,
+                 double se, double sc, T* r) {
+  Aff<T> wc;
+  if (!calc_world_to_cam_trans(p[0], p[1], p[2], sb, se, p[6][0], sc, &wc)) return false;
+  Aff<T> dti = (dti_size == 12) ? array_to_affine_transform(p[3]) : array_to_rigid_transform(p[3]);
+  T s = p[4][0];
+  for (int i = 0; i < 9; i++) dti.R[i] *= s;
+  T z[3] = {T(meas[0]), T(meas[1]), T(meas[2])};
+  T M[3], Mw[3];
+  apply(dti, z, M);
+  Aff<T> inv = affine_inverse(wc);
+  apply(inv, M, Mw);
+  for (int i = 0; i < 3; i++) r[i] = T(weight) * (p[5][i] - Mw[i]);
+  return true;
+}
+
+// --------------------------------------------------------------- evaluation
+struct CamProblem {
+  const mvba_problem_desc* d;
+  const double* params;
+};
+
+static const int kBase[8] = {MVBA_JAC_BASE_BEG, MVBA_JAC_BASE_END, MVBA_JAC_BASE_REF_TO_CAM,
+                             MVBA_JAC_BASE_XYZ, MVBA_JAC_BASE_OFFSET, MVBA_JAC_BASE_FOCAL,
+                             MVBA_JAC_BASE_CENTER, MVBA_JAC_BASE_DIST};
+static const int kFixedSize[7] = {7, 7, 7, 3, 1, 1, 2};
+
+static thread_local std::string g_err;
+
+// Evaluate one residual block in the requested mode. J: 56+2K doubles (Ceres layout
+// rows per MVBA_JAC_BASE_*), constant blocks left at zero.
+static int eval_one(const mvba_problem_desc* d, const double* params, int64_t i, int mode,
+                    double* r, double* J) {
+  const int32_t* blk = d->residual_blocks + 8 * i;
+  int cam = d->residual_camera[i];
+  int K = d->camera_dist_size[cam];
+  double h0 = d->camera_half_size[2 * cam], h1 = d->camera_half_size[2 * cam + 1];
+  double m0 = d->residual_meas[2 * i], m1 = d->residual_meas[2 * i + 1];
+  double sb = d->residual_stamps[3 * i], se = d->residual_stamps[3 * i + 1],
+         sc = d->residual_stamps[3 * i + 2];
+  int sizes[8];
+  for (int b = 0; b < 7; b++) sizes[b] = kFixedSize[b];
+  sizes[7] = K;
+  // Local copies of the blocks (Ceres copies parameters before differencing).
+  std::vector<double> buf[8];
+  for (int b = 0; b < 8; b++) {
+    int n = (b == 7) ? std::max(K, 1) : sizes[b];
+    buf[b].assign(n, 0.0);
+    int bs = d->block_size[blk[b]];
+    for (int j = 0; j < std::min(n, bs); j++) buf[b][j] = params[d->block_offset[blk[b]] + j];
+  }
+  const double* pd[8];
+  for (int b = 0; b < 8; b++) pd[b] = buf[b].data();
+  if (!cam_error<double>(pd, K, h0, h1, m0, m1, sb, se, sc, r)) return MVBA_E_ALPHA_RANGE;
+  if (mode == 0 || J == nullptr) return MVBA_OK;
+  for (int b = 0; b < 8; b++) {
+    if (d->block_constant[blk[b]]) continue;  // jacobians[b] == NULL
+    for (int j = 0; j < sizes[b]; j++) {
+      double jc[2];
+      if (mode == 1) {
+        // Ceres 1.14 numeric_diff.h, CENTRAL [ext].
+        const double x = buf[b][j];
+        const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
+        const double delta = std::max(min_step, std::fabs(x) * 1e-6);
+        double rp[2], rm[2];
+        buf[b][j] = x + delta;
+        if (!cam_error<double>(pd, K, h0, h1, m0, m1, sb, se, sc, rp)) return MVBA_E_ALPHA_RANGE;
+        double one_over_delta = 1.0 / delta;
+        buf[b][j] = x - delta;
+        if (!cam_error<double>(pd, K, h0, h1, m0, m1, sb, se, sc, rm)) return MVBA_E_ALPHA_RANGE;
+        one_over_delta /= 2;
+        buf[b][j] = x;
+        jc[0] = (rp[0] - rm[0]) * one_over_delta;
+        jc[1] = (rp[1] - rm[1]) * one_over_delta;
+      } else {
+        std::vector<Dual> db[8];
+        const Dual* pdd[8];
+        for (int bb = 0; bb < 8; bb++) {
+          db[bb].resize(buf[bb].size());
+          for (size_t q = 0; q < buf[bb].size(); q++) db[bb][q] = Dual(buf[bb][q], 0.0);
+          pdd[bb] = db[bb].data();
+        }
+        db[b][j].d = 1.0;
+        Dual rr[2];
+        if (!cam_error<Dual>(pdd, K, h0, h1, m0, m1, sb, se, sc, rr)) return MVBA_E_ALPHA_RANGE;
+        jc[0] = rr[0].d;
+        jc[1] = rr[1].d;
+      }
+      J[kBase[b] + 0 * sizes[b] + j] = jc[0];
+      J[kBase[b] + 1 * sizes[b] + j] = jc[1];
+    }
+  }
+  return MVBA_OK;
+}
+
+}  // namespace oracle
+
+using namespace oracle;
+
+extern "C" {
+
+// Validation mirroring BracketedCamError's ctor (rig_calibrator.cc:433-440) and
+// SetDistortion (camera_params.cc:199-206).
+int oracle_validate(const mvba_problem_desc* d) {
+  for (int c = 0; c < d->num_cameras; c++)
+    if (!distortion_size_valid(d->camera_dist_size[c])) {
+      g_err = "Recieved irregular distortion vector size. Size = " + std::to_string(d->camera_dist_size[c]);
+      return MVBA_E_BAD_DISTORTION;
+    }
+  for (int64_t i = 0; i < d->num_residuals; i++) {
+    const int32_t* blk = d->residual_blocks + 8 * i;
+    for (int b = 0; b < 7; b++)
+      if (d->block_size[blk[b]] != kFixedSize[b]) {
+        g_err = "BracketedCamError: The block sizes were not set up properly.";
+        return MVBA_E_BLOCK_SIZES;
+      }
+    int K = d->camera_dist_size[d->residual_camera[i]];
+    if (K > 0 && d->block_size[blk[7]] != K) {
+      g_err = "BracketedCamError: The block sizes were not set up properly.";
+      return MVBA_E_BLOCK_SIZES;
+    }
+  }
+  return MVBA_OK;
+}
+
+const char* oracle_last_error(void) { return g_err.c_str(); }
+
+int oracle_jacobian_stride(const mvba_problem_desc* d) {
+  int kmax = 0;
+  for (int c = 0; c < d->num_cameras; c++) kmax = std::max(kmax, (int)d->camera_dist_size[c]);
+  return MVBA_JAC_BASE_DIST + 2 * kmax;
+}
+
+// mode: 0 residuals only, 1 Ceres central differences, 2 forward-mode exact.
+// flags: MVBA_EVAL_APPLY_LOSS applies Cauchy(cauchy_threshold) via the Ceres corrector.
+// Residual range [begin, end) lets a caller time a bounded sample.
+int oracle_evaluate(const mvba_problem_desc* d, const double* params, int mode, int flags,
+                    double cauchy_threshold, int64_t begin, int64_t end, double* cost,
+                    double* residuals, double* jacobian) {
+  int st = oracle_validate(d);
+  if (st != MVBA_OK) return st;
+  const int stride = oracle_jacobian_stride(d);
+  if (end < 0 || end > d->num_residuals) end = d->num_residuals;
+  const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
+  const double b = cauchy_threshold * cauchy_threshold, c = 1.0 / b;
+  double total = 0.0;
+  std::vector<double> Jtmp(stride);
+  for (int64_t i = begin; i < end; i++) {
+    double r[2];
+    double* J = nullptr;
+    if (jacobian && mode != 0) {
+      J = jacobian + (i - begin) * stride;
+      std::fill(J, J + stride, 0.0);
+    }
+    st = eval_one(d, params, i, mode, r, J);
+    if (st != MVBA_OK) {
+      g_err = "Out of bounds in interpolation.";
+      return st;
+    }
+    double s = r[0] * r[0] + r[1] * r[1];
+    if (!loss) {
+      total += 0.5 * s;
+    } else {
+      // Ceres 1.14 CauchyLoss::Evaluate + Corrector (rho'' < 0 branch).
+      const double sum = 1.0 + s * c;
+      const double inv = 1.0 / sum;
+      const double rho0 = b * std::log(sum);
+      const double rho1 = std::max(std::numeric_limits<double>::min(), inv);
+      total += 0.5 * rho0;
+      const double sr = std::sqrt(rho1);
+      r[0] *= sr;
+      r[1] *= sr;
+      if (J) for (int k = 0; k < stride; k++) J[k] *= sr;
+    }
+    if (residuals) {
+      residuals[2 * (i - begin)] = r[0];
+      residuals[2 * (i - begin) + 1] = r[1];
+    }
+  }
+  if (cost) *cost = total;
+  return MVBA_OK;
+}
+
+// Multi-threaded evaluation over residual blocks (Ceres ProgramEvaluator runs
+// residual blocks in parallel with num_threads = FLAGS_num_opt_threads,
+// rig_calibrator.cc:1913). Timing path of bench.py's cpu_baseline; raw
+// residuals/Jacobians (no loss), Ceres layout.
+int oracle_evaluate_mt(const mvba_problem_desc* d, const double* params, int mode, int flags,
+                       double cauchy_threshold, int64_t begin, int64_t end, int threads,
+                       double* residuals, double* jacobian) {
+  int st = oracle_validate(d);
+  if (st != MVBA_OK) return st;
+  const int stride = oracle_jacobian_stride(d);
+  if (end < 0 || end > d->num_residuals) end = d->num_residuals;
+  int bad = 0;
+#pragma omp parallel for schedule(dynamic, 64) num_threads(threads) reduction(| : bad)
+  for (int64_t i = begin; i < end; i++) {
+    double r[2];
+    double* J = nullptr;
+    if (jacobian && mode != 0) {
+      J = jacobian + (i - begin) * stride;
+      std::fill(J, J + stride, 0.0);
+    }
+    if (eval_one(d, params, i, mode, r, J) != MVBA_OK) bad |= 1;
+    residuals[2 * (i - begin)] = r[0];
+    residuals[2 * (i - begin) + 1] = r[1];
+  }
+  if (bad) {
+    g_err = "Out of bounds in interpolation.";
+    return MVBA_E_ALPHA_RANGE;
+  }
+  return MVBA_OK;
+}
+
+// World-to-camera transform of one residual block's image (12 doubles:
+// row-major R then t). Used by the known-answer tests.
+int oracle_world_to_cam(const double* beg, const double* end, const double* ref_to_cam,
+                        double beg_stamp, double end_stamp, double offset, double cam_stamp,
+                        double* out12) {
+  Aff<double> a;
+  if (!calc_world_to_cam_trans(beg, end, ref_to_cam, beg_stamp, end_stamp, offset, cam_stamp, &a))
+    return MVBA_E_ALPHA_RANGE;
+  for (int k = 0; k < 9; k++) out12[k] = a.R[k];
+  for (int k = 0; k < 3; k++) out12[9 + k] = a.t[k];
+  return MVBA_OK;
+}
+
+// DistortCentered + half size, for unit tests of the camera model alone.
+int oracle_distort(double u0, double u1, double f, double c0, double c1, const double* k, int K,
+                   double h0, double h1, double* out2) {
+  if (!distortion_size_valid(K)) return MVBA_E_BAD_DISTORTION;
+  distort<double>(u0, u1, f, c0, c1, k, K, h0, h1, &out2[0], &out2[1]);
+  return MVBA_OK;
+}
+
+// BracketedDepthError for one block set; mode 0 residual, 1 numeric diff, 2 exact.
+// blocks: 7 pointers [beg, end, ref_to_cam, depth_to_image, scale, xyz, offset];
+// J rows (3 x size_b row-major per block) concatenated in block order, constant
+// blocks (constant[b] != 0) zero-filled. Returns the number of J doubles written.
+int oracle_depth_error(const double* const* blocks, int dti_size, const uint8_t* constant,
+                       double weight, const double* meas, double sb, double se, double sc,
+                       int mode, double* r3, double* J) {
+  int sizes[7] = {7, 7, 7, dti_size, 1, 3, 1};
+  if (dti_size != 7 && dti_size != 12) return -MVBA_E_DEPTH_BLOCK_SIZES;
+  std::vector<double> buf[7];
+  const double* pd[7];
+  for (int b = 0; b < 7; b++) {
+    buf[b].assign(blocks[b], blocks[b] + sizes[b]);
+    pd[b] = buf[b].data();
+  }
+  if (!depth_error<double>(pd, dti_size, weight, meas, sb, se, sc, r3)) return -MVBA_E_ALPHA_RANGE;
+  if (mode == 0 || !J) return 0;
+  int off = 0;
+  for (int b = 0; b < 7; b++) {
+    for (int j = 0; j < sizes[b]; j++) {
+      double jc[3] = {0, 0, 0};
+      if (!constant[b]) {
+        if (mode == 1) {
+          const double x = buf[b][j];
+          const double delta = std::max(std::sqrt(std::numeric_limits<double>::epsilon()), std::fabs(x) * 1e-6);
+          double rp[3], rm[3];
+          buf[b][j] = x + delta;
+          depth_error<double>(pd, dti_size, weight, meas, sb, se, sc, rp);
+          double ood = 1.0 / delta;
+          buf[b][j] = x - delta;
+          depth_error<double>(pd, dti_size, weight, meas, sb, se, sc, rm);
+          ood /= 2;
+          buf[b][j] = x;
+          for (int q = 0; q < 3; q++) jc[q] = (rp[q] - rm[q]) * ood;
+        } else {
+          std::vector<Dual> db[7];
+          const Dual* pdd[7];
+          for (int bb = 0; bb < 7; bb++) {
+            db[bb].resize(sizes[bb]);
+            for (int q = 0; q < sizes[bb]; q++) db[bb][q] = Dual(buf[bb][q], 0.0);
+            pdd[bb] = db[bb].data();
+          }
+          db[b][j].d = 1.0;
+          Dual rr[3];
+          depth_error<Dual>(pdd, dti_size, weight, meas, sb, se, sc, rr);
+          for (int q = 0; q < 3; q++) jc[q] = rr[q].d;
+        }
+      }
+      for (int q = 0; q < 3; q++) J[off + q * sizes[b] + j] = jc[q];
+    }
+    off += 3 * sizes[b];
+  }
+  return off;
+}
+
+// rig_calibrator.cc:753-789: 25/50/75/100th percentiles of |r| per name.
+// names: residual name id per residual (already mapped to sorted std::map order by
+// the caller), out: [num_names * 4] values and [num_names] counts.
+void oracle_residual_stats(const double* residuals, const int32_t* name_ids, int64_t n,
+                           int32_t num_names, double* out, int64_t* counts) {
+  std::vector<std::vector<double>> stats(num_names);
+  for (int64_t i = 0; i < n; i++) stats[name_ids[i]].push_back(std::fabs(residuals[i]));
+  for (int k = 0; k < num_names; k++) {
+    std::vector<double>& v = stats[k];
+    std::sort(v.begin(), v.end());
+    int len = (int)v.size();
+    counts[k] = len;
+    if (len == 0) { for (int q = 0; q < 4; q++) out[4 * k + q] = NAN; continue; }
+    out[4 * k + 0] = v[(int)(0.25 * len)];
+    out[4 * k + 1] = v[(int)(0.50 * len)];
+    out[4 * k + 2] = v[(int)(0.75 * len)];
+    out[4 * k + 3] = v[len - 1];
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,157 @@
+"""ctypes loader of the CPU oracle (liboracle_mvba.so).
+
+TEST INFRASTRUCTURE ONLY — importable from tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker. PARITY UNPINNED against the
+reference binary (see oracle.cpp header and DESIGN.md "Oracle").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle_mvba.so")
+
+RESIDUAL, NUMDIFF, ANALYTIC = 0, 1, 2
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    lib.oracle_evaluate.restype = C.c_int
+    lib.oracle_evaluate.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_double,
+                                    C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.oracle_evaluate_mt.restype = C.c_int
+    lib.oracle_evaluate_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_double,
+                                       C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p]
+    lib.oracle_validate.restype = C.c_int
+    lib.oracle_validate.argtypes = [C.c_void_p]
+    lib.oracle_last_error.restype = C.c_char_p
+    lib.oracle_jacobian_stride.restype = C.c_int
+    lib.oracle_jacobian_stride.argtypes = [C.c_void_p]
+    lib.oracle_world_to_cam.restype = C.c_int
+    lib.oracle_world_to_cam.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_double, C.c_double,
+                                        C.c_double, C.c_double, C.c_void_p]
+    lib.oracle_distort.restype = C.c_int
+    lib.oracle_distort.argtypes = [C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
+                                   C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p]
+    lib.oracle_depth_error.restype = C.c_int
+    lib.oracle_depth_error.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_double, C.c_void_p,
+                                       C.c_double, C.c_double, C.c_double, C.c_int, C.c_void_p,
+                                       C.c_void_p]
+    lib.oracle_residual_stats.restype = None
+    lib.oracle_residual_stats.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p,
+                                          C.c_void_p]
+    _lib = lib
+    return lib
+
+
+class OracleError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"oracle status {status}: {msg}")
+        self.status = status
+
+
+def evaluate(problem, mode=ANALYTIC, apply_loss=False, robust_threshold=3.0, begin=0, end=-1):
+    """Evaluate a CamProblem on the CPU. Returns (cost, r [n,2], J [n,stride] or None)."""
+    lib = load()
+    desc = problem.desc()
+    n = problem.num_residuals if end < 0 else end - begin
+    stride = lib.oracle_jacobian_stride(C.byref(desc))
+    r = np.empty((n, 2))
+    J = np.zeros((n, stride)) if mode != RESIDUAL else None
+    cost = C.c_double()
+    flags = 0x4 if apply_loss else 0
+    st = lib.oracle_evaluate(C.byref(desc), problem.params.ctypes.data, mode, flags,
+                             float(robust_threshold), int(begin), int(end), C.byref(cost),
+                             r.ctypes.data, J.ctypes.data if J is not None else None)
+    if st != 0:
+        raise OracleError(st, lib.oracle_last_error().decode())
+    return cost.value, r, J
+
+
+def evaluate_mt(problem, mode=NUMDIFF, begin=0, end=-1, threads=1, want_jac=True):
+    """Multi-threaded (OpenMP over residual blocks, like Ceres num_threads) timing
+    path for the cpu_baseline: writes residuals and Jacobian rows."""
+    lib = load()
+    desc = problem.desc()
+    n = problem.num_residuals if end < 0 else end - begin
+    stride = lib.oracle_jacobian_stride(C.byref(desc))
+    r = np.empty((n, 2))
+    J = np.zeros((n, stride)) if want_jac else None
+    st = lib.oracle_evaluate_mt(C.byref(desc), problem.params.ctypes.data, mode, 0, 3.0,
+                                int(begin), int(end), int(threads), r.ctypes.data,
+                                J.ctypes.data if J is not None else None)
+    if st != 0:
+        raise OracleError(st, lib.oracle_last_error().decode())
+    return r, J
+
+
+def validate(problem):
+    lib = load()
+    desc = problem.desc()
+    st = lib.oracle_validate(C.byref(desc))
+    return st, lib.oracle_last_error().decode()
+
+
+def world_to_cam(beg, end, r2c, sb, se, off, sc):
+    lib = load()
+    out = np.empty(12)
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (beg, end, r2c)]
+    st = lib.oracle_world_to_cam(arrs[0].ctypes.data, arrs[1].ctypes.data, arrs[2].ctypes.data,
+                                 sb, se, off, sc, out.ctypes.data)
+    if st != 0:
+        raise OracleError(st, "Out of bounds in interpolation.")
+    return out[:9].reshape(3, 3), out[9:]
+
+
+def distort(u, f, c, k, half):
+    lib = load()
+    k = np.ascontiguousarray(k, dtype=np.float64)
+    out = np.empty(2)
+    st = lib.oracle_distort(float(u[0]), float(u[1]), float(f), float(c[0]), float(c[1]),
+                            k.ctypes.data if k.size else None, int(k.size), float(half[0]),
+                            float(half[1]), out.ctypes.data)
+    if st != 0:
+        raise OracleError(st, "Recieved irregular distortion vector size.")
+    return out
+
+
+def depth_error(blocks, constant, weight, meas, sb, se, sc, mode=ANALYTIC):
+    """BracketedDepthError (rig_calibrator.cc:547-583). blocks: 7 arrays."""
+    lib = load()
+    arrs = [np.ascontiguousarray(b, dtype=np.float64) for b in blocks]
+    ptrs = (C.c_void_p * 7)(*[a.ctypes.data for a in arrs])
+    const = np.ascontiguousarray(constant, dtype=np.uint8)
+    m = np.ascontiguousarray(meas, dtype=np.float64)
+    r = np.empty(3)
+    nj = 3 * sum(a.size for a in arrs)
+    J = np.zeros(nj)
+    st = lib.oracle_depth_error(ptrs, arrs[3].size, const.ctypes.data, float(weight), m.ctypes.data,
+                                sb, se, sc, mode, r.ctypes.data, J.ctypes.data)
+    if st < 0:
+        raise OracleError(-st, "depth error")
+    return r, J
+
+
+def residual_stats(residuals, name_ids, num_names):
+    lib = load()
+    r = np.ascontiguousarray(residuals, dtype=np.float64)
+    ids = np.ascontiguousarray(name_ids, dtype=np.int32)
+    out = np.empty(4 * num_names)
+    cnt = np.empty(num_names, dtype=np.int64)
+    lib.oracle_residual_stats(r.ctypes.data, ids.ctypes.data, r.size, num_names, out.ctypes.data,
+                              cnt.ctypes.data)
+    return out.reshape(num_names, 4), cnt
