@@ -63,18 +63,40 @@ def fd_bound(problem, J_ref, pix_scale):
     eps = np.finfo(float).eps
     n, stride = J_ref.shape
     bound = np.zeros((n, stride))
+    half = problem.camera_half_size
     for i in range(n):
         blks = problem.residual_blocks[i]
+        cam = problem.residual_camera[i]
+        K = int(problem.camera_dist_size[cam])
         for b in range(8):
             vals = problem.block_values(blks[b])
-            size = len(vals) if b == 7 else (7, 7, 7, 3, 1, 1, 2)[b]
-            if b == 7:
-                size = int(problem.camera_dist_size[problem.residual_camera[i]])
+            size = (7, 7, 7, 3, 1, 1, 2)[b] if b < 7 else K
             for j in range(size):
                 delta = max(np.sqrt(eps), 1e-6 * abs(vals[j]))
                 tb = 64 * eps * max(pix_scale[i], 1.0) / delta
                 for row in range(2):
                     bound[i, JAC_BASE[b] + row * size + j] = tb
+        if K >= 20:
+            # RPC denominator coefficient b with monomial m: f = N/D(b), so
+            # f''' = -6 q (m/D)^3 with q = N/D and m/D = -J/q: truncation of the
+            # central difference delta^2 |f'''| / 6 = delta^2 |J|^3 / q^2 (x2 for
+            # the higher-order terms; it exceeds |J| where FD is meaningless).
+            nh = K // 2
+            deg = int(round(np.sqrt(2.0 * nh + 5.0) / 2.0 - 1.5))
+            nl = (deg + 1) * (deg + 2) // 2
+            vals = problem.block_values(blks[7])
+            meas = problem.residual_meas[i]
+            for row, lo in ((0, nl), (1, 3 * nl - 1)):
+                r = J_ref[i]  # exact Jacobian row block
+                for j in range(lo, lo + nl - 1):
+                    col = JAC_BASE[7] + row * K + j
+                    delta = max(np.sqrt(eps), 1e-6 * abs(vals[j]))
+                    q = max(abs(meas[row] - half[cam][row]), 1.0)
+                    x = delta * abs(r[col]) / q  # relative change of D over one step
+                    if x > 0.02:
+                        bound[i, col] = np.inf  # FD series diverges: the reference's FD column is not a derivative
+                    else:
+                        bound[i, col] += 3.0 * delta ** 2 * abs(r[col]) ** 3 / q ** 2
     return bound + 1e-6 * np.abs(J_ref).max(axis=0, keepdims=True)
 
 

@@ -1,0 +1,81 @@
+"""GPU test of the header-only Ceres adapter (include/mvba/ceres_surface.h),
+driven the way Ceres drives a CostFunction (tests/cpp/test_ceres_surface.cpp)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from multiview_amd import rig
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(ROOT, "tests", "cpp", "test_ceres_surface")
+
+
+def _write(fh, arr, dtype):
+    a = np.ascontiguousarray(arr, dtype=dtype).reshape(-1)
+    fh.write(np.int64(a.size).tobytes())
+    fh.write(a.tobytes())
+
+
+def _read(fh, dtype):
+    n = int(np.frombuffer(fh.read(8), dtype=np.int64)[0])
+    return np.frombuffer(fh.read(n * np.dtype(dtype).itemsize), dtype=dtype)
+
+
+def test_ceres_adapter(tmp_path, oracle):
+    if not os.path.exists(BIN):
+        subprocess.run(["make", "-s", "-C", os.path.dirname(BIN)], check=True)
+    R = rig.make_rig(num_sensors=3, num_ref=12, num_points=150, obs_per_point=5,
+                     models=["radtan", "rpc1", "fov"], seed=31)
+    P = rig.build_problem(R)
+    params2 = P.params.copy()
+    params2 += np.random.default_rng(1).normal(0, 1e-4, params2.shape) * (P.params != 0)
+    src = tmp_path / "prob.bin"
+    with open(src, "wb") as fh:
+        _write(fh, P.block_size, np.int32)
+        _write(fh, P.block_offset, np.int64)
+        _write(fh, P.params, np.float64)
+        _write(fh, P.camera_dist_size, np.int32)
+        _write(fh, P.camera_half_size, np.float64)
+        _write(fh, P.residual_blocks, np.int32)
+        _write(fh, P.residual_camera, np.int32)
+        _write(fh, P.residual_meas, np.float64)
+        _write(fh, P.residual_stamps, np.float64)
+        _write(fh, params2, np.float64)
+    out = tmp_path / "out.bin"
+    subprocess.run([BIN, str(src), str(out)], check=True, timeout=120)
+    n = P.num_residuals
+    stride = P.jacobian_stride()
+    with open(out, "rb") as fh:
+        R0, J0 = _read(fh, np.float64), _read(fh, np.float64)
+        J1 = _read(fh, np.float64)
+        R2, J2 = _read(fh, np.float64), _read(fh, np.float64)
+        R4, J4 = _read(fh, np.float64), _read(fh, np.float64)
+        R5, J5 = _read(fh, np.float64), _read(fh, np.float64)
+        flags = _read(fh, np.int32)
+    # full Jacobians: the adapter evaluates every block (all free)
+    Pf = rig.build_problem(R)
+    Pf.block_constant[:] = 0
+    _, r_o, J_o = oracle.evaluate(Pf, oracle.ANALYTIC)
+    P2 = rig.build_problem(R)
+    P2.block_constant[:] = 0
+    P2.params = params2
+    _, r_o2, J_o2 = oracle.evaluate(P2, oracle.ANALYTIC)
+
+    def close(r, J, r_ref, J_ref):
+        colmax = np.maximum(np.abs(J_ref).max(axis=0), 1e-12)
+        return (np.abs(r.reshape(n, 2) - r_ref).max() <= 1e-9 * 1024 and
+                (np.abs(J.reshape(n, stride) - J_ref) / colmax).max() <= 1e-9)
+
+    assert flags[0] == 1 and close(R0, J0, r_o, J_o)
+    J1 = J1.reshape(n, stride)
+    assert flags[1] == 1
+    assert np.all(J1[:, 14:28] == 0) and np.all(J1[:, 56:] == 0)  # NULL blocks untouched
+    assert np.allclose(J1[:, :14], J_o[:, :14], rtol=0, atol=1e-9 * np.abs(J_o).max())
+    assert flags[2] == 1 and flags[3] == 1 and close(R2, J2, r_o2, J_o2)  # one GPU pass
+    assert flags[4] == 0  # point not in user memory -> Evaluate() false
+    assert flags[5] == 1 and flags[6] == 1 and close(R4, J4, r_o, J_o)
+    assert flags[7] == 0 and close(R5, J5, r_o2, J_o2)

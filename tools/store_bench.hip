@@ -1,0 +1,72 @@
+// store_bench.hip — write-bandwidth ceilings for K1's output pattern on gfx950.
+// Pattern = P column planes of N doubles; each wavefront writes, for every plane,
+// its own contiguous chunk (64 lanes x E doubles). Variants: E = 1 (dwordx2) or
+// 2 (dwordx4), nontemporal or plain stores, chunk start aligned or misaligned.
+// Usage: store_bench [N] [P]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+template <int E, bool NT>
+__global__ void __launch_bounds__(256) k_planes(double* __restrict__ J, long ld, int planes, long n, int shift) {
+  const long wave = (long)(blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const long base = wave * 64 * E + shift;
+  const long i = base + (long)lane * E;
+  if (i + E > n) return;
+  const double v = (double)(i & 1023);
+  for (int p = 0; p < planes; p++) {
+    double* dst = J + (long)p * ld + i;
+    if (E == 1) {
+      if (NT) __builtin_nontemporal_store(v + p, dst);
+      else *dst = v + p;
+    } else {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      d2 w = {v + p, v - p};
+      if (NT) __builtin_nontemporal_store(w, (d2*)dst);
+      else *(d2*)dst = w;
+    }
+  }
+}
+
+template <int E, bool NT>
+float run(double* J, long ld, int planes, long n, int shift, int reps) {
+  long waves = (n - shift) / (64 * E);
+  int blocks = (int)((waves * 64 + 255) / 256);
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  hipLaunchKernelGGL((k_planes<E, NT>), dim3(blocks), dim3(256), 0, 0, J, ld, planes, n, shift);
+  CHECK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++)
+    hipLaunchKernelGGL((k_planes<E, NT>), dim3(blocks), dim3(256), 0, 0, J, ld, planes, n, shift);
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+int main(int argc, char** argv) {
+  long n = argc > 1 ? atol(argv[1]) : 1000000;
+  int planes = argc > 2 ? atoi(argv[2]) : 56;
+  long ld = ((n + 255) / 256) * 256;
+  double* J;
+  CHECK(hipMalloc(&J, sizeof(double) * ld * planes));
+  const double bytes = 8.0 * n * planes;
+  struct { const char* name; float ms; } res[8];
+  int k = 0;
+  res[k++] = {"dwordx2 nt   aligned", run<1, true>(J, ld, planes, n, 0, 20)};
+  res[k++] = {"dwordx2 plain aligned", run<1, false>(J, ld, planes, n, 0, 20)};
+  res[k++] = {"dwordx4 nt   aligned", run<2, true>(J, ld, planes, n, 0, 20)};
+  res[k++] = {"dwordx4 plain aligned", run<2, false>(J, ld, planes, n, 0, 20)};
+  res[k++] = {"dwordx2 nt   shift 8B", run<1, true>(J, ld, planes, n, 1, 20)};
+  res[k++] = {"dwordx4 nt   shift 16B", run<2, true>(J, ld, planes, n, 2, 20)};
+  for (int i = 0; i < k; i++)
+    printf("%-24s %8.3f ms  %7.1f GB/s\n", res[i].name, res[i].ms, bytes / (res[i].ms * 1e-3) / 1e9);
+  CHECK(hipFree(J));
+  return 0;
+}
