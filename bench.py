@@ -106,7 +106,7 @@ def main():
     ev = Evaluator(P, device=dev)
     ev.set_params()
     n = ev.num_residuals
-    ld = ((n + 63) // 64) * 64
+    ld = ev.ld
     res = torch.empty((2, ld), dtype=torch.float64, device="cuda")
     jac = torch.empty((ev.stride, ld), dtype=torch.float64, device="cuda")
     stream = torch.cuda.current_stream()

@@ -142,13 +142,14 @@ typedef struct mvba_options {
  * then by image frame; see DESIGN.md "HBM layout"). */
 typedef struct mvba_device_view {
   int64_t num_residuals;
+  int64_t num_slots;       /* device slots (residuals + line-alignment padding) */
   int64_t ld;              /* leading dimension (elements) of residual/Jacobian planes */
   int32_t jac_rows;        /* 56 + 2*K_max rows per residual */
   int32_t max_dist_size;   /* K_max */
   double* residuals;       /* [2][ld]  plane 0 = x residual, plane 1 = y residual */
   double* jacobian;        /* [jac_rows][ld] column planes */
-  const int64_t* order;    /* [num_residuals] device position -> AddResidualBlock index */
-  const uint8_t* row_written; /* [num_residuals] bit b set = block b written (non-constant) */
+  const int64_t* order;    /* [num_slots] device slot -> AddResidualBlock index, -1 = padding */
+  const uint8_t* row_written; /* [num_slots] bit b set = block b written (non-constant) */
 } mvba_device_view;
 
 /* Library / device queries. */
@@ -184,7 +185,8 @@ int32_t mvba_jacobian_stride(const struct mvba_handle* h);
 
 /* Device-resident evaluation (no host transfer). Outputs go to the library's
  * buffers (see mvba_device_buffers) or, if d_residuals/d_jacobian are non-null,
- * into caller-owned device memory with leading dimension ld (>= num_residuals).
+ * into caller-owned device memory with leading dimension ld (>= mvba_num_slots(),
+ * multiple of 16; base pointers 128-byte aligned).
  * Asynchronous on hip_stream (NULL = default stream). Errors raised by the
  * kernels (interpolation alpha out of range) are reported by mvba_sync_status(). */
 mvba_status mvba_evaluate_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
@@ -192,13 +194,16 @@ mvba_status mvba_evaluate_device(struct mvba_handle* h, int32_t flags, double ca
                                  void* hip_stream);
 mvba_status mvba_device_buffers(struct mvba_handle* h, mvba_device_view* view);
 /* Host copy of the device order: out[p] = AddResidualBlock index of device
- * position p (num_residuals int64). */
+ * slot p, -1 for padding (mvba_num_slots() int64). */
 mvba_status mvba_residual_order(const struct mvba_handle* h, int64_t* out);
 /* Wait for the stream and convert any device-side error word into a status. */
 mvba_status mvba_sync_status(struct mvba_handle* h, void* hip_stream);
 
 /* Counts for reporting. */
 int64_t mvba_num_residuals(const struct mvba_handle* h);
+/* Device slots = residuals + padding that line-aligns every frame's range; device
+ * output planes need ld >= mvba_num_slots(), ld a multiple of 16. */
+int64_t mvba_num_slots(const struct mvba_handle* h);
 int64_t mvba_num_frames(const struct mvba_handle* h);
 int64_t mvba_num_points(const struct mvba_handle* h);
 /* Algorithmic HBM bytes of one materialised evaluation (residual+Jacobian),

@@ -71,6 +71,7 @@ class Options(C.Structure):
 class DeviceView(C.Structure):
     _fields_ = [
         ("num_residuals", C.c_int64),
+        ("num_slots", C.c_int64),
         ("ld", C.c_int64),
         ("jac_rows", C.c_int32),
         ("max_dist_size", C.c_int32),
@@ -99,6 +100,7 @@ SIGNATURES = {
     "mvba_sync_status": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mvba_residual_order": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mvba_num_residuals": (C.c_int64, [C.c_void_p]),
+    "mvba_num_slots": (C.c_int64, [C.c_void_p]),
     "mvba_num_frames": (C.c_int64, [C.c_void_p]),
     "mvba_num_points": (C.c_int64, [C.c_void_p]),
     "mvba_eval_bytes": (C.c_double, [C.c_void_p, C.c_int32]),

@@ -29,10 +29,9 @@ using mvba::FrameDesc;
 using mvba::Segment;
 
 extern "C" {
-hipError_t mvba_launch_points(const double* params, const int64_t* pt_off, const uint8_t* pt_free,
-                              int64_t npts, double4* pts, hipStream_t s);
-hipError_t mvba_launch_frames(const FrameDesc* fd, int64_t nframes, const double* params,
-                              double* frec, int* err, hipStream_t s);
+hipError_t mvba_launch_prep(const FrameDesc* fd, int64_t nframes, const double* params,
+                            double* frec, const int64_t* pt_off, const uint8_t* pt_free, int64_t npts,
+                            double4* pts, int gen, int* err, hipStream_t s);
 hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
                            const FrameDesc* fd, const double* frec, const double* params,
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
@@ -90,9 +89,9 @@ hipError_t upload(T** p, const std::vector<T>& v) {
 struct mvba_handle {
   int device = 0;
   std::string err;
-  int64_t nres = 0, nframes = 0, npts = 0, nparams = 0;
+  int64_t nres = 0, nslots = 0, nframes = 0, npts = 0, nparams = 0;
   int kmax = 0, jac_rows = 0;
-  std::vector<int64_t> order;        // device position -> insertion index
+  std::vector<int64_t> order;        // device slot -> insertion index (-1 = padding)
   std::vector<uint8_t> row_written;  // device position -> block bitmask
   std::vector<int16_t> pos_K;        // device position -> distortion length
   std::vector<Group> groups;
@@ -115,6 +114,7 @@ struct mvba_handle {
   int64_t ld = 0;
   bool params_set = false;
   bool prep_done = false;
+  int gen = 0;  // generation of the last prep launch (error word protocol)
 
   std::vector<double> h_res, h_J;  // host staging for mvba_evaluate
 
@@ -329,13 +329,32 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     return res_frame[a] < res_frame[b];
   });
 
-  std::vector<int32_t> obs_pid(N);
-  std::vector<double2> obs_meas(N);
-  h->order.resize(N);
-  h->row_written.resize(N);
-  h->pos_K.resize(N);
+  // Device slots: every frame's residuals start on a 128-byte line (16 doubles),
+  // so each wavefront's 64-element store chunk per Jacobian plane is line-aligned
+  // (misaligned chunks write at ~60% of the aligned rate: tools/store_bench.hip).
+  constexpr int64_t kAlign = 16;
+  int64_t nslots = 0;
+  {
+    int32_t prev_fr = -1;
+    int prev_g = -1;
+    for (int64_t p = 0; p < N; p++) {
+      const int64_t i = idx[p];
+      const int g = grank[d->residual_camera[i]];
+      if (res_frame[i] != prev_fr || g != prev_g) nslots = (nslots + kAlign - 1) / kAlign * kAlign;
+      prev_fr = res_frame[i];
+      prev_g = g;
+      nslots++;
+    }
+    nslots = (nslots + kAlign - 1) / kAlign * kAlign;
+  }
+  h->nslots = nslots;
+  std::vector<int32_t> obs_pid(nslots, 0);
+  std::vector<double2> obs_meas(nslots, make_double2(0.0, 0.0));
+  h->order.assign(nslots, -1);
+  h->row_written.assign(nslots, 0);
+  h->pos_K.assign(nslots, 0);
   std::vector<Segment> segs;
-  segs.reserve(N / 32 + keys.size() + 1);
+  segs.reserve(N / 32 + frames.size() + keys.size() + 1);
   h->groups.resize(keys.size());
   double bytes_res = 0.0, bytes_jac = 0.0;
   for (size_t g = 0; g < keys.size(); g++) {
@@ -343,39 +362,46 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     h->groups[g].deg = keys[g] % 16;
   }
   int cur_group = -1;
+  int32_t cur_frame = -1;
+  int64_t slot = 0;
   for (int64_t p = 0; p < N; p++) {
     const int64_t i = idx[p];
     const int g = grank[d->residual_camera[i]];
     const int32_t fr = res_frame[i];
-    if (g != cur_group) {
+    const bool new_group = (g != cur_group);
+    if (new_group) {
       if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
       cur_group = g;
       h->groups[g].seg_begin = (int32_t)segs.size();
-      h->groups[g].res_begin = p;
     }
+    if (new_group || fr != cur_frame) {
+      slot = (slot + kAlign - 1) / kAlign * kAlign;
+      cur_frame = fr;
+    }
+    if (new_group) h->groups[g].res_begin = slot;
     h->groups[g].res_count++;
-    if (segs.empty() || segs.back().frame != fr || segs.back().count == 64 ||
-        (int32_t)segs.size() == h->groups[g].seg_begin) {
-      Segment s;
-      s.begin = (int32_t)p;
-      s.count = 0;
-      s.frame = fr;
-      s.pad = 0;
-      segs.push_back(s);
+    if (new_group || segs.back().frame != fr || segs.back().count == 64) {
+      Segment sg;
+      sg.begin = (int32_t)slot;
+      sg.count = 0;
+      sg.frame = fr;
+      sg.pad = 0;
+      segs.push_back(sg);
     }
     segs.back().count++;
-    obs_pid[p] = res_pt[i];
-    obs_meas[p] = make_double2(d->residual_meas[2 * i], d->residual_meas[2 * i + 1]);
-    h->order[p] = i;
+    obs_pid[slot] = res_pt[i];
+    obs_meas[slot] = make_double2(d->residual_meas[2 * i], d->residual_meas[2 * i + 1]);
+    h->order[slot] = i;
     const int mask = frames[fr].free_mask | (pt_free[res_pt[i]] ? (1 << MVBA_BLK_XYZ) : 0);
-    h->row_written[p] = (uint8_t)mask;
-    h->pos_K[p] = (int16_t)frames[fr].K;
-    // Algorithmic bytes (DESIGN.md "Roofline"): meas 16 + point index 4 + point 24 + r 16.
+    h->row_written[slot] = (uint8_t)mask;
+    h->pos_K[slot] = (int16_t)frames[fr].K;
+    // Algorithmic bytes: meas 16 + point index 4 + point 24 + r 16.
     bytes_res += 16.0 + 4.0 + 24.0 + 16.0;
     int cols = 0;
     for (int b = 0; b < 8; b++)
       if (mask & (1 << b)) cols += (b == 7) ? frames[fr].K : kFixedSize[b];
     bytes_jac += 16.0 * cols;
+    slot++;
   }
   if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
   h->bytes_res = bytes_res;
@@ -434,10 +460,11 @@ int32_t mvba_jacobian_stride(const mvba_handle* h) { return h ? h->jac_rows : 0;
 
 mvba_status mvba_residual_order(const mvba_handle* h, int64_t* out) {
   if (!h || !out) return MVBA_E_INVALID;
-  std::memcpy(out, h->order.data(), h->order.size() * sizeof(int64_t));
+  std::memcpy(out, h->order.data(), h->order.size() * sizeof(int64_t));  // nslots entries
   return MVBA_OK;
 }
 int64_t mvba_num_residuals(const mvba_handle* h) { return h ? h->nres : 0; }
+int64_t mvba_num_slots(const mvba_handle* h) { return h ? h->nslots : 0; }
 int64_t mvba_num_frames(const mvba_handle* h) { return h ? h->nframes : 0; }
 int64_t mvba_num_points(const mvba_handle* h) { return h ? h->npts : 0; }
 
@@ -448,7 +475,7 @@ double mvba_eval_bytes(const mvba_handle* h, int32_t flags) {
 
 static mvba_status ensure_outputs(mvba_handle* h) {
   if (h->d_res) return MVBA_OK;
-  h->ld = ((h->nres + 63) / 64) * 64;
+  h->ld = ((h->nslots + 63) / 64) * 64;
   if (h->ld == 0) h->ld = 64;
   hipError_t e = dalloc(&h->d_res, (size_t)(2 * h->ld));
   if (e == hipSuccess) e = dalloc(&h->d_J, (size_t)h->jac_rows * (size_t)h->ld);
@@ -468,8 +495,8 @@ mvba_status mvba_evaluate_device(mvba_handle* h, int32_t flags, double cauchy_th
     d_res = h->d_res;
     d_J = (flags & MVBA_EVAL_JACOBIAN) ? h->d_J : nullptr;
     ld = h->ld;
-  } else if (ld < h->nres) {
-    return h->fail(MVBA_E_INVALID, "leading dimension smaller than the number of residuals");
+  } else if (ld < h->nslots || (ld % 16) != 0) {
+    return h->fail(MVBA_E_INVALID, "leading dimension must be >= mvba_num_slots() and a multiple of 16");
   }
   if ((flags & MVBA_EVAL_JACOBIAN) && !d_J)
     return h->fail(MVBA_E_INVALID, "Jacobian requested without a Jacobian buffer");
@@ -481,9 +508,11 @@ mvba_status mvba_evaluate_device(mvba_handle* h, int32_t flags, double cauchy_th
   }
   hipError_t e = hipSuccess;
   if (!(flags & MVBA_EVAL_SKIP_PREP)) {
-    e = hipMemsetAsync(h->d_err, 0, sizeof(int), s);
-    if (e == hipSuccess) e = mvba_launch_points(h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts, s);
-    if (e == hipSuccess) e = mvba_launch_frames(h->d_fd, h->nframes, h->d_params, h->d_frec, h->d_err, s);
+    // The error word is never reset: K0 raises it to this evaluation's
+    // generation (atomicMax), so a stale error from an earlier call is ignored.
+    h->gen++;
+    e = mvba_launch_prep(h->d_fd, h->nframes, h->d_params, h->d_frec, h->d_pt_off, h->d_pt_free,
+                         h->npts, h->d_pts, h->gen, h->d_err, s);
     h->prep_done = true;
   } else if (!h->prep_done) {
     return h->fail(MVBA_E_INVALID, "MVBA_EVAL_SKIP_PREP before any full evaluation");
@@ -510,7 +539,7 @@ mvba_status mvba_sync_status(mvba_handle* h, void* stream) {
   int err = 0;
   e = hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_sync_status copy");
-  if (err & 1) return h->fail(MVBA_E_ALPHA_RANGE, "Out of bounds in interpolation.");
+  if (err >= h->gen && h->gen > 0) return h->fail(MVBA_E_ALPHA_RANGE, "Out of bounds in interpolation.");
   return MVBA_OK;
 }
 
@@ -519,6 +548,7 @@ mvba_status mvba_device_buffers(mvba_handle* h, mvba_device_view* v) {
   mvba_status st = ensure_outputs(h);
   if (st != MVBA_OK) return st;
   v->num_residuals = h->nres;
+  v->num_slots = h->nslots;
   v->ld = h->ld;
   v->jac_rows = h->jac_rows;
   v->max_dist_size = h->kmax;
@@ -542,7 +572,7 @@ mvba_status mvba_evaluate(mvba_handle* h, int32_t flags, double cauchy_threshold
   if (st != MVBA_OK) return st;
   st = mvba_sync_status(h, nullptr);
   if (st != MVBA_OK) return st;
-  const int64_t N = h->nres, ld = h->ld;
+  const int64_t N = h->nres, S = h->nslots, ld = h->ld;
   h->h_res.resize((size_t)(2 * ld));
   hipError_t e = hipMemcpy(h->h_res.data(), h->d_res, (size_t)(2 * ld) * sizeof(double), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate residual copy");
@@ -554,26 +584,24 @@ mvba_status mvba_evaluate(mvba_handle* h, int32_t flags, double cauchy_threshold
   const double b = cauchy_threshold * cauchy_threshold;
   const double c = loss ? 1.0 / b : 0.0;
   const int stride = h->jac_rows;
-  std::vector<double> scale(loss ? N : 0);
-  double total = 0.0;
-  // Cost is summed in AddResidualBlock order (Problem::Evaluate, num_threads = 1).
-  std::vector<double> cost_dev((size_t)N);
+  std::vector<double> cost_ins(cost ? (size_t)N : 0);
 #pragma omp parallel for schedule(static)
-  for (int64_t p = 0; p < N; p++) {
+  for (int64_t p = 0; p < S; p++) {
+    const int64_t i = h->order[p];
+    if (i < 0) continue;  // padding slot
     const double r0 = h->h_res[p], r1 = h->h_res[ld + p];
     const double s2 = r0 * r0 + r1 * r1;
     double sr = 1.0, ci;
     if (!loss) {
       ci = 0.5 * s2;
     } else {
+      // Ceres 1.14 CauchyLoss + Corrector [ext]
       const double sum = 1.0 + s2 * c;
       const double inv = 1.0 / sum;
       ci = 0.5 * (b * std::log(sum));
       sr = std::sqrt(std::max(std::numeric_limits<double>::min(), inv));
-      scale[p] = sr;
     }
-    cost_dev[p] = ci;
-    const int64_t i = h->order[p];
+    if (cost) cost_ins[i] = ci;
     if (residuals) {
       residuals[2 * i] = r0 * sr;
       residuals[2 * i + 1] = r1 * sr;
@@ -596,9 +624,9 @@ mvba_status mvba_evaluate(mvba_handle* h, int32_t flags, double cauchy_threshold
     }
   }
   if (cost) {
-    std::vector<double> by_ins((size_t)N);
-    for (int64_t p = 0; p < N; p++) by_ins[h->order[p]] = cost_dev[p];
-    for (int64_t i = 0; i < N; i++) total += by_ins[i];
+    // Summed in AddResidualBlock order (Problem::Evaluate with num_threads = 1).
+    double total = 0.0;
+    for (int64_t i = 0; i < N; i++) total += cost_ins[i];
     *cost = total;
   }
   return MVBA_OK;

@@ -1,13 +1,13 @@
 // mvba_kernels.hip — gfx950 kernels of the rig_calibrator evaluator.
 //
-//   k_points  : gather triangulated points from the packed parameter vector into
-//               32-byte records (x, y, z, free) — one coalesced 2x16 B load per
-//               observation later.
-//   k_frames  (K0): per image frame, world_to_cam (R_wc, t_wc) and the analytic
-//               derivative generators of the 22 pose columns. Restates
-//               calc_world_to_cam_trans / calc_interp_world_to_ref /
+//   k_prep    one launch of
+//     K0 (frames): per image frame, world_to_cam (R_wc, t_wc) and the analytic
+//               derivative generators of the 22 pose columns, 16 lanes per frame.
+//               Restates calc_world_to_cam_trans / calc_interp_world_to_ref /
 //               array_to_rigid_transform / linearInterp (rig_calibrator.cc:322-390,
-//               dense_map_utils.cc:171-178, :315-329; Eigen 3.4 slerp [ext]).
+//               dense_map_utils.cc:171-178, :315-329; Eigen 3.4 slerp [ext]);
+//     point gather: xyz blocks of the packed parameter vector into 32-byte
+//               records (x, y, z, free) — two 16 B loads per observation later.
 //   k_obs<M>  (K1): per observation residual + analytic Jacobian, one lane per
 //               observation, one wavefront per frame segment. Restates
 //               BracketedCamError::operator() (rig_calibrator.cc:447-482) and
@@ -41,6 +41,7 @@ __device__ __forceinline__ void quat_to_rot(double x, double y, double z, double
 }
 
 // Eigen Quaternion(Matrix3d) [ext]: Shepperd's method. q = (x, y, z, w).
+// Written with constant indices only (no scratch memory).
 __device__ __forceinline__ void rot_to_quat(const double* m, double* q) {
   double t = m[0] + m[4] + m[8];
   if (t > 0.0) {
@@ -50,17 +51,32 @@ __device__ __forceinline__ void rot_to_quat(const double* m, double* q) {
     q[0] = (m[7] - m[5]) * t;
     q[1] = (m[2] - m[6]) * t;
     q[2] = (m[3] - m[1]) * t;
-  } else {
-    int i = 0;
-    if (m[4] > m[0]) i = 1;
-    if (m[8] > m[3 * i + i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    t = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
-    q[i] = 0.5 * t;
+    return;
+  }
+  int i = 0;
+  if (m[4] > m[0]) i = 1;
+  if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
+  if (i == 0) {  // j = 1, k = 2
+    t = sqrt(m[0] - m[4] - m[8] + 1.0);
+    q[0] = 0.5 * t;
     t = 0.5 / t;
-    q[3] = (m[3 * k + j] - m[3 * j + k]) * t;
-    q[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-    q[k] = (m[3 * k + i] + m[3 * i + k]) * t;
+    q[3] = (m[7] - m[5]) * t;
+    q[1] = (m[3] + m[1]) * t;
+    q[2] = (m[6] + m[2]) * t;
+  } else if (i == 1) {  // j = 2, k = 0
+    t = sqrt(m[4] - m[8] - m[0] + 1.0);
+    q[1] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[2] - m[6]) * t;
+    q[2] = (m[7] + m[5]) * t;
+    q[0] = (m[1] + m[3]) * t;
+  } else {  // i = 2, j = 0, k = 1
+    t = sqrt(m[8] - m[0] - m[4] + 1.0);
+    q[2] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[3] - m[1]) * t;
+    q[0] = (m[2] + m[6]) * t;
+    q[1] = (m[5] + m[7]) * t;
   }
 }
 
@@ -124,45 +140,34 @@ __device__ __forceinline__ void put_col(double* rec, int k, const double* om, co
   o[3] = dt[0] - c[0]; o[4] = dt[1] - c[1]; o[5] = dt[2] - c[2];
 }
 
-// ------------------------------------------------------------ k_points
-__global__ void __launch_bounds__(256) k_points(const double* __restrict__ params,
-                                                const int64_t* __restrict__ pt_off,
-                                                const uint8_t* __restrict__ pt_free, int64_t npts,
-                                                double4* __restrict__ pts) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npts) return;
-  const int64_t o = pt_off[p];
-  pts[p] = make_double4(params[o], params[o + 1], params[o + 2], pt_free[p] ? 1.0 : 0.0);
-}
+// ------------------------------------------------------------ prep (K0 + point gather)
+// One launch: blocks [0, frame_blocks) run K0 with kThreadsPerFrame lanes per
+// frame (each lane recomputes the frame's common part and emits a subset of the
+// 22 pose columns); the remaining blocks gather the points.
+constexpr int kThreadsPerFrame = 16;
+constexpr int kPrepBlock = 256;
 
-// ------------------------------------------------------------ K0: frames
-__global__ void __launch_bounds__(64) k_frames(const FrameDesc* __restrict__ fd, int64_t nframes,
-                                               const double* __restrict__ params,
-                                               double* __restrict__ frec, int* __restrict__ err) {
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nframes) return;
-  const FrameDesc F = fd[f];
-  double* rec = frec + f * kFrameRecDoubles;
-  for (int k = 12; k < kFrameRecDoubles; k++) rec[k] = 0.0;
+__device__ void frame_columns(const FrameDesc& F, const double* __restrict__ params, double* rec,
+                              int sub, int gen, int* err) {
   const double* p0 = params + F.off[MVBA_BLK_BEG];
   double R0[9], qh0[4], in0;
   rigid(p0, R0, qh0, &in0);
   const double t0[3] = {p0[0], p0[1], p0[2]};
-  const double zero3[3] = {0.0, 0.0, 0.0};
 
   if (F.sb == F.se) {
     // rig_calibrator.cc:371-374 — reference camera or --no_rig: T = rigid(p0).
-    for (int k = 0; k < 9; k++) rec[k] = R0[k];
-    rec[9] = t0[0]; rec[10] = t0[1]; rec[11] = t0[2];
-    for (int j = 0; j < 3; j++) {
-      double e[3] = {0.0, 0.0, 0.0};
-      e[j] = 1.0;
-      put_col(rec, j, zero3, e, t0);
+    if (sub == 0) {
+      for (int k = 0; k < 9; k++) rec[k] = R0[k];
+      rec[9] = t0[0]; rec[10] = t0[1]; rec[11] = t0[2];
     }
-    for (int k = 0; k < 4; k++) {
-      double om[3];
-      quat_generator(qh0, 2.0 * in0, k, om);
-      put_col(rec, 3 + k, om, zero3, t0);
+    for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
+      double om[3] = {0.0, 0.0, 0.0}, dt[3] = {0.0, 0.0, 0.0};
+      if (k < 3) {
+        dt[k] = 1.0;
+      } else if (k < 7) {
+        quat_generator(qh0, 2.0 * in0, k - 3, om);
+      }
+      put_col(rec, k, om, dt, t0);
     }
     return;
   }
@@ -178,7 +183,7 @@ __global__ void __launch_bounds__(64) k_frames(const FrameDesc* __restrict__ fd,
 
   // rig_calibrator.cc:343-346 (big stamps subtracted first).
   const double alpha = ((F.sc - F.sb) - off) / (F.se - F.sb);
-  if (alpha < 0.0 || alpha > 1.0) atomicOr(err, 1);
+  if (sub == 0 && (alpha < 0.0 || alpha > 1.0)) atomicMax(err, gen);
 
   // linearInterp with Eigen slerp [ext] (dense_map_utils.cc:315-329).
   double q0[4], q1[4];
@@ -227,60 +232,75 @@ __global__ void __launch_bounds__(64) k_frames(const FrameDesc* __restrict__ fd,
       Rw[3 * r + c] = R2[3 * r + 0] * Ri[c] + R2[3 * r + 1] * Ri[3 + c] + R2[3 * r + 2] * Ri[6 + c];
     tw[r] = R2[3 * r + 0] * ti[0] + R2[3 * r + 1] * ti[1] + R2[3 * r + 2] * ti[2] + t2[r];
   }
-  for (int k = 0; k < 9; k++) rec[k] = Rw[k];
-  rec[9] = tw[0]; rec[10] = tw[1]; rec[11] = tw[2];
-
-  // Translation columns of beg / end / ref_to_cam.
-  for (int j = 0; j < 3; j++) {
-    const double cj[3] = {R2[j], R2[3 + j], R2[6 + j]};
-    const double a0[3] = {(1.0 - alpha) * cj[0], (1.0 - alpha) * cj[1], (1.0 - alpha) * cj[2]};
-    const double a1[3] = {alpha * cj[0], alpha * cj[1], alpha * cj[2]};
-    double e[3] = {0.0, 0.0, 0.0};
-    e[j] = 1.0;
-    put_col(rec, j, zero3, a0, tw);
-    put_col(rec, 7 + j, zero3, a1, tw);
-    put_col(rec, 14 + j, zero3, e, tw);
+  if (sub == 0) {
+    for (int k = 0; k < 9; k++) rec[k] = Rw[k];
+    rec[9] = tw[0]; rec[10] = tw[1]; rec[11] = tw[2];
   }
-  // Quaternion columns of beg (k=3..6) and end (k=10..13) through slerp.
-  for (int side = 0; side < 2; side++) {
-    const double* qh = side ? qh1 : qh0;
-    const double sc = (side ? sig1 * in1 : sig0 * in0);
-    const double* qo = side ? q0 : q1;  // the other endpoint
-    for (int k = 0; k < 4; k++) {
+
+  for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
+    double om[3] = {0.0, 0.0, 0.0}, dt[3] = {0.0, 0.0, 0.0};
+    if (k < 3 || (k >= 7 && k < 10) || (k >= 14 && k < 17)) {
+      // translation columns of beg / end / ref_to_cam
+      const int j = (k < 3) ? k : (k < 10) ? k - 7 : k - 14;
+      const double scale = (k < 3) ? (1.0 - alpha) : (k < 10) ? alpha : 0.0;
+      if (k >= 14) {
+        dt[j] = 1.0;
+      } else {
+        dt[0] = scale * R2[j]; dt[1] = scale * R2[3 + j]; dt[2] = scale * R2[6 + j];
+      }
+    } else if (k < 14) {
+      // quaternion columns of beg (3..6) and end (10..13) through slerp
+      const bool side = (k >= 10);
+      const int kk = side ? k - 10 : k - 3;
+      const double* qh = side ? qh1 : qh0;
+      const double sc = side ? sig1 * in1 : sig0 * in0;
+      const double* qo = side ? q0 : q1;
       double dq[4];
-      for (int m = 0; m < 4; m++) dq[m] = sc * ((m == k ? 1.0 : 0.0) - qh[m] * qh[k]);
+      for (int m = 0; m < 4; m++) dq[m] = sc * ((m == kk ? 1.0 : 0.0) - qh[m] * qh[kk]);
       const double dD = sgn * (qo[0] * dq[0] + qo[1] * dq[1] + qo[2] * dq[2] + qo[3] * dq[3]);
       const double dth = dth_dD * dD;
       const double ws = side ? w1 : w0;
       double dqi[4];
       for (int m = 0; m < 4; m++) dqi[m] = ws * dq[m] + dw0_dth * dth * q0[m] + dw1_dth * dth * q1[m];
-      double omi[3], om[3];
+      double omi[3];
       tangent_generator(dqi, qi, omi);
       matvec(R2, omi, om);
-      put_col(rec, (side ? 10 : 3) + k, om, zero3, tw);
+    } else if (k < 21) {
+      // ref_to_cam quaternion: dR_wc = [w]x R_wc, dt_wc = w x (t_wc - t2)
+      quat_generator(qh2, 2.0 * in2, k - 17, om);
+      const double tt[3] = {tw[0] - t2[0], tw[1] - t2[1], tw[2] - t2[2]};
+      cross(om, tt, dt);
+    } else {
+      // timestamp offset: d alpha / d offset = -1 / (se - sb)
+      const double da = -1.0 / (F.se - F.sb);
+      double dqi[4];
+      for (int m = 0; m < 4; m++) dqi[m] = (dw0_da * q0[m] + dw1_da * q1[m]) * da;
+      double omi[3];
+      tangent_generator(dqi, qi, omi);
+      matvec(R2, omi, om);
+      const double dti[3] = {(t1[0] - t0[0]) * da, (t1[1] - t0[1]) * da, (t1[2] - t0[2]) * da};
+      matvec(R2, dti, dt);
     }
+    put_col(rec, k, om, dt, tw);
   }
-  // ref_to_cam quaternion columns: dR_wc = [w]x R_wc, dt_wc = w x (t_wc - t2).
-  for (int k = 0; k < 4; k++) {
-    double om[3], dt[3], d2[3];
-    quat_generator(qh2, 2.0 * in2, k, om);
-    const double tt[3] = {tw[0] - t2[0], tw[1] - t2[1], tw[2] - t2[2]};
-    cross(om, tt, d2);
-    dt[0] = d2[0]; dt[1] = d2[1]; dt[2] = d2[2];
-    put_col(rec, 17 + k, om, dt, tw);
-  }
-  // Timestamp offset column: d alpha / d offset = -1 / (se - sb).
-  {
-    const double da = -1.0 / (F.se - F.sb);
-    double dqi[4];
-    for (int m = 0; m < 4; m++) dqi[m] = (dw0_da * q0[m] + dw1_da * q1[m]) * da;
-    double omi[3], om[3];
-    tangent_generator(dqi, qi, omi);
-    matvec(R2, omi, om);
-    const double dti[3] = {(t1[0] - t0[0]) * da, (t1[1] - t0[1]) * da, (t1[2] - t0[2]) * da};
-    double dt[3];
-    matvec(R2, dti, dt);
-    put_col(rec, 21, om, dt, tw);
+}
+
+__global__ void __launch_bounds__(kPrepBlock) k_prep(const FrameDesc* __restrict__ fd, int64_t nframes,
+                                                     int32_t frame_blocks, const double* __restrict__ params,
+                                                     double* __restrict__ frec, const int64_t* __restrict__ pt_off,
+                                                     const uint8_t* __restrict__ pt_free, int64_t npts,
+                                                     double4* __restrict__ pts, int gen, int* __restrict__ err) {
+  if ((int)blockIdx.x < frame_blocks) {
+    const int64_t t = (int64_t)blockIdx.x * kPrepBlock + threadIdx.x;
+    const int64_t f = t / kThreadsPerFrame;
+    if (f >= nframes) return;
+    const FrameDesc F = fd[f];
+    frame_columns(F, params, frec + f * kFrameRecDoubles, (int)(t % kThreadsPerFrame), gen, err);
+  } else {
+    const int64_t p = (int64_t)(blockIdx.x - frame_blocks) * kPrepBlock + threadIdx.x;
+    if (p >= npts) return;
+    const int64_t o = pt_off[p];
+    pts[p] = make_double4(params[o], params[o + 1], params[o + 2], pt_free[p] ? 1.0 : 0.0);
   }
 }
 
@@ -555,21 +575,14 @@ __global__ void __launch_bounds__(256) k_obs(
 // ------------------------------------------------------------ launchers
 extern "C" {
 
-hipError_t mvba_launch_points(const double* params, const int64_t* pt_off, const uint8_t* pt_free,
-                              int64_t npts, double4* pts, hipStream_t s) {
-  if (npts <= 0) return hipSuccess;
-  const int64_t blocks = (npts + 255) / 256;
-  hipLaunchKernelGGL(mvba::k_points, dim3((unsigned)blocks), dim3(256), 0, s, params, pt_off,
-                     pt_free, npts, pts);
-  return hipGetLastError();
-}
-
-hipError_t mvba_launch_frames(const mvba::FrameDesc* fd, int64_t nframes, const double* params,
-                              double* frec, int* err, hipStream_t s) {
-  if (nframes <= 0) return hipSuccess;
-  const int64_t blocks = (nframes + 63) / 64;
-  hipLaunchKernelGGL(mvba::k_frames, dim3((unsigned)blocks), dim3(64), 0, s, fd, nframes, params,
-                     frec, err);
+hipError_t mvba_launch_prep(const mvba::FrameDesc* fd, int64_t nframes, const double* params,
+                            double* frec, const int64_t* pt_off, const uint8_t* pt_free, int64_t npts,
+                            double4* pts, int gen, int* err, hipStream_t s) {
+  const int64_t fb = (nframes * mvba::kThreadsPerFrame + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
+  const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
+  if (fb + pb == 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_prep, dim3((unsigned)(fb + pb)), dim3(mvba::kPrepBlock), 0, s, fd, nframes,
+                     (int32_t)fb, params, frec, pt_off, pt_free, npts, pts, gen, err);
   return hipGetLastError();
 }
 

@@ -28,6 +28,8 @@ class Evaluator:
         self.h = h
         self.stride = int(self.lib.mvba_jacobian_stride(self.h))
         self.num_residuals = int(self.lib.mvba_num_residuals(self.h))
+        self.num_slots = int(self.lib.mvba_num_slots(self.h))
+        self.ld = ((self.num_slots + 63) // 64) * 64
         self.num_frames = int(self.lib.mvba_num_frames(self.h))
         self.num_points = int(self.lib.mvba_num_points(self.h))
 
@@ -84,8 +86,8 @@ class Evaluator:
         return v
 
     def order(self) -> np.ndarray:
-        """device position -> AddResidualBlock index."""
-        out = np.empty(self.num_residuals, dtype=np.int64)
+        """device slot -> AddResidualBlock index (-1 = padding slot)."""
+        out = np.empty(self.num_slots, dtype=np.int64)
         _lib.check(self.lib.mvba_residual_order(self.h, out.ctypes.data), self.h)
         return out
 

@@ -54,16 +54,23 @@ def golden_jacobian_row(case, stride):
     return J
 
 
-def fd_bound(problem, J_ref, pix_scale):
-    """Rounding bound of the reference's central differences per column
-    (Ceres 1.14 numeric_diff.h [ext]): |err| <~ eps*|pixel|/delta_j, with
-    delta_j = max(sqrt(eps), 1e-6*|x_j|); plus truncation (1e-6 relative)."""
+def fd_bound(problem, J_ref, r_ref):
+    """Error bound of the reference's central differences per Jacobian entry
+    (Ceres 1.14 numeric_diff.h [ext]) with delta_j = max(sqrt(eps), 1e-6*|x_j|):
+      * rounding: 64 eps |pixel| / delta_j;
+      * RPC denominator coefficient b (monomial m): the residual is EXACTLY
+        N / (D0 + b m) in b, whose central difference equals the derivative
+        times 1 / (1 - x^2), x = delta m / D = delta |J| / |q|, q = N/D. So the
+        FD error is |J| x^2 / (1 - x^2); for x >= 0.5 the FD column is not a
+        derivative and the entry is not compared (bound = inf);
+      * 1e-6 of the column maximum for everything else (truncation)."""
     from multiview_amd._lib import JAC_BASE
 
     eps = np.finfo(float).eps
     n, stride = J_ref.shape
     bound = np.zeros((n, stride))
     half = problem.camera_half_size
+    pix = np.maximum(np.abs(problem.residual_meas + r_ref).max(axis=1), 1.0)
     for i in range(n):
         blks = problem.residual_blocks[i]
         cam = problem.residual_camera[i]
@@ -73,30 +80,24 @@ def fd_bound(problem, J_ref, pix_scale):
             size = (7, 7, 7, 3, 1, 1, 2)[b] if b < 7 else K
             for j in range(size):
                 delta = max(np.sqrt(eps), 1e-6 * abs(vals[j]))
-                tb = 64 * eps * max(pix_scale[i], 1.0) / delta
+                tb = 64 * eps * pix[i] / delta
                 for row in range(2):
                     bound[i, JAC_BASE[b] + row * size + j] = tb
         if K >= 20:
-            # RPC denominator coefficient b with monomial m: f = N/D(b), so
-            # f''' = -6 q (m/D)^3 with q = N/D and m/D = -J/q: truncation of the
-            # central difference delta^2 |f'''| / 6 = delta^2 |J|^3 / q^2 (x2 for
-            # the higher-order terms; it exceeds |J| where FD is meaningless).
             nh = K // 2
             deg = int(round(np.sqrt(2.0 * nh + 5.0) / 2.0 - 1.5))
             nl = (deg + 1) * (deg + 2) // 2
             vals = problem.block_values(blks[7])
-            meas = problem.residual_meas[i]
             for row, lo in ((0, nl), (1, 3 * nl - 1)):
-                r = J_ref[i]  # exact Jacobian row block
+                q = abs(r_ref[i, row] + problem.residual_meas[i, row] - half[cam][row])
                 for j in range(lo, lo + nl - 1):
                     col = JAC_BASE[7] + row * K + j
                     delta = max(np.sqrt(eps), 1e-6 * abs(vals[j]))
-                    q = max(abs(meas[row] - half[cam][row]), 1.0)
-                    x = delta * abs(r[col]) / q  # relative change of D over one step
-                    if x > 0.02:
-                        bound[i, col] = np.inf  # FD series diverges: the reference's FD column is not a derivative
+                    x = delta * abs(J_ref[i, col]) / max(q, 1e-300)
+                    if x >= 0.5:
+                        bound[i, col] = np.inf
                     else:
-                        bound[i, col] += 3.0 * delta ** 2 * abs(r[col]) ** 3 / q ** 2
+                        bound[i, col] += 1.01 * abs(J_ref[i, col]) * x * x / (1.0 - x * x)
     return bound + 1e-6 * np.abs(J_ref).max(axis=0, keepdims=True)
 
 

@@ -33,9 +33,20 @@ def test_numdiff_matches_analytic_within_fd_bound(oracle):
     P = rig.build_problem(R)
     _, r, Jn = oracle.evaluate(P, oracle.NUMDIFF)
     _, _, Ja = oracle.evaluate(P, oracle.ANALYTIC)
-    pix = np.abs(P.residual_meas).max(axis=1)
-    bound = fd_bound(P, Ja, pix)
-    assert (np.abs(Jn - Ja) <= bound).all()
+    assert (np.abs(Jn - Ja) <= fd_bound(P, Ja, r)).all()
+
+
+@pytest.mark.parametrize("model", ["rpc2", "rpc3", "fov"])
+def test_numdiff_rpc_fd_error_is_exactly_rational(oracle, model):
+    # The reference's FD error on RPC denominator columns is the rational factor
+    # 1/(1-x^2); everything else within rounding/truncation.
+    for seed in (1, 2):
+        R = rig.make_rig(num_sensors=3, num_ref=12, num_points=120, obs_per_point=5,
+                         models=[model] * 3, seed=seed)
+        P = rig.build_problem(R)
+        _, r, Jn = oracle.evaluate(P, oracle.NUMDIFF)
+        _, _, Ja = oracle.evaluate(P, oracle.ANALYTIC)
+        assert (np.abs(Jn - Ja) <= fd_bound(P, Ja, r)).all()
 
 
 def _identity_problem(K, coeffs, X=(0.0, 0.0, 3.0), center=(515.0, 382.0), f=600.0):

@@ -5,6 +5,8 @@ Tolerances (DESIGN.md "Parity"):
   Jacobian         |J_gpu - J_exact| <= 1e-9 * max(column max, 1e-12)   (exact = oracle dual numbers)
   vs reference FD  |J_gpu - J_numdiff| <= central-difference rounding bound (fd_bound)
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -39,14 +41,14 @@ def _check(P, ev, oracle, apply_loss=False, numdiff=True):
     assert np.all((J_o == 0) | (J_g != 0) | (np.abs(J_o) < 1e-12 * colmax))
     if numdiff and not apply_loss:
         _, _, J_n = oracle.evaluate(P, oracle.NUMDIFF)
-        assert np.all(np.abs(J_g - J_n) <= fd_bound(P, J_o, pix))
+        assert np.all(np.abs(J_g - J_n) <= fd_bound(P, J_o, r_o))
 
 
 @pytest.mark.parametrize("name", list(MODEL_SETS))
 def test_parity_small_rig(oracle, name):
     models = MODEL_SETS[name]
     R = rig.make_rig(num_sensors=len(models), num_ref=24, num_points=300, obs_per_point=5,
-                     models=models, seed=hash(name) % 1000)
+                     models=models, seed=zlib.crc32(name.encode()) % 1000)
     P = rig.build_problem(R)
     with Evaluator(P) as ev:
         ev.set_params()
@@ -91,18 +93,21 @@ def test_device_loss_flag_matches_host_corrector(oracle):
     P = rig.build_problem(R)
     with Evaluator(P) as ev:
         ev.set_params()
-        ld = ((ev.num_residuals + 63) // 64) * 64
+        ld = ev.ld
         res = torch.zeros((2, ld), dtype=torch.float64, device="cuda")
         jac = torch.zeros((ev.stride, ld), dtype=torch.float64, device="cuda")
         ev.evaluate_device(jacobian=True, apply_loss=True, robust_threshold=3.0, residuals=res, jac=jac, ld=ld)
         ev.sync()
         order = ev.order()
+        valid = order >= 0
+        assert valid.sum() == ev.num_residuals
+        assert np.array_equal(np.sort(order[valid]), np.arange(ev.num_residuals))
         _, r_o, J_o = oracle.evaluate(P, oracle.ANALYTIC, apply_loss=True)
-        r_d = res.cpu().numpy()[:, :ev.num_residuals].T
-        J_d = jac.cpu().numpy()[:, :ev.num_residuals].T
-        assert np.abs(r_d - r_o[order]).max() <= 1e-9 * 1024
+        r_d = res.cpu().numpy()[:, :ev.num_slots].T[valid]
+        J_d = jac.cpu().numpy()[:, :ev.num_slots].T[valid]
+        assert np.abs(r_d - r_o[order[valid]]).max() <= 1e-9 * 1024
         colmax = np.maximum(np.abs(J_o).max(axis=0), 1e-12)
-        assert (np.abs(J_d - J_o[order]) / colmax).max() <= 1e-9
+        assert (np.abs(J_d - J_o[order[valid]]) / colmax).max() <= 1e-9
 
 
 CASES = golden_cases()
@@ -153,8 +158,7 @@ def test_full_size_c2_properties(oracle):
     P = rig.build_problem(R)
     with Evaluator(P) as ev:
         ev.set_params()
-        n = ev.num_residuals
-        ld = ((n + 63) // 64) * 64
+        n, S, ld = ev.num_residuals, ev.num_slots, ev.ld
         r1 = torch.empty((2, ld), dtype=torch.float64, device="cuda")
         j1 = torch.empty((ev.stride, ld), dtype=torch.float64, device="cuda")
         r2 = torch.empty_like(r1)
@@ -164,19 +168,21 @@ def test_full_size_c2_properties(oracle):
         ev.evaluate_device(True, residuals=r2, jac=j2, ld=ld)
         ev.evaluate_device(False, residuals=r3, jac=None, ld=ld)
         ev.sync()
-        assert torch.equal(r1[:, :n], r2[:, :n])
-        assert torch.equal(r1[:, :n], r3[:, :n])
         order = ev.order()
-        assert np.array_equal(np.sort(order), np.arange(n))
+        valid = torch.from_numpy(order >= 0).cuda()
+        assert torch.equal(r1[:, :S][:, valid], r2[:, :S][:, valid])
+        assert torch.equal(r1[:, :S][:, valid], r3[:, :S][:, valid])
+        assert np.array_equal(np.sort(order[order >= 0]), np.arange(n))
+        assert S <= n + 16 * ev.num_frames + 16
         rng = np.random.default_rng(5)
-        pos = np.sort(rng.choice(n, 4000, replace=False))
+        slots = np.nonzero(order >= 0)[0]
+        pos = np.sort(rng.choice(slots, 4000, replace=False))
         idx = order[pos]
         sub = P.subset(idx)
         _, r_o, J_o = oracle.evaluate(sub, oracle.ANALYTIC)
-        J1 = j1[:, :n].cpu().numpy()
-        r_g = r1[:, :n].cpu().numpy()[:, pos].T
+        J1 = j1[:, :S].cpu().numpy()
+        r_g = r1[:, :S].cpu().numpy()[:, pos].T
         J_g = J1[:, pos].T
-        # only rows written for these residuals are meaningful
         pix = np.maximum(np.abs(sub.residual_meas + r_o).max(axis=1), 1.0)
         assert np.all(np.abs(r_g - r_o) <= 1e-9 * pix[:, None])
         colmax = np.maximum(np.abs(J_o).max(axis=0), 1e-12)
