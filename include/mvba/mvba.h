@@ -199,6 +199,36 @@ mvba_status mvba_residual_order(const struct mvba_handle* h, int64_t* out);
 /* Wait for the stream and convert any device-side error word into a status. */
 mvba_status mvba_sync_status(struct mvba_handle* h, void* hip_stream);
 
+/* ---- Normal equations (K2): gradient and block-diagonal Hessian ----------
+ * For the solver (Ceres' Jacobi preconditioner of ITERATIVE_SCHUR, and the
+ * RCCL all-reduce of per-pose blocks when observations are sharded by landmark).
+ * With J the Jacobian of the (optionally Cauchy-corrected) residuals r:
+ *   gradient g = J^T r, Hessian blocks H_bb = J_b^T J_b per parameter block b,
+ * in two compact layouts:
+ *   camera side: every non-constant, non-point block in block-id order;
+ *     g at goff[b] (size_b doubles), H_bb row-major at hoff[b] (size_b^2);
+ *   point side : point index p (mvba_point_block_map), g at 3p, H packed
+ *     (xx xy xz yy yz zz) at 6p.
+ * cost (nullable) = sum over residual blocks of 0.5*|r|^2 (or 0.5*rho). */
+typedef struct mvba_lin_layout {
+  int64_t cam_grad_size;   /* doubles */
+  int64_t cam_hess_size;   /* doubles */
+  int64_t num_points;
+  int32_t num_cam_blocks;
+  int32_t supported;       /* 0 if a camera model is outside the Gram path (RPC degree > 3) */
+} mvba_lin_layout;
+
+mvba_status mvba_lin_layout_info(const struct mvba_handle* h, mvba_lin_layout* out);
+/* [num_cam_blocks] each, nullable */
+mvba_status mvba_cam_block_map(const struct mvba_handle* h, int32_t* block_ids, int64_t* goff,
+                               int64_t* hoff);
+/* [num_points]: parameter block id of point index p */
+mvba_status mvba_point_block_map(const struct mvba_handle* h, int32_t* block_ids);
+/* flags: MVBA_EVAL_APPLY_LOSS, MVBA_EVAL_SKIP_PREP. Asynchronous on hip_stream. */
+mvba_status mvba_linearize_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                  double* d_cam_grad, double* d_cam_hess, double* d_pt_grad,
+                                  double* d_pt_hess, double* d_cost, void* hip_stream);
+
 /* Counts for reporting. */
 int64_t mvba_num_residuals(const struct mvba_handle* h);
 /* Device slots = residuals + padding that line-aligns every frame's range; device

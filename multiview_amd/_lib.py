@@ -82,6 +82,16 @@ class DeviceView(C.Structure):
     ]
 
 
+class LinLayout(C.Structure):
+    _fields_ = [
+        ("cam_grad_size", C.c_int64),
+        ("cam_hess_size", C.c_int64),
+        ("num_points", C.c_int64),
+        ("num_cam_blocks", C.c_int32),
+        ("supported", C.c_int32),
+    ]
+
+
 # Every symbol include/mvba/mvba.h declares, with (restype, argtypes).
 SIGNATURES = {
     "mvba_abi_version": (C.c_int, []),
@@ -104,6 +114,11 @@ SIGNATURES = {
     "mvba_num_frames": (C.c_int64, [C.c_void_p]),
     "mvba_num_points": (C.c_int64, [C.c_void_p]),
     "mvba_eval_bytes": (C.c_double, [C.c_void_p, C.c_int32]),
+    "mvba_lin_layout_info": (C.c_int, [C.c_void_p, C.POINTER(LinLayout)]),
+    "mvba_cam_block_map": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_point_block_map": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mvba_linearize_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
 }
 
 _lib = None

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -32,6 +33,19 @@ extern "C" {
 hipError_t mvba_launch_prep(const FrameDesc* fd, int64_t nframes, const double* params,
                             double* frec, const int64_t* pt_off, const uint8_t* pt_free, int64_t npts,
                             double4* pts, int gen, int* err, hipStream_t s);
+int mvba_gram_width(int model, int deg);
+size_t mvba_frame_lin_size(void);
+hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchunks, const Segment* segs,
+                            const FrameDesc* fd, const double* frec, const double* params,
+                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                            double* slab, int32_t flags, double cauchy_c, hipStream_t s);
+hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16, const FrameDesc* fd,
+                              const double* frec, const double* slab, double* grad, double* hess,
+                              double* cost, hipStream_t s);
+hipError_t mvba_launch_points_lin(const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
+                                  const double2* po_meas, const FrameDesc* fd, const double* frec,
+                                  const double* params, const double4* pts, double* pgrad, double* phess,
+                                  int32_t flags, double cauchy_c, hipStream_t s);
 hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
                            const FrameDesc* fd, const double* frec, const double* params,
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
@@ -67,6 +81,10 @@ struct Group {
   int model = 0, deg = 0;
   int32_t seg_begin = 0, seg_count = 0;
   int64_t res_begin = 0, res_count = 0;
+  // linearization (K2): chunks of <= 4 segments of one frame, slab per chunk
+  int32_t chunk_begin = 0, chunk_count = 0;
+  int64_t slab_base = 0;
+  int32_t gram_width = 0, w16 = 0;
 };
 
 template <class T>
@@ -118,6 +136,21 @@ struct mvba_handle {
 
   std::vector<double> h_res, h_J;  // host staging for mvba_evaluate
 
+  // linearization (K2): camera-side compact layout, chunks, point CSR
+  bool lin_ok = false;
+  std::string lin_err;
+  int64_t cam_grad_size = 0, cam_hess_size = 0, slab_size = 0;
+  int32_t max_w16 = 0;
+  std::vector<int32_t> cam_block_ids;   // camera-side blocks in block-id order
+  std::vector<int64_t> cam_goff, cam_hoff;
+  std::vector<int32_t> pt_block_ids;    // point index -> block id
+  int4* d_chunks = nullptr;
+  void* d_frame_lin = nullptr;
+  double* d_slab = nullptr;
+  int64_t* d_pt_begin = nullptr;
+  int32_t* d_po_frame = nullptr;
+  double2* d_po_meas = nullptr;
+
   mvba_status fail(mvba_status st, const std::string& msg) {
     err = msg;
     return st;
@@ -132,7 +165,8 @@ static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
-                  h->d_row_written, h->d_err, h->d_res, h->d_J};
+                  h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
+                  h->d_slab, h->d_pt_begin, h->d_po_frame, h->d_po_meas};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -272,6 +306,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   std::unordered_map<Key, int32_t, KeyHash> frame_index;
   frame_index.reserve(1024);
   std::vector<FrameDesc> frames;
+  std::vector<std::array<int32_t, 8>> frame_blocks;
   std::vector<int32_t> res_frame(N);
   for (int64_t i = 0; i < N; i++) {
     const int32_t* blk = d->residual_blocks + 8 * i;
@@ -303,6 +338,9 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     F.free_mask = mask;
     const int32_t id = (int32_t)frames.size();
     frames.push_back(F);
+    std::array<int32_t, 8> fb;
+    for (int b = 0; b < 8; b++) fb[b] = blk[b];
+    frame_blocks.push_back(fb);
     frame_index.emplace(k, id);
     res_frame[i] = id;
   }
@@ -407,6 +445,90 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   h->bytes_res = bytes_res;
   h->bytes_jac = bytes_jac;
 
+  // ---- linearization structures (K2)
+  std::vector<int4> chunks;
+  std::vector<mvba::FrameLinHost> flin(frames.size());
+  std::vector<int64_t> pt_begin;
+  std::vector<int32_t> po_frame;
+  std::vector<double2> po_meas;
+  {
+    h->lin_ok = true;
+    for (const Group& G : h->groups)
+      if (G.model == mvba::kModelRpc && G.deg > mvba::kMaxLinRpcDegree) {
+        h->lin_ok = false;
+        h->lin_err = "linearization supports RPC degree <= 3";
+      }
+    // camera-side blocks: not constant, not a point block, in block-id order
+    std::vector<uint8_t> is_point(d->num_blocks, 0);
+    for (auto& kv : pt_index) is_point[kv.first] = 1;
+    h->pt_block_ids.resize(h->npts);
+    for (auto& kv : pt_index) h->pt_block_ids[kv.second] = kv.first;
+    std::vector<int64_t> goff_of(d->num_blocks, -1), hoff_of(d->num_blocks, -1);
+    for (int b = 0; b < d->num_blocks; b++) {
+      if (is_point[b] || d->block_constant[b]) continue;
+      const int64_t sz = d->block_size[b];
+      goff_of[b] = h->cam_grad_size;
+      hoff_of[b] = h->cam_hess_size;
+      h->cam_block_ids.push_back(b);
+      h->cam_goff.push_back(h->cam_grad_size);
+      h->cam_hoff.push_back(h->cam_hess_size);
+      h->cam_grad_size += sz;
+      h->cam_hess_size += sz * sz;
+    }
+    int64_t slab_base = 0;
+    for (Group& G : h->groups) {
+      G.chunk_begin = (int32_t)chunks.size();
+      G.gram_width = h->lin_ok ? mvba_gram_width(G.model, G.deg) : 0;
+      G.w16 = (G.gram_width + 15) / 16 * 16;
+      h->max_w16 = std::max(h->max_w16, G.w16);
+      const int64_t SL = (int64_t)G.w16 * G.w16 + 1;
+      G.slab_base = slab_base;
+      int32_t local = 0;
+      for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++) {
+        const Segment& sg = segs[sidx];
+        if (chunks.size() == (size_t)G.chunk_begin || chunks.back().z != sg.frame ||
+            chunks.back().y == mvba::kChunkSegs) {
+          int4 c;
+          c.x = sidx;
+          c.y = 0;
+          c.z = sg.frame;
+          c.w = local++;
+          chunks.push_back(c);
+          mvba::FrameLinHost& L = flin[sg.frame];
+          if (L.chunk_count == 0) L.slab_off = slab_base + (int64_t)c.w * SL;
+          L.chunk_count++;
+          L.width = G.gram_width;
+          L.w16 = G.w16;
+        }
+        chunks.back().y++;
+      }
+      G.chunk_count = (int32_t)chunks.size() - G.chunk_begin;
+      slab_base += (int64_t)G.chunk_count * SL;
+    }
+    h->slab_size = slab_base;
+    for (size_t f = 0; f < frames.size(); f++) {
+      for (int b = 0; b < 8; b++) {
+        const int32_t bid = frame_blocks[f][b];
+        const bool used = (b != MVBA_BLK_XYZ) && (b != MVBA_BLK_DIST || frames[f].K > 0);
+        flin[f].goff[b] = used ? goff_of[bid] : -1;
+        flin[f].hoff[b] = used ? hoff_of[bid] : -1;
+      }
+    }
+    // point-ordered copy of the observation records (CSR point -> residuals)
+    std::vector<int64_t> cnt(h->npts + 1, 0);
+    for (int64_t i = 0; i < N; i++) cnt[res_pt[i] + 1]++;
+    for (int64_t p = 0; p < h->npts; p++) cnt[p + 1] += cnt[p];
+    pt_begin = cnt;
+    po_frame.resize(N);
+    po_meas.resize(N);
+    std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+    for (int64_t i = 0; i < N; i++) {
+      const int64_t j = fill[res_pt[i]]++;
+      po_frame[j] = res_frame[i];
+      po_meas[j] = make_double2(d->residual_meas[2 * i], d->residual_meas[2 * i + 1]);
+    }
+  }
+
   // ---- upload
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) {
@@ -425,6 +547,18 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_row_written, h->row_written));
   chk(dalloc(&h->d_err, 1));
   if (e == hipSuccess) chk(hipMemset(h->d_err, 0, sizeof(int)));
+  chk(upload(&h->d_chunks, chunks));
+  {
+    void* p = nullptr;
+    chk(hipMalloc(&p, std::max<size_t>(flin.size(), 1) * sizeof(mvba::FrameLinHost)));
+    h->d_frame_lin = p;
+    if (e == hipSuccess && !flin.empty())
+      chk(hipMemcpy(p, flin.data(), flin.size() * sizeof(mvba::FrameLinHost), hipMemcpyHostToDevice));
+  }
+  chk(dalloc(&h->d_slab, (size_t)std::max<int64_t>(h->slab_size, 1)));
+  chk(upload(&h->d_pt_begin, pt_begin));
+  chk(upload(&h->d_po_frame, po_frame));
+  chk(upload(&h->d_po_meas, po_meas));
   if (e != hipSuccess) {
     g_create_error = std::string("HIP error during mvba_create: ") + hipGetErrorString(e);
     free_all(h);
@@ -556,6 +690,77 @@ mvba_status mvba_device_buffers(mvba_handle* h, mvba_device_view* v) {
   v->jacobian = h->d_J;
   v->order = h->d_order;
   v->row_written = h->d_row_written;
+  return MVBA_OK;
+}
+
+mvba_status mvba_lin_layout_info(const mvba_handle* h, mvba_lin_layout* out) {
+  if (!h || !out) return MVBA_E_INVALID;
+  out->cam_grad_size = h->cam_grad_size;
+  out->cam_hess_size = h->cam_hess_size;
+  out->num_points = h->npts;
+  out->num_cam_blocks = (int32_t)h->cam_block_ids.size();
+  out->supported = h->lin_ok ? 1 : 0;
+  return MVBA_OK;
+}
+
+mvba_status mvba_cam_block_map(const mvba_handle* h, int32_t* block_ids, int64_t* goff, int64_t* hoff) {
+  if (!h) return MVBA_E_INVALID;
+  const size_t n = h->cam_block_ids.size();
+  if (block_ids) std::memcpy(block_ids, h->cam_block_ids.data(), n * sizeof(int32_t));
+  if (goff) std::memcpy(goff, h->cam_goff.data(), n * sizeof(int64_t));
+  if (hoff) std::memcpy(hoff, h->cam_hoff.data(), n * sizeof(int64_t));
+  return MVBA_OK;
+}
+
+mvba_status mvba_point_block_map(const mvba_handle* h, int32_t* block_ids) {
+  if (!h || !block_ids) return MVBA_E_INVALID;
+  std::memcpy(block_ids, h->pt_block_ids.data(), h->pt_block_ids.size() * sizeof(int32_t));
+  return MVBA_OK;
+}
+
+mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                  double* d_cam_grad, double* d_cam_hess, double* d_pt_grad,
+                                  double* d_pt_hess, double* d_cost, void* stream) {
+  if (!h) return MVBA_E_INVALID;
+  if (!h->lin_ok) return h->fail(MVBA_E_INVALID, h->lin_err);
+  if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
+  if ((h->cam_grad_size && (!d_cam_grad || !d_cam_hess)) || (h->npts && (!d_pt_grad || !d_pt_hess)))
+    return h->fail(MVBA_E_INVALID, "null output buffer");
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  if (mvba_frame_lin_size() != sizeof(mvba::FrameLinHost))
+    return h->fail(MVBA_E_INVALID, "FrameLin layout mismatch between host and device code");
+  hipStream_t s = (hipStream_t)stream;
+  double cauchy_c = 0.0;
+  if (flags & MVBA_EVAL_APPLY_LOSS) {
+    if (!(cauchy_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
+    cauchy_c = 1.0 / (cauchy_threshold * cauchy_threshold);
+  }
+  hipError_t e = hipSuccess;
+  if (!(flags & MVBA_EVAL_SKIP_PREP)) {
+    h->gen++;
+    e = mvba_launch_prep(h->d_fd, h->nframes, h->d_params, h->d_frec, h->d_pt_off, h->d_pt_free,
+                         h->npts, h->d_pts, h->gen, h->d_err, s);
+    h->prep_done = true;
+  } else if (!h->prep_done) {
+    return h->fail(MVBA_E_INVALID, "MVBA_EVAL_SKIP_PREP before any full evaluation");
+  }
+  const int32_t lflags = flags & MVBA_EVAL_APPLY_LOSS;
+  for (size_t g = 0; g < h->groups.size() && e == hipSuccess; g++) {
+    const Group& G = h->groups[g];
+    e = mvba_launch_gram(G.model, G.deg, h->d_chunks + G.chunk_begin, G.chunk_count, h->d_segs, h->d_fd,
+                         h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
+                         h->d_slab + G.slab_base, lflags, cauchy_c, s);
+  }
+  if (e == hipSuccess && h->cam_grad_size) e = hipMemsetAsync(d_cam_grad, 0, h->cam_grad_size * sizeof(double), s);
+  if (e == hipSuccess && h->cam_hess_size) e = hipMemsetAsync(d_cam_hess, 0, h->cam_hess_size * sizeof(double), s);
+  if (e == hipSuccess && d_cost) e = hipMemsetAsync(d_cost, 0, sizeof(double), s);
+  if (e == hipSuccess)
+    e = mvba_launch_expand(h->d_frame_lin, (int32_t)h->nframes, h->max_w16, h->d_fd, h->d_frec, h->d_slab,
+                           d_cam_grad, d_cam_hess, d_cost, s);
+  if (e == hipSuccess)
+    e = mvba_launch_points_lin(h->d_pt_begin, h->npts, h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec,
+                               h->d_params, h->d_pts, d_pt_grad, d_pt_hess, lflags, cauchy_c, s);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_linearize_device launch");
   return MVBA_OK;
 }
 

@@ -304,16 +304,193 @@ __global__ void __launch_bounds__(kPrepBlock) k_prep(const FrameDesc* __restrict
   }
 }
 
-// ------------------------------------------------------------ K1: observations
+// ------------------------------------------------------------ observation model
+// Projection + distortion of one observation (rig_calibrator.cc:470-479,
+// camera_params.cc:260-314, rpc_distortion.cc:116-160) with the pieces of its
+// analytic derivative that every consumer needs.
+struct Proj {
+  double Xc[3];
+  double nx, ny;           // hnormalized(Xc)
+  double u0, u1;           // f * (nx, ny): centred undistorted pixel
+  double d0, d1;           // distorted pixel (half size added back)
+  double A00, A01, A10, A11;  // d(d)/d(u)
+  double df0, df1;         // total d(d)/d(f)
+  double m0, m1, r2;       // FOV / RADTAN: u / f, |u/f|^2
+  double aux0, aux1, aux2, aux3;  // FOV: f dconv/dw; RPC: 1/Dx, 1/Dy, Nx/Dx, Ny/Dy
+};
+
 template <int MODEL, int DEG>
-struct Distortion;
+__device__ __forceinline__ void project(const double* __restrict__ rec, double X0, double X1, double X2,
+                                        double f, double c0, double c1, const double* __restrict__ kd,
+                                        int K, double h0, double h1, Proj& o) {
+  // X = world_to_cam * X (rig_calibrator.cc:470)
+  o.Xc[0] = rec[0] * X0 + rec[1] * X1 + rec[2] * X2 + rec[9];
+  o.Xc[1] = rec[3] * X0 + rec[4] * X1 + rec[5] * X2 + rec[10];
+  o.Xc[2] = rec[6] * X0 + rec[7] * X1 + rec[8] * X2 + rec[11];
+  // u = f .* X.hnormalized() (:473)
+  o.nx = o.Xc[0] / o.Xc[2];
+  o.ny = o.Xc[1] / o.Xc[2];
+  const double u0 = f * o.nx, u1 = f * o.ny;
+  o.u0 = u0;
+  o.u1 = u1;
+  o.m0 = o.m1 = o.r2 = 0.0;
+  o.aux0 = o.aux1 = o.aux2 = o.aux3 = 0.0;
+  if constexpr (MODEL == kModelNone) {
+    // camera_params.cc:268 then + half size (:414)
+    o.d0 = ((u0 + c0) - h0) + h0;
+    o.d1 = ((u1 + c1) - h1) + h1;
+    o.A00 = 1.0; o.A01 = 0.0; o.A10 = 0.0; o.A11 = 1.0;
+    o.df0 = o.nx; o.df1 = o.ny;
+  } else if constexpr (MODEL == kModelFov) {
+    // camera_params.cc:269-281, precalcs :185-190
+    const double w = kd[0];
+    const double tw2 = tan(0.5 * w);
+    const double pc1 = 1.0 / w, pc2 = 2.0 * tw2;
+    const double m0 = u0 / f, m1 = u1 / f;
+    const double ru = sqrt(m0 * m0 + m1 * m1);
+    const double a = ru * pc2;
+    const double at = atan(a);
+    const double rd = at * pc1;
+    double conv = 1.0, dconv_dru = 0.0, dconv_dw = 0.0;
+    if (ru > 1e-5) {
+      conv = rd / ru;
+      const double den = 1.0 / (1.0 + a * a);
+      dconv_dru = (pc1 * pc2 * den - conv) / ru;
+      dconv_dw = (ru * pc1 * (1.0 + tw2 * tw2) * den - at / (w * w)) / ru;
+    }
+    o.d0 = ((c0 - h0) + conv * (m0 * f)) + h0;
+    o.d1 = ((c1 - h1) + conv * (m1 * f)) + h1;
+    const double g = (ru > 1e-5) ? dconv_dru / ru : 0.0;
+    o.A00 = conv + g * m0 * m0; o.A01 = g * m0 * m1;
+    o.A10 = g * m1 * m0;        o.A11 = conv + g * m1 * m1;
+    o.df0 = conv * m0; o.df1 = conv * m1;
+    o.m0 = m0; o.m1 = m1;
+    o.aux0 = f * dconv_dw;
+  } else if constexpr (MODEL == kModelRadtan) {
+    // camera_params.cc:282-308 (Tsai)
+    const double k1 = kd[0], k2 = kd[1], p1 = kd[2], p2 = kd[3];
+    const double k3 = (K == 5) ? kd[4] : 0.0;
+    const double m0 = u0 / f, m1 = u1 / f;
+    const double r2 = m0 * m0 + m1 * m1;
+    const double radial = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2;
+    double e0 = radial * m0, e1 = radial * m1;
+    e0 += 2.0 * p1 * m0 * m1 + p2 * (r2 + 2.0 * m0 * m0);
+    e1 += p1 * (r2 + 2.0 * m1 * m1) + 2.0 * p2 * m0 * m1;
+    o.d0 = (e0 * f + (c0 - h0)) + h0;
+    o.d1 = (e1 * f + (c1 - h1)) + h1;
+    const double drad = k1 + 2.0 * k2 * r2 + 3.0 * k3 * r2 * r2;
+    const double cross_t = 2.0 * drad * m0 * m1 + 2.0 * p1 * m0 + 2.0 * p2 * m1;
+    o.A00 = radial + 2.0 * drad * m0 * m0 + 2.0 * p1 * m1 + 6.0 * p2 * m0;
+    o.A01 = cross_t;
+    o.A10 = cross_t;
+    o.A11 = radial + 2.0 * drad * m1 * m1 + 6.0 * p1 * m1 + 2.0 * p2 * m0;
+    o.df0 = e0; o.df1 = e1;
+    o.m0 = m0; o.m1 = m1; o.r2 = r2;
+  } else {
+    // RPC of degree DEG (rpc_distortion.cc:116-160); coefficients
+    // [num_x(nl) | den_x(nl-1) | num_y(nl) | den_y(nl-1)], nl = (D+1)(D+2)/2.
+    double px[DEG + 1], py[DEG + 1];
+    double vx = 1.0, vy = 1.0;
+#pragma unroll
+    for (int k = 0; k <= DEG; k++) {
+      px[k] = vx; vx *= u0;
+      py[k] = vy; vy *= u1;
+    }
+    double N[4] = {0.0, 1.0, 0.0, 1.0};  // Nx, Dx, Ny, Dy
+    double Nx_[4] = {0.0, 0.0, 0.0, 0.0}, Ny_[4] = {0.0, 0.0, 0.0, 0.0};
+    int ci = 0;
+#pragma unroll
+    for (int cnt = 0; cnt < 4; cnt++) {
+      const int start = (cnt & 1);
+#pragma unroll
+      for (int dg = start; dg <= DEG; dg++) {
+#pragma unroll
+        for (int q = 0; q <= dg; q++) {
+          const double a = kd[ci];
+          N[cnt] += a * px[dg - q] * py[q];
+          if (dg - q > 0) Nx_[cnt] += a * (double)(dg - q) * px[dg - q - 1] * py[q];
+          if (q > 0) Ny_[cnt] += a * (double)q * px[dg - q] * py[q - 1];
+          ci++;
+        }
+      }
+    }
+    o.d0 = N[0] / N[1] + h0;
+    o.d1 = N[2] / N[3] + h1;
+    const double iDx = 1.0 / N[1], iDy = 1.0 / N[3];
+    const double qx = N[0] * iDx, qy = N[2] * iDy;
+    o.A00 = (Nx_[0] - qx * Nx_[1]) * iDx; o.A01 = (Ny_[0] - qx * Ny_[1]) * iDx;
+    o.A10 = (Nx_[2] - qy * Nx_[3]) * iDy; o.A11 = (Ny_[2] - qy * Ny_[3]) * iDy;
+    o.df0 = o.A00 * o.nx + o.A01 * o.ny;
+    o.df1 = o.A10 * o.nx + o.A11 * o.ny;
+    o.aux0 = iDx; o.aux1 = iDy; o.aux2 = qx; o.aux3 = qy;
+  }
+}
 
-// Common output of a distortion model at one observation.
-//   d     : distorted pixel (with the half size added back)
-//   A     : d(d)/d(u) (u = f * hnormalized(Xc))
-//   df    : total d(d)/d(f)
-// and writes its own distortion block columns.
+// Number of distortion columns that can be non-zero (RPC: the undistortion
+// half is structurally zero).
+template <int MODEL, int DEG>
+__host__ __device__ constexpr int live_dist_cols(int K) {
+  return MODEL == kModelRpc ? 2 * ((DEG + 1) * (DEG + 2)) - 2 : (MODEL == kModelNone ? 0 : K);
+}
 
+// Distortion block columns of one observation, emitted as emit(c, v_row0, v_row1)
+// for c < live_dist_cols (scaled by s = fs or the loss factor).
+template <int MODEL, int DEG, class Emit>
+__device__ __forceinline__ void dist_columns(const Proj& o, double f, int K, double s, Emit&& emit) {
+  if constexpr (MODEL == kModelFov) {
+    emit(0, o.m0 * o.aux0 * s, o.m1 * o.aux0 * s);
+  } else if constexpr (MODEL == kModelRadtan) {
+    const double fs = f * s;
+    const double m0 = o.m0, m1 = o.m1, r2 = o.r2, r4 = r2 * r2;
+    emit(0, fs * r2 * m0, fs * r2 * m1);
+    emit(1, fs * r4 * m0, fs * r4 * m1);
+    emit(2, fs * 2.0 * m0 * m1, fs * (r2 + 2.0 * m1 * m1));
+    emit(3, fs * (r2 + 2.0 * m0 * m0), fs * 2.0 * m0 * m1);
+    if (K == 5) emit(4, fs * r4 * r2 * m0, fs * r4 * r2 * m1);
+  } else if constexpr (MODEL == kModelRpc) {
+    double px[DEG + 1], py[DEG + 1];
+    double vx = 1.0, vy = 1.0;
+#pragma unroll
+    for (int k = 0; k <= DEG; k++) {
+      px[k] = vx; vx *= o.u0;
+      py[k] = vy; vy *= o.u1;
+    }
+    const double iDx = o.aux0 * s, iDy = o.aux1 * s;
+    const double mqx = -o.aux2 * iDx, mqy = -o.aux3 * iDy;  // -(N/D)/D
+    int ci = 0;
+#pragma unroll
+    for (int cnt = 0; cnt < 4; cnt++) {
+      const int start = (cnt & 1);
+      const double sc = (cnt == 0) ? iDx : (cnt == 1) ? mqx : (cnt == 2) ? iDy : mqy;
+#pragma unroll
+      for (int dg = start; dg <= DEG; dg++) {
+#pragma unroll
+        for (int q = 0; q <= dg; q++) {
+          const double v = sc * px[dg - q] * py[q];
+          if (cnt < 2) emit(ci, v, 0.0);
+          else emit(ci, 0.0, v);
+          ci++;
+        }
+      }
+    }
+  }
+  (void)f; (void)K; (void)o; (void)s;
+}
+
+__device__ __forceinline__ double loss_scale(double r0, double r1, int32_t flags, double cauchy_c,
+                                             double* half_rho) {
+  const double s = r0 * r0 + r1 * r1;
+  if (flags & MVBA_EVAL_APPLY_LOSS) {
+    // Ceres 1.14 CauchyLoss + Corrector [ext]: scale by sqrt(rho'), rho = b log(1 + s c).
+    const double sum = 1.0 + s * cauchy_c;
+    *half_rho = 0.5 * (log(sum) / cauchy_c);
+    return sqrt(fmax(DBL_MIN, 1.0 / sum));
+  }
+  *half_rho = 0.5 * s;
+  return 1.0;
+}
+
+// ------------------------------------------------------------ K1: observations
 __device__ __forceinline__ void stj(double* J, int64_t ld, int row, int64_t i, double v) {
   __builtin_nontemporal_store(v, J + (int64_t)row * ld + i);
 }
@@ -341,143 +518,33 @@ __global__ void __launch_bounds__(256) k_obs(
   const double c0 = params[F.off[MVBA_BLK_CENTER]];
   const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
   const double* __restrict__ kd = params + F.off[MVBA_BLK_DIST];
-  const double h0 = F.h0, h1 = F.h1;
   const int free_mask = F.free_mask;
-  const bool want_jac = (flags & MVBA_EVAL_JACOBIAN) != 0;
+  const int K = F.K;
 
-  const int pid = obs_pid[i];
-  const double4 P = pts[pid];
+  const double4 P = pts[obs_pid[i]];
   const double2 meas = obs_meas[i];
+  Proj o;
+  project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, kd, K, F.h0, F.h1, o);
 
-  // X = world_to_cam * X (rig_calibrator.cc:470)
-  double Xc[3];
-  Xc[0] = rec[0] * P.x + rec[1] * P.y + rec[2] * P.z + rec[9];
-  Xc[1] = rec[3] * P.x + rec[4] * P.y + rec[5] * P.z + rec[10];
-  Xc[2] = rec[6] * P.x + rec[7] * P.y + rec[8] * P.z + rec[11];
-  // u = f .* X.hnormalized() (:473)
-  const double nx = Xc[0] / Xc[2];
-  const double ny = Xc[1] / Xc[2];
-  const double u0 = f * nx, u1 = f * ny;
-
-  double d0, d1, A00, A01, A10, A11, df0, df1;
-  // Model-specific intermediates kept for the distortion columns.
-  double m0 = 0, m1 = 0, r2 = 0, aux0 = 0, aux1 = 0, aux2 = 0;
-  if constexpr (MODEL == kModelNone) {
-    // camera_params.cc:268 then + half size (:414)
-    d0 = ((u0 + c0) - h0) + h0;
-    d1 = ((u1 + c1) - h1) + h1;
-    A00 = 1.0; A01 = 0.0; A10 = 0.0; A11 = 1.0;
-    df0 = nx; df1 = ny;
-  } else if constexpr (MODEL == kModelFov) {
-    // camera_params.cc:269-281, precalcs :185-190
-    const double w = kd[0];
-    const double tw2 = tan(0.5 * w);
-    const double pc1 = 1.0 / w, pc2 = 2.0 * tw2;
-    m0 = u0 / f; m1 = u1 / f;
-    const double ru = sqrt(m0 * m0 + m1 * m1);
-    const double a = ru * pc2;
-    const double at = atan(a);
-    const double rd = at * pc1;
-    double conv = 1.0, dconv_dru = 0.0, dconv_dw = 0.0;
-    if (ru > 1e-5) {
-      conv = rd / ru;
-      const double den = 1.0 / (1.0 + a * a);
-      dconv_dru = (pc1 * pc2 * den - conv) / ru;
-      dconv_dw = (ru * pc1 * (1.0 + tw2 * tw2) * den - at / (w * w)) / ru;
-    }
-    d0 = ((c0 - h0) + conv * (m0 * f)) + h0;
-    d1 = ((c1 - h1) + conv * (m1 * f)) + h1;
-    const double g = (ru > 1e-5) ? dconv_dru / ru : 0.0;
-    A00 = conv + g * m0 * m0; A01 = g * m0 * m1;
-    A10 = g * m1 * m0;        A11 = conv + g * m1 * m1;
-    df0 = conv * m0; df1 = conv * m1;
-    aux0 = f * dconv_dw;
-  } else if constexpr (MODEL == kModelRadtan) {
-    // camera_params.cc:282-308 (Tsai)
-    const double k1 = kd[0], k2 = kd[1], p1 = kd[2], p2 = kd[3];
-    const double k3 = (F.K == 5) ? kd[4] : 0.0;
-    m0 = u0 / f; m1 = u1 / f;
-    r2 = m0 * m0 + m1 * m1;
-    const double radial = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2;
-    double e0 = radial * m0, e1 = radial * m1;
-    e0 += 2.0 * p1 * m0 * m1 + p2 * (r2 + 2.0 * m0 * m0);
-    e1 += p1 * (r2 + 2.0 * m1 * m1) + 2.0 * p2 * m0 * m1;
-    d0 = (e0 * f + (c0 - h0)) + h0;
-    d1 = (e1 * f + (c1 - h1)) + h1;
-    const double drad = k1 + 2.0 * k2 * r2 + 3.0 * k3 * r2 * r2;
-    const double cross_t = 2.0 * drad * m0 * m1 + 2.0 * p1 * m0 + 2.0 * p2 * m1;
-    A00 = radial + 2.0 * drad * m0 * m0 + 2.0 * p1 * m1 + 6.0 * p2 * m0;
-    A01 = cross_t;
-    A10 = cross_t;
-    A11 = radial + 2.0 * drad * m1 * m1 + 6.0 * p1 * m1 + 2.0 * p2 * m0;
-    df0 = e0; df1 = e1;
-  } else {
-    // RPC of degree DEG (rpc_distortion.cc:116-160); coefficients
-    // [num_x(nl) | den_x(nl-1) | num_y(nl) | den_y(nl-1)], nl = (D+1)(D+2)/2.
-    constexpr int nl = (DEG + 1) * (DEG + 2) / 2;
-    double px[DEG + 1], py[DEG + 1];
-    double vx = 1.0, vy = 1.0;
-#pragma unroll
-    for (int k = 0; k <= DEG; k++) {
-      px[k] = vx; vx *= u0;
-      py[k] = vy; vy *= u1;
-    }
-    double N[4] = {0.0, 1.0, 0.0, 1.0};  // Nx, Dx, Ny, Dy
-    double Nx_[4] = {0.0, 0.0, 0.0, 0.0}, Ny_[4] = {0.0, 0.0, 0.0, 0.0};  // d/dx, d/dy
-    int ci = 0;
-#pragma unroll
-    for (int cnt = 0; cnt < 4; cnt++) {
-      const int start = (cnt & 1);
-#pragma unroll
-      for (int dg = start; dg <= DEG; dg++) {
-#pragma unroll
-        for (int q = 0; q <= dg; q++) {
-          const double a = kd[ci];
-          N[cnt] += a * px[dg - q] * py[q];
-          if (dg - q > 0) Nx_[cnt] += a * (double)(dg - q) * px[dg - q - 1] * py[q];
-          if (q > 0) Ny_[cnt] += a * (double)q * px[dg - q] * py[q - 1];
-          ci++;
-        }
-      }
-    }
-    (void)nl;
-    d0 = N[0] / N[1] + h0;
-    d1 = N[2] / N[3] + h1;
-    const double iDx = 1.0 / N[1], iDy = 1.0 / N[3];
-    const double qx = N[0] * iDx, qy = N[2] * iDy;
-    A00 = (Nx_[0] - qx * Nx_[1]) * iDx; A01 = (Ny_[0] - qx * Ny_[1]) * iDx;
-    A10 = (Nx_[2] - qy * Nx_[3]) * iDy; A11 = (Ny_[2] - qy * Ny_[3]) * iDy;
-    df0 = A00 * nx + A01 * ny;
-    df1 = A10 * nx + A11 * ny;
-    aux0 = iDx; aux1 = iDy; aux2 = qx; m0 = qy; m1 = 0.0;
-    r2 = 0.0;
-    // keep powers for the coefficient columns below (recomputed, cheap)
-  }
-
-  double r0 = d0 - meas.x;  // rig_calibrator.cc:478-479
-  double r1 = d1 - meas.y;
-  double sr = 1.0;
-  if (flags & MVBA_EVAL_APPLY_LOSS) {
-    // Ceres 1.14 CauchyLoss + Corrector [ext]: scale by sqrt(rho').
-    const double s = r0 * r0 + r1 * r1;
-    const double inv = 1.0 / (1.0 + s * cauchy_c);
-    sr = sqrt(fmax(DBL_MIN, inv));
-    r0 *= sr;
-    r1 *= sr;
-  }
+  double r0 = o.d0 - meas.x;  // rig_calibrator.cc:478-479
+  double r1 = o.d1 - meas.y;
+  double half_rho;
+  const double sr = loss_scale(r0, r1, flags, cauchy_c, &half_rho);
+  r0 *= sr;
+  r1 *= sr;
   if (res) {
     __builtin_nontemporal_store(r0, res + i);
     __builtin_nontemporal_store(r1, res + ld + i);
   }
-  if (!want_jac) return;
+  if (!(flags & MVBA_EVAL_JACOBIAN)) return;
 
   // G = A * du/dXc, du/dXc = (f/z) [[1, 0, -nx], [0, 1, -ny]]; scaled by the loss.
-  const double fz = f / Xc[2] * sr;
-  double G0[3] = {fz * A00, fz * A01, -fz * (A00 * nx + A01 * ny)};
-  double G1[3] = {fz * A10, fz * A11, -fz * (A10 * nx + A11 * ny)};
+  const double fz = f / o.Xc[2] * sr;
+  const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+  const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
   double a0[3], a1[3];
-  cross(Xc, G0, a0);
-  cross(Xc, G1, a1);
+  cross(o.Xc, G0, a0);
+  cross(o.Xc, G1, a1);
 
   // Pose columns: blocks beg (0), end (1), ref_to_cam (2), offset (4).
 #pragma unroll
@@ -489,9 +556,9 @@ __global__ void __launch_bounds__(256) k_obs(
     const int base = (blk == 3) ? MVBA_JAC_BASE_OFFSET : 14 * blk;
 #pragma unroll
     for (int c = 0; c < ncol; c++) {
-      const double* o = rec + 12 + 6 * (k0 + c);
-      const double j0 = a0[0] * o[0] + a0[1] * o[1] + a0[2] * o[2] + G0[0] * o[3] + G0[1] * o[4] + G0[2] * o[5];
-      const double j1 = a1[0] * o[0] + a1[1] * o[1] + a1[2] * o[2] + G1[0] * o[3] + G1[1] * o[4] + G1[2] * o[5];
+      const double* w = rec + 12 + 6 * (k0 + c);
+      const double j0 = a0[0] * w[0] + a0[1] * w[1] + a0[2] * w[2] + G0[0] * w[3] + G0[1] * w[4] + G0[2] * w[5];
+      const double j1 = a1[0] * w[0] + a1[1] * w[1] + a1[2] * w[2] + G1[0] * w[3] + G1[1] * w[4] + G1[2] * w[5];
       stj(J, ld, base + c, i, j0);
       stj(J, ld, base + ncol + c, i, j1);
     }
@@ -507,8 +574,8 @@ __global__ void __launch_bounds__(256) k_obs(
     }
   }
   if (free_mask & (1 << MVBA_BLK_FOCAL)) {
-    stj(J, ld, MVBA_JAC_BASE_FOCAL, i, df0 * sr);
-    stj(J, ld, MVBA_JAC_BASE_FOCAL + 1, i, df1 * sr);
+    stj(J, ld, MVBA_JAC_BASE_FOCAL, i, o.df0 * sr);
+    stj(J, ld, MVBA_JAC_BASE_FOCAL + 1, i, o.df1 * sr);
   }
   if (free_mask & (1 << MVBA_BLK_CENTER)) {
     const double cc = (MODEL == kModelRpc) ? 0.0 : sr;  // RPC ignores the optical centre
@@ -518,56 +585,314 @@ __global__ void __launch_bounds__(256) k_obs(
     stj(J, ld, MVBA_JAC_BASE_CENTER + 3, i, cc);
   }
   if (!(free_mask & (1 << MVBA_BLK_DIST))) return;
-  if constexpr (MODEL == kModelFov) {
-    stj(J, ld, MVBA_JAC_BASE_DIST + 0, i, m0 * aux0 * sr);
-    stj(J, ld, MVBA_JAC_BASE_DIST + 1, i, m1 * aux0 * sr);
-  } else if constexpr (MODEL == kModelRadtan) {
-    const int K = F.K;
-    const double fs = f * sr;
-    const double r4 = r2 * r2;
-    const double cols0[5] = {r2 * m0, r4 * m0, 2.0 * m0 * m1, r2 + 2.0 * m0 * m0, r4 * r2 * m0};
-    const double cols1[5] = {r2 * m1, r4 * m1, r2 + 2.0 * m1 * m1, 2.0 * m0 * m1, r4 * r2 * m1};
-    for (int c = 0; c < K; c++) {
-      stj(J, ld, MVBA_JAC_BASE_DIST + c, i, fs * cols0[c]);
-      stj(J, ld, MVBA_JAC_BASE_DIST + K + c, i, fs * cols1[c]);
-    }
-  } else if constexpr (MODEL == kModelRpc) {
-    constexpr int nl = (DEG + 1) * (DEG + 2) / 2;
-    constexpr int nhalf = 4 * nl - 2;  // distortion coefficients used
-    constexpr int K = 2 * nhalf;
-    double px[DEG + 1], py[DEG + 1];
-    double vx = 1.0, vy = 1.0;
-#pragma unroll
-    for (int k = 0; k <= DEG; k++) {
-      px[k] = vx; vx *= u0;
-      py[k] = vy; vy *= u1;
-    }
-    const double iDx = aux0 * sr, iDy = aux1 * sr;
-    const double mqx = -aux2 * iDx, mqy = -m0 * iDy;  // -(N/D)/D
-    int ci = 0;
-#pragma unroll
-    for (int cnt = 0; cnt < 4; cnt++) {
-      const int start = (cnt & 1);
-      const double s = (cnt == 0) ? iDx : (cnt == 1) ? mqx : (cnt == 2) ? iDy : mqy;
-      const int row = (cnt < 2) ? 0 : 1;
-#pragma unroll
-      for (int dg = start; dg <= DEG; dg++) {
-#pragma unroll
-        for (int q = 0; q <= dg; q++) {
-          const double mono = px[dg - q] * py[q];
-          stj(J, ld, MVBA_JAC_BASE_DIST + row * K + ci, i, s * mono);
-          stj(J, ld, MVBA_JAC_BASE_DIST + (1 - row) * K + ci, i, 0.0);
-          ci++;
-        }
-      }
-    }
+  dist_columns<MODEL, DEG>(o, f, K, sr, [&](int c, double v0, double v1) {
+    stj(J, ld, MVBA_JAC_BASE_DIST + c, i, v0);
+    stj(J, ld, MVBA_JAC_BASE_DIST + K + c, i, v1);
+  });
+  if constexpr (MODEL == kModelRpc) {
     // Undistortion half: structurally zero.
-#pragma unroll 4
-    for (int c = nhalf; c < K; c++) {
+    for (int c = live_dist_cols<MODEL, DEG>(K); c < K; c++) {
       stj(J, ld, MVBA_JAC_BASE_DIST + c, i, 0.0);
       stj(J, ld, MVBA_JAC_BASE_DIST + K + c, i, 0.0);
     }
   }
+}
+
+// ------------------------------------------------------------ K2a: camera-side Gram
+// Normal equations, camera side. For a frame f, every pose column is
+// J_k = Z w_k with Z_i = [Xc x G_i | G_i] (per observation, 6 numbers per row)
+// and w_k = [omega_k; v_k] (per frame), so the frame's whole camera-camera block
+// follows from the Gram matrix of B = [Z | J_focal | J_center | J_dist | r]
+// (2 rows per observation): B^T B holds Z^T Z, Z^T J_intr, J_intr^T J_intr and
+// the gradients Z^T r, J_intr^T r (k_expand applies w). The Gram product is a
+// K = 128-deep GEMM per wave: fp64 MFMA v_mfma_f64_16x16x4 with B staged in LDS
+// as [column][row] (row stride kGramLd doubles, conflict-free reads).
+// One wave = one chunk (<= kChunkSegs segments of one frame, mvba_types.h); accumulators stay
+// in registers across the chunk; the chunk's Gram goes to a slab (no atomics).
+constexpr int kGramLd = 130;  // 128 rows + 2 pad doubles: bank-conflict-free reads
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2v __attribute__((ext_vector_type(2)));
+
+template <int MODEL, int DEG>
+struct GramShape {
+  static constexpr int kDist = (MODEL == kModelNone) ? 0 : (MODEL == kModelFov) ? 1
+                             : (MODEL == kModelRadtan) ? 5 : 2 * ((DEG + 1) * (DEG + 2)) - 2;
+  static constexpr int kWidth = 6 + 1 + 2 + kDist + 1;  // Z | focal | center | dist | r
+  static constexpr int kTiles = (kWidth + 15) / 16;
+  static constexpr int kPairs = kTiles * (kTiles + 1) / 2;
+  static constexpr int kColR = kWidth - 1;              // residual column
+};
+
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(64) k_gram(
+    const int4* __restrict__ chunks, int32_t nchunks, const Segment* __restrict__ segs,
+    const FrameDesc* __restrict__ fd, const double* __restrict__ frec,
+    const double* __restrict__ params, const double4* __restrict__ pts,
+    const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
+    double* __restrict__ slab, int32_t flags, double cauchy_c) {
+  using S = GramShape<MODEL, DEG>;
+  constexpr int T = S::kTiles;
+  constexpr int NP = S::kPairs;
+  constexpr int SLAB = T * 16 * T * 16 + 1;  // Gram (full square, upper tiles) + cost
+  extern __shared__ double lds[];            // [T*16][kGramLd]
+  const int lane = threadIdx.x;
+  const int ch = blockIdx.x;
+  if (ch >= nchunks) return;
+  const int4 c = chunks[ch];  // seg_begin, seg_count, frame, slab index
+  const int frame = __builtin_amdgcn_readfirstlane(c.z);
+  const FrameDesc& F = fd[frame];
+  const double* __restrict__ rec = frec + (int64_t)frame * kFrameRecDoubles;
+  const double f = params[F.off[MVBA_BLK_FOCAL]];
+  const double c0 = params[F.off[MVBA_BLK_CENTER]];
+  const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
+  const double* __restrict__ kd = params + F.off[MVBA_BLK_DIST];
+  const int K = F.K;
+
+  dbl4 acc[NP];
+#pragma unroll
+  for (int p = 0; p < NP; p++) acc[p] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double cost = 0.0;
+
+  // zero the padding columns once (they stay zero)
+  for (int col = S::kWidth; col < T * 16; col++)
+    *(dbl2v*)&lds[col * kGramLd + 2 * lane] = dbl2v{0.0, 0.0};
+
+  for (int sidx = 0; sidx < c.y; sidx++) {
+    const Segment sg = segs[c.x + sidx];
+    const int count = __builtin_amdgcn_readfirstlane(sg.count);
+    const int64_t i = (int64_t)sg.begin + lane;
+    double row0[S::kWidth], row1[S::kWidth];
+#pragma unroll
+    for (int q = 0; q < S::kWidth; q++) row0[q] = row1[q] = 0.0;
+    if (lane < count) {
+      const double4 P = pts[obs_pid[i]];
+      const double2 meas = obs_meas[i];
+      Proj o;
+      project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, kd, K, F.h0, F.h1, o);
+      double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
+      double half_rho;
+      const double sr = loss_scale(r0, r1, flags, cauchy_c, &half_rho);
+      cost += half_rho;
+      const double fz = f / o.Xc[2] * sr;
+      const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+      const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
+      double a0[3], a1[3];
+      cross(o.Xc, G0, a0);
+      cross(o.Xc, G1, a1);
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        row0[q] = a0[q]; row0[3 + q] = G0[q];
+        row1[q] = a1[q]; row1[3 + q] = G1[q];
+      }
+      row0[6] = o.df0 * sr;
+      row1[6] = o.df1 * sr;
+      const double cc = (MODEL == kModelRpc) ? 0.0 : sr;
+      row0[7] = cc; row0[8] = 0.0;
+      row1[7] = 0.0; row1[8] = cc;
+      dist_columns<MODEL, DEG>(o, f, K, sr, [&](int q, double v0, double v1) {
+        row0[9 + q] = v0;
+        row1[9 + q] = v1;
+      });
+      row0[S::kColR] = r0 * sr;
+      row1[S::kColR] = r1 * sr;
+    }
+    // stage B (this segment's 128 rows) in LDS as [column][row]
+#pragma unroll
+    for (int q = 0; q < S::kWidth; q++) *(dbl2v*)&lds[q * kGramLd + 2 * lane] = dbl2v{row0[q], row1[q]};
+    __syncthreads();
+    const int col = lane & 15, rsub = lane >> 4;
+#pragma unroll 4
+    for (int st = 0; st < 32; st++) {
+      const int row = 4 * st + rsub;
+      double v[T];
+#pragma unroll
+      for (int t = 0; t < T; t++) v[t] = lds[(t * 16 + col) * kGramLd + row];
+      int p = 0;
+#pragma unroll
+      for (int ti = 0; ti < T; ti++)
+#pragma unroll
+        for (int tj = ti; tj < T; tj++) {
+          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ti], v[tj], acc[p], 0, 0, 0);
+          p++;
+        }
+    }
+    __syncthreads();
+  }
+  // chunk Gram -> slab: lane holds G[(lane>>4) + 4r][lane & 15] of each tile pair
+  double* out = slab + (int64_t)c.w * SLAB;
+  const int W16 = T * 16;
+  int p = 0;
+#pragma unroll
+  for (int ti = 0; ti < T; ti++)
+#pragma unroll
+    for (int tj = ti; tj < T; tj++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        out[(ti * 16 + (lane >> 4) + 4 * r) * W16 + tj * 16 + (lane & 15)] = acc[p][r];
+      p++;
+    }
+  // chunk cost: wave reduction
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cost += __shfl_xor(cost, off, 64);
+  if (lane == 0) out[W16 * W16] = cost;
+}
+
+// ------------------------------------------------------------ K2 expand (per frame)
+// Sums the frame's chunk Grams and scatters gradient and block-diagonal Hessian
+// of every free camera-side block: pose blocks via w (J_pose = Z w), intrinsics
+// directly. Outputs are shared by frames (atomics): layout per block =
+// gradient at goff, row-major size x size Hessian at hoff.
+struct FrameLin {
+  int64_t slab_off;                  // offset (doubles) of this frame's first chunk slab
+  int32_t chunk_count;               // consecutive chunk slabs of w16*w16+1 doubles
+  int32_t width, w16;                // Gram width and padded width
+  int32_t pad;
+  int64_t goff[8];                   // camera-side gradient offsets per block (-1: constant/none)
+  int64_t hoff[8];                   // camera-side Hessian offsets per block
+};
+
+__global__ void __launch_bounds__(64) k_expand(const FrameLin* __restrict__ fl, int32_t nframes,
+                                               const FrameDesc* __restrict__ fd,
+                                               const double* __restrict__ frec,
+                                               const double* __restrict__ slab,
+                                               double* __restrict__ grad, double* __restrict__ hess,
+                                               double* __restrict__ cost) {
+  extern __shared__ double sh[];  // Gram [w16*w16+1] then w [6*22] then T [6*22]
+  const int f = blockIdx.x;
+  if (f >= nframes) return;
+  const FrameLin L = fl[f];
+  const int W16 = L.w16, Wd = L.width;
+  const int n = W16 * W16 + 1;
+  const int SL = n;
+  double* G = sh;
+  double* w = sh + n;
+  double* Tm = w + 6 * kPoseCols;
+  for (int e = threadIdx.x; e < n; e += 64) {
+    double acc = 0.0;
+    for (int c = 0; c < L.chunk_count; c++) acc += slab[L.slab_off + (int64_t)c * SL + e];
+    G[e] = acc;
+  }
+  const double* rec = frec + (int64_t)f * kFrameRecDoubles;
+  for (int e = threadIdx.x; e < 6 * kPoseCols; e += 64) {
+    const int k = e / 6, a = e % 6;
+    w[a * kPoseCols + k] = rec[12 + 6 * k + a];
+  }
+  __syncthreads();
+  // Gram is stored in upper tiles only: read (a,b) with a <= b from the upper part
+  auto g = [&](int a, int b) -> double { return (a / 16 <= b / 16) ? G[a * W16 + b] : G[b * W16 + a]; };
+  // T = G_ZZ w (6 x 22)
+  for (int e = threadIdx.x; e < 6 * kPoseCols; e += 64) {
+    const int a = e / kPoseCols, k = e % kPoseCols;
+    double t = 0.0;
+    for (int b = 0; b < 6; b++) t += g(a, b) * w[b * kPoseCols + k];
+    Tm[e] = t;
+  }
+  __syncthreads();
+  const int R = Wd - 1;  // residual column
+  const FrameDesc& F = fd[f];
+  // pose blocks: beg(0) cols 0..6, end(1) 7..13, ref_to_cam(2) 14..20, offset(4) 21
+  for (int blk = 0; blk < 4; blk++) {
+    const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+    if (L.goff[b] < 0) continue;
+    const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
+    for (int e = threadIdx.x; e < ncol; e += 64) {
+      double gv = 0.0;
+      for (int a = 0; a < 6; a++) gv += w[a * kPoseCols + k0 + e] * g(a, R);
+      atomicAdd(&grad[L.goff[b] + e], gv);
+    }
+    for (int e = threadIdx.x; e < ncol * ncol; e += 64) {
+      const int kk = e / ncol, kc = e % ncol;
+      double hv = 0.0;
+      for (int a = 0; a < 6; a++) hv += w[a * kPoseCols + k0 + kk] * Tm[a * kPoseCols + k0 + kc];
+      atomicAdd(&hess[L.hoff[b] + e], hv);
+    }
+  }
+  // intrinsics: focal col 6, center cols 7..8, dist cols 9.. (live columns)
+  const int nd = Wd - 10;  // live distortion columns in the Gram
+  const int blocks[3] = {MVBA_BLK_FOCAL, MVBA_BLK_CENTER, MVBA_BLK_DIST};
+  const int c0s[3] = {6, 7, 9};
+  const int ncs[3] = {1, 2, nd < F.K ? nd : F.K};  // radtan K=4: 4 of the 5 Gram columns
+  for (int q = 0; q < 3; q++) {
+    const int b = blocks[q];
+    if (L.goff[b] < 0) continue;
+    const int nc = ncs[q], cs = c0s[q];
+    const int bs = (b == MVBA_BLK_DIST) ? F.K : nc;  // Hessian row length (RPC: K incl. zero half)
+    for (int e = threadIdx.x; e < nc; e += 64) atomicAdd(&grad[L.goff[b] + e], g(cs + e, R));
+    for (int e = threadIdx.x; e < nc * nc; e += 64) {
+      const int r = e / nc, cc = e % nc;
+      atomicAdd(&hess[L.hoff[b] + r * bs + cc], g(cs + r, cs + cc));
+    }
+  }
+  if (threadIdx.x == 0 && cost) {
+    double cv = 0.0;
+    for (int c = 0; c < L.chunk_count; c++) cv += slab[L.slab_off + (int64_t)c * SL + W16 * W16];
+    atomicAdd(cost, cv);
+  }
+}
+
+// ------------------------------------------------------------ K2b: point side
+// One lane per point: loop over its observations (point-ordered copy of the
+// observation records), recompute the projection, accumulate V_p = J_p^T J_p
+// (packed xx xy xz yy yz zz) and g_p = J_p^T r. No atomics.
+template <int MODEL, int DEG>
+__device__ __forceinline__ void point_obs(const FrameDesc& F, const double* __restrict__ rec,
+                                          const double* __restrict__ params, double X0, double X1,
+                                          double X2, double2 meas, int32_t flags, double cauchy_c,
+                                          double* V, double* g) {
+  const double f = params[F.off[MVBA_BLK_FOCAL]];
+  const double c0 = params[F.off[MVBA_BLK_CENTER]];
+  const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
+  Proj o;
+  project<MODEL, DEG>(rec, X0, X1, X2, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+  const double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
+  double half_rho;
+  const double sr = loss_scale(r0, r1, flags, cauchy_c, &half_rho);
+  const double fz = f / o.Xc[2] * sr;
+  const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+  const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
+  double J0[3], J1[3];
+  for (int c = 0; c < 3; c++) {
+    J0[c] = G0[0] * rec[c] + G0[1] * rec[3 + c] + G0[2] * rec[6 + c];
+    J1[c] = G1[0] * rec[c] + G1[1] * rec[3 + c] + G1[2] * rec[6 + c];
+  }
+  const double rr0 = r0 * sr, rr1 = r1 * sr;
+  V[0] += J0[0] * J0[0] + J1[0] * J1[0];
+  V[1] += J0[0] * J0[1] + J1[0] * J1[1];
+  V[2] += J0[0] * J0[2] + J1[0] * J1[2];
+  V[3] += J0[1] * J0[1] + J1[1] * J1[1];
+  V[4] += J0[1] * J0[2] + J1[1] * J1[2];
+  V[5] += J0[2] * J0[2] + J1[2] * J1[2];
+  for (int c = 0; c < 3; c++) g[c] += J0[c] * rr0 + J1[c] * rr1;
+}
+
+__global__ void __launch_bounds__(256) k_points_lin(
+    const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
+    const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, double* __restrict__ pgrad, double* __restrict__ phess,
+    int32_t flags, double cauchy_c) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npts) return;
+  const double4 X = pts[p];
+  double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+  if (X.w != 0.0) {
+    for (int64_t j = pt_begin[p]; j < pt_begin[p + 1]; j++) {
+      const int32_t fr = po_frame[j];
+      const FrameDesc& F = fd[fr];
+      const double* rec = frec + (int64_t)fr * kFrameRecDoubles;
+      const double2 m = po_meas[j];
+      const int K = F.K;
+      if (K == 0) point_obs<kModelNone, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      else if (K == 1) point_obs<kModelFov, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      else if (K == 4 || K == 5) point_obs<kModelRadtan, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      else if (K == 20) point_obs<kModelRpc, 1>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      else if (K == 44) point_obs<kModelRpc, 2>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      else if (K == 76) point_obs<kModelRpc, 3>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+    }
+  }
+  for (int c = 0; c < 3; c++) pgrad[3 * p + c] = g[c];
+  for (int c = 0; c < 6; c++) phess[6 * p + c] = V[c];
 }
 
 }  // namespace mvba
@@ -586,6 +911,25 @@ hipError_t mvba_launch_prep(const mvba::FrameDesc* fd, int64_t nframes, const do
   return hipGetLastError();
 }
 
+#define MVBA_SWITCH_MODEL(model, deg, CALL)                        \
+  switch (model) {                                                 \
+    case mvba::kModelNone: CALL(mvba::kModelNone, 0); break;       \
+    case mvba::kModelFov: CALL(mvba::kModelFov, 0); break;         \
+    case mvba::kModelRadtan: CALL(mvba::kModelRadtan, 0); break;   \
+    case mvba::kModelRpc:                                          \
+      switch (deg) {                                               \
+        case 1: CALL(mvba::kModelRpc, 1); break;                   \
+        case 2: CALL(mvba::kModelRpc, 2); break;                   \
+        case 3: CALL(mvba::kModelRpc, 3); break;                   \
+        case 4: CALL(mvba::kModelRpc, 4); break;                   \
+        case 5: CALL(mvba::kModelRpc, 5); break;                   \
+        case 6: CALL(mvba::kModelRpc, 6); break;                   \
+        default: return hipErrorInvalidValue;                      \
+      }                                                            \
+      break;                                                       \
+    default: return hipErrorInvalidValue;                          \
+  }
+
 // model: ModelKind; deg: RPC degree (1..kMaxRpcDegree) when model == kModelRpc.
 hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_t nseg,
                            const mvba::FrameDesc* fd, const double* frec, const double* params,
@@ -594,28 +938,83 @@ hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_
                            hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((nseg + 3) / 4);
-#define MVBA_LAUNCH(M, D)                                                                      \
+#define MVBA_OBS(M, D)                                                                          \
   hipLaunchKernelGGL((mvba::k_obs<M, D>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec, \
                      params, pts, obs_pid, obs_meas, res, J, ld, flags, cauchy_c)
+  MVBA_SWITCH_MODEL(model, deg, MVBA_OBS)
+#undef MVBA_OBS
+  return hipGetLastError();
+}
+
+// Gram shape of a model (host side, for slab sizing and the expand step).
+int mvba_gram_width(int model, int deg) {
   switch (model) {
-    case mvba::kModelNone: MVBA_LAUNCH(mvba::kModelNone, 0); break;
-    case mvba::kModelFov: MVBA_LAUNCH(mvba::kModelFov, 0); break;
-    case mvba::kModelRadtan: MVBA_LAUNCH(mvba::kModelRadtan, 0); break;
+    case mvba::kModelNone: return mvba::GramShape<mvba::kModelNone, 0>::kWidth;
+    case mvba::kModelFov: return mvba::GramShape<mvba::kModelFov, 0>::kWidth;
+    case mvba::kModelRadtan: return mvba::GramShape<mvba::kModelRadtan, 0>::kWidth;
     case mvba::kModelRpc:
       switch (deg) {
-        case 1: MVBA_LAUNCH(mvba::kModelRpc, 1); break;
-        case 2: MVBA_LAUNCH(mvba::kModelRpc, 2); break;
-        case 3: MVBA_LAUNCH(mvba::kModelRpc, 3); break;
-        case 4: MVBA_LAUNCH(mvba::kModelRpc, 4); break;
-        case 5: MVBA_LAUNCH(mvba::kModelRpc, 5); break;
-        case 6: MVBA_LAUNCH(mvba::kModelRpc, 6); break;
+        case 1: return mvba::GramShape<mvba::kModelRpc, 1>::kWidth;
+        case 2: return mvba::GramShape<mvba::kModelRpc, 2>::kWidth;
+        case 3: return mvba::GramShape<mvba::kModelRpc, 3>::kWidth;
+        default: return -1;  // the MFMA Gram path covers RPC degree <= 3
+      }
+    default: return -1;
+  }
+}
+
+hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchunks,
+                            const mvba::Segment* segs, const mvba::FrameDesc* fd, const double* frec,
+                            const double* params, const double4* pts, const int32_t* obs_pid,
+                            const double2* obs_meas, double* slab, int32_t flags, double cauchy_c,
+                            hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+#define MVBA_GRAM(M, D)                                                                              \
+  {                                                                                                  \
+    const size_t lds = sizeof(double) * mvba::GramShape<M, D>::kTiles * 16 * mvba::kGramLd;          \
+    hipLaunchKernelGGL((mvba::k_gram<M, D>), dim3((unsigned)nchunks), dim3(64), lds, s, chunks, nchunks, \
+                       segs, fd, frec, params, pts, obs_pid, obs_meas, slab, flags, cauchy_c);        \
+  }
+  switch (model) {
+    case mvba::kModelNone: MVBA_GRAM(mvba::kModelNone, 0); break;
+    case mvba::kModelFov: MVBA_GRAM(mvba::kModelFov, 0); break;
+    case mvba::kModelRadtan: MVBA_GRAM(mvba::kModelRadtan, 0); break;
+    case mvba::kModelRpc:
+      switch (deg) {
+        case 1: MVBA_GRAM(mvba::kModelRpc, 1); break;
+        case 2: MVBA_GRAM(mvba::kModelRpc, 2); break;
+        case 3: MVBA_GRAM(mvba::kModelRpc, 3); break;
         default: return hipErrorInvalidValue;
       }
       break;
     default: return hipErrorInvalidValue;
   }
-#undef MVBA_LAUNCH
+#undef MVBA_GRAM
   return hipGetLastError();
 }
+
+hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16,
+                              const mvba::FrameDesc* fd, const double* frec, const double* slab,
+                              double* grad, double* hess, double* cost, hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  const size_t lds = sizeof(double) * ((size_t)max_w16 * max_w16 + 1 + 2 * 6 * mvba::kPoseCols);
+  hipLaunchKernelGGL(mvba::k_expand, dim3((unsigned)nframes), dim3(64), lds, s,
+                     (const mvba::FrameLin*)fl, nframes, fd, frec, slab, grad, hess, cost);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_points_lin(const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
+                                  const double2* po_meas, const mvba::FrameDesc* fd,
+                                  const double* frec, const double* params, const double4* pts,
+                                  double* pgrad, double* phess, int32_t flags, double cauchy_c,
+                                  hipStream_t s) {
+  if (npts <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_points_lin, dim3((unsigned)((npts + 255) / 256)), dim3(256), 0, s,
+                     pt_begin, npts, po_frame, po_meas, fd, frec, params, pts, pgrad, phess, flags,
+                     cauchy_c);
+  return hipGetLastError();
+}
+
+size_t mvba_frame_lin_size(void) { return sizeof(mvba::FrameLin); }
 
 }  // extern "C"

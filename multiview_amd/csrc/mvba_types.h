@@ -46,6 +46,19 @@ enum ModelKind : int32_t {
 };
 
 constexpr int kMaxRpcDegree = 6;
+constexpr int kMaxLinRpcDegree = 3;
+constexpr int kChunkSegs = 4;       // segments per K2a chunk (one wave)  // the MFMA Gram linearization covers RPC degree <= 3
+
+// Per-frame record of the linearization (K2 expand); mirrors mvba::FrameLin in
+// mvba_kernels.hip (checked with mvba_frame_lin_size()).
+struct FrameLinHost {
+  int64_t slab_off;
+  int32_t chunk_count;
+  int32_t width, w16;
+  int32_t pad;
+  int64_t goff[8];
+  int64_t hoff[8];
+};
 
 }  // namespace mvba
 

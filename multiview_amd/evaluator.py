@@ -95,6 +95,34 @@ class Evaluator:
         flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0)
         return float(self.lib.mvba_eval_bytes(self.h, flags))
 
+    # ------------------------------------------------------- normal equations
+    def lin_layout(self) -> dict:
+        L = _lib.LinLayout()
+        _lib.check(self.lib.mvba_lin_layout_info(self.h, C.byref(L)), self.h)
+        nb = L.num_cam_blocks
+        ids = np.empty(nb, dtype=np.int32)
+        goff = np.empty(nb, dtype=np.int64)
+        hoff = np.empty(nb, dtype=np.int64)
+        _lib.check(self.lib.mvba_cam_block_map(self.h, ids.ctypes.data, goff.ctypes.data,
+                                               hoff.ctypes.data), self.h)
+        pids = np.empty(L.num_points, dtype=np.int32)
+        _lib.check(self.lib.mvba_point_block_map(self.h, pids.ctypes.data), self.h)
+        return dict(cam_grad_size=L.cam_grad_size, cam_hess_size=L.cam_hess_size,
+                    num_points=L.num_points, supported=bool(L.supported), cam_block_ids=ids,
+                    cam_goff=goff, cam_hoff=hoff, point_block_ids=pids)
+
+    def linearize_device(self, cam_grad, cam_hess, pt_grad, pt_hess, cost=None,
+                         apply_loss: bool = False, robust_threshold: float = 3.0, stream=None,
+                         skip_prep: bool = False):
+        """Gradient and block-diagonal Hessian into caller-owned torch float64
+        CUDA tensors (layouts: include/mvba/mvba.h, mvba_linearize_device)."""
+        flags = (_lib.EVAL_APPLY_LOSS if apply_loss else 0) | (_lib.EVAL_SKIP_PREP if skip_prep else 0)
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        st = self.lib.mvba_linearize_device(self.h, flags, float(robust_threshold), ptr(cam_grad),
+                                            ptr(cam_hess), ptr(pt_grad), ptr(pt_hess), ptr(cost),
+                                            C.c_void_p(stream or 0))
+        _lib.check(st, self.h)
+
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
             self.lib.mvba_destroy(self.h)
