@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0, help="residuals in the CPU sample (0 = auto)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, default) or gloo (rehearsal of the multi-rank path on one GPU)")
     return ap.parse_args()
 
 
@@ -89,8 +91,12 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -188,6 +194,61 @@ def main():
         },
         "gen_s": t_gen,
     }
+    # ---- phase B: normal equations (K2) + the per-iteration exchange (§8e)
+    from multiview_amd.dist import NormalEquationBuffer, check_layouts_agree
+
+    L = ev.lin_layout()
+    lin = None
+    if L["supported"]:
+        if world > 1:
+            check_layouts_agree(L, P.block_size, device="cuda")
+        buf = NormalEquationBuffer(L, device="cuda")
+        pg = torch.empty(3 * L["num_points"], dtype=torch.float64, device="cuda")
+        ph = torch.empty(6 * L["num_points"], dtype=torch.float64, device="cuda")
+
+        def lin_step(events=None):
+            if events is not None:
+                events[0].record(stream)
+            ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, apply_loss=True,
+                                robust_threshold=3.0, stream=sh)
+            if events is not None:
+                events[1].record(stream)
+            if world > 1:
+                buf.allreduce()
+            if events is not None:
+                events[2].record(stream)
+
+        for _ in range(args.warmup):
+            lin_step()
+        torch.cuda.synchronize()
+        levs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            lin_step(levs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ldt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(ldt, op=dist.ReduceOp.MAX)
+        ev.sync(sh)
+        lin_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in levs]))
+        ar_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in levs]))
+        lin = {
+            "what": "K2 linearization (Cauchy-corrected J^T r, block-diagonal J^T J: camera side "
+                    "via fp64 MFMA Gram, point side) + RCCL all-reduce of the camera blocks",
+            "evals_per_s": total_evals / float(ldt.item()),
+            "ms_per_step": 1e3 * float(ldt.item()) / args.steps,
+            "kernel_ms": lin_ms,
+            "allreduce_ms": ar_ms if world > 1 else 0.0,
+            "allreduce_bytes": buf.payload_bytes if world > 1 else 0,
+            "cam_params": L["cam_grad_size"],
+        }
+    line["linearize"] = lin
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(P, args.cpu_sample)
     if rank == 0:
