@@ -40,12 +40,14 @@ hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchu
                             const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
                             double* slab, int32_t flags, double cauchy_c, hipStream_t s);
 hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16, const FrameDesc* fd,
-                              const double* frec, const double* slab, double* grad, double* hess,
-                              double* cost, hipStream_t s);
-hipError_t mvba_launch_points_lin(const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
-                                  const double2* po_meas, const FrameDesc* fd, const double* frec,
-                                  const double* params, const double4* pts, double* pgrad, double* phess,
-                                  int32_t flags, double cauchy_c, hipStream_t s);
+                              const double* frec, const double* slab, double* rep, int64_t ng, int64_t nh,
+                              double* grad, double* hess, double* cost, hipStream_t s);
+int mvba_num_replicas(void);
+hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, int64_t npts,
+                                  const int32_t* po_frame, const double2* po_meas, const FrameDesc* fd,
+                                  const double* frec, const double* params, const double4* pts,
+                                  double* pgrad, double* phess, int32_t flags, double cauchy_c,
+                                  hipStream_t s);
 hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
                            const FrameDesc* fd, const double* frec, const double* params,
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
@@ -147,6 +149,7 @@ struct mvba_handle {
   int4* d_chunks = nullptr;
   void* d_frame_lin = nullptr;
   double* d_slab = nullptr;
+  double* d_rep = nullptr;  // kReplicas copies of [cam_grad | cam_hess | cost], kept zero between calls
   int64_t* d_pt_begin = nullptr;
   int32_t* d_po_frame = nullptr;
   double2* d_po_meas = nullptr;
@@ -166,7 +169,7 @@ static void free_all(mvba_handle* h) {
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
-                  h->d_slab, h->d_pt_begin, h->d_po_frame, h->d_po_meas};
+                  h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -556,6 +559,11 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       chk(hipMemcpy(p, flin.data(), flin.size() * sizeof(mvba::FrameLinHost), hipMemcpyHostToDevice));
   }
   chk(dalloc(&h->d_slab, (size_t)std::max<int64_t>(h->slab_size, 1)));
+  {
+    const size_t nrep = (size_t)mvba_num_replicas() * (size_t)(h->cam_grad_size + h->cam_hess_size + 1);
+    chk(dalloc(&h->d_rep, nrep));
+    if (e == hipSuccess) chk(hipMemset(h->d_rep, 0, nrep * sizeof(double)));
+  }
   chk(upload(&h->d_pt_begin, pt_begin));
   chk(upload(&h->d_po_frame, po_frame));
   chk(upload(&h->d_po_meas, po_meas));
@@ -751,15 +759,14 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
                          h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
                          h->d_slab + G.slab_base, lflags, cauchy_c, s);
   }
-  if (e == hipSuccess && h->cam_grad_size) e = hipMemsetAsync(d_cam_grad, 0, h->cam_grad_size * sizeof(double), s);
-  if (e == hipSuccess && h->cam_hess_size) e = hipMemsetAsync(d_cam_hess, 0, h->cam_hess_size * sizeof(double), s);
-  if (e == hipSuccess && d_cost) e = hipMemsetAsync(d_cost, 0, sizeof(double), s);
   if (e == hipSuccess)
     e = mvba_launch_expand(h->d_frame_lin, (int32_t)h->nframes, h->max_w16, h->d_fd, h->d_frec, h->d_slab,
-                           d_cam_grad, d_cam_hess, d_cost, s);
+                           h->d_rep, h->cam_grad_size, h->cam_hess_size, d_cam_grad, d_cam_hess, d_cost, s);
   if (e == hipSuccess)
-    e = mvba_launch_points_lin(h->d_pt_begin, h->npts, h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec,
-                               h->d_params, h->d_pts, d_pt_grad, d_pt_hess, lflags, cauchy_c, s);
+    e = mvba_launch_points_lin(h->groups.size() == 1 ? h->groups[0].model : -1,
+                               h->groups.size() == 1 ? h->groups[0].deg : 0, h->d_pt_begin, h->npts,
+                               h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
+                               d_pt_grad, d_pt_hess, lflags, cauchy_c, s);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_linearize_device launch");
   return MVBA_OK;
 }

@@ -741,8 +741,12 @@ __global__ void __launch_bounds__(64) k_gram(
 // ------------------------------------------------------------ K2 expand (per frame)
 // Sums the frame's chunk Grams and scatters gradient and block-diagonal Hessian
 // of every free camera-side block: pose blocks via w (J_pose = Z w), intrinsics
-// directly. Outputs are shared by frames (atomics): layout per block =
-// gradient at goff, row-major size x size Hessian at hoff.
+// directly. Layout per block: gradient at goff, row-major size x size Hessian at
+// hoff. Camera blocks shared by many frames (a sensor's
+// extrinsics/intrinsics: ~1000 frames at c2) would serialise on atomics, so
+// frame f adds into replica (f mod kReplicas) of the output and k_rep_reduce
+// sums the replicas (and re-zeroes them for the next call).
+constexpr int kReplicas = 32;
 struct FrameLin {
   int64_t slab_off;                  // offset (doubles) of this frame's first chunk slab
   int32_t chunk_count;               // consecutive chunk slabs of w16*w16+1 doubles
@@ -756,8 +760,7 @@ __global__ void __launch_bounds__(64) k_expand(const FrameLin* __restrict__ fl, 
                                                const FrameDesc* __restrict__ fd,
                                                const double* __restrict__ frec,
                                                const double* __restrict__ slab,
-                                               double* __restrict__ grad, double* __restrict__ hess,
-                                               double* __restrict__ cost) {
+                                               double* __restrict__ rep, int64_t ng, int64_t nh) {
   extern __shared__ double sh[];  // Gram [w16*w16+1] then w [6*22] then T [6*22]
   const int f = blockIdx.x;
   if (f >= nframes) return;
@@ -791,6 +794,9 @@ __global__ void __launch_bounds__(64) k_expand(const FrameLin* __restrict__ fl, 
   __syncthreads();
   const int R = Wd - 1;  // residual column
   const FrameDesc& F = fd[f];
+  double* grad = rep + (int64_t)(f & (kReplicas - 1)) * (ng + nh + 1);
+  double* hess = grad + ng;
+  double* cost = hess + nh;
   // pose blocks: beg(0) cols 0..6, end(1) 7..13, ref_to_cam(2) 14..20, offset(4) 21
   for (int blk = 0; blk < 4; blk++) {
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
@@ -824,11 +830,28 @@ __global__ void __launch_bounds__(64) k_expand(const FrameLin* __restrict__ fl, 
       atomicAdd(&hess[L.hoff[b] + r * bs + cc], g(cs + r, cs + cc));
     }
   }
-  if (threadIdx.x == 0 && cost) {
+  if (threadIdx.x == 0) {
     double cv = 0.0;
     for (int c = 0; c < L.chunk_count; c++) cv += slab[L.slab_off + (int64_t)c * SL + W16 * W16];
     atomicAdd(cost, cv);
   }
+}
+
+__global__ void __launch_bounds__(256) k_rep_reduce(double* __restrict__ rep, int64_t ng, int64_t nh,
+                                                    double* __restrict__ grad, double* __restrict__ hess,
+                                                    double* __restrict__ cost) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t stride = ng + nh + 1;
+  if (e >= stride) return;
+  double acc = 0.0;
+#pragma unroll 8
+  for (int r = 0; r < kReplicas; r++) {
+    acc += rep[r * stride + e];
+    rep[r * stride + e] = 0.0;
+  }
+  if (e < ng) grad[e] = acc;
+  else if (e < ng + nh) hess[e - ng] = acc;
+  else if (cost) *cost = acc;
 }
 
 // ------------------------------------------------------------ K2b: point side
@@ -866,33 +889,57 @@ __device__ __forceinline__ void point_obs(const FrameDesc& F, const double* __re
   for (int c = 0; c < 3; c++) g[c] += J0[c] * rr0 + J1[c] * rr1;
 }
 
+// kLanesPerPoint lanes per point (each takes every kLanesPerPoint-th observation),
+// combined with two xor-shuffles. MODEL < 0: mixed camera models (runtime
+// dispatch per observation); otherwise the single model of the problem.
+constexpr int kLanesPerPoint = 4;
+
+template <int MODEL, int DEG>
 __global__ void __launch_bounds__(256) k_points_lin(
     const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, double* __restrict__ pgrad, double* __restrict__ phess,
     int32_t flags, double cauchy_c) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npts) return;
-  const double4 X = pts[p];
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = t / kLanesPerPoint;
+  const int sub = (int)(t % kLanesPerPoint);
+  const bool valid = p < npts;
   double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-  if (X.w != 0.0) {
-    for (int64_t j = pt_begin[p]; j < pt_begin[p + 1]; j++) {
+  const double4 X = valid ? pts[p] : make_double4(0, 0, 0, 0);
+  if (valid && X.w != 0.0) {
+    const int64_t jb = pt_begin[p], je = pt_begin[p + 1];
+    for (int64_t j = jb + sub; j < je; j += kLanesPerPoint) {
       const int32_t fr = po_frame[j];
       const FrameDesc& F = fd[fr];
       const double* rec = frec + (int64_t)fr * kFrameRecDoubles;
       const double2 m = po_meas[j];
-      const int K = F.K;
-      if (K == 0) point_obs<kModelNone, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
-      else if (K == 1) point_obs<kModelFov, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
-      else if (K == 4 || K == 5) point_obs<kModelRadtan, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
-      else if (K == 20) point_obs<kModelRpc, 1>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
-      else if (K == 44) point_obs<kModelRpc, 2>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
-      else if (K == 76) point_obs<kModelRpc, 3>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      if constexpr (MODEL >= 0) {
+        point_obs<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      } else {
+        const int K = F.K;
+        if (K == 0) point_obs<kModelNone, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 1) point_obs<kModelFov, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 4 || K == 5) point_obs<kModelRadtan, 0>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 20) point_obs<kModelRpc, 1>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 44) point_obs<kModelRpc, 2>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 76) point_obs<kModelRpc, 3>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+      }
     }
   }
-  for (int c = 0; c < 3; c++) pgrad[3 * p + c] = g[c];
-  for (int c = 0; c < 6; c++) phess[6 * p + c] = V[c];
+#pragma unroll
+  for (int off = 1; off < kLanesPerPoint; off <<= 1) {
+#pragma unroll
+    for (int c = 0; c < 6; c++) V[c] += __shfl_xor(V[c], off, 64);
+#pragma unroll
+    for (int c = 0; c < 3; c++) g[c] += __shfl_xor(g[c], off, 64);
+  }
+  if (!valid) return;
+  // lane `sub` writes entries sub, sub + 4, ... of the 9 outputs
+  for (int c = sub; c < 9; c += kLanesPerPoint) {
+    if (c < 3) pgrad[3 * p + c] = g[c];
+    else phess[6 * p + (c - 3)] = V[c - 3];
+  }
 }
 
 }  // namespace mvba
@@ -995,23 +1042,51 @@ hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchu
 
 hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16,
                               const mvba::FrameDesc* fd, const double* frec, const double* slab,
-                              double* grad, double* hess, double* cost, hipStream_t s) {
-  if (nframes <= 0) return hipSuccess;
-  const size_t lds = sizeof(double) * ((size_t)max_w16 * max_w16 + 1 + 2 * 6 * mvba::kPoseCols);
-  hipLaunchKernelGGL(mvba::k_expand, dim3((unsigned)nframes), dim3(64), lds, s,
-                     (const mvba::FrameLin*)fl, nframes, fd, frec, slab, grad, hess, cost);
+                              double* rep, int64_t ng, int64_t nh, double* grad, double* hess,
+                              double* cost, hipStream_t s) {
+  if (nframes > 0) {
+    const size_t lds = sizeof(double) * ((size_t)max_w16 * max_w16 + 1 + 2 * 6 * mvba::kPoseCols);
+    hipLaunchKernelGGL(mvba::k_expand, dim3((unsigned)nframes), dim3(64), lds, s,
+                       (const mvba::FrameLin*)fl, nframes, fd, frec, slab, rep, ng, nh);
+  }
+  const int64_t n = ng + nh + 1;
+  hipLaunchKernelGGL(mvba::k_rep_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rep, ng, nh,
+                     grad, hess, cost);
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_points_lin(const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
-                                  const double2* po_meas, const mvba::FrameDesc* fd,
-                                  const double* frec, const double* params, const double4* pts,
-                                  double* pgrad, double* phess, int32_t flags, double cauchy_c,
-                                  hipStream_t s) {
+int mvba_num_replicas(void) { return mvba::kReplicas; }
+
+// model < 0: mixed models (runtime dispatch).
+hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, int64_t npts,
+                                  const int32_t* po_frame, const double2* po_meas,
+                                  const mvba::FrameDesc* fd, const double* frec, const double* params,
+                                  const double4* pts, double* pgrad, double* phess, int32_t flags,
+                                  double cauchy_c, hipStream_t s) {
   if (npts <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_points_lin, dim3((unsigned)((npts + 255) / 256)), dim3(256), 0, s,
-                     pt_begin, npts, po_frame, po_meas, fd, frec, params, pts, pgrad, phess, flags,
-                     cauchy_c);
+  const unsigned blocks = (unsigned)((npts * mvba::kLanesPerPoint + 255) / 256);
+#define MVBA_PTS(M, D)                                                                                \
+  hipLaunchKernelGGL((mvba::k_points_lin<M, D>), dim3(blocks), dim3(256), 0, s, pt_begin, npts,      \
+                     po_frame, po_meas, fd, frec, params, pts, pgrad, phess, flags, cauchy_c)
+  if (model < 0) {
+    MVBA_PTS(-1, 0);
+  } else {
+    switch (model) {
+      case mvba::kModelNone: MVBA_PTS(mvba::kModelNone, 0); break;
+      case mvba::kModelFov: MVBA_PTS(mvba::kModelFov, 0); break;
+      case mvba::kModelRadtan: MVBA_PTS(mvba::kModelRadtan, 0); break;
+      case mvba::kModelRpc:
+        switch (deg) {
+          case 1: MVBA_PTS(mvba::kModelRpc, 1); break;
+          case 2: MVBA_PTS(mvba::kModelRpc, 2); break;
+          case 3: MVBA_PTS(mvba::kModelRpc, 3); break;
+          default: return hipErrorInvalidValue;
+        }
+        break;
+      default: return hipErrorInvalidValue;
+    }
+  }
+#undef MVBA_PTS
   return hipGetLastError();
 }
 
