@@ -241,6 +241,78 @@ int64_t mvba_num_points(const struct mvba_handle* h);
  * 16 (residual) + 16 * (written Jacobian columns). */
 double mvba_eval_bytes(const struct mvba_handle* h, int32_t flags);
 
+/* ---- Solver: GPU-resident Levenberg-Marquardt ----------------------------
+ * Replaces ceres::Solve(options, &problem, &summary) of rig_calibrator.cc:1910-1919
+ * (linear_solver_type = ITERATIVE_SCHUR, gradient/function tolerance 1e-16,
+ * parameter_tolerance = FLAGS_parameter_tolerance, max_num_iterations =
+ * FLAGS_num_iterations) for a problem made of BracketedCamError blocks.
+ * Trust-region LM with Ceres 1.14's step control, Jacobi column scaling and
+ * stopping rules [ext]; the reduced camera system is solved matrix-free by
+ * preconditioned CG on the implicit Schur complement (points eliminated).
+ * The solution is left in the handle's parameters (mvba_get_params).
+ *
+ * Sharded solves: each rank's handle holds all camera-side
+ * blocks and the observations of its landmark range; `allreduce` (non-null)
+ * is called with an in-place device buffer to sum (op MVBA_REDUCE_SUM) or max
+ * (MVBA_REDUCE_MAX) across ranks. The library synchronises its stream before
+ * the call; the callback must return with the result in the buffer (e.g.
+ * ncclAllReduce + stream sync, or torch.distributed.all_reduce). It is called
+ * once per linearization (camera gradient + block Hessians + cost), once per
+ * CG iteration (the reduced-system product) and for a few scalars per step. */
+enum { MVBA_REDUCE_SUM = 0, MVBA_REDUCE_MAX = 1 };
+typedef int32_t (*mvba_allreduce_fn)(double* device_buf, int64_t count, int32_t op, void* hip_stream,
+                                     void* user);
+
+enum { MVBA_CONVERGENCE = 0, MVBA_NO_CONVERGENCE = 1, MVBA_FAILURE = 2 };
+
+typedef struct mvba_solver_options {
+  int32_t max_num_iterations;          /* Solver::Options default 50; rig_calibrator passes its flag */
+  double function_tolerance;           /* 1e-16 in rig_calibrator (:1916) */
+  double gradient_tolerance;           /* 1e-16 (:1915) */
+  double parameter_tolerance;          /* FLAGS_parameter_tolerance (:1917) */
+  double initial_trust_region_radius;  /* 1e4 */
+  double max_trust_region_radius;      /* 1e16 */
+  double min_trust_region_radius;      /* 1e-32 */
+  double min_lm_diagonal;              /* 1e-6 */
+  double max_lm_diagonal;              /* 1e32 */
+  double min_relative_decrease;        /* 1e-3 */
+  double eta;                          /* 0.1: CG q-criterion tolerance */
+  int32_t min_linear_solver_iterations; /* 0 */
+  int32_t max_linear_solver_iterations; /* 500 */
+  int32_t max_num_consecutive_invalid_steps; /* 5 */
+  int32_t jacobi_scaling;              /* 1 */
+  int32_t use_loss;                    /* Cauchy loss on every residual block */
+  double robust_threshold;             /* CauchyLoss(robust_threshold) (rig_calibrator.cc:394-411) */
+  const double* lower_bounds;          /* host, [num_param_doubles] or NULL (-inf) */
+  const double* upper_bounds;          /* host, [num_param_doubles] or NULL (+inf) */
+  int32_t progress_to_stdout;          /* minimizer_progress_to_stdout (:1914) */
+  mvba_allreduce_fn allreduce;         /* NULL: single rank */
+  void* allreduce_user;
+} mvba_solver_options;
+
+typedef struct mvba_solver_summary {
+  double initial_cost;
+  double final_cost;
+  int32_t num_iterations;              /* LM iterations after iteration 0 */
+  int32_t num_successful_steps;
+  int32_t num_unsuccessful_steps;
+  int32_t num_linear_iterations;       /* total CG iterations */
+  int32_t termination_type;            /* MVBA_CONVERGENCE / NO_CONVERGENCE / FAILURE */
+  int32_t pad;
+  double total_time_s;
+  double linearize_time_s;             /* Jacobian / normal equations (incl. exchange) */
+  double linear_solver_time_s;         /* CG + back-substitution */
+  double eval_time_s;                  /* candidate-point cost evaluations */
+  char message[256];
+} mvba_solver_summary;
+
+void mvba_solver_default_options(mvba_solver_options* o);
+/* Runs LM from the handle's current parameters (mvba_set_params first). */
+mvba_status mvba_solve(struct mvba_handle* h, const mvba_solver_options* o, mvba_solver_summary* summary,
+                       void* hip_stream);
+/* Copy the handle's current packed parameter vector to host memory. */
+mvba_status mvba_get_params(struct mvba_handle* h, double* packed);
+
 #ifdef __cplusplus
 }
 #endif

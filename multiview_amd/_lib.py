@@ -92,6 +92,58 @@ class LinLayout(C.Structure):
     ]
 
 
+REDUCE_SUM, REDUCE_MAX = 0, 1
+CONVERGENCE, NO_CONVERGENCE, FAILURE = 0, 1, 2
+
+# int32_t (*)(double* device_buf, int64_t count, int32_t op, void* stream, void* user)
+AllreduceFn = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p)
+
+
+class SolverOptions(C.Structure):
+    _fields_ = [
+        ("max_num_iterations", C.c_int32),
+        ("function_tolerance", C.c_double),
+        ("gradient_tolerance", C.c_double),
+        ("parameter_tolerance", C.c_double),
+        ("initial_trust_region_radius", C.c_double),
+        ("max_trust_region_radius", C.c_double),
+        ("min_trust_region_radius", C.c_double),
+        ("min_lm_diagonal", C.c_double),
+        ("max_lm_diagonal", C.c_double),
+        ("min_relative_decrease", C.c_double),
+        ("eta", C.c_double),
+        ("min_linear_solver_iterations", C.c_int32),
+        ("max_linear_solver_iterations", C.c_int32),
+        ("max_num_consecutive_invalid_steps", C.c_int32),
+        ("jacobi_scaling", C.c_int32),
+        ("use_loss", C.c_int32),
+        ("robust_threshold", C.c_double),
+        ("lower_bounds", C.c_void_p),
+        ("upper_bounds", C.c_void_p),
+        ("progress_to_stdout", C.c_int32),
+        ("allreduce", AllreduceFn),
+        ("allreduce_user", C.c_void_p),
+    ]
+
+
+class SolverSummary(C.Structure):
+    _fields_ = [
+        ("initial_cost", C.c_double),
+        ("final_cost", C.c_double),
+        ("num_iterations", C.c_int32),
+        ("num_successful_steps", C.c_int32),
+        ("num_unsuccessful_steps", C.c_int32),
+        ("num_linear_iterations", C.c_int32),
+        ("termination_type", C.c_int32),
+        ("pad", C.c_int32),
+        ("total_time_s", C.c_double),
+        ("linearize_time_s", C.c_double),
+        ("linear_solver_time_s", C.c_double),
+        ("eval_time_s", C.c_double),
+        ("message", C.c_char * 256),
+    ]
+
+
 # Every symbol include/mvba/mvba.h declares, with (restype, argtypes).
 SIGNATURES = {
     "mvba_abi_version": (C.c_int, []),
@@ -119,6 +171,9 @@ SIGNATURES = {
     "mvba_point_block_map": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mvba_linearize_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
+    "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),
+    "mvba_get_params": (C.c_int, [C.c_void_p, C.c_void_p]),
 }
 
 _lib = None

@@ -1,0 +1,329 @@
+// mvba_device.h — device-side math shared by the evaluator kernels
+// (mvba_kernels.hip) and the solver kernels (mvba_solver.hip).
+#ifndef MVBA_DEVICE_H_
+#define MVBA_DEVICE_H_
+
+#include <hip/hip_runtime.h>
+#include <cfloat>
+#include <cstdint>
+
+#include "mvba_types.h"
+#include "../../include/mvba/mvba.h"
+
+namespace mvba {
+
+
+// ------------------------------------------------------------ small helpers
+__device__ __forceinline__ void quat_to_rot(double x, double y, double z, double w, double* R) {
+  // Eigen QuaternionBase::toRotationMatrix [ext], no normalisation.
+  const double tx = 2.0 * x, ty = 2.0 * y, tz = 2.0 * z;
+  const double twx = tx * w, twy = ty * w, twz = tz * w;
+  const double txx = tx * x, txy = ty * x, txz = tz * x;
+  const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+  R[0] = 1.0 - (tyy + tzz); R[1] = txy - twz;         R[2] = txz + twy;
+  R[3] = txy + twz;         R[4] = 1.0 - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
+}
+
+// Eigen Quaternion(Matrix3d) [ext]: Shepperd's method. q = (x, y, z, w).
+// Written with constant indices only (no scratch memory).
+__device__ __forceinline__ void rot_to_quat(const double* m, double* q) {
+  double t = m[0] + m[4] + m[8];
+  if (t > 0.0) {
+    t = sqrt(t + 1.0);
+    q[3] = 0.5 * t;
+    t = 0.5 / t;
+    q[0] = (m[7] - m[5]) * t;
+    q[1] = (m[2] - m[6]) * t;
+    q[2] = (m[3] - m[1]) * t;
+    return;
+  }
+  int i = 0;
+  if (m[4] > m[0]) i = 1;
+  if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
+  if (i == 0) {  // j = 1, k = 2
+    t = sqrt(m[0] - m[4] - m[8] + 1.0);
+    q[0] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[7] - m[5]) * t;
+    q[1] = (m[3] + m[1]) * t;
+    q[2] = (m[6] + m[2]) * t;
+  } else if (i == 1) {  // j = 2, k = 0
+    t = sqrt(m[4] - m[8] - m[0] + 1.0);
+    q[1] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[2] - m[6]) * t;
+    q[2] = (m[7] + m[5]) * t;
+    q[0] = (m[1] + m[3]) * t;
+  } else {  // i = 2, j = 0, k = 1
+    t = sqrt(m[8] - m[0] - m[4] + 1.0);
+    q[2] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[3] - m[1]) * t;
+    q[0] = (m[2] + m[6]) * t;
+    q[1] = (m[5] + m[7]) * t;
+  }
+}
+
+// array_to_rigid_transform (dense_map_utils.cc:171-178): normalised quaternion,
+// its rotation and 1/|q| (for the derivative through normalize()).
+__device__ __forceinline__ void rigid(const double* p, double* R, double* qh, double* inv_norm) {
+  double x = p[3], y = p[4], z = p[5], w = p[6];
+  const double n2 = x * x + y * y + z * z + w * w;
+  double in = 1.0;
+  if (n2 > 0.0) {
+    const double n = sqrt(n2);
+    x /= n; y /= n; z /= n; w /= n;
+    in = 1.0 / n;
+  }
+  qh[0] = x; qh[1] = y; qh[2] = z; qh[3] = w;
+  *inv_norm = in;
+  quat_to_rot(x, y, z, w, R);
+}
+
+// Left generator of d R(q/|q|) / d q_raw[k]:  omega = (2/|q|) vec(e_k (x) q^*).
+__device__ __forceinline__ void quat_generator(const double* qh, double s, int k, double* om) {
+  const double vx = qh[0], vy = qh[1], vz = qh[2], w = qh[3];
+  switch (k) {
+    case 0: om[0] = s * w;   om[1] = s * vz;  om[2] = -s * vy; break;
+    case 1: om[0] = -s * vz; om[1] = s * w;   om[2] = s * vx;  break;
+    case 2: om[0] = s * vy;  om[1] = -s * vx; om[2] = s * w;   break;
+    default: om[0] = -s * vx; om[1] = -s * vy; om[2] = -s * vz; break;
+  }
+}
+
+// omega for a tangent perturbation dq of the (unit) quaternion q:
+// 2 vec(dq (x) q^*) = 2 (q_w dq_v - dq_w q_v - dq_v x q_v).
+__device__ __forceinline__ void tangent_generator(const double* dq, const double* q, double* om) {
+  const double cx = dq[1] * q[2] - dq[2] * q[1];
+  const double cy = dq[2] * q[0] - dq[0] * q[2];
+  const double cz = dq[0] * q[1] - dq[1] * q[0];
+  om[0] = 2.0 * (q[3] * dq[0] - dq[3] * q[0] - cx);
+  om[1] = 2.0 * (q[3] * dq[1] - dq[3] * q[1] - cy);
+  om[2] = 2.0 * (q[3] * dq[2] - dq[3] * q[2] - cz);
+}
+
+__device__ __forceinline__ void matvec(const double* R, const double* a, double* b) {
+  b[0] = R[0] * a[0] + R[1] * a[1] + R[2] * a[2];
+  b[1] = R[3] * a[0] + R[4] * a[1] + R[5] * a[2];
+  b[2] = R[6] * a[0] + R[7] * a[1] + R[8] * a[2];
+}
+
+__device__ __forceinline__ void cross(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Write one pose column record: omega, v = dt - omega x t.
+__device__ __forceinline__ void put_col(double* rec, int k, const double* om, const double* dt,
+                                        const double* t) {
+  double c[3];
+  cross(om, t, c);
+  double* o = rec + 12 + 6 * k;
+  o[0] = om[0]; o[1] = om[1]; o[2] = om[2];
+  o[3] = dt[0] - c[0]; o[4] = dt[1] - c[1]; o[5] = dt[2] - c[2];
+}
+
+// ------------------------------------------------------------ observation model
+// Projection + distortion of one observation (rig_calibrator.cc:470-479,
+// camera_params.cc:260-314, rpc_distortion.cc:116-160) with the pieces of its
+// analytic derivative that every consumer needs.
+struct Proj {
+  double Xc[3];
+  double nx, ny;           // hnormalized(Xc)
+  double u0, u1;           // f * (nx, ny): centred undistorted pixel
+  double d0, d1;           // distorted pixel (half size added back)
+  double A00, A01, A10, A11;  // d(d)/d(u)
+  double df0, df1;         // total d(d)/d(f)
+  double m0, m1, r2;       // FOV / RADTAN: u / f, |u/f|^2
+  double aux0, aux1, aux2, aux3;  // FOV: f dconv/dw; RPC: 1/Dx, 1/Dy, Nx/Dx, Ny/Dy
+};
+
+template <int MODEL, int DEG>
+__device__ __forceinline__ void project(const double* __restrict__ rec, double X0, double X1, double X2,
+                                        double f, double c0, double c1, const double* __restrict__ kd,
+                                        int K, double h0, double h1, Proj& o) {
+  // X = world_to_cam * X (rig_calibrator.cc:470)
+  o.Xc[0] = rec[0] * X0 + rec[1] * X1 + rec[2] * X2 + rec[9];
+  o.Xc[1] = rec[3] * X0 + rec[4] * X1 + rec[5] * X2 + rec[10];
+  o.Xc[2] = rec[6] * X0 + rec[7] * X1 + rec[8] * X2 + rec[11];
+  // u = f .* X.hnormalized() (:473)
+  o.nx = o.Xc[0] / o.Xc[2];
+  o.ny = o.Xc[1] / o.Xc[2];
+  const double u0 = f * o.nx, u1 = f * o.ny;
+  o.u0 = u0;
+  o.u1 = u1;
+  o.m0 = o.m1 = o.r2 = 0.0;
+  o.aux0 = o.aux1 = o.aux2 = o.aux3 = 0.0;
+  if constexpr (MODEL == kModelNone) {
+    // camera_params.cc:268 then + half size (:414)
+    o.d0 = ((u0 + c0) - h0) + h0;
+    o.d1 = ((u1 + c1) - h1) + h1;
+    o.A00 = 1.0; o.A01 = 0.0; o.A10 = 0.0; o.A11 = 1.0;
+    o.df0 = o.nx; o.df1 = o.ny;
+  } else if constexpr (MODEL == kModelFov) {
+    // camera_params.cc:269-281, precalcs :185-190
+    const double w = kd[0];
+    const double tw2 = tan(0.5 * w);
+    const double pc1 = 1.0 / w, pc2 = 2.0 * tw2;
+    const double m0 = u0 / f, m1 = u1 / f;
+    const double ru = sqrt(m0 * m0 + m1 * m1);
+    const double a = ru * pc2;
+    const double at = atan(a);
+    const double rd = at * pc1;
+    double conv = 1.0, dconv_dru = 0.0, dconv_dw = 0.0;
+    if (ru > 1e-5) {
+      conv = rd / ru;
+      const double den = 1.0 / (1.0 + a * a);
+      dconv_dru = (pc1 * pc2 * den - conv) / ru;
+      dconv_dw = (ru * pc1 * (1.0 + tw2 * tw2) * den - at / (w * w)) / ru;
+    }
+    o.d0 = ((c0 - h0) + conv * (m0 * f)) + h0;
+    o.d1 = ((c1 - h1) + conv * (m1 * f)) + h1;
+    const double g = (ru > 1e-5) ? dconv_dru / ru : 0.0;
+    o.A00 = conv + g * m0 * m0; o.A01 = g * m0 * m1;
+    o.A10 = g * m1 * m0;        o.A11 = conv + g * m1 * m1;
+    o.df0 = conv * m0; o.df1 = conv * m1;
+    o.m0 = m0; o.m1 = m1;
+    o.aux0 = f * dconv_dw;
+  } else if constexpr (MODEL == kModelRadtan) {
+    // camera_params.cc:282-308 (Tsai)
+    const double k1 = kd[0], k2 = kd[1], p1 = kd[2], p2 = kd[3];
+    const double k3 = (K == 5) ? kd[4] : 0.0;
+    const double m0 = u0 / f, m1 = u1 / f;
+    const double r2 = m0 * m0 + m1 * m1;
+    const double radial = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2;
+    double e0 = radial * m0, e1 = radial * m1;
+    e0 += 2.0 * p1 * m0 * m1 + p2 * (r2 + 2.0 * m0 * m0);
+    e1 += p1 * (r2 + 2.0 * m1 * m1) + 2.0 * p2 * m0 * m1;
+    o.d0 = (e0 * f + (c0 - h0)) + h0;
+    o.d1 = (e1 * f + (c1 - h1)) + h1;
+    const double drad = k1 + 2.0 * k2 * r2 + 3.0 * k3 * r2 * r2;
+    const double cross_t = 2.0 * drad * m0 * m1 + 2.0 * p1 * m0 + 2.0 * p2 * m1;
+    o.A00 = radial + 2.0 * drad * m0 * m0 + 2.0 * p1 * m1 + 6.0 * p2 * m0;
+    o.A01 = cross_t;
+    o.A10 = cross_t;
+    o.A11 = radial + 2.0 * drad * m1 * m1 + 6.0 * p1 * m1 + 2.0 * p2 * m0;
+    o.df0 = e0; o.df1 = e1;
+    o.m0 = m0; o.m1 = m1; o.r2 = r2;
+  } else {
+    // RPC of degree DEG (rpc_distortion.cc:116-160); coefficients
+    // [num_x(nl) | den_x(nl-1) | num_y(nl) | den_y(nl-1)], nl = (D+1)(D+2)/2.
+    double px[DEG + 1], py[DEG + 1];
+    double vx = 1.0, vy = 1.0;
+#pragma unroll
+    for (int k = 0; k <= DEG; k++) {
+      px[k] = vx; vx *= u0;
+      py[k] = vy; vy *= u1;
+    }
+    double N[4] = {0.0, 1.0, 0.0, 1.0};  // Nx, Dx, Ny, Dy
+    double Nx_[4] = {0.0, 0.0, 0.0, 0.0}, Ny_[4] = {0.0, 0.0, 0.0, 0.0};
+    int ci = 0;
+#pragma unroll
+    for (int cnt = 0; cnt < 4; cnt++) {
+      const int start = (cnt & 1);
+#pragma unroll
+      for (int dg = start; dg <= DEG; dg++) {
+#pragma unroll
+        for (int q = 0; q <= dg; q++) {
+          const double a = kd[ci];
+          N[cnt] += a * px[dg - q] * py[q];
+          if (dg - q > 0) Nx_[cnt] += a * (double)(dg - q) * px[dg - q - 1] * py[q];
+          if (q > 0) Ny_[cnt] += a * (double)q * px[dg - q] * py[q - 1];
+          ci++;
+        }
+      }
+    }
+    o.d0 = N[0] / N[1] + h0;
+    o.d1 = N[2] / N[3] + h1;
+    const double iDx = 1.0 / N[1], iDy = 1.0 / N[3];
+    const double qx = N[0] * iDx, qy = N[2] * iDy;
+    o.A00 = (Nx_[0] - qx * Nx_[1]) * iDx; o.A01 = (Ny_[0] - qx * Ny_[1]) * iDx;
+    o.A10 = (Nx_[2] - qy * Nx_[3]) * iDy; o.A11 = (Ny_[2] - qy * Ny_[3]) * iDy;
+    o.df0 = o.A00 * o.nx + o.A01 * o.ny;
+    o.df1 = o.A10 * o.nx + o.A11 * o.ny;
+    o.aux0 = iDx; o.aux1 = iDy; o.aux2 = qx; o.aux3 = qy;
+  }
+}
+
+// Number of distortion columns that can be non-zero (RPC: the undistortion
+// half is structurally zero).
+template <int MODEL, int DEG>
+__host__ __device__ constexpr int live_dist_cols(int K) {
+  return MODEL == kModelRpc ? 2 * ((DEG + 1) * (DEG + 2)) - 2 : (MODEL == kModelNone ? 0 : K);
+}
+
+// Distortion block columns of one observation, emitted as emit(c, v_row0, v_row1)
+// for c < live_dist_cols (scaled by s = fs or the loss factor).
+template <int MODEL, int DEG, class Emit>
+__device__ __forceinline__ void dist_columns(const Proj& o, double f, int K, double s, Emit&& emit) {
+  if constexpr (MODEL == kModelFov) {
+    emit(0, o.m0 * o.aux0 * s, o.m1 * o.aux0 * s);
+  } else if constexpr (MODEL == kModelRadtan) {
+    const double fs = f * s;
+    const double m0 = o.m0, m1 = o.m1, r2 = o.r2, r4 = r2 * r2;
+    emit(0, fs * r2 * m0, fs * r2 * m1);
+    emit(1, fs * r4 * m0, fs * r4 * m1);
+    emit(2, fs * 2.0 * m0 * m1, fs * (r2 + 2.0 * m1 * m1));
+    emit(3, fs * (r2 + 2.0 * m0 * m0), fs * 2.0 * m0 * m1);
+    if (K == 5) emit(4, fs * r4 * r2 * m0, fs * r4 * r2 * m1);
+  } else if constexpr (MODEL == kModelRpc) {
+    double px[DEG + 1], py[DEG + 1];
+    double vx = 1.0, vy = 1.0;
+#pragma unroll
+    for (int k = 0; k <= DEG; k++) {
+      px[k] = vx; vx *= o.u0;
+      py[k] = vy; vy *= o.u1;
+    }
+    const double iDx = o.aux0 * s, iDy = o.aux1 * s;
+    const double mqx = -o.aux2 * iDx, mqy = -o.aux3 * iDy;  // -(N/D)/D
+    int ci = 0;
+#pragma unroll
+    for (int cnt = 0; cnt < 4; cnt++) {
+      const int start = (cnt & 1);
+      const double sc = (cnt == 0) ? iDx : (cnt == 1) ? mqx : (cnt == 2) ? iDy : mqy;
+#pragma unroll
+      for (int dg = start; dg <= DEG; dg++) {
+#pragma unroll
+        for (int q = 0; q <= dg; q++) {
+          const double v = sc * px[dg - q] * py[q];
+          if (cnt < 2) emit(ci, v, 0.0);
+          else emit(ci, 0.0, v);
+          ci++;
+        }
+      }
+    }
+  }
+  (void)f; (void)K; (void)o; (void)s;
+}
+
+__device__ __forceinline__ double loss_scale(double r0, double r1, int32_t flags, double cauchy_c,
+                                             double* half_rho) {
+  const double s = r0 * r0 + r1 * r1;
+  if (flags & MVBA_EVAL_APPLY_LOSS) {
+    // Ceres 1.14 CauchyLoss + Corrector [ext]: scale by sqrt(rho'), rho = b log(1 + s c).
+    const double sum = 1.0 + s * cauchy_c;
+    *half_rho = 0.5 * (log(sum) / cauchy_c);
+    return sqrt(fmax(DBL_MIN, 1.0 / sum));
+  }
+  *half_rho = 0.5 * s;
+  return 1.0;
+}
+
+// Per-frame record of the linearization (K2 expand), see mvba_kernels.hip.
+struct FrameLin {
+  int64_t slab_off;                  // offset (doubles) of this frame's first chunk slab
+  int32_t chunk_count;               // consecutive chunk slabs of w16*w16+1 doubles
+  int32_t width, w16;                // Gram width and padded width
+  int32_t first_chunk;               // global index of the frame's first chunk
+  int64_t goff[8];                   // camera-side gradient offsets per block (-1: constant/none)
+  int64_t hoff[8];                   // camera-side Hessian offsets per block
+};
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+typedef double dbl2v __attribute__((ext_vector_type(2)));
+
+}  // namespace mvba
+
+#endif  // MVBA_DEVICE_H_

@@ -23,153 +23,20 @@
 #include <unordered_map>
 #include <vector>
 
-#include "../../include/mvba/mvba.h"
-#include "mvba_types.h"
-
-using mvba::FrameDesc;
-using mvba::Segment;
-
-extern "C" {
-hipError_t mvba_launch_prep(const FrameDesc* fd, int64_t nframes, const double* params,
-                            double* frec, const int64_t* pt_off, const uint8_t* pt_free, int64_t npts,
-                            double4* pts, int gen, int* err, hipStream_t s);
-int mvba_gram_width(int model, int deg);
-size_t mvba_frame_lin_size(void);
-hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchunks, const Segment* segs,
-                            const FrameDesc* fd, const double* frec, const double* params,
-                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
-                            double* slab, int32_t flags, double cauchy_c, hipStream_t s);
-hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16, const FrameDesc* fd,
-                              const double* frec, const double* slab, double* rep, int64_t ng, int64_t nh,
-                              double* grad, double* hess, double* cost, hipStream_t s);
-int mvba_num_replicas(void);
-hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, int64_t npts,
-                                  const int32_t* po_frame, const double2* po_meas, const FrameDesc* fd,
-                                  const double* frec, const double* params, const double4* pts,
-                                  double* pgrad, double* phess, int32_t flags, double cauchy_c,
-                                  hipStream_t s);
-hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
-                           const FrameDesc* fd, const double* frec, const double* params,
-                           const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
-                           double* res, double* J, int64_t ld, int32_t flags, double cauchy_c,
-                           hipStream_t s);
-}
+#include "mvba_internal.h"
 
 namespace {
-
 thread_local std::string g_create_error;
-
-constexpr int kFixedSize[7] = {7, 7, 7, 3, 1, 1, 2};
-
-int rpc_degree(int n) { return static_cast<int>(std::round(std::sqrt(2.0 * n + 5.0) / 2.0 - 1.5)); }
-int rpc_num_dist_params(int d) { return 2 * (d + 1) * (d + 2) - 2; }
-
-// camera_params.cc:169-208 / rpc_distortion.cc:53-57 size rules.
-// Returns model kind, or -1 if SetDistortion would LOG(FATAL).
-int model_of(int K, int* deg) {
-  *deg = 0;
-  if (K == 0) return mvba::kModelNone;
-  if (K == 1) return mvba::kModelFov;
-  if (K == 4 || K == 5) return mvba::kModelRadtan;
-  if (K % 2 != 0) return -1;
-  const int n = K / 2;
-  const int d = rpc_degree(n);
-  if (rpc_num_dist_params(d) != n || d <= 0) return -1;
-  *deg = d;
-  return mvba::kModelRpc;
-}
-
-struct Group {
-  int model = 0, deg = 0;
-  int32_t seg_begin = 0, seg_count = 0;
-  int64_t res_begin = 0, res_count = 0;
-  // linearization (K2): chunks of <= 4 segments of one frame, slab per chunk
-  int32_t chunk_begin = 0, chunk_count = 0;
-  int64_t slab_base = 0;
-  int32_t gram_width = 0, w16 = 0;
-};
-
-template <class T>
-hipError_t dalloc(T** p, size_t n) {
-  *p = nullptr;
-  if (n == 0) n = 1;
-  return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
-}
-
-template <class T>
-hipError_t upload(T** p, const std::vector<T>& v) {
-  hipError_t e = dalloc(p, v.size());
-  if (e != hipSuccess) return e;
-  if (v.empty()) return hipSuccess;
-  return hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
-}
-
 }  // namespace
-
-struct mvba_handle {
-  int device = 0;
-  std::string err;
-  int64_t nres = 0, nslots = 0, nframes = 0, npts = 0, nparams = 0;
-  int kmax = 0, jac_rows = 0;
-  std::vector<int64_t> order;        // device slot -> insertion index (-1 = padding)
-  std::vector<uint8_t> row_written;  // device position -> block bitmask
-  std::vector<int16_t> pos_K;        // device position -> distortion length
-  std::vector<Group> groups;
-  double bytes_res = 0.0, bytes_jac = 0.0;
-
-  double* d_params = nullptr;
-  FrameDesc* d_fd = nullptr;
-  double* d_frec = nullptr;
-  int64_t* d_pt_off = nullptr;
-  uint8_t* d_pt_free = nullptr;
-  double4* d_pts = nullptr;
-  int32_t* d_obs_pid = nullptr;
-  double2* d_obs_meas = nullptr;
-  Segment* d_segs = nullptr;
-  int64_t* d_order = nullptr;
-  uint8_t* d_row_written = nullptr;
-  int* d_err = nullptr;
-  double* d_res = nullptr;  // library-owned outputs, allocated lazily
-  double* d_J = nullptr;
-  int64_t ld = 0;
-  bool params_set = false;
-  bool prep_done = false;
-  int gen = 0;  // generation of the last prep launch (error word protocol)
-
-  std::vector<double> h_res, h_J;  // host staging for mvba_evaluate
-
-  // linearization (K2): camera-side compact layout, chunks, point CSR
-  bool lin_ok = false;
-  std::string lin_err;
-  int64_t cam_grad_size = 0, cam_hess_size = 0, slab_size = 0;
-  int32_t max_w16 = 0;
-  std::vector<int32_t> cam_block_ids;   // camera-side blocks in block-id order
-  std::vector<int64_t> cam_goff, cam_hoff;
-  std::vector<int32_t> pt_block_ids;    // point index -> block id
-  int4* d_chunks = nullptr;
-  void* d_frame_lin = nullptr;
-  double* d_slab = nullptr;
-  double* d_rep = nullptr;  // kReplicas copies of [cam_grad | cam_hess | cost], kept zero between calls
-  int64_t* d_pt_begin = nullptr;
-  int32_t* d_po_frame = nullptr;
-  double2* d_po_meas = nullptr;
-
-  mvba_status fail(mvba_status st, const std::string& msg) {
-    err = msg;
-    return st;
-  }
-  mvba_status hip_fail(hipError_t e, const char* where) {
-    err = std::string("HIP error in ") + where + ": " + hipGetErrorString(e);
-    return MVBA_E_HIP;
-  }
-};
 
 static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
-                  h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas};
+                  h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po};
+  solver_state_free(h->solver);
+  h->solver = nullptr;
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -454,6 +321,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   std::vector<int64_t> pt_begin;
   std::vector<int32_t> po_frame;
   std::vector<double2> po_meas;
+  std::vector<int32_t> slot_po;
   {
     h->lin_ok = true;
     for (const Group& G : h->groups)
@@ -477,6 +345,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       h->cam_hoff.push_back(h->cam_hess_size);
       h->cam_grad_size += sz;
       h->cam_hess_size += sz * sz;
+      for (int64_t q = 0; q < sz; q++) h->cam_poff.push_back(d->block_offset[b] + q);
     }
     int64_t slab_base = 0;
     for (Group& G : h->groups) {
@@ -498,7 +367,10 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
           c.w = local++;
           chunks.push_back(c);
           mvba::FrameLinHost& L = flin[sg.frame];
-          if (L.chunk_count == 0) L.slab_off = slab_base + (int64_t)c.w * SL;
+          if (L.chunk_count == 0) {
+            L.slab_off = slab_base + (int64_t)c.w * SL;
+            L.first_chunk = (int32_t)chunks.size() - 1;
+          }
           L.chunk_count++;
           L.width = G.gram_width;
           L.w16 = G.w16;
@@ -525,11 +397,17 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     po_frame.resize(N);
     po_meas.resize(N);
     std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+    std::vector<int32_t> po_of(N);
     for (int64_t i = 0; i < N; i++) {
       const int64_t j = fill[res_pt[i]]++;
+      po_of[i] = (int32_t)j;
       po_frame[j] = res_frame[i];
       po_meas[j] = make_double2(d->residual_meas[2 * i], d->residual_meas[2 * i + 1]);
     }
+    slot_po.assign(nslots, -1);
+    for (int64_t p = 0; p < nslots; p++)
+      if (h->order[p] >= 0) slot_po[p] = po_of[h->order[p]];
+    h->nchunks = (int32_t)chunks.size();
   }
 
   // ---- upload
@@ -567,6 +445,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_pt_begin, pt_begin));
   chk(upload(&h->d_po_frame, po_frame));
   chk(upload(&h->d_po_meas, po_meas));
+  chk(upload(&h->d_slot_po, slot_po));
   if (e != hipSuccess) {
     g_create_error = std::string("HIP error during mvba_create: ") + hipGetErrorString(e);
     free_all(h);

@@ -1,0 +1,165 @@
+// mvba_internal.h — handle layout shared by the host-side translation units
+// (mvba_host.cpp: problem compilation + evaluation; mvba_solve.cpp: the LM driver).
+// Not part of the public ABI.
+#ifndef MVBA_INTERNAL_H_
+#define MVBA_INTERNAL_H_
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/mvba/mvba.h"
+#include "mvba_types.h"
+
+using mvba::FrameDesc;
+using mvba::Segment;
+
+struct SolverState;  // mvba_solve.cpp
+void solver_state_free(SolverState* s);
+
+extern "C" {
+hipError_t mvba_launch_prep(const FrameDesc* fd, int64_t nframes, const double* params,
+                            double* frec, const int64_t* pt_off, const uint8_t* pt_free, int64_t npts,
+                            double4* pts, int gen, int* err, hipStream_t s);
+int mvba_gram_width(int model, int deg);
+size_t mvba_frame_lin_size(void);
+hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchunks, const Segment* segs,
+                            const FrameDesc* fd, const double* frec, const double* params,
+                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                            double* slab, int32_t flags, double cauchy_c, hipStream_t s);
+hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16, const FrameDesc* fd,
+                              const double* frec, const double* slab, double* rep, int64_t ng, int64_t nh,
+                              double* grad, double* hess, double* cost, hipStream_t s);
+int mvba_num_replicas(void);
+hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, int64_t npts,
+                                  const int32_t* po_frame, const double2* po_meas, const FrameDesc* fd,
+                                  const double* frec, const double* params, const double4* pts,
+                                  double* pgrad, double* phess, int32_t flags, double cauchy_c,
+                                  hipStream_t s);
+hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
+                           const FrameDesc* fd, const double* frec, const double* params,
+                           const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                           double* res, double* J, int64_t ld, int32_t flags, double cauchy_c,
+                           hipStream_t s);
+}
+
+namespace mvba_internal {
+
+constexpr int kFixedSize[7] = {7, 7, 7, 3, 1, 1, 2};
+
+inline int rpc_degree(int n) { return static_cast<int>(std::round(std::sqrt(2.0 * n + 5.0) / 2.0 - 1.5)); }
+inline int rpc_num_dist_params(int d) { return 2 * (d + 1) * (d + 2) - 2; }
+
+// camera_params.cc:169-208 / rpc_distortion.cc:53-57 size rules.
+// Returns model kind, or -1 if SetDistortion would LOG(FATAL).
+inline int model_of(int K, int* deg) {
+  *deg = 0;
+  if (K == 0) return mvba::kModelNone;
+  if (K == 1) return mvba::kModelFov;
+  if (K == 4 || K == 5) return mvba::kModelRadtan;
+  if (K % 2 != 0) return -1;
+  const int n = K / 2;
+  const int d = rpc_degree(n);
+  if (rpc_num_dist_params(d) != n || d <= 0) return -1;
+  *deg = d;
+  return mvba::kModelRpc;
+}
+
+struct Group {
+  int model = 0, deg = 0;
+  int32_t seg_begin = 0, seg_count = 0;
+  int64_t res_begin = 0, res_count = 0;
+  // linearization (K2): chunks of <= 4 segments of one frame, slab per chunk
+  int32_t chunk_begin = 0, chunk_count = 0;
+  int64_t slab_base = 0;
+  int32_t gram_width = 0, w16 = 0;
+};
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+}
+
+template <class T>
+hipError_t upload(T** p, const std::vector<T>& v) {
+  hipError_t e = dalloc(p, v.size());
+  if (e != hipSuccess) return e;
+  if (v.empty()) return hipSuccess;
+  return hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+}  // namespace mvba_internal
+
+using namespace mvba_internal;
+
+struct mvba_handle {
+  int device = 0;
+  std::string err;
+  int64_t nres = 0, nslots = 0, nframes = 0, npts = 0, nparams = 0;
+  int kmax = 0, jac_rows = 0;
+  std::vector<int64_t> order;        // device slot -> insertion index (-1 = padding)
+  std::vector<uint8_t> row_written;  // device position -> block bitmask
+  std::vector<int16_t> pos_K;        // device position -> distortion length
+  std::vector<Group> groups;
+  double bytes_res = 0.0, bytes_jac = 0.0;
+
+  double* d_params = nullptr;
+  FrameDesc* d_fd = nullptr;
+  double* d_frec = nullptr;
+  int64_t* d_pt_off = nullptr;
+  uint8_t* d_pt_free = nullptr;
+  double4* d_pts = nullptr;
+  int32_t* d_obs_pid = nullptr;
+  double2* d_obs_meas = nullptr;
+  Segment* d_segs = nullptr;
+  int64_t* d_order = nullptr;
+  uint8_t* d_row_written = nullptr;
+  int* d_err = nullptr;
+  double* d_res = nullptr;  // library-owned outputs, allocated lazily
+  double* d_J = nullptr;
+  int64_t ld = 0;
+  bool params_set = false;
+  bool prep_done = false;
+  int gen = 0;  // generation of the last prep launch (error word protocol)
+
+  std::vector<double> h_res, h_J;  // host staging for mvba_evaluate
+
+  // linearization (K2): camera-side compact layout, chunks, point CSR
+  bool lin_ok = false;
+  std::string lin_err;
+  int64_t cam_grad_size = 0, cam_hess_size = 0, slab_size = 0;
+  int32_t max_w16 = 0;
+  std::vector<int32_t> cam_block_ids;   // camera-side blocks in block-id order
+  std::vector<int64_t> cam_goff, cam_hoff;
+  std::vector<int32_t> pt_block_ids;    // point index -> block id
+  int4* d_chunks = nullptr;
+  void* d_frame_lin = nullptr;
+  double* d_slab = nullptr;
+  double* d_rep = nullptr;  // kReplicas copies of [cam_grad | cam_hess | cost], kept zero between calls
+  int64_t* d_pt_begin = nullptr;
+  int32_t* d_po_frame = nullptr;
+  double2* d_po_meas = nullptr;
+  int32_t* d_slot_po = nullptr;          // device slot -> point-order index (-1 = padding)
+  std::vector<int64_t> cam_poff;         // camera-side entry -> packed parameter offset
+  int32_t nchunks = 0;
+
+  SolverState* solver = nullptr;         // LM state, allocated by the first mvba_solve
+
+  mvba_status fail(mvba_status st, const std::string& msg) {
+    err = msg;
+    return st;
+  }
+  mvba_status hip_fail(hipError_t e, const char* where) {
+    err = std::string("HIP error in ") + where + ": " + hipGetErrorString(e);
+    return MVBA_E_HIP;
+  }
+};
+
+
+#endif  // MVBA_INTERNAL_H_

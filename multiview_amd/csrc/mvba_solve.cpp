@@ -1,0 +1,865 @@
+// mvba_solve.cpp — GPU-resident Levenberg-Marquardt driver (mvba_solve).
+//
+// Replaces ceres::Solve with linear_solver_type = ITERATIVE_SCHUR and the
+// default JACOBI preconditioner (rig_calibrator.cc:1910-1919) for problems of
+// BracketedCamError blocks. Control flow follows Ceres 1.14 [ext, not vendored]:
+//   trust_region_minimizer.cc     Minimize / IterationZero / ComputeTrustRegionStep /
+//                                 ParameterToleranceReached / FunctionToleranceReached /
+//                                 HandleSuccessfulStep / HandleInvalidStep, Jacobi
+//                                 column scaling fixed at iteration 0;
+//   levenberg_marquardt_strategy.cc  diagonal clamp, radius update
+//                                 radius /= max(1/3, 1-(2rho-1)^3), reject: /= 2,4,8...;
+//   iterative_schur_complement_solver.cc + implicit_schur_complement.cc
+//                                 CG on S = F'F + D_f^2 - F'E (E'E + D_e^2)^-1 E'F with
+//                                 the block-diagonal (F'F + D_f^2)^-1 preconditioner;
+//   conjugate_gradients_solver.cc  q-criterion termination (eta), residual reset every 10;
+//   line_search.cc (ArmijoLineSearch)  projected line search when bounds are active.
+// All vectors live in HBM; the host only sees scalars (dot products, costs).
+#include <algorithm>
+#include <chrono>
+#include <complex>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+
+#include "mvba_internal.h"
+
+extern "C" {
+int mvba_solver_dir_stride(void);
+int mvba_solver_slabb_stride(void);
+int mvba_solver_vec_replicas(void);
+hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const FrameDesc* fd, const double* frec,
+                                 const double* x, double* dir, hipStream_t s);
+hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
+                              const double2* po_meas, const FrameDesc* fd, const double* frec,
+                              const double* params, const double4* pts, const double* dir, const double* tinit,
+                              const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
+                              double* sq_partial, int32_t flags, double cauchy_c, hipStream_t s,
+                              int64_t* nblocks_out);
+hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
+                              const Segment* segs, const FrameDesc* fd, const double* frec, const double* params,
+                              const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                              const int32_t* slot_po, const double* ubuf, double* slabb, int32_t flags,
+                              double cauchy_c, hipStream_t s);
+hipError_t mvba_launch_dir_expand(const void* fl, int32_t nframes, const FrameDesc* fd, const double* frec,
+                                  const double* slabb, double* yrep, int64_t ng, double* y, hipStream_t s);
+hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, hipStream_t s);
+hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
+                             hipStream_t s);
+hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, double* out,
+                           hipStream_t s);
+hipError_t mvba_launch_sum(int64_t n, const double* partial, double* out, hipStream_t s);
+hipError_t mvba_launch_block_chol(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
+                                  const double* hess, const double* d, double* fac, hipStream_t s);
+hipError_t mvba_launch_block_solve(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
+                                   const double* fac, const double* r, double* z, hipStream_t s);
+hipError_t mvba_launch_extract_diag(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
+                                    const double* hess, int64_t npts, const double* V, int64_t ng, double* c,
+                                    hipStream_t s);
+hipError_t mvba_launch_jacobi_scale(int64_t n, const double* c, double* sc, hipStream_t s);
+hipError_t mvba_launch_lm_diag(int64_t n, const double* c, const double* sc, double inv_radius, double dmin,
+                               double dmax, double* d, hipStream_t s);
+hipError_t mvba_launch_gather(int64_t ncam, const int64_t* cam_poff, int64_t npts, const int64_t* pt_off,
+                              const uint8_t* pt_free, const double* params, double* out, hipStream_t s);
+hipError_t mvba_launch_scatter(int64_t ncam, const int64_t* cam_poff, int64_t npts, const int64_t* pt_off,
+                               const uint8_t* pt_free, const double* in, double* params, hipStream_t s);
+hipError_t mvba_launch_plus(int64_t n, const double* x, const double* delta, const double* lower,
+                            const double* upper, double* out, hipStream_t s);
+hipError_t mvba_launch_proj_grad_max(int64_t n, const double* x, const double* g, const double* lower,
+                                     const double* upper, double* partial, double* out, hipStream_t s);
+hipError_t mvba_launch_cost(int model, int deg, const Segment* segs, int32_t nseg, const FrameDesc* fd,
+                            const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
+                            const double2* obs_meas, int32_t flags, double cauchy_c, double* partial, hipStream_t s,
+                            int64_t* nblocks_out);
+}
+
+// Device + pinned host state of one handle's solver (allocated by the first mvba_solve).
+struct SolverState {
+  int64_t ng = 0, nh = 0, np = 0, nc = 0;  // camera grad/hess sizes, points, compact size ng + 3 np
+  int32_t nblocks = 0;
+  double* lin = nullptr;      // [ng | nh | 1]: camera gradient, block Hessians, cost (one all-reduce)
+  double* phess = nullptr;    // [6 np] point Hessians V_p
+  double* G = nullptr;        // [nc] compact gradient
+  double* cdiag = nullptr;    // [nc] diag(J^T J)
+  double* sc = nullptr;       // [nc] Jacobi scaling (iteration 0)
+  double* dmp = nullptr;      // [nc] LM damping (unscaled)
+  double* fac = nullptr;      // [nh] Cholesky factors of the preconditioner blocks
+  double* x = nullptr;        // [nc] current point (compact)
+  double* xn = nullptr;       // [nc] candidate point
+  double* delta = nullptr;    // [nc] step (camera part = CG solution)
+  double* scr = nullptr;      // [nc] scratch
+  double* lo = nullptr;       // [nc] bounds (compact) or null
+  double* hi = nullptr;
+  double *b = nullptr, *r = nullptr, *z = nullptr, *p = nullptr, *q = nullptr, *tmp = nullptr;  // [ng]
+  double* yrep = nullptr;     // [replicas * ng], kept zero between products
+  double* dir = nullptr;      // [nframes * dir stride]
+  double* zbuf = nullptr;     // [8 N] point-order z_o | J_pt rows
+  double* ubuf = nullptr;     // [2 N]
+  double* slabb = nullptr;    // [nchunks * slab stride]
+  double* partial = nullptr;  // [npartial]
+  double* scal = nullptr;     // [32] device scalars
+  double* hscal = nullptr;    // [32] pinned host mirror
+  int64_t npartial = 0;
+  int32_t* bsize = nullptr;
+  int64_t *goff = nullptr, *hoff = nullptr, *cam_poff = nullptr;
+};
+
+void solver_state_free(SolverState* S) {
+  if (!S) return;
+  void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
+                  S->hi, S->b, S->r, S->z, S->p, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->ubuf,
+                  S->slabb, S->partial, S->scal, S->bsize, S->goff, S->hoff, S->cam_poff};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (S->hscal) (void)hipHostFree(S->hscal);
+  delete S;
+}
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+struct HipErr {
+  hipError_t e;
+  const char* where;
+};
+
+#define HCHK(x)                                   \
+  do {                                            \
+    hipError_t e_ = (x);                          \
+    if (e_ != hipSuccess) throw HipErr{e_, #x};   \
+  } while (0)
+
+struct StatusErr {
+  mvba_status st;
+  std::string msg;
+};
+
+SolverState* alloc_state(mvba_handle* h) {
+  SolverState* S = new SolverState();
+  S->ng = h->cam_grad_size;
+  S->nh = h->cam_hess_size;
+  S->np = h->npts;
+  S->nc = S->ng + 3 * S->np;
+  S->nblocks = (int32_t)h->cam_block_ids.size();
+  const int64_t N = h->nres;
+  const int64_t ng1 = std::max<int64_t>(S->ng, 1);
+  try {
+    HCHK(dalloc(&S->lin, (size_t)(S->ng + S->nh + 1)));
+    HCHK(dalloc(&S->phess, (size_t)(6 * S->np)));
+    for (double** v : {&S->G, &S->cdiag, &S->sc, &S->dmp, &S->x, &S->xn, &S->delta, &S->scr})
+      HCHK(dalloc(v, (size_t)S->nc));
+    HCHK(dalloc(&S->fac, (size_t)S->nh));
+    for (double** v : {&S->b, &S->r, &S->z, &S->p, &S->q, &S->tmp}) HCHK(dalloc(v, (size_t)ng1));
+    const size_t nrep = (size_t)mvba_solver_vec_replicas() * (size_t)ng1;
+    HCHK(dalloc(&S->yrep, nrep));
+    HCHK(hipMemset(S->yrep, 0, nrep * sizeof(double)));
+    HCHK(dalloc(&S->dir, (size_t)(h->nframes * mvba_solver_dir_stride())));
+    HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
+    HCHK(dalloc(&S->ubuf, (size_t)(2 * N)));
+    HCHK(dalloc(&S->slabb, (size_t)h->nchunks * (size_t)mvba_solver_slabb_stride()));
+    int64_t ncost = 0;
+    for (const Group& G : h->groups) ncost = std::max<int64_t>(ncost, (G.seg_count + 3) / 4);
+    S->npartial = std::max<int64_t>({256, (S->np * 4 + 255) / 256, ncost});
+    HCHK(dalloc(&S->partial, (size_t)S->npartial));
+    HCHK(dalloc(&S->scal, 32));
+    HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hscal), 32 * sizeof(double)));
+    std::vector<int32_t> bs(S->nblocks);
+    for (int32_t k = 0; k < S->nblocks; k++) {
+      const int32_t bid = h->cam_block_ids[k];
+      const int64_t next = (k + 1 < S->nblocks) ? h->cam_goff[k + 1] : S->ng;
+      (void)bid;
+      bs[k] = (int32_t)(next - h->cam_goff[k]);
+    }
+    HCHK(upload(&S->bsize, bs));
+    HCHK(upload(&S->goff, h->cam_goff));
+    HCHK(upload(&S->hoff, h->cam_hoff));
+    HCHK(upload(&S->cam_poff, h->cam_poff));
+  } catch (...) {
+    solver_state_free(S);
+    throw;
+  }
+  return S;
+}
+
+class Solver {
+ public:
+  Solver(mvba_handle* h, const mvba_solver_options& o, hipStream_t s) : h_(h), o_(o), s_(s), S_(h->solver) {
+    flags_ = o.use_loss ? MVBA_EVAL_APPLY_LOSS : 0;
+    cauchy_c_ = o.use_loss ? 1.0 / (o.robust_threshold * o.robust_threshold) : 0.0;
+    single_model_ = h->groups.size() == 1;
+  }
+
+  void run(mvba_solver_summary* sum);
+
+ private:
+  mvba_handle* h_;
+  const mvba_solver_options& o_;
+  hipStream_t s_;
+  SolverState* S_;
+  int32_t flags_;
+  double cauchy_c_;
+  bool single_model_;
+  bool bounded_ = false;
+
+  int pa_model() const { return single_model_ ? h_->groups[0].model : -1; }
+  int pa_deg() const { return single_model_ ? h_->groups[0].deg : 0; }
+
+  void exchange(double* buf, int64_t n, int32_t op) {
+    if (!o_.allreduce || n <= 0) return;
+    HCHK(hipStreamSynchronize(s_));
+    if (o_.allreduce(buf, n, op, (void*)s_, o_.allreduce_user) != 0)
+      throw StatusErr{MVBA_E_INVALID, "allreduce callback failed"};
+  }
+
+  // Fetch device scalars scal[0..n) to the pinned mirror (one sync).
+  const double* fetch(int n) {
+    HCHK(hipMemcpyAsync(S_->hscal, S_->scal, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s_));
+    HCHK(hipStreamSynchronize(s_));
+    return S_->hscal;
+  }
+
+  void dot(int64_t n, const double* a, const double* b, int slot) {
+    HCHK(mvba_launch_dot(n, a, b, S_->partial, S_->scal + slot, s_));
+  }
+
+  void prep() {
+    h_->gen++;
+    HCHK(mvba_launch_prep(h_->d_fd, h_->nframes, h_->d_params, h_->d_frec, h_->d_pt_off, h_->d_pt_free, h_->npts,
+                          h_->d_pts, h_->gen, h_->d_err, s_));
+    h_->prep_done = true;
+  }
+
+  void check_alpha() {
+    HCHK(hipStreamSynchronize(s_));
+    int err = 0;
+    HCHK(hipMemcpy(&err, h_->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (err >= h_->gen && h_->gen > 0) throw StatusErr{MVBA_E_ALPHA_RANGE, "Out of bounds in interpolation."};
+  }
+
+  // Jacobian at the handle's parameters -> lin (all-reduced), G, phess, cdiag. Returns cost.
+  double linearize() {
+    mvba_status st = mvba_linearize_device(h_, flags_, o_.robust_threshold, S_->lin, S_->lin + S_->ng,
+                                           S_->G + S_->ng, S_->phess, S_->lin + S_->ng + S_->nh, (void*)s_);
+    if (st != MVBA_OK) throw StatusErr{st, h_->err};
+    check_alpha();
+    exchange(S_->lin, S_->ng + S_->nh + 1, MVBA_REDUCE_SUM);
+    if (S_->ng)
+      HCHK(hipMemcpyAsync(S_->G, S_->lin, (size_t)S_->ng * sizeof(double), hipMemcpyDeviceToDevice, s_));
+    HCHK(mvba_launch_extract_diag(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->np, S_->phess,
+                                  S_->ng, S_->cdiag, s_));
+    double c = 0.0;
+    HCHK(hipMemcpyAsync(&c, S_->lin + S_->ng + S_->nh, sizeof(double), hipMemcpyDeviceToHost, s_));
+    HCHK(hipStreamSynchronize(s_));
+    return c;
+  }
+
+  // Cost at the handle's parameters (prep + cost kernels), summed over ranks.
+  double cost() {
+    prep();
+    double* acc = S_->scal + 16;
+    HCHK(hipMemsetAsync(acc, 0, sizeof(double), s_));
+    for (const Group& G : h_->groups) {
+      int64_t nb = 0;
+      HCHK(mvba_launch_cost(G.model, G.deg, h_->d_segs + G.seg_begin, G.seg_count, h_->d_fd, h_->d_frec,
+                            h_->d_params, h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, flags_, cauchy_c_,
+                            S_->partial, s_, &nb));
+      HCHK(mvba_launch_sum(nb, S_->partial, S_->scal + 17, s_));
+      HCHK(mvba_launch_axpby(1, 1.0, acc, 1.0, S_->scal + 17, acc, s_));
+    }
+    check_alpha();
+    exchange(acc, 1, MVBA_REDUCE_SUM);
+    HCHK(hipMemcpyAsync(S_->hscal + 16, acc, sizeof(double), hipMemcpyDeviceToHost, s_));
+    HCHK(hipStreamSynchronize(s_));
+    return S_->hscal[16];
+  }
+
+  // pass B over every model group, frame expand, cross-rank sum: y = F' u
+  void reduce_frames(double* y) {
+    for (const Group& G : h_->groups)
+      HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
+                              h_->d_segs, h_->d_fd, h_->d_frec, h_->d_params, h_->d_pts, h_->d_obs_pid,
+                              h_->d_obs_meas, h_->d_slot_po, S_->ubuf, S_->slabb, flags_, cauchy_c_, s_));
+    HCHK(mvba_launch_dir_expand(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->slabb, S_->yrep,
+                                S_->ng, y, s_));
+    exchange(y, S_->ng, MVBA_REDUCE_SUM);
+  }
+
+  // y = S x (implicit Schur complement with damping)
+  void apply_schur(const double* xv, double* y) {
+    HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, s_));
+    HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
+                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, nullptr, S_->phess, S_->dmp + S_->ng,
+                            S_->zbuf, S_->ubuf, nullptr, nullptr, flags_, cauchy_c_, s_, nullptr));
+    reduce_frames(y);
+    HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, s_));
+  }
+
+  // b = -(g_c - W (V+D)^-1 g_p)
+  void schur_rhs() {
+    HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
+                            h_->d_frec, h_->d_params, h_->d_pts, nullptr, S_->G + S_->ng, S_->phess,
+                            S_->dmp + S_->ng, S_->zbuf, S_->ubuf, nullptr, nullptr, flags_, cauchy_c_, s_,
+                            nullptr));
+    reduce_frames(S_->tmp);  // = -W w
+    HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
+  }
+
+  struct CgResult {
+    int iters = 0;
+    int status = 0;  // 0 success, 1 no convergence (usable), 2 failure
+  };
+
+  // PCG on S delta_c = b (conjugate_gradients_solver.cc [ext])
+  CgResult cg() {
+    CgResult R;
+    const int64_t n = S_->ng;
+    double* xv = S_->delta;
+    HCHK(hipMemsetAsync(xv, 0, (size_t)std::max<int64_t>(n, 1) * sizeof(double), s_));
+    if (n == 0) return R;
+    dot(n, S_->b, S_->b, 0);
+    const double norm_b = std::sqrt(fetch(1)[0]);
+    if (norm_b == 0.0) return R;
+    // r = b - A x = b (x = 0), Q0 = -x'(b + r) = 0
+    HCHK(hipMemcpyAsync(S_->r, S_->b, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s_));
+    double Q0 = 0.0, rho = 1.0;
+    HCHK(mvba_launch_block_solve(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->fac, S_->r, S_->z, s_));
+    dot(n, S_->r, S_->z, 0);
+    double rho_next = fetch(1)[0];
+    auto bad = [](double v) { return v == 0.0 || std::isinf(v) || std::isnan(v); };
+    for (int i = 1;; i++) {
+      R.iters = i;
+      const double last_rho = rho;
+      rho = rho_next;
+      if (bad(rho)) {
+        R.status = 2;
+        break;
+      }
+      if (i == 1) {
+        HCHK(hipMemcpyAsync(S_->p, S_->z, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s_));
+      } else {
+        const double beta = rho / last_rho;
+        if (bad(beta)) {
+          R.status = 2;
+          break;
+        }
+        HCHK(mvba_launch_axpby(n, 1.0, S_->z, beta, S_->p, S_->p, s_));
+      }
+      apply_schur(S_->p, S_->q);
+      dot(n, S_->p, S_->q, 0);
+      const double pq = fetch(1)[0];
+      if (pq <= 0.0 || std::isinf(pq) || std::isnan(pq)) {
+        R.status = 1;  // "Matrix is indefinite": NO_CONVERGENCE, x kept
+        break;
+      }
+      const double alpha = rho / pq;
+      if (std::isinf(alpha)) {
+        R.status = 2;
+        break;
+      }
+      HCHK(mvba_launch_axpby(n, 1.0, xv, alpha, S_->p, xv, s_));
+      if (i % 10 == 0) {
+        apply_schur(xv, S_->tmp);
+        HCHK(mvba_launch_axpby(n, 1.0, S_->b, -1.0, S_->tmp, S_->r, s_));
+      } else {
+        HCHK(mvba_launch_axpby(n, 1.0, S_->r, -alpha, S_->q, S_->r, s_));
+      }
+      HCHK(mvba_launch_block_solve(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->fac, S_->r, S_->z, s_));
+      dot(n, xv, S_->b, 0);
+      dot(n, xv, S_->r, 1);
+      dot(n, S_->r, S_->z, 2);
+      const double* hs = fetch(3);
+      const double Q1 = -(hs[0] + hs[1]);
+      rho_next = hs[2];
+      const double zeta = i * (Q1 - Q0) / Q1;
+      if (zeta < o_.eta && i >= o_.min_linear_solver_iterations) break;
+      Q0 = Q1;
+      if (i >= o_.max_linear_solver_iterations) {
+        R.status = 1;
+        break;
+      }
+    }
+    return R;
+  }
+
+  // delta_p = -(V+D)^-1 (g_p + W' delta_c); returns model cost change -(g'delta + |J delta|^2 / 2)
+  double back_substitute() {
+    int64_t nb = 0;
+    HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
+                               s_));
+    HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
+                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
+                            S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial, flags_, cauchy_c_,
+                            s_, &nb));
+    HCHK(mvba_launch_sum(nb, S_->partial, S_->scal + 0, s_));  // |J delta|^2 (local observations)
+    HCHK(mvba_launch_axpby(3 * S_->np, -1.0, S_->delta + S_->ng, 0.0, nullptr, S_->delta + S_->ng, s_));
+    dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
+    exchange(S_->scal, 2, MVBA_REDUCE_SUM);
+    dot(S_->ng, S_->G, S_->delta, 2);  // g_c' delta_c (global already)
+    const double* hs = fetch(3);
+    return -(hs[1] + hs[2] + 0.5 * hs[0]);
+  }
+
+  // max |x - P(x - g)| and |x - P(x - g)|, over ranks
+  double grad_max_norm() {
+    // camera part is identical on every rank: take it from the compact vector once,
+    // points part is rank-local; MAX-reduce the combination.
+    HCHK(mvba_launch_proj_grad_max(S_->nc, S_->x, S_->G, S_->lo, S_->hi, S_->partial, S_->scal + 0, s_));
+    exchange(S_->scal, 1, MVBA_REDUCE_MAX);
+    return fetch(1)[0];
+  }
+
+  // |x|^2 split: camera part (global) + point part summed over ranks
+  double norm2_compact(const double* v) {
+    dot(3 * S_->np, v + S_->ng, v + S_->ng, 0);
+    exchange(S_->scal, 1, MVBA_REDUCE_SUM);
+    dot(S_->ng, v, v, 1);
+    const double* hs = fetch(2);
+    return hs[0] + hs[1];
+  }
+
+  double step_norm2() {  // |xn - x|^2, difference formed explicitly
+    HCHK(mvba_launch_axpby(S_->nc, 1.0, S_->xn, -1.0, S_->x, S_->scr, s_));
+    return norm2_compact(S_->scr);
+  }
+
+  // a.b over the compact vector: camera part is replicated on every rank, point part summed
+  double dot_global(const double* a, const double* b) {
+    dot(3 * S_->np, a + S_->ng, b + S_->ng, 0);
+    exchange(S_->scal, 1, MVBA_REDUCE_SUM);
+    dot(S_->ng, a, b, 1);
+    const double* hs = fetch(2);
+    return hs[0] + hs[1];
+  }
+
+  void set_params_from(const double* v) {
+    HCHK(mvba_launch_scatter(S_->ng, S_->cam_poff, S_->np, h_->d_pt_off, h_->d_pt_free, v, h_->d_params, s_));
+  }
+
+  double armijo(double x_cost, double gtd, bool* relinearized);
+};
+
+// ---- polynomial interpolation of the line search (Ceres polynomial.cc [ext])
+struct Sample {
+  double x = 0.0, f = 0.0, g = 0.0;
+  bool fv = false, gv = false;
+};
+
+double poly_eval(const std::vector<double>& c, double x) {  // highest degree first
+  double v = 0.0;
+  for (double a : c) v = v * x + a;
+  return v;
+}
+
+// FindInterpolatingPolynomial: value and gradient constraints, square system.
+std::vector<double> interpolating_polynomial(const std::vector<Sample>& smp) {
+  int m = 0;
+  for (const Sample& s : smp) m += (s.fv ? 1 : 0) + (s.gv ? 1 : 0);
+  const int deg = m - 1;
+  std::vector<double> A((size_t)m * m, 0.0), rhs(m, 0.0);
+  int row = 0;
+  for (const Sample& s : smp) {
+    if (s.fv) {
+      for (int j = 0; j <= deg; j++) A[row * m + j] = std::pow(s.x, deg - j);
+      rhs[row++] = s.f;
+    }
+    if (s.gv) {
+      for (int j = 0; j < deg; j++) A[row * m + j] = (deg - j) * std::pow(s.x, deg - j - 1);
+      rhs[row++] = s.g;
+    }
+  }
+  // Gaussian elimination with partial pivoting (m <= 6)
+  std::vector<int> perm(m);
+  for (int i = 0; i < m; i++) perm[i] = i;
+  for (int k = 0; k < m; k++) {
+    int piv = k;
+    for (int i = k + 1; i < m; i++)
+      if (std::fabs(A[i * m + k]) > std::fabs(A[piv * m + k])) piv = i;
+    if (piv != k) {
+      for (int j = 0; j < m; j++) std::swap(A[k * m + j], A[piv * m + j]);
+      std::swap(rhs[k], rhs[piv]);
+    }
+    const double d = A[k * m + k];
+    if (d == 0.0) continue;
+    for (int i = k + 1; i < m; i++) {
+      const double f = A[i * m + k] / d;
+      for (int j = k; j < m; j++) A[i * m + j] -= f * A[k * m + j];
+      rhs[i] -= f * rhs[k];
+    }
+  }
+  std::vector<double> c(m, 0.0);
+  for (int i = m - 1; i >= 0; i--) {
+    double v = rhs[i];
+    for (int j = i + 1; j < m; j++) v -= A[i * m + j] * c[j];
+    c[i] = (A[i * m + i] != 0.0) ? v / A[i * m + i] : 0.0;
+  }
+  return c;
+}
+
+// Real parts of all roots (FindPolynomialRoots with imaginary == NULL), Durand-Kerner.
+std::vector<double> root_real_parts(std::vector<double> c) {
+  while (!c.empty() && c[0] == 0.0) c.erase(c.begin());
+  const int n = (int)c.size() - 1;
+  std::vector<double> out;
+  if (n < 1) return out;
+  if (n == 1) {
+    out.push_back(-c[1] / c[0]);
+    return out;
+  }
+  if (n == 2) {
+    const double a = c[0], b = c[1], cc = c[2], disc = b * b - 4 * a * cc;
+    if (disc < 0) {
+      out.push_back(-b / (2 * a));
+      out.push_back(-b / (2 * a));
+    } else {
+      const double sq = std::sqrt(disc);
+      out.push_back((-b + sq) / (2 * a));
+      out.push_back((-b - sq) / (2 * a));
+    }
+    return out;
+  }
+  typedef std::complex<double> cd;
+  std::vector<cd> z(n);
+  const cd seed(0.4, 0.9);
+  z[0] = 1.0;
+  for (int i = 1; i < n; i++) z[i] = z[i - 1] * seed;
+  auto P = [&](cd x) {
+    cd v = 0.0;
+    for (double a : c) v = v * x + a / c[0];
+    return v;
+  };
+  for (int it = 0; it < 500; it++) {
+    double moved = 0.0;
+    for (int i = 0; i < n; i++) {
+      cd den = 1.0;
+      for (int j = 0; j < n; j++)
+        if (j != i) den *= (z[i] - z[j]);
+      const cd dz = P(z[i]) / den;
+      z[i] -= dz;
+      moved = std::max(moved, std::abs(dz));
+    }
+    if (moved < 1e-15) break;
+  }
+  for (const cd& r : z) out.push_back(r.real());
+  return out;
+}
+
+// MinimizeInterpolatingPolynomial over [lo, hi]
+double minimize_interpolant(const std::vector<Sample>& smp, double lo, double hi) {
+  const std::vector<double> poly = interpolating_polynomial(smp);
+  double bx = 0.5 * (lo + hi), bv = poly_eval(poly, bx);
+  auto consider = [&](double x) {
+    if (x < lo || x > hi) return;
+    const double v = poly_eval(poly, x);
+    if (v < bv) {
+      bv = v;
+      bx = x;
+    }
+  };
+  consider(lo);
+  consider(hi);
+  if (poly.size() > 2) {
+    std::vector<double> der;
+    const int deg = (int)poly.size() - 1;
+    for (int j = 0; j < deg; j++) der.push_back(poly[j] * (deg - j));
+    for (double r : root_real_parts(der)) consider(r);
+  }
+  for (const Sample& s : smp) consider(s.x);
+  return bx;
+}
+
+// Projected Armijo search along delta (TrustRegionMinimizer::DoLineSearch with
+// ARMIJO + CUBIC interpolation [ext]): scales delta in place on success.
+double Solver::armijo(double x_cost, double gtd, bool* relinearized) {
+  const double kSuff = 1e-4, kMaxContr = 1e-3, kMinContr = 0.6, kMinStep = 1e-9;
+  const int kMaxIter = 20;
+  HCHK(mvba_launch_proj_grad_max(S_->nc, S_->delta, S_->delta, nullptr, nullptr, S_->partial, S_->scal, s_));
+  exchange(S_->scal, 1, MVBA_REDUCE_MAX);
+  const double dmax = fetch(1)[0];
+  auto eval = [&](double a, bool want_grad) {
+    Sample smp;
+    smp.x = a;
+    HCHK(mvba_launch_axpby(S_->nc, a, S_->delta, 0.0, nullptr, S_->scr, s_));
+    HCHK(mvba_launch_plus(S_->nc, S_->x, S_->scr, S_->lo, S_->hi, S_->xn, s_));
+    set_params_from(S_->xn);
+    smp.f = cost();
+    smp.fv = std::isfinite(smp.f);
+    if (want_grad && smp.fv) {
+      linearize();
+      *relinearized = true;
+      smp.g = dot_global(S_->delta, S_->G);
+      smp.gv = std::isfinite(smp.g);
+    }
+    return smp;
+  };
+  Sample init;
+  init.x = 0.0;
+  init.f = x_cost;
+  init.g = gtd;
+  init.fv = init.gv = true;
+  Sample prev, cur = eval(1.0, false);
+  int it = 0;
+  while (!cur.fv || cur.f > x_cost + kSuff * gtd * cur.x) {
+    if (++it >= kMaxIter) return 1.0;
+    double step;
+    if (!cur.fv) {
+      step = std::min(std::max(cur.x * 0.5, kMaxContr * cur.x), kMinContr * cur.x);
+    } else {
+      if (!cur.gv) cur = eval(cur.x, true);
+      std::vector<Sample> smp{init, cur};
+      if (prev.fv) smp.push_back(prev);
+      step = minimize_interpolant(smp, kMaxContr * cur.x, kMinContr * cur.x);
+    }
+    if (step * dmax < kMinStep) return 1.0;
+    prev = cur;
+    cur = eval(step, false);
+  }
+  if (cur.x != 1.0) HCHK(mvba_launch_axpby(S_->nc, cur.x, S_->delta, 0.0, nullptr, S_->delta, s_));
+  return cur.x;
+}
+
+void Solver::run(mvba_solver_summary* sum) {
+  const double t0 = now_s();
+  const int64_t nc = S_->nc;
+  // bounds in compact form (+-inf for constant points)
+  bounded_ = false;
+  if (S_->lo) (void)hipFree(S_->lo);
+  if (S_->hi) (void)hipFree(S_->hi);
+  S_->lo = S_->hi = nullptr;
+  if (o_.lower_bounds || o_.upper_bounds) {
+    std::vector<int64_t> pt_off(S_->np);
+    std::vector<uint8_t> pt_free(S_->np);
+    if (S_->np) {
+      HCHK(hipMemcpy(pt_off.data(), h_->d_pt_off, S_->np * sizeof(int64_t), hipMemcpyDeviceToHost));
+      HCHK(hipMemcpy(pt_free.data(), h_->d_pt_free, S_->np, hipMemcpyDeviceToHost));
+    }
+    const double inf = std::numeric_limits<double>::infinity();
+    auto build = [&](const double* src, double fill, double** dst) {
+      if (!src) return;
+      std::vector<double> v(nc, fill);
+      for (int64_t e = 0; e < S_->ng; e++) v[e] = src[h_->cam_poff[e]];
+      for (int64_t p = 0; p < S_->np; p++)
+        if (pt_free[p])
+          for (int c = 0; c < 3; c++) v[S_->ng + 3 * p + c] = src[pt_off[p] + c];
+      for (double b : v)
+        if (std::isfinite(b)) bounded_ = true;
+      HCHK(upload(dst, v));
+    };
+    build(o_.lower_bounds, -inf, &S_->lo);
+    build(o_.upper_bounds, inf, &S_->hi);
+  }
+
+  HCHK(mvba_launch_gather(S_->ng, S_->cam_poff, S_->np, h_->d_pt_off, h_->d_pt_free, h_->d_params, S_->x, s_));
+  double tl = now_s();
+  double x_cost = linearize();
+  sum->linearize_time_s += now_s() - tl;
+  sum->initial_cost = x_cost;
+  const double* scale = nullptr;
+  if (o_.jacobi_scaling) {
+    HCHK(mvba_launch_jacobi_scale(nc, S_->cdiag, S_->sc, s_));
+    scale = S_->sc;
+  }
+  double gmax = grad_max_norm();
+  double x_norm = std::sqrt(norm2_compact(S_->x));
+  double radius = o_.initial_trust_region_radius, decrease = 2.0;
+  int iteration = 0, invalid = 0;
+  bool successful = true;
+  sum->num_successful_steps = 1;  // iteration 0 counts, as in Ceres' summary
+  auto row = [&](double cost, double change, double step, double ratio, int ls, double it_time) {
+    if (!o_.progress_to_stdout) return;
+    if (iteration == 0)
+      std::printf("iter      cost      cost_change  |gradient|   |step|    tr_ratio  tr_radius  ls_iter  "
+                  "iter_time  total_time\n");
+    std::printf("% 4d % 8e   % 3.2e   % 3.2e  % 3.2e  % 3.2e % 3.2e     % 4d   % 3.2e   % 3.2e\n", iteration, cost,
+                change, gmax, step, ratio, radius, ls, it_time, now_s() - t0);
+    std::fflush(stdout);
+  };
+  row(x_cost, 0.0, 0.0, 0.0, 0, now_s() - t0);
+  auto finish = [&](int type, const std::string& msg) {
+    sum->termination_type = type;
+    std::snprintf(sum->message, sizeof(sum->message), "%s", msg.c_str());
+  };
+  char buf[256];
+  for (;;) {
+    // FinalizeIterationAndCheckIfMinimizerCanContinue
+    if (iteration >= o_.max_num_iterations) {
+      std::snprintf(buf, sizeof(buf), "Maximum number of iterations reached. Number of iterations: %d.", iteration);
+      finish(MVBA_NO_CONVERGENCE, buf);
+      break;
+    }
+    if (successful && gmax <= o_.gradient_tolerance) {
+      std::snprintf(buf, sizeof(buf), "Gradient tolerance reached. Gradient max norm: %e <= %e", gmax,
+                    o_.gradient_tolerance);
+      finish(MVBA_CONVERGENCE, buf);
+      break;
+    }
+    if (radius <= o_.min_trust_region_radius) {
+      std::snprintf(buf, sizeof(buf), "Minimum trust region radius reached. Trust region radius: %e <= %e", radius,
+                    o_.min_trust_region_radius);
+      finish(MVBA_CONVERGENCE, buf);
+      break;
+    }
+    iteration++;
+    const double it0 = now_s();
+    // ComputeTrustRegionStep (LevenbergMarquardtStrategy::ComputeStep)
+    const double ts = now_s();
+    HCHK(mvba_launch_lm_diag(nc, S_->cdiag, scale, 1.0 / radius, o_.min_lm_diagonal, o_.max_lm_diagonal, S_->dmp,
+                             s_));
+    HCHK(mvba_launch_block_chol(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->dmp, S_->fac, s_));
+    schur_rhs();
+    const CgResult cgr = cg();
+    sum->num_linear_iterations += cgr.iters;
+    bool valid = cgr.status != 2;
+    double mcc = 0.0;
+    if (valid) {
+      mcc = back_substitute();
+      valid = std::isfinite(mcc) && mcc > 0.0;
+    }
+    sum->linear_solver_time_s += now_s() - ts;
+    if (!valid) {
+      // HandleInvalidStep
+      if (++invalid >= o_.max_num_consecutive_invalid_steps) {
+        std::snprintf(buf, sizeof(buf),
+                      "Number of consecutive invalid steps more than Solver::Options::max_num_consecutive_invalid_steps: %d",
+                      o_.max_num_consecutive_invalid_steps);
+        finish(MVBA_FAILURE, buf);
+        break;
+      }
+      radius /= decrease;
+      decrease *= 2.0;
+      successful = false;
+      sum->num_unsuccessful_steps++;
+      row(x_cost, 0.0, 0.0, 0.0, cgr.iters, now_s() - it0);
+      continue;
+    }
+    invalid = 0;
+    bool relinearized = false;
+    const double te = now_s();
+    if (bounded_) {
+      // g'delta: model change = -(g'delta + |J delta|^2/2) has g'delta in it; recompute directly
+      const double gtd = dot_global(S_->G, S_->delta);
+      armijo(x_cost, gtd, &relinearized);
+    }
+    // ComputeCandidatePointAndEvaluateCost
+    HCHK(mvba_launch_plus(nc, S_->x, S_->delta, S_->lo, S_->hi, S_->xn, s_));
+    set_params_from(S_->xn);
+    double cand = cost();
+    if (!std::isfinite(cand)) cand = std::numeric_limits<double>::max();
+    sum->eval_time_s += now_s() - te;
+    const double step_norm = std::sqrt(step_norm2());
+    auto restore_x = [&]() {
+      set_params_from(S_->x);
+      prep();
+    };
+    if (step_norm <= o_.parameter_tolerance * (x_norm + o_.parameter_tolerance)) {
+      std::snprintf(buf, sizeof(buf), "Parameter tolerance reached. Relative step_norm: %e <= %e.",
+                    step_norm / (x_norm + o_.parameter_tolerance), o_.parameter_tolerance);
+      finish(MVBA_CONVERGENCE, buf);
+      restore_x();
+      break;
+    }
+    const double change = x_cost - cand;
+    if (std::fabs(change) <= o_.function_tolerance * x_cost) {
+      std::snprintf(buf, sizeof(buf), "Function tolerance reached. |cost_change|/cost: %e <= %e",
+                    std::fabs(change) / x_cost, o_.function_tolerance);
+      finish(MVBA_CONVERGENCE, buf);
+      restore_x();
+      break;
+    }
+    const double ratio = change / mcc;
+    if (ratio > o_.min_relative_decrease) {
+      // HandleSuccessfulStep: x = candidate, re-linearize there
+      std::swap(S_->x, S_->xn);
+      x_norm = std::sqrt(norm2_compact(S_->x));
+      tl = now_s();
+      x_cost = linearize();
+      sum->linearize_time_s += now_s() - tl;
+      gmax = grad_max_norm();
+      radius = std::min(o_.max_trust_region_radius,
+                        radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * ratio - 1.0, 3)));
+      decrease = 2.0;
+      successful = true;
+      sum->num_successful_steps++;
+      row(x_cost, change, step_norm, ratio, cgr.iters, now_s() - it0);
+    } else {
+      // HandleUnsuccessfulStep
+      radius /= decrease;
+      decrease *= 2.0;
+      successful = false;
+      sum->num_unsuccessful_steps++;
+      restore_x();
+      if (relinearized) linearize();
+      row(cand, change, step_norm, ratio, cgr.iters, now_s() - it0);
+    }
+  }
+  HCHK(hipStreamSynchronize(s_));
+  sum->num_iterations = iteration;
+  sum->final_cost = x_cost;
+  sum->total_time_s = now_s() - t0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void mvba_solver_default_options(mvba_solver_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->max_num_iterations = 50;
+  o->function_tolerance = 1e-6;
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+  o->min_relative_decrease = 1e-3;
+  o->eta = 1e-1;
+  o->min_linear_solver_iterations = 0;
+  o->max_linear_solver_iterations = 500;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->jacobi_scaling = 1;
+  o->use_loss = 0;
+  o->robust_threshold = 0.0;
+}
+
+mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver_summary* summary,
+                       void* stream) {
+  if (!h || !o || !summary) return MVBA_E_INVALID;
+  std::memset(summary, 0, sizeof(*summary));
+  if (!h->lin_ok) return h->fail(MVBA_E_INVALID, h->lin_err);
+  if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
+  if (o->use_loss && !(o->robust_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
+  if (o->max_num_iterations < 0 || o->max_linear_solver_iterations < 1 || !(o->initial_trust_region_radius > 0.0))
+    return h->fail(MVBA_E_INVALID, "invalid solver options");
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  try {
+    if (!h->solver) h->solver = alloc_state(h);
+    Solver sv(h, *o, (hipStream_t)stream);
+    sv.run(summary);
+  } catch (const HipErr& e) {
+    std::snprintf(summary->message, sizeof(summary->message), "HIP error");
+    summary->termination_type = MVBA_FAILURE;
+    return h->hip_fail(e.e, e.where);
+  } catch (const StatusErr& e) {
+    summary->termination_type = MVBA_FAILURE;
+    std::snprintf(summary->message, sizeof(summary->message), "%s", e.msg.c_str());
+    return h->fail(e.st, e.msg);
+  } catch (const std::bad_alloc&) {
+    return h->fail(MVBA_E_INVALID, "host allocation failed");
+  }
+  return MVBA_OK;
+}
+
+mvba_status mvba_get_params(mvba_handle* h, double* packed) {
+  if (!h || !packed) return MVBA_E_INVALID;
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  hipError_t e = hipMemcpy(packed, h->d_params, (size_t)h->nparams * sizeof(double), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_get_params");
+  return MVBA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,783 @@
+// mvba_solver.hip — gfx950 kernels of the GPU-resident Levenberg-Marquardt
+// solver (replacing ceres::Solve with ITERATIVE_SCHUR, rig_calibrator.cc:1910-1919).
+//
+// The Schur complement S = U - W V^-1 W^T over the camera-side parameters is
+// never formed: S x is applied matrix-free in two passes per CG iteration,
+//   pass A (point order, 4 lanes/point): z_o = J_cam,o x  (via the frame's
+//          generators: J_pose = Z w, so J_pose x = Z (w x)), t_p = sum J_pt^T z_o,
+//          w_p = (V_p + D_p)^-1 t_p, u_o = z_o - J_pt w_p;
+//   pass B (frame order, one wave per frame chunk): y_frame = sum Z^T u_o,
+//          sum J_intr^T u_o; k_dir_expand maps y_frame through w to the pose
+//          columns: S x = J_cam^T u (+ LM damping).
+// Same two passes give the reduced right-hand side and the point back-substitution.
+#include "mvba_device.h"
+
+namespace mvba {
+
+constexpr int kDirStride = 64;     // per-frame direction record: u (6) | x_intr (<= 58)
+constexpr int kSlabB = 64;         // per-chunk pass-B record: Z^T u (6) | J_I^T u (<= 58)
+constexpr int kVecReplicas = 32;
+constexpr int kLanesPerPointS = 4;
+
+// Camera-side columns of one observation at a frame, as a row pair:
+// Z (6), intrinsics (focal, center 2, live distortion nd), J_pt (3), corrected r.
+template <int MODEL, int DEG>
+__device__ __forceinline__ void obs_rows(const FrameDesc& F, const double* __restrict__ rec,
+                                         const double* __restrict__ params, double X0, double X1,
+                                         double X2, double2 meas, int32_t flags, double cauchy_c,
+                                         double* Z0, double* Z1, double* I0, double* I1, double* P0,
+                                         double* P1, double* r, double* half_rho) {
+  const double f = params[F.off[MVBA_BLK_FOCAL]];
+  const double c0 = params[F.off[MVBA_BLK_CENTER]];
+  const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
+  Proj o;
+  project<MODEL, DEG>(rec, X0, X1, X2, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+  const double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
+  const double sr = loss_scale(r0, r1, flags, cauchy_c, half_rho);
+  r[0] = r0 * sr;
+  r[1] = r1 * sr;
+  const double fz = f / o.Xc[2] * sr;
+  const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+  const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
+  double a0[3], a1[3];
+  cross(o.Xc, G0, a0);
+  cross(o.Xc, G1, a1);
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    Z0[q] = a0[q]; Z0[3 + q] = G0[q];
+    Z1[q] = a1[q]; Z1[3 + q] = G1[q];
+    P0[q] = G0[0] * rec[q] + G0[1] * rec[3 + q] + G0[2] * rec[6 + q];
+    P1[q] = G1[0] * rec[q] + G1[1] * rec[3 + q] + G1[2] * rec[6 + q];
+  }
+  I0[0] = o.df0 * sr;
+  I1[0] = o.df1 * sr;
+  const double cc = (MODEL == kModelRpc) ? 0.0 : sr;
+  I0[1] = cc; I0[2] = 0.0;
+  I1[1] = 0.0; I1[2] = cc;
+  dist_columns<MODEL, DEG>(o, f, F.K, sr, [&](int q, double v0, double v1) {
+    I0[3 + q] = v0;
+    I1[3 + q] = v1;
+  });
+}
+
+template <int MODEL, int DEG>
+struct RowShape {
+  static constexpr int kDist = (MODEL == kModelNone) ? 0 : (MODEL == kModelFov) ? 1
+                             : (MODEL == kModelRadtan) ? 5 : 2 * ((DEG + 1) * (DEG + 2)) - 2;
+  static constexpr int kIntr = 3 + kDist;  // focal, center (2), live distortion
+};
+
+// ------------------------------------------------------------ per-frame direction
+// dir_f = [ w_f x_pose (6) | x_focal | x_center (2) | x_dist (live) ]
+__global__ void __launch_bounds__(64) k_frame_dir(const FrameLin* __restrict__ fl, int32_t nframes,
+                                                  const FrameDesc* __restrict__ fd,
+                                                  const double* __restrict__ frec,
+                                                  const double* __restrict__ x, double* __restrict__ dir) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nframes) return;
+  const FrameLin L = fl[f];
+  const double* w = frec + (int64_t)f * kFrameRecDoubles + 12;
+  double u[6] = {0, 0, 0, 0, 0, 0};
+  for (int blk = 0; blk < 4; blk++) {
+    const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+    if (L.goff[b] < 0) continue;
+    const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
+    for (int c = 0; c < ncol; c++) {
+      const double xv = x[L.goff[b] + c];
+      const double* wk = w + 6 * (k0 + c);
+      for (int a = 0; a < 6; a++) u[a] += wk[a] * xv;
+    }
+  }
+  double* d = dir + (int64_t)f * kDirStride;
+  for (int a = 0; a < 6; a++) d[a] = u[a];
+  const int nd = L.width - 10;
+  const int K = fd[f].K;
+  d[6] = L.goff[MVBA_BLK_FOCAL] >= 0 ? x[L.goff[MVBA_BLK_FOCAL]] : 0.0;
+  d[7] = L.goff[MVBA_BLK_CENTER] >= 0 ? x[L.goff[MVBA_BLK_CENTER]] : 0.0;
+  d[8] = L.goff[MVBA_BLK_CENTER] >= 0 ? x[L.goff[MVBA_BLK_CENTER] + 1] : 0.0;
+  for (int q = 0; q < nd; q++)
+    d[9 + q] = (L.goff[MVBA_BLK_DIST] >= 0 && q < K) ? x[L.goff[MVBA_BLK_DIST] + q] : 0.0;
+}
+
+// ------------------------------------------------------------ pass A (point order)
+// For each point: z_o = J_cam x (dir != null) for its observations, t = tinit +
+// sum J_pt^T z_o, w = (V + diag(dp))^-1 t, u_o = z_o - J_pt w.
+// store_u: write u_o (point order, 2 doubles); wout: w per point (3, nullable);
+// sq_partial: per-block sum of |u_o|^2 (nullable); gdot_partial: per-block sum
+// of g_p . w (nullable, with gp).
+__device__ __forceinline__ void solve3(const double* V, const double* dp, const double* t, double* w) {
+  // (V + diag(dp)) w = t, V packed xx xy xz yy yz zz; explicit inverse by cofactors
+  const double a = V[0] + dp[0], b = V[1], c = V[2];
+  const double d = V[3] + dp[1], e = V[4], f = V[5] + dp[2];
+  const double A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
+  const double det = a * A + b * B + c * C;
+  if (!(fabs(det) > 0.0)) {
+    w[0] = w[1] = w[2] = 0.0;
+    return;
+  }
+  const double id = 1.0 / det;
+  const double D = a * f - c * c, E = b * c - a * e, Fv = a * d - b * b;
+  w[0] = (A * t[0] + B * t[1] + C * t[2]) * id;
+  w[1] = (B * t[0] + D * t[1] + E * t[2]) * id;
+  w[2] = (C * t[0] + E * t[1] + Fv * t[2]) * id;
+}
+
+template <int MODEL, int DEG>
+__device__ __forceinline__ void pass_a_obs(const FrameDesc& F, const double* __restrict__ rec,
+                                           const double* __restrict__ params, const double* dirf,
+                                           double4 X, double2 m, int32_t flags, double cauchy_c,
+                                           double* z, double* P0, double* P1) {
+  using RS = RowShape<MODEL, DEG>;
+  double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], r[2], hr;
+#pragma unroll
+  for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;
+  obs_rows<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, Z0, Z1, I0, I1, P0, P1, r, &hr);
+  z[0] = z[1] = 0.0;
+  if (dirf) {
+#pragma unroll
+    for (int a = 0; a < 6; a++) {
+      z[0] += Z0[a] * dirf[a];
+      z[1] += Z1[a] * dirf[a];
+    }
+#pragma unroll
+    for (int q = 0; q < RS::kIntr; q++) {
+      z[0] += I0[q] * dirf[6 + q];
+      z[1] += I1[q] * dirf[6 + q];
+    }
+  }
+}
+
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(256) k_pass_a(
+    const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
+    const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, const double* __restrict__ dir,
+    const double* __restrict__ tinit, const double* __restrict__ V, const double* __restrict__ dp,
+    double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
+    double* __restrict__ sq_partial, int32_t flags, double cauchy_c) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = t / kLanesPerPointS;
+  const int sub = (int)(t % kLanesPerPointS);
+  const bool valid = p < npts;
+  double tv[3] = {0.0, 0.0, 0.0};
+  double4 X = make_double4(0, 0, 0, 0);
+  int64_t jb = 0, je = 0;
+  if (valid) {
+    X = pts[p];
+    jb = pt_begin[p];
+    je = pt_begin[p + 1];
+    for (int64_t j = jb + sub; j < je; j += kLanesPerPointS) {
+      const int32_t fr = po_frame[j];
+      const FrameDesc& F = fd[fr];
+      const double* rec = frec + (int64_t)fr * kFrameRecDoubles;
+      double z[2], P0[3], P1[3];
+      const double* dirf = dir ? dir + (int64_t)fr * kDirStride : nullptr;
+      const double2 m = po_meas[j];
+      if constexpr (MODEL >= 0) {
+        pass_a_obs<MODEL, DEG>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+      } else {
+        const int K = F.K;
+        if (K == 0) pass_a_obs<kModelNone, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+        else if (K == 1) pass_a_obs<kModelFov, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+        else if (K == 4 || K == 5) pass_a_obs<kModelRadtan, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+        else if (K == 20) pass_a_obs<kModelRpc, 1>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+        else if (K == 44) pass_a_obs<kModelRpc, 2>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+        else pass_a_obs<kModelRpc, 3>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+      }
+      double* zr = zbuf + 8 * j;
+      zr[0] = z[0]; zr[1] = z[1];
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        zr[2 + q] = P0[q];
+        zr[5 + q] = P1[q];
+        tv[q] += P0[q] * z[0] + P1[q] * z[1];
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < kLanesPerPointS; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < 3; q++) tv[q] += __shfl_xor(tv[q], off, 64);
+  double w[3] = {0.0, 0.0, 0.0};
+  double sq = 0.0;
+  if (valid && X.w != 0.0) {
+    if (tinit)
+      for (int q = 0; q < 3; q++) tv[q] += tinit[3 * p + q];
+    solve3(V + 6 * p, dp + 3 * p, tv, w);
+  }
+  if (valid) {
+    if (wout && sub == 0)
+      for (int q = 0; q < 3; q++) wout[3 * p + q] = w[q];
+    for (int64_t j = jb + sub; j < je; j += kLanesPerPointS) {
+      const double* zr = zbuf + 8 * j;
+      const double u0 = zr[0] - (zr[2] * w[0] + zr[3] * w[1] + zr[4] * w[2]);
+      const double u1 = zr[1] - (zr[5] * w[0] + zr[6] * w[1] + zr[7] * w[2]);
+      if (ubuf) {
+        ubuf[2 * j] = u0;
+        ubuf[2 * j + 1] = u1;
+      }
+      sq += u0 * u0 + u1 * u1;
+    }
+  }
+  if (sq_partial) {
+    __shared__ double red[256];
+    red[threadIdx.x] = sq;
+    __syncthreads();
+    for (int s2 = 128; s2 > 0; s2 >>= 1) {
+      if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) sq_partial[blockIdx.x] = red[0];
+  }
+}
+
+// ------------------------------------------------------------ pass B (frame order)
+// One wave per frame chunk: sum over its observations of Z^T u_o and J_I^T u_o,
+// wave-reduced, written to the chunk's slab record (no atomics).
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(64) k_pass_b(
+    const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
+    const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
+    const double2* __restrict__ obs_meas, const int32_t* __restrict__ slot_po,
+    const double* __restrict__ ubuf, double* __restrict__ slabb, int32_t flags, double cauchy_c) {
+  using RS = RowShape<MODEL, DEG>;
+  constexpr int NA = 6 + RS::kIntr;
+  const int lane = threadIdx.x;
+  const int ch = blockIdx.x;
+  if (ch >= nchunks) return;
+  const int4 c = chunks[ch];
+  const int frame = __builtin_amdgcn_readfirstlane(c.z);
+  const FrameDesc& F = fd[frame];
+  const double* __restrict__ rec = frec + (int64_t)frame * kFrameRecDoubles;
+  double acc[NA];
+#pragma unroll
+  for (int q = 0; q < NA; q++) acc[q] = 0.0;
+  for (int sidx = 0; sidx < c.y; sidx++) {
+    const Segment sg = segs[c.x + sidx];
+    const int count = __builtin_amdgcn_readfirstlane(sg.count);
+    if (lane < count) {
+      const int64_t i = (int64_t)sg.begin + lane;
+      const double4 X = pts[obs_pid[i]];
+      double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], P0[3], P1[3], r[2], hr;
+#pragma unroll
+      for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;
+      obs_rows<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, obs_meas[i], flags, cauchy_c, Z0, Z1, I0, I1, P0,
+                           P1, r, &hr);
+      const int64_t j = slot_po[i];  // point-order index of this observation
+      const double u0 = ubuf[2 * j], u1 = ubuf[2 * j + 1];
+#pragma unroll
+      for (int a = 0; a < 6; a++) acc[a] += Z0[a] * u0 + Z1[a] * u1;
+#pragma unroll
+      for (int q = 0; q < RS::kIntr; q++) acc[6 + q] += I0[q] * u0 + I1[q] * u1;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NA; q++) {
+    double v = acc[q];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    acc[q] = v;
+  }
+  if (lane == 0) {
+    double* out = slabb + (int64_t)(chunk_base + ch) * kSlabB;
+#pragma unroll
+    for (int q = 0; q < NA; q++) out[q] = acc[q];
+  }
+}
+
+// Per frame: sum chunk records, map through w to the pose columns, add into
+// replica (f mod kVecReplicas) of the camera-side vector.
+__global__ void __launch_bounds__(64) k_dir_expand(const FrameLin* __restrict__ fl, int32_t nframes,
+                                                   const FrameDesc* __restrict__ fd,
+                                                   const double* __restrict__ frec,
+                                                   const double* __restrict__ slabb,
+                                                   double* __restrict__ yrep, int64_t ng) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nframes) return;
+  const FrameLin L = fl[f];
+  const int NA = L.width - 1;  // 6 + intrinsics (the Gram width minus the residual column)
+  double acc[kSlabB];
+  for (int q = 0; q < NA; q++) acc[q] = 0.0;
+  for (int c = 0; c < L.chunk_count; c++) {
+    const double* s = slabb + (int64_t)(L.first_chunk + c) * kSlabB;
+    for (int q = 0; q < NA; q++) acc[q] += s[q];
+  }
+  double* y = yrep + (int64_t)(f & (kVecReplicas - 1)) * ng;
+  const double* w = frec + (int64_t)f * kFrameRecDoubles + 12;
+  for (int blk = 0; blk < 4; blk++) {
+    const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+    if (L.goff[b] < 0) continue;
+    const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
+    for (int cc = 0; cc < ncol; cc++) {
+      const double* wk = w + 6 * (k0 + cc);
+      double v = 0.0;
+      for (int a = 0; a < 6; a++) v += wk[a] * acc[a];
+      atomicAdd(&y[L.goff[b] + cc], v);
+    }
+  }
+  if (L.goff[MVBA_BLK_FOCAL] >= 0) atomicAdd(&y[L.goff[MVBA_BLK_FOCAL]], acc[6]);
+  if (L.goff[MVBA_BLK_CENTER] >= 0) {
+    atomicAdd(&y[L.goff[MVBA_BLK_CENTER]], acc[7]);
+    atomicAdd(&y[L.goff[MVBA_BLK_CENTER] + 1], acc[8]);
+  }
+  const int nd = NA - 9;
+  const int K = fd[f].K;
+  if (L.goff[MVBA_BLK_DIST] >= 0)
+    for (int q = 0; q < nd && q < K; q++) atomicAdd(&y[L.goff[MVBA_BLK_DIST] + q], acc[9 + q]);
+}
+
+// y = sum_r yrep[r]; replicas re-zeroed.
+__global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yrep, int64_t n,
+                                                        double* __restrict__ y) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double acc = 0.0;
+#pragma unroll 8
+  for (int r = 0; r < kVecReplicas; r++) {
+    acc += yrep[r * n + e];
+    yrep[r * n + e] = 0.0;
+  }
+  y[e] = acc;
+}
+
+// y += diag .* x (LM damping; applied after the cross-rank sum so it counts once)
+__global__ void k_add_diag(int64_t n, const double* __restrict__ diag, const double* __restrict__ x,
+                           double* __restrict__ y) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) y[e] += diag[e] * x[e];
+}
+
+// ------------------------------------------------------------ vectors / blocks
+// out = a*x + b*y (+ c*z)
+__global__ void k_axpby(int64_t n, double a, const double* __restrict__ x, double b,
+                        const double* __restrict__ y, double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) out[e] = a * x[e] + (y ? b * y[e] : 0.0);
+}
+
+// partial[block] = sum x.y (256-thread blocks)
+__global__ void __launch_bounds__(256) k_dot(int64_t n, const double* __restrict__ x,
+                                             const double* __restrict__ y, double* __restrict__ partial) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
+    acc += x[e] * (y ? y[e] : x[e]);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// out[0] = sum partial[0..n)
+__global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict__ partial,
+                                             double* __restrict__ out) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int64_t e = threadIdx.x; e < n; e += 256) acc += partial[e];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// Block-Jacobi preconditioner: Cholesky factor (in place, lower) of H_bb + diag(d)
+// per camera block (one thread per block; blocks are <= 76 wide).
+__global__ void k_block_chol(int32_t nblocks, const int64_t* __restrict__ goff,
+                             const int64_t* __restrict__ hoff, const int32_t* __restrict__ bsize,
+                             const double* __restrict__ hess, const double* __restrict__ d,
+                             double* __restrict__ fac) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const int n = bsize[b];
+  const double* H = hess + hoff[b];
+  double* Lm = fac + hoff[b];
+  const double* db = d + goff[b];
+  for (int i = 0; i < n; i++)
+    for (int j = 0; j < n; j++) Lm[i * n + j] = (j <= i) ? H[i * n + j] + (i == j ? db[i] : 0.0) : 0.0;
+  for (int j = 0; j < n; j++) {
+    double s = Lm[j * n + j];
+    for (int k = 0; k < j; k++) s -= Lm[j * n + k] * Lm[j * n + k];
+    // singular directions (e.g. constant-zero columns) fall back to identity
+    const double dj = (s > 1e-300) ? sqrt(s) : 1.0;
+    Lm[j * n + j] = dj;
+    for (int i = j + 1; i < n; i++) {
+      double v = Lm[i * n + j];
+      for (int k = 0; k < j; k++) v -= Lm[i * n + k] * Lm[j * n + k];
+      Lm[i * n + j] = (s > 1e-300) ? v / dj : 0.0;
+    }
+  }
+}
+
+// z = (L L^T)^-1 r per block
+__global__ void k_block_solve(int32_t nblocks, const int64_t* __restrict__ goff,
+                              const int64_t* __restrict__ hoff, const int32_t* __restrict__ bsize,
+                              const double* __restrict__ fac, const double* __restrict__ r,
+                              double* __restrict__ z) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const int n = bsize[b];
+  const double* Lm = fac + hoff[b];
+  const double* rb = r + goff[b];
+  double* zb = z + goff[b];
+  for (int i = 0; i < n; i++) {
+    double v = rb[i];
+    for (int k = 0; k < i; k++) v -= Lm[i * n + k] * zb[k];
+    zb[i] = v / Lm[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double v = zb[i];
+    for (int k = i + 1; k < n; k++) v -= Lm[k * n + i] * zb[k];
+    zb[i] = v / Lm[i * n + i];
+  }
+}
+
+// ---- compact free-parameter vectors: [camera-side entries (layout order) | 3 per point]
+// c = diag(J^T J) in compact order (camera blocks' Hessian diagonals, then V_p diagonals)
+__global__ void k_extract_diag(int32_t nblocks, const int64_t* __restrict__ goff, const int64_t* __restrict__ hoff,
+                               const int32_t* __restrict__ bsize, const double* __restrict__ hess, int64_t npts,
+                               const double* __restrict__ V, int64_t ng, double* __restrict__ c) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nblocks) {
+    const int n = bsize[t];
+    for (int i = 0; i < n; i++) c[goff[t] + i] = hess[hoff[t] + i * n + i];
+  } else if (t - nblocks < npts) {
+    const int64_t p = t - nblocks;
+    c[ng + 3 * p] = V[6 * p];
+    c[ng + 3 * p + 1] = V[6 * p + 3];
+    c[ng + 3 * p + 2] = V[6 * p + 5];
+  }
+}
+
+// Jacobi column scaling of Ceres' TrustRegionMinimizer [ext]: s = 1/(1+sqrt(c)),
+// computed once from the iteration-0 Jacobian.
+__global__ void k_jacobi_scale(int64_t n, const double* __restrict__ c, double* __restrict__ sc) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n) sc[e] = 1.0 / (1.0 + sqrt(c[e]));
+}
+
+// LevenbergMarquardtStrategy::ComputeStep [ext] on the scaled Jacobian J S:
+// D~^2 = clamp(s^2 c, min, max) / radius; unscaled damping = D~^2 / s^2.
+__global__ void k_lm_diag(int64_t n, const double* __restrict__ c, const double* __restrict__ sc,
+                          double inv_radius, double dmin, double dmax, double* __restrict__ d) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const double s2 = sc ? sc[e] * sc[e] : 1.0;
+  d[e] = fmin(fmax(s2 * c[e], dmin), dmax) * inv_radius / s2;
+}
+
+// compact <- packed parameters (constant points read as 0)
+__global__ void k_gather(int64_t ncam, const int64_t* __restrict__ cam_poff, int64_t npts,
+                         const int64_t* __restrict__ pt_off, const uint8_t* __restrict__ pt_free,
+                         const double* __restrict__ params, double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < ncam) {
+    out[e] = params[cam_poff[e]];
+  } else if (e < ncam + 3 * npts) {
+    const int64_t q = e - ncam, p = q / 3;
+    out[e] = pt_free[p] ? params[pt_off[p] + q % 3] : 0.0;
+  }
+}
+
+// packed parameters <- compact (constant points untouched)
+__global__ void k_scatter(int64_t ncam, const int64_t* __restrict__ cam_poff, int64_t npts,
+                          const int64_t* __restrict__ pt_off, const uint8_t* __restrict__ pt_free,
+                          const double* __restrict__ in, double* __restrict__ params) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < ncam) {
+    params[cam_poff[e]] = in[e];
+  } else if (e < ncam + 3 * npts) {
+    const int64_t q = e - ncam, p = q / 3;
+    if (pt_free[p]) params[pt_off[p] + q % 3] = in[e];
+  }
+}
+
+// out = Plus(x, delta) with bounds (ParameterBlock::Plus + box projection [ext])
+__global__ void k_plus(int64_t n, const double* __restrict__ x, const double* __restrict__ delta,
+                       const double* __restrict__ lower, const double* __restrict__ upper,
+                       double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  double v = x[e] + delta[e];
+  if (lower) v = fmax(v, lower[e]);
+  if (upper) v = fmin(v, upper[e]);
+  out[e] = v;
+}
+
+// partial[block] = max |x - Plus(x, -g)| (projected gradient, Ceres' gradient_max_norm)
+__global__ void __launch_bounds__(256) k_proj_grad_max(int64_t n, const double* __restrict__ x,
+                                                       const double* __restrict__ g,
+                                                       const double* __restrict__ lower,
+                                                       const double* __restrict__ upper,
+                                                       double* __restrict__ partial) {
+  __shared__ double red[256];
+  double m = 0.0;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    double v = x[e] - g[e];
+    if (lower) v = fmax(v, lower[e]);
+    if (upper) v = fmin(v, upper[e]);
+    m = fmax(m, fabs(x[e] - v));
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) k_max(int64_t n, const double* __restrict__ partial,
+                                             double* __restrict__ out) {
+  __shared__ double red[256];
+  double m = 0.0;
+  for (int64_t e = threadIdx.x; e < n; e += 256) m = fmax(m, partial[e]);
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// cost only (sum 0.5 rho) of one model group, partial per 256-thread block
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(256) k_cost(const Segment* __restrict__ segs, int32_t nseg,
+                                              const FrameDesc* __restrict__ fd,
+                                              const double* __restrict__ frec,
+                                              const double* __restrict__ params,
+                                              const double4* __restrict__ pts,
+                                              const int32_t* __restrict__ obs_pid,
+                                              const double2* __restrict__ obs_meas, int32_t flags,
+                                              double cauchy_c, double* __restrict__ partial) {
+  __shared__ double red[4];
+  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  double hr = 0.0;
+  if (wave < nseg) {
+    const Segment sg = segs[wave];
+    const int count = __builtin_amdgcn_readfirstlane(sg.count);
+    const int frame = __builtin_amdgcn_readfirstlane(sg.frame);
+    if (lane < count) {
+      const int64_t i = (int64_t)sg.begin + lane;
+      const FrameDesc& F = fd[frame];
+      const double* rec = frec + (int64_t)frame * kFrameRecDoubles;
+      const double4 X = pts[obs_pid[i]];
+      const double2 m = obs_meas[i];
+      Proj o;
+      project<MODEL, DEG>(rec, X.x, X.y, X.z, params[F.off[MVBA_BLK_FOCAL]], params[F.off[MVBA_BLK_CENTER]],
+                          params[F.off[MVBA_BLK_CENTER] + 1], params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+      loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) hr += __shfl_xor(hr, off, 64);
+  if (lane == 0) red[threadIdx.x >> 6] = hr;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+}  // namespace mvba
+
+// ------------------------------------------------------------ launchers
+#define MVBA_SOLVER_SWITCH(model, deg, CALL)                       \
+  switch (model) {                                                 \
+    case mvba::kModelNone: CALL(mvba::kModelNone, 0); break;       \
+    case mvba::kModelFov: CALL(mvba::kModelFov, 0); break;         \
+    case mvba::kModelRadtan: CALL(mvba::kModelRadtan, 0); break;   \
+    case mvba::kModelRpc:                                          \
+      switch (deg) {                                               \
+        case 1: CALL(mvba::kModelRpc, 1); break;                   \
+        case 2: CALL(mvba::kModelRpc, 2); break;                   \
+        case 3: CALL(mvba::kModelRpc, 3); break;                   \
+        default: return hipErrorInvalidValue;                      \
+      }                                                            \
+      break;                                                       \
+    default: return hipErrorInvalidValue;                          \
+  }
+
+extern "C" {
+
+int mvba_solver_dir_stride(void) { return mvba::kDirStride; }
+int mvba_solver_slabb_stride(void) { return mvba::kSlabB; }
+int mvba_solver_vec_replicas(void) { return mvba::kVecReplicas; }
+
+hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
+                                 const double* x, double* dir, hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_frame_dir, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s,
+                     (const mvba::FrameLin*)fl, nframes, fd, frec, x, dir);
+  return hipGetLastError();
+}
+
+// model < 0: mixed camera models (runtime dispatch per observation)
+hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
+                              const double2* po_meas, const mvba::FrameDesc* fd, const double* frec,
+                              const double* params, const double4* pts, const double* dir, const double* tinit,
+                              const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
+                              double* sq_partial, int32_t flags, double cauchy_c, hipStream_t s,
+                              int64_t* nblocks_out) {
+  const unsigned blocks = (unsigned)((npts * mvba::kLanesPerPointS + 255) / 256);
+  if (nblocks_out) *nblocks_out = blocks;
+  if (npts <= 0) return hipSuccess;
+  if (model < 0) {
+    hipLaunchKernelGGL((mvba::k_pass_a<-1, 0>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, fd,
+                       frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, flags, cauchy_c);
+    return hipGetLastError();
+  }
+#define MVBA_PA(M, D)                                                                                      \
+  hipLaunchKernelGGL((mvba::k_pass_a<M, D>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, \
+                     fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, flags, cauchy_c)
+  MVBA_SOLVER_SWITCH(model, deg, MVBA_PA)
+#undef MVBA_PA
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
+                              const mvba::Segment* segs, const mvba::FrameDesc* fd, const double* frec,
+                              const double* params, const double4* pts, const int32_t* obs_pid,
+                              const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* slabb,
+                              int32_t flags, double cauchy_c, hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+#define MVBA_PB(M, D)                                                                                      \
+  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks,       \
+                     chunk_base, segs, fd, frec, params, pts, obs_pid, obs_meas, slot_po, ubuf, slabb, flags, \
+                     cauchy_c)
+  MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)
+#undef MVBA_PB
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_dir_expand(const void* fl, int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
+                                  const double* slabb, double* yrep, int64_t ng, double* y, hipStream_t s) {
+  if (nframes > 0)
+    hipLaunchKernelGGL(mvba::k_dir_expand, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s,
+                       (const mvba::FrameLin*)fl, nframes, fd, frec, slabb, yrep, ng);
+  if (ng > 0)
+    hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, y);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_add_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, diag, x, y);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
+                             hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_axpby, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a, x, b, y, out);
+  return hipGetLastError();
+}
+
+// dot(x, y) -> out (device scalar) via partials[256]
+hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, double* out,
+                           hipStream_t s) {
+  const int blocks = 256;
+  hipLaunchKernelGGL(mvba::k_dot, dim3(blocks), dim3(256), 0, s, n, x, y, partial);
+  hipLaunchKernelGGL(mvba::k_sum, dim3(1), dim3(256), 0, s, (int64_t)blocks, partial, out);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_sum(int64_t n, const double* partial, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(mvba::k_sum, dim3(1), dim3(256), 0, s, n, partial, out);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_block_chol(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
+                                  const double* hess, const double* d, double* fac, hipStream_t s) {
+  if (nblocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_block_chol, dim3((unsigned)((nblocks + 63) / 64)), dim3(64), 0, s, nblocks, goff,
+                     hoff, bsize, hess, d, fac);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_block_solve(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
+                                   const double* fac, const double* r, double* z, hipStream_t s) {
+  if (nblocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_block_solve, dim3((unsigned)((nblocks + 63) / 64)), dim3(64), 0, s, nblocks, goff,
+                     hoff, bsize, fac, r, z);
+  return hipGetLastError();
+}
+
+static inline dim3 grid1(int64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+hipError_t mvba_launch_extract_diag(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
+                                    const double* hess, int64_t npts, const double* V, int64_t ng, double* c,
+                                    hipStream_t s) {
+  const int64_t n = nblocks + npts;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_extract_diag, grid1(n), dim3(256), 0, s, nblocks, goff, hoff, bsize, hess, npts, V,
+                     ng, c);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_jacobi_scale(int64_t n, const double* c, double* sc, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_jacobi_scale, grid1(n), dim3(256), 0, s, n, c, sc);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_lm_diag(int64_t n, const double* c, const double* sc, double inv_radius, double dmin,
+                               double dmax, double* d, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_lm_diag, grid1(n), dim3(256), 0, s, n, c, sc, inv_radius, dmin, dmax, d);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_gather(int64_t ncam, const int64_t* cam_poff, int64_t npts, const int64_t* pt_off,
+                              const uint8_t* pt_free, const double* params, double* out, hipStream_t s) {
+  const int64_t n = ncam + 3 * npts;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_gather, grid1(n), dim3(256), 0, s, ncam, cam_poff, npts, pt_off, pt_free, params, out);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_scatter(int64_t ncam, const int64_t* cam_poff, int64_t npts, const int64_t* pt_off,
+                               const uint8_t* pt_free, const double* in, double* params, hipStream_t s) {
+  const int64_t n = ncam + 3 * npts;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_scatter, grid1(n), dim3(256), 0, s, ncam, cam_poff, npts, pt_off, pt_free, in, params);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_plus(int64_t n, const double* x, const double* delta, const double* lower,
+                            const double* upper, double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_plus, grid1(n), dim3(256), 0, s, n, x, delta, lower, upper, out);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_proj_grad_max(int64_t n, const double* x, const double* g, const double* lower,
+                                     const double* upper, double* partial, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(mvba::k_proj_grad_max, dim3(256), dim3(256), 0, s, n, x, g, lower, upper, partial);
+  hipLaunchKernelGGL(mvba::k_max, dim3(1), dim3(256), 0, s, (int64_t)256, partial, out);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_cost(int model, int deg, const mvba::Segment* segs, int32_t nseg, const mvba::FrameDesc* fd,
+                            const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
+                            const double2* obs_meas, int32_t flags, double cauchy_c, double* partial, hipStream_t s,
+                            int64_t* nblocks_out) {
+  const unsigned blocks = (unsigned)((nseg + 3) / 4);
+  if (nblocks_out) *nblocks_out = blocks;
+  if (nseg <= 0) return hipSuccess;
+#define MVBA_CO(M, D)                                                                                       \
+  hipLaunchKernelGGL((mvba::k_cost<M, D>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec, params, pts, \
+                     obs_pid, obs_meas, flags, cauchy_c, partial)
+  MVBA_SOLVER_SWITCH(model, deg, MVBA_CO)
+#undef MVBA_CO
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -55,7 +55,7 @@ struct FrameLinHost {
   int64_t slab_off;
   int32_t chunk_count;
   int32_t width, w16;
-  int32_t pad;
+  int32_t first_chunk;
   int64_t goff[8];
   int64_t hoff[8];
 };

@@ -67,3 +67,63 @@ class NormalEquationBuffer:
         import torch.distributed as dist
 
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+
+
+_HIP = None
+
+
+def _hip():
+    """libamdhip64 (already loaded by torch) for raw-pointer copies in the callback."""
+    global _HIP
+    if _HIP is None:
+        import ctypes as C
+
+        lib = C.CDLL("libamdhip64.so")
+        lib.hipMemcpy.restype = C.c_int
+        lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        _HIP = lib
+    return _HIP
+
+
+class SolverExchange:
+    """The mvba_allreduce_fn of a sharded mvba_solve, over torch.distributed.
+
+    The library hands a raw device pointer; it is staged through a persistent
+    buffer (device memory for RCCL — backend "nccl" — host memory for gloo),
+    all-reduced in place, and copied back. Calls are synchronous, as the ABI
+    requires."""
+
+    H2D, D2H, D2D = 1, 2, 3
+
+    def __init__(self, device=None):
+        import torch
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.on_device = dist.get_backend() == "nccl"
+        self.device = device if self.on_device else "cpu"
+        self.buf = torch.empty(0, dtype=torch.float64, device=self.device)
+        self.calls = 0
+        self.doubles = 0
+
+    def __call__(self, ptr: int, count: int, op: int):
+        import torch
+
+        if self.buf.numel() < count:
+            self.buf = torch.empty(max(count, 2 * self.buf.numel()), dtype=torch.float64, device=self.device)
+        view = self.buf[:count]
+        nbytes = count * 8
+        kind_in = self.D2D if self.on_device else self.D2H
+        kind_out = self.D2D if self.on_device else self.H2D
+        hip = _hip()
+        if self.on_device:
+            torch.cuda.synchronize(self.device)
+        if hip.hipMemcpy(view.data_ptr(), ptr, nbytes, kind_in) != 0:
+            raise RuntimeError("hipMemcpy into the exchange buffer failed")
+        self.dist.all_reduce(view, op=self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX)
+        if self.on_device:
+            torch.cuda.synchronize(self.device)
+        if hip.hipMemcpy(ptr, view.data_ptr(), nbytes, kind_out) != 0:
+            raise RuntimeError("hipMemcpy out of the exchange buffer failed")
+        self.calls += 1
+        self.doubles += count

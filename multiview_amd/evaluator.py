@@ -123,6 +123,23 @@ class Evaluator:
                                             C.c_void_p(stream or 0))
         _lib.check(st, self.h)
 
+    # ---------------------------------------------------------------- solver
+    def get_params(self) -> np.ndarray:
+        out = np.empty(self.problem.params.size, dtype=np.float64)
+        _lib.check(self.lib.mvba_get_params(self.h, out.ctypes.data), self.h)
+        return out
+
+    def solve(self, options: "_lib.SolverOptions | None" = None, stream=None, **kw) -> dict:
+        """Levenberg-Marquardt on the GPU from the current parameters
+        (mvba_solve; ceres::Solve replacement). Keyword arguments override
+        fields of mvba_solver_default_options. Returns the summary as a dict;
+        the solution stays in the handle (get_params)."""
+        o = options or default_solver_options(**kw)
+        s = _lib.SolverSummary()
+        st = self.lib.mvba_solve(self.h, C.byref(o), C.byref(s), C.c_void_p(stream or 0))
+        _lib.check(st, self.h)
+        return summary_dict(s)
+
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
             self.lib.mvba_destroy(self.h)
@@ -139,3 +156,49 @@ class Evaluator:
 
     def __exit__(self, *a):
         self.close()
+
+
+def default_solver_options(**kw) -> _lib.SolverOptions:
+    """mvba_solver_default_options, then overrides (lower_bounds/upper_bounds as
+    numpy arrays over the packed parameter vector; allreduce as a Python callable
+    ``f(device_ptr, count, op) -> None``)."""
+    lib = _lib.load()
+    o = _lib.SolverOptions()
+    lib.mvba_solver_default_options(C.byref(o))
+    keep = []
+    for k, v in kw.items():
+        if k in ("lower_bounds", "upper_bounds"):
+            if v is None:
+                continue
+            arr = np.ascontiguousarray(v, dtype=np.float64)
+            keep.append(arr)
+            setattr(o, k, arr.ctypes.data)
+        elif k == "allreduce":
+            if v is None:
+                continue
+
+            def _cb(ptr, count, op, stream, user, _f=v):
+                try:
+                    _f(ptr, count, op)
+                    return 0
+                except Exception as e:  # noqa: BLE001 - reported as a failed status
+                    print(f"allreduce callback failed: {e!r}")
+                    return 1
+            fn = _lib.AllreduceFn(_cb)
+            keep.append(fn)
+            o.allreduce = fn
+        else:
+            if not hasattr(o, k):
+                raise AttributeError(f"unknown solver option {k}")
+            setattr(o, k, v)
+    o._keep = keep  # keep arrays / callback alive for the call
+    return o
+
+
+def summary_dict(s: _lib.SolverSummary) -> dict:
+    return dict(initial_cost=s.initial_cost, final_cost=s.final_cost, num_iterations=s.num_iterations,
+                num_successful_steps=s.num_successful_steps, num_unsuccessful_steps=s.num_unsuccessful_steps,
+                num_linear_iterations=s.num_linear_iterations, termination_type=s.termination_type,
+                total_time_s=s.total_time_s, linearize_time_s=s.linearize_time_s,
+                linear_solver_time_s=s.linear_solver_time_s, eval_time_s=s.eval_time_s,
+                message=s.message.decode(errors="replace"))

@@ -541,3 +541,35 @@ CONFIGS = {
     "c3": dict(num_sensors=3, num_ref=3000, num_points=1000000, obs_per_point=10.0, models=["rpc2"] * 3, seed=1003),
     "c4": dict(num_sensors=8, num_ref=2500, num_points=5000000, obs_per_point=10.0, models=["radtan"] * 8, seed=1004),
 }
+
+
+def offset_bounds(rig: Rig, problem: CamProblem, flags: FloatFlags | None = None, max_change: float = 1.0):
+    """Lower/upper bounds (packed vector, +-inf elsewhere) of the floated timestamp
+    offsets: the range keeping every bracketed image inside its bracket, clamped to
+    offset +- timestamp_offsets_max_change and tightened by 1e-5
+    (dense_map_utils.cc:1603-1656, applied at rig_calibrator.cc:1741-1745)."""
+    flags = flags or FloatFlags()
+    lower = np.full(problem.params.size, -np.inf)
+    upper = np.full(problem.params.size, np.inf)
+    if flags.no_rig or not flags.float_timestamp_offsets:
+        return lower, upper
+    ns = rig.num_sensors
+    lo = np.full(ns, -1.0e100)
+    hi = np.full(ns, 1.0e100)
+    for k in range(len(rig.cam_type)):
+        t = rig.cam_type[k]
+        if t == 0:
+            continue
+        lo[t] = max(lo[t], rig.cam_stamp[k] - rig.ref_stamps[rig.cam_end[k]])
+        hi[t] = min(hi[t], rig.cam_stamp[k] - rig.ref_stamps[rig.cam_beg[k]])
+    # offsets block of sensor s: residual_blocks[:, 4] for that camera
+    for s in range(1, ns):
+        sel = np.nonzero(problem.residual_camera == s)[0]
+        if sel.size == 0:
+            continue
+        b = int(problem.residual_blocks[sel[0], 4])
+        o = int(problem.block_offset[b])
+        cur = problem.params[o]
+        lower[o] = max(lo[s], cur - max_change) + 1.0e-5
+        upper[o] = min(hi[s], cur + max_change) - 1.0e-5
+    return lower, upper

@@ -1,0 +1,154 @@
+"""CPU reference of the solver path — TEST INFRASTRUCTURE ONLY.
+
+Levenberg-Marquardt with the control flow of Ceres 1.14's TrustRegionMinimizer +
+LevenbergMarquardtStrategy [ext, not vendored] (the solver rig_calibrator.cc:1910-1919
+configures), with EXACT linear solves (dense Cholesky of J'J + D) in place of
+ITERATIVE_SCHUR's truncated CG, on the Jacobian of oracle.cpp (the restatement of
+BracketedCamError, rig_calibrator.cc:419-514). Used by tests to check that
+mvba_solve converges to the same parameters. Parity unpinned (Ceres is absent from
+this image: no reference solver run is available to compare trajectories with).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from . import oracle_py
+
+FIXED = (7, 7, 7, 3, 1, 1, 2)
+
+
+def _columns(P):
+    """Free parameter columns: non-constant blocks referenced by residuals, in
+    block-id order (points included)."""
+    K_of = P.camera_dist_size[P.residual_camera]
+    used = np.zeros(len(P.block_size), dtype=bool)
+    for b in range(7):
+        used[P.residual_blocks[:, b]] = True
+    used[P.residual_blocks[K_of > 0, 7]] = True
+    free = np.nonzero(used & (P.block_constant == 0))[0]
+    col = np.full(len(P.block_size), -1, dtype=np.int64)
+    pos = 0
+    idx = []
+    for b in free:
+        col[b] = pos
+        o, n = int(P.block_offset[b]), int(P.block_size[b])
+        idx.extend(range(o, o + n))
+        pos += n
+    return col, np.array(idx, dtype=np.int64)
+
+
+def _jacobian(P, params, col, ncols, use_loss, thr):
+    from multiview_amd._lib import JAC_BASE
+    Q = dataclasses.replace(P, params=params)
+    cost, r, J = oracle_py.evaluate(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
+    N = P.num_residuals
+    D = np.zeros((2 * N, ncols))
+    K_of = P.camera_dist_size[P.residual_camera]
+    rows = np.arange(N)
+    for b in range(8):
+        size = FIXED[b] if b < 7 else None
+        for K in (np.unique(K_of) if b == 7 else [None]):
+            sel = rows if b < 7 else rows[K_of == K]
+            n = size if b < 7 else int(K)
+            if n == 0 or sel.size == 0:
+                continue
+            c0 = col[P.residual_blocks[sel, b]]
+            ok = c0 >= 0
+            Jb = J[sel, JAC_BASE[b]:JAC_BASE[b] + 2 * n].reshape(-1, 2, n)
+            for k in range(n):
+                for comp in range(2):
+                    np.add.at(D, (2 * sel[ok] + comp, c0[ok] + k), Jb[ok, comp, k])
+    return cost, r.reshape(-1), D
+
+
+def _cost(P, params, use_loss, thr):
+    Q = dataclasses.replace(P, params=params)
+    c, _, _ = oracle_py.evaluate(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
+    return c
+
+
+def solve(P, max_num_iterations=50, function_tolerance=1e-6, gradient_tolerance=1e-10,
+          parameter_tolerance=1e-8, use_loss=False, robust_threshold=3.0, lower_bounds=None,
+          upper_bounds=None, initial_trust_region_radius=1e4, jacobi_scaling=True):
+    """Returns (packed params, summary dict). Bounds: packed arrays (projection only,
+    no line search: used by tests on problems where the bounds are inactive)."""
+    col, idx = _columns(P)
+    n = idx.size
+    params = P.params.copy()
+    lo = lower_bounds[idx] if lower_bounds is not None else None
+    hi = upper_bounds[idx] if upper_bounds is not None else None
+
+    def plus(x, d):
+        v = x + d
+        if lo is not None:
+            v = np.maximum(v, lo)
+        if hi is not None:
+            v = np.minimum(v, hi)
+        return v
+
+    def with_x(x):
+        p = params.copy()
+        p[idx] = x
+        return p
+
+    x = params[idx].copy()
+    cost, r, J = _jacobian(P, with_x(x), col, n, use_loss, robust_threshold)
+    g = J.T @ r
+    c = np.einsum("ij,ij->j", J, J)
+    s = 1.0 / (1.0 + np.sqrt(c)) if jacobi_scaling else np.ones(n)
+    gmax = np.abs(x - plus(x, -g)).max() if n else 0.0
+    radius, decrease = initial_trust_region_radius, 2.0
+    it, successful = 0, True
+    summary = dict(initial_cost=cost, iterations=0, successful=1, unsuccessful=0, message="")
+    while True:
+        if it >= max_num_iterations:
+            summary["message"] = "max iterations"
+            break
+        if successful and gmax <= gradient_tolerance:
+            summary["message"] = "gradient tolerance"
+            break
+        if radius <= 1e-32:
+            summary["message"] = "min radius"
+            break
+        it += 1
+        dg = np.clip(s * s * c, 1e-6, 1e32) / radius / (s * s)
+        A = J.T @ J + np.diag(dg)
+        delta = -np.linalg.solve(A, g)
+        Jd = J @ delta
+        mcc = -(g @ delta + 0.5 * Jd @ Jd)
+        if not (mcc > 0):
+            radius /= decrease
+            decrease *= 2
+            successful = False
+            summary["unsuccessful"] += 1
+            continue
+        xn = plus(x, delta)
+        cand = _cost(P, with_x(xn), use_loss, robust_threshold)
+        xnorm = np.linalg.norm(x)
+        if np.linalg.norm(xn - x) <= parameter_tolerance * (xnorm + parameter_tolerance):
+            summary["message"] = "parameter tolerance"
+            break
+        change = cost - cand
+        if abs(change) <= function_tolerance * cost:
+            summary["message"] = "function tolerance"
+            break
+        ratio = change / mcc
+        if ratio > 1e-3:
+            x = xn
+            cost, r, J = _jacobian(P, with_x(x), col, n, use_loss, robust_threshold)
+            g = J.T @ r
+            c = np.einsum("ij,ij->j", J, J)
+            gmax = np.abs(x - plus(x, -g)).max()
+            radius = min(1e16, radius / max(1.0 / 3.0, 1.0 - (2.0 * ratio - 1.0) ** 3))
+            decrease = 2.0
+            successful = True
+            summary["successful"] += 1
+        else:
+            radius /= decrease
+            decrease *= 2
+            successful = False
+            summary["unsuccessful"] += 1
+    summary.update(final_cost=cost, iterations=it)
+    return with_x(x), summary

@@ -1,0 +1,264 @@
+"""GPU Levenberg-Marquardt (mvba_solve) against the CPU reference LM
+(oracle/lm_reference.py: Ceres 1.14 control flow, exact dense linear solves).
+
+* one LM iteration with CG run to convergence (eta ~ 0) must equal the exact
+  step: relative 1e-8;
+* full solves (Ceres tolerances of rig_calibrator.cc:1914-1917) must converge to
+  the same parameters: |dx| <= 1e-6 max(1, |x|) (north_star), cost rtol 1e-9;
+* a landmark-sharded solve over two ranks (gloo exchange through the
+  mvba_allreduce_fn callback, both ranks on cuda:0) must match the unsharded one.
+Problems keep the reference poses constant (camera_poses_to_float empty) so the
+minimum is unique (no gauge freedom)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from multiview_amd import rig
+from multiview_amd.evaluator import Evaluator
+
+pytestmark = pytest.mark.gpu
+
+TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
+FLAGS = rig.FloatFlags(camera_poses_to_float=())
+
+
+def _problem(models, seed, num_points=300, flags=FLAGS):
+    R = rig.make_rig(num_sensors=len(models), num_ref=12, num_points=num_points, obs_per_point=5,
+                     models=models, seed=seed)
+    P = rig.build_problem(R, flags)
+    return R, P
+
+
+def _close(a, b, rel):
+    return np.abs(a - b).max() <= rel * max(1.0, np.abs(b).max())
+
+
+def _free_mask(P):
+    m = np.zeros(P.params.size, dtype=bool)
+    for b in np.nonzero(P.block_constant == 0)[0]:
+        o = int(P.block_offset[b])
+        m[o:o + int(P.block_size[b])] = True
+    return m
+
+
+@pytest.mark.parametrize("use_loss", [False, True])
+def test_one_exact_step_matches_dense_lm(use_loss):
+    from oracle import lm_reference
+
+    _, P = _problem(["radtan", "fov", "rpc1"], seed=31)
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=1, use_loss=use_loss, **TOL)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=2000, use_loss=int(use_loss),
+                     robust_threshold=3.0, **TOL)
+        x = ev.get_params()
+    assert np.isclose(s["initial_cost"], s_ref["initial_cost"], rtol=1e-11)
+    assert s["num_iterations"] == 1
+    m = _free_mask(P)
+    assert _close(x[m], x_ref[m], 1e-8), np.abs(x[m] - x_ref[m]).max()
+    assert np.array_equal(x[~m], P.params[~m])
+
+
+def _poses(P, x):
+    """Free 7-parameter blocks as (t, q/|q| with qw >= 0): the cost only sees the
+    normalized quaternion (array_to_rigid_transform, dense_map_utils.cc:171-178),
+    so |q| is a gauge direction the comparison must ignore."""
+    out = []
+    for b in np.nonzero((P.block_size == 7) & (P.block_constant == 0))[0]:
+        o = int(P.block_offset[b])
+        q = x[o + 3:o + 7] / np.linalg.norm(x[o + 3:o + 7])
+        out.append(np.r_[x[o:o + 3], q * np.sign(q[3])])
+    return np.array(out)
+
+
+def _others(P, x):
+    m = np.zeros(x.size, dtype=bool)
+    for b in np.nonzero((P.block_size != 7) & (P.block_constant == 0))[0]:
+        o = int(P.block_offset[b])
+        m[o:o + int(P.block_size[b])] = True
+    return x[m]
+
+
+INTR_ALL = ("focal_length", "optical_center", "distortion")
+
+
+@pytest.mark.parametrize("models,use_loss,intr", [
+    (["radtan", "fov", "none"], False, INTR_ALL),
+    (["radtan", "fov", "none"], True, INTR_ALL),
+    (["none", "none", "none"], False, INTR_ALL),
+    (["rpc2", "rpc2"], True, ("focal_length", "optical_center")),
+])
+def test_converged_params_match_cpu_lm(models, use_loss, intr):
+    """Poses within 1e-6 (north_star) and every other free parameter within 1e-6
+    relative of the CPU LM. (Two CPU runs with different initial radii agree to
+    ~5e-10 on poses and ~5e-8 elsewhere on these problems.)"""
+    from oracle import lm_reference
+
+    R = rig.make_rig(num_sensors=len(models), num_ref=12, num_points=300, obs_per_point=5, models=models,
+                     seed=43 + len(models) + int(use_loss))
+    P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=(), intrinsics_to_float=intr))
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=use_loss, **TOL)
+    assert s_ref["message"] in ("parameter tolerance", "function tolerance", "gradient tolerance")
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=200, use_loss=int(use_loss), robust_threshold=3.0, **TOL)
+        x = ev.get_params()
+    assert s["termination_type"] == 0, s["message"]
+    assert s["final_cost"] < s["initial_cost"]
+    assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-9)
+    assert np.abs(_poses(P, x) - _poses(P, x_ref)).max() <= 1e-6
+    assert _close(_others(P, x), _others(P, x_ref), 1e-6)
+
+
+def test_ill_conditioned_rpc_reaches_same_cost():
+    """RPC distortion floated with focal and center is ill-conditioned (CPU runs
+    with different radii differ by ~1e-3 in RPC coefficients): require the same
+    final cost and a parameter difference invisible to the cost at the CPU's
+    solution, 0.5 dx' J'J dx <= 1e-9 cost."""
+    from oracle import lm_reference
+
+    R = rig.make_rig(num_sensors=3, num_ref=12, num_points=300, obs_per_point=5,
+                     models=["radtan", "fov", "rpc1"], seed=43)
+    P = rig.build_problem(R, FLAGS)
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, **TOL)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=200, **TOL)
+        x = ev.get_params()
+    assert s["termination_type"] == 0, s["message"]
+    assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-9)
+    col, idx = lm_reference._columns(P)
+    _, _, J = lm_reference._jacobian(P, x_ref, col, idx.size, False, 3.0)
+    dx = x[idx] - x_ref[idx]
+    # quaternion-norm gauge: compare at equal |q| by removing the component along q
+    for b in np.nonzero((P.block_size == 7) & (P.block_constant == 0))[0]:
+        c = col[b] + 3
+        q = x_ref[idx[c:c + 4]]
+        dx[c:c + 4] -= q * (dx[c:c + 4] @ q) / (q @ q)
+    Jd = J @ dx
+    assert 0.5 * Jd @ Jd <= 1e-9 * s_ref["final_cost"]
+
+
+def test_bounded_offsets_and_callback_path():
+    """Floated timestamp offsets carry the reference's bracket bounds; a no-op
+    allreduce callback (single rank) must not change the result."""
+    R, P = _problem(["radtan", "radtan", "fov"], seed=55)
+    lo, hi = rig.offset_bounds(R, P, FLAGS)
+    assert np.isfinite(lo).sum() == 2
+    calls = []
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s0 = ev.solve(max_num_iterations=100, lower_bounds=lo, upper_bounds=hi, **TOL)
+        x0 = ev.get_params()
+        ev.set_params()
+        s1 = ev.solve(max_num_iterations=100, lower_bounds=lo, upper_bounds=hi,
+                      allreduce=lambda ptr, n, op: calls.append((n, op)), **TOL)
+        x1 = ev.get_params()
+    assert calls and all(op in (0, 1) for _, op in calls)
+    assert s0["termination_type"] == 0 and s1["termination_type"] == 0
+    assert np.array_equal(x0, x1)
+    assert np.all(x0 >= lo) and np.all(x0 <= hi)
+
+
+def test_solver_rejects_bad_options():
+    from multiview_amd._lib import MvbaError
+
+    _, P = _problem(["radtan"], seed=60, num_points=50)
+    with Evaluator(P) as ev:
+        with pytest.raises(MvbaError):
+            ev.solve()  # parameters not set
+        ev.set_params()
+        with pytest.raises(MvbaError):
+            ev.solve(use_loss=1, robust_threshold=0.0)
+        with pytest.raises(MvbaError):
+            ev.solve(max_linear_solver_iterations=0)
+
+
+# ---------------------------------------------------------------- sharded solve
+CFG = dict(num_sensors=3, num_ref=12, num_points=400, obs_per_point=5, models=["radtan", "fov", "rpc1"], seed=77)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cam_values(ev, P):
+    L = ev.lin_layout()
+    return np.concatenate([P.block_values(int(b)) for b in L["cam_block_ids"]])
+
+
+def _shard_worker(rank, world, port, out_dir):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    from multiview_amd.dist import SolverExchange, check_layouts_agree, shard_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_range(CFG["num_points"], world, rank)
+    R = rig.make_rig(**dict(CFG, point_range=(lo, hi)))
+    P = rig.build_problem(R, FLAGS)
+    with Evaluator(P, device=0) as ev:
+        check_layouts_agree(ev.lin_layout(), P.block_size)
+        ev.set_params()
+        ex = SolverExchange()
+        s = ev.solve(max_num_iterations=100, allreduce=ex, **TOL)
+        P.params = ev.get_params()
+        cam = _cam_values(ev, P)
+        pts = np.concatenate([P.block_values(int(b)) for b in ev.lin_layout()["point_block_ids"]])
+    np.save(os.path.join(out_dir, f"cam{rank}.npy"), cam)
+    np.save(os.path.join(out_dir, f"pts{rank}.npy"), pts)
+    np.save(os.path.join(out_dir, f"cost{rank}.npy"), np.array([s["final_cost"], s["termination_type"]]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_solve_matches_unsharded(tmp_path):
+    import torch.multiprocessing as mp
+
+    from multiview_amd.dist import shard_range
+
+    world = 2
+    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    cams = [np.load(tmp_path / f"cam{r}.npy") for r in range(world)]
+    pts = np.concatenate([np.load(tmp_path / f"pts{r}.npy") for r in range(world)])
+    costs = [np.load(tmp_path / f"cost{r}.npy") for r in range(world)]
+    assert np.array_equal(cams[0], cams[1])
+    assert costs[0][1] == 0 and costs[0][0] == costs[1][0]
+    # unsharded problem = union of the shards' landmarks
+    parts = [rig.make_rig(**dict(CFG, point_range=shard_range(CFG["num_points"], world, r))) for r in range(world)]
+    R0 = parts[0]
+    off = 0
+    xyz, init_xyz, pid, cid, pix = [], [], [], [], []
+    for Rk in parts:
+        xyz.append(Rk.xyz)
+        init_xyz.append(Rk.init["xyz"])
+        pid.append(Rk.obs_pid + off)
+        cid.append(Rk.obs_cid)
+        pix.append(Rk.obs_pix)
+        off += Rk.xyz.shape[0]
+    R0.xyz = np.concatenate(xyz)
+    R0.init["xyz"] = np.concatenate(init_xyz)
+    R0.obs_pid, R0.obs_cid, R0.obs_pix = np.concatenate(pid), np.concatenate(cid), np.concatenate(pix)
+    P = rig.build_problem(R0, FLAGS)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=100, **TOL)
+        P.params = ev.get_params()
+        cam = _cam_values(ev, P)
+        pts_ref = np.concatenate([P.block_values(int(b)) for b in ev.lin_layout()["point_block_ids"]])
+    assert s["termination_type"] == 0
+    assert np.isclose(costs[0][0], s["final_cost"], rtol=1e-9)
+    assert _close(cams[0], cam, 1e-6)
+    # point order: first use in residual order = shard 0's points then shard 1's
+    assert _close(pts, pts_ref, 1e-6)
