@@ -26,33 +26,37 @@
 
 extern "C" {
 int mvba_solver_dir_stride(void);
-int mvba_solver_slabb_stride(void);
 int mvba_solver_vec_replicas(void);
+int64_t mvba_pass_a_blocks(int64_t npts);
 hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const FrameDesc* fd, const double* frec,
                                  const double* x, double* dir, hipStream_t s);
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
                               const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
-                              double* sq_partial, int32_t flags, double cauchy_c, hipStream_t s,
-                              int64_t* nblocks_out);
+                              double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
+                              hipStream_t s);
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
-                              const Segment* segs, const FrameDesc* fd, const double* frec, const double* params,
-                              const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
-                              const int32_t* slot_po, const double* ubuf, double* slabb, int32_t flags,
-                              double cauchy_c, hipStream_t s);
-hipError_t mvba_launch_dir_expand(const void* fl, int32_t nframes, const FrameDesc* fd, const double* frec,
-                                  const double* slabb, double* yrep, int64_t ng, double* y, hipStream_t s);
-hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, hipStream_t s);
+                              const Segment* segs, const FrameDesc* fd, const void* fl, const double* frec,
+                              const double* params, const double4* pts, const int32_t* obs_pid,
+                              const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* yrep,
+                              int64_t ng, int32_t flags, double cauchy_c, hipStream_t s);
+hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
+                                      double* partial, unsigned* counter, double* dot_out, hipStream_t s);
+hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
+                                unsigned* counter, double* dot_out, hipStream_t s);
+hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* goff, const int64_t* hoff,
+                                 const int32_t* bsize, const double* minv, int32_t mode, double alpha, const double* p,
+                                 const double* q, const double* b, double* x, const double* r_in, double* r_out,
+                                 double* z, double* partial, unsigned* counters, double* out, hipStream_t s);
 hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
                              hipStream_t s);
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, double* out,
                            hipStream_t s);
 hipError_t mvba_launch_sum(int64_t n, const double* partial, double* out, hipStream_t s);
-hipError_t mvba_launch_block_chol(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
-                                  const double* hess, const double* d, double* fac, hipStream_t s);
-hipError_t mvba_launch_block_solve(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
-                                   const double* fac, const double* r, double* z, hipStream_t s);
+hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int64_t* goff, const int64_t* hoff,
+                                  const int32_t* bsize, const double* hess, const double* d, double* minv,
+                                  hipStream_t s);
 hipError_t mvba_launch_extract_diag(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
                                     const double* hess, int64_t npts, const double* V, int64_t ng, double* c,
                                     hipStream_t s);
@@ -83,32 +87,34 @@ struct SolverState {
   double* cdiag = nullptr;    // [nc] diag(J^T J)
   double* sc = nullptr;       // [nc] Jacobi scaling (iteration 0)
   double* dmp = nullptr;      // [nc] LM damping (unscaled)
-  double* fac = nullptr;      // [nh] Cholesky factors of the preconditioner blocks
+  double* fac = nullptr;      // [nh] explicit inverses of the preconditioner blocks
   double* x = nullptr;        // [nc] current point (compact)
   double* xn = nullptr;       // [nc] candidate point
   double* delta = nullptr;    // [nc] step (camera part = CG solution)
   double* scr = nullptr;      // [nc] scratch
   double* lo = nullptr;       // [nc] bounds (compact) or null
   double* hi = nullptr;
-  double *b = nullptr, *r = nullptr, *z = nullptr, *p = nullptr, *q = nullptr, *tmp = nullptr;  // [ng]
+  double *b = nullptr, *r = nullptr, *r2 = nullptr, *z = nullptr, *p = nullptr, *q = nullptr, *tmp = nullptr;  // [ng]
   double* yrep = nullptr;     // [replicas * ng], kept zero between products
   double* dir = nullptr;      // [nframes * dir stride]
   double* zbuf = nullptr;     // [8 N] point-order z_o | J_pt rows
   double* ubuf = nullptr;     // [2 N]
-  double* slabb = nullptr;    // [nchunks * slab stride]
   double* partial = nullptr;  // [npartial]
   double* scal = nullptr;     // [32] device scalars
+  unsigned* cnt = nullptr;    // [8] grid-reduction counters (kept zero between kernels)
   double* hscal = nullptr;    // [32] pinned host mirror
   int64_t npartial = 0;
   int32_t* bsize = nullptr;
+  int32_t* emap = nullptr;    // camera entry -> camera block
+  int32_t max_bsize = 0;
   int64_t *goff = nullptr, *hoff = nullptr, *cam_poff = nullptr;
 };
 
 void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
-                  S->hi, S->b, S->r, S->z, S->p, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->ubuf,
-                  S->slabb, S->partial, S->scal, S->bsize, S->goff, S->hoff, S->cam_poff};
+                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->ubuf,
+                  S->cnt, S->partial, S->scal, S->bsize, S->emap, S->goff, S->hoff, S->cam_poff};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (S->hscal) (void)hipHostFree(S->hscal);
@@ -152,17 +158,18 @@ SolverState* alloc_state(mvba_handle* h) {
     for (double** v : {&S->G, &S->cdiag, &S->sc, &S->dmp, &S->x, &S->xn, &S->delta, &S->scr})
       HCHK(dalloc(v, (size_t)S->nc));
     HCHK(dalloc(&S->fac, (size_t)S->nh));
-    for (double** v : {&S->b, &S->r, &S->z, &S->p, &S->q, &S->tmp}) HCHK(dalloc(v, (size_t)ng1));
+    for (double** v : {&S->b, &S->r, &S->r2, &S->z, &S->p, &S->q, &S->tmp}) HCHK(dalloc(v, (size_t)ng1));
     const size_t nrep = (size_t)mvba_solver_vec_replicas() * (size_t)ng1;
     HCHK(dalloc(&S->yrep, nrep));
     HCHK(hipMemset(S->yrep, 0, nrep * sizeof(double)));
     HCHK(dalloc(&S->dir, (size_t)(h->nframes * mvba_solver_dir_stride())));
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
     HCHK(dalloc(&S->ubuf, (size_t)(2 * N)));
-    HCHK(dalloc(&S->slabb, (size_t)h->nchunks * (size_t)mvba_solver_slabb_stride()));
+    HCHK(dalloc(&S->cnt, 8));
+    HCHK(hipMemset(S->cnt, 0, 8 * sizeof(unsigned)));
     int64_t ncost = 0;
     for (const Group& G : h->groups) ncost = std::max<int64_t>(ncost, (G.seg_count + 3) / 4);
-    S->npartial = std::max<int64_t>({256, (S->np * 4 + 255) / 256, ncost});
+    S->npartial = std::max<int64_t>({3072, mvba_pass_a_blocks(S->np), ncost});
     HCHK(dalloc(&S->partial, (size_t)S->npartial));
     HCHK(dalloc(&S->scal, 32));
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hscal), 32 * sizeof(double)));
@@ -174,6 +181,12 @@ SolverState* alloc_state(mvba_handle* h) {
       bs[k] = (int32_t)(next - h->cam_goff[k]);
     }
     HCHK(upload(&S->bsize, bs));
+    std::vector<int32_t> em((size_t)S->ng);
+    for (int32_t k = 0; k < S->nblocks; k++) {
+      S->max_bsize = std::max(S->max_bsize, bs[k]);
+      for (int32_t e = 0; e < bs[k]; e++) em[(size_t)(h->cam_goff[k] + e)] = k;
+    }
+    HCHK(upload(&S->emap, em));
     HCHK(upload(&S->goff, h->cam_goff));
     HCHK(upload(&S->hoff, h->cam_hoff));
     HCHK(upload(&S->cam_poff, h->cam_poff));
@@ -276,34 +289,39 @@ class Solver {
     return S_->hscal[16];
   }
 
-  // pass B over every model group, frame expand, cross-rank sum: y = F' u
-  void reduce_frames(double* y) {
+  // pass B over every model group into the replicas, then y = sum of replicas.
+  // Single rank: damping and the x.y dot are fused into the replica reduction
+  // (dot -> scal[dot_slot]); sharded: cross-rank sum of y first.
+  void reduce_frames(double* y, const double* xv, int dot_slot) {
     for (const Group& G : h_->groups)
       HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
-                              h_->d_segs, h_->d_fd, h_->d_frec, h_->d_params, h_->d_pts, h_->d_obs_pid,
-                              h_->d_obs_meas, h_->d_slot_po, S_->ubuf, S_->slabb, flags_, cauchy_c_, s_));
-    HCHK(mvba_launch_dir_expand(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->slabb, S_->yrep,
-                                S_->ng, y, s_));
+                              h_->d_segs, h_->d_fd, h_->d_frame_lin, h_->d_frec, h_->d_params, h_->d_pts,
+                              h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, S_->ubuf, S_->yrep, S_->ng, flags_,
+                              cauchy_c_, s_));
+    const bool fuse = xv && !o_.allreduce;
+    HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr, y, S_->partial,
+                                    S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, s_));
     exchange(y, S_->ng, MVBA_REDUCE_SUM);
+    if (xv && !fuse)
+      HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, s_));
   }
 
-  // y = S x (implicit Schur complement with damping)
-  void apply_schur(const double* xv, double* y) {
+  // y = S x (implicit Schur complement with damping); x.y -> scal[dot_slot]
+  void apply_schur(const double* xv, double* y, int dot_slot) {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, s_));
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, nullptr, S_->phess, S_->dmp + S_->ng,
-                            S_->zbuf, S_->ubuf, nullptr, nullptr, flags_, cauchy_c_, s_, nullptr));
-    reduce_frames(y);
-    HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, s_));
+                            S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_, cauchy_c_, s_));
+    reduce_frames(y, xv, dot_slot);
   }
 
   // b = -(g_c - W (V+D)^-1 g_p)
   void schur_rhs() {
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, nullptr, S_->G + S_->ng, S_->phess,
-                            S_->dmp + S_->ng, S_->zbuf, S_->ubuf, nullptr, nullptr, flags_, cauchy_c_, s_,
-                            nullptr));
-    reduce_frames(S_->tmp);  // = -W w
+                            S_->dmp + S_->ng, S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_,
+                            cauchy_c_, s_));
+    reduce_frames(S_->tmp, nullptr, 0);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
   }
 
@@ -312,7 +330,8 @@ class Solver {
     int status = 0;  // 0 success, 1 no convergence (usable), 2 failure
   };
 
-  // PCG on S delta_c = b (conjugate_gradients_solver.cc [ext])
+  // PCG on S delta_c = b (conjugate_gradients_solver.cc [ext]). Device-side
+  // scalars: per iteration two host reads (p'q; then x'b, x'r, r'z together).
   CgResult cg() {
     CgResult R;
     const int64_t n = S_->ng;
@@ -322,12 +341,16 @@ class Solver {
     dot(n, S_->b, S_->b, 0);
     const double norm_b = std::sqrt(fetch(1)[0]);
     if (norm_b == 0.0) return R;
-    // r = b - A x = b (x = 0), Q0 = -x'(b + r) = 0
-    HCHK(hipMemcpyAsync(S_->r, S_->b, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s_));
+    // r is double-buffered: each update reads S_->r and writes S_->r2, then they swap
+    auto upd = [&](int32_t mode, double alpha, const double* q) {
+      HCHK(mvba_launch_cg_update(n, S_->emap, S_->goff, S_->hoff, S_->bsize, S_->fac, mode, alpha, S_->p, q, S_->b, xv,
+                                 S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, s_));
+      std::swap(S_->r, S_->r2);
+    };
+    // r = b (x = 0); z = M^-1 r; rho = r'z. Q0 = -x'(b + r) = 0
+    upd(4 | 8, 0.0, nullptr);
+    double rho_next = fetch(11)[10];
     double Q0 = 0.0, rho = 1.0;
-    HCHK(mvba_launch_block_solve(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->fac, S_->r, S_->z, s_));
-    dot(n, S_->r, S_->z, 0);
-    double rho_next = fetch(1)[0];
     auto bad = [](double v) { return v == 0.0 || std::isinf(v) || std::isnan(v); };
     for (int i = 1;; i++) {
       R.iters = i;
@@ -347,8 +370,7 @@ class Solver {
         }
         HCHK(mvba_launch_axpby(n, 1.0, S_->z, beta, S_->p, S_->p, s_));
       }
-      apply_schur(S_->p, S_->q);
-      dot(n, S_->p, S_->q, 0);
+      apply_schur(S_->p, S_->q, 0);
       const double pq = fetch(1)[0];
       if (pq <= 0.0 || std::isinf(pq) || std::isnan(pq)) {
         R.status = 1;  // "Matrix is indefinite": NO_CONVERGENCE, x kept
@@ -359,20 +381,16 @@ class Solver {
         R.status = 2;
         break;
       }
-      HCHK(mvba_launch_axpby(n, 1.0, xv, alpha, S_->p, xv, s_));
-      if (i % 10 == 0) {
-        apply_schur(xv, S_->tmp);
-        HCHK(mvba_launch_axpby(n, 1.0, S_->b, -1.0, S_->tmp, S_->r, s_));
+      if (i % 10 == 0) {  // residual reset: r = b - A x
+        upd(1, alpha, S_->q);
+        apply_schur(xv, S_->tmp, 1);
+        upd(4 | 8, 0.0, S_->tmp);
       } else {
-        HCHK(mvba_launch_axpby(n, 1.0, S_->r, -alpha, S_->q, S_->r, s_));
+        upd(1 | 2 | 8, alpha, S_->q);
       }
-      HCHK(mvba_launch_block_solve(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->fac, S_->r, S_->z, s_));
-      dot(n, xv, S_->b, 0);
-      dot(n, xv, S_->r, 1);
-      dot(n, S_->r, S_->z, 2);
-      const double* hs = fetch(3);
-      const double Q1 = -(hs[0] + hs[1]);
-      rho_next = hs[2];
+      const double* hs = fetch(11);
+      const double Q1 = -(hs[8] + hs[9]);
+      rho_next = hs[10];
       const double zeta = i * (Q1 - Q0) / Q1;
       if (zeta < o_.eta && i >= o_.min_linear_solver_iterations) break;
       Q0 = Q1;
@@ -386,14 +404,12 @@ class Solver {
 
   // delta_p = -(V+D)^-1 (g_p + W' delta_c); returns model cost change -(g'delta + |J delta|^2 / 2)
   double back_substitute() {
-    int64_t nb = 0;
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
                                s_));
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
-                            S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial, flags_, cauchy_c_,
-                            s_, &nb));
-    HCHK(mvba_launch_sum(nb, S_->partial, S_->scal + 0, s_));  // |J delta|^2 (local observations)
+                            S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial, S_->cnt + 5,
+                            S_->scal + 0, flags_, cauchy_c_, s_));  // |J delta|^2 (local observations)
     HCHK(mvba_launch_axpby(3 * S_->np, -1.0, S_->delta + S_->ng, 0.0, nullptr, S_->delta + S_->ng, s_));
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);
@@ -707,7 +723,8 @@ void Solver::run(mvba_solver_summary* sum) {
     const double ts = now_s();
     HCHK(mvba_launch_lm_diag(nc, S_->cdiag, scale, 1.0 / radius, o_.min_lm_diagonal, o_.max_lm_diagonal, S_->dmp,
                              s_));
-    HCHK(mvba_launch_block_chol(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->dmp, S_->fac, s_));
+    HCHK(mvba_launch_block_prec(S_->nblocks, S_->max_bsize, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->dmp,
+                                S_->fac, s_));
     schur_rhs();
     const CgResult cgr = cg();
     sum->num_linear_iterations += cgr.iters;

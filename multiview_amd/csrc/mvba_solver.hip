@@ -6,18 +6,16 @@
 //   pass A (point order, 4 lanes/point): z_o = J_cam,o x  (via the frame's
 //          generators: J_pose = Z w, so J_pose x = Z (w x)), t_p = sum J_pt^T z_o,
 //          w_p = (V_p + D_p)^-1 t_p, u_o = z_o - J_pt w_p;
-//   pass B (frame order, one wave per frame chunk): y_frame = sum Z^T u_o,
-//          sum J_intr^T u_o; k_dir_expand maps y_frame through w to the pose
-//          columns: S x = J_cam^T u (+ LM damping).
+//   pass B (frame order, one wave per frame chunk): y_frame = sum Z^T u_o and
+//          sum J_intr^T u_o, mapped through w to the pose columns in the same
+//          kernel: S x = J_cam^T u (+ LM damping).
 // Same two passes give the reduced right-hand side and the point back-substitution.
 #include "mvba_device.h"
 
 namespace mvba {
 
 constexpr int kDirStride = 64;     // per-frame direction record: u (6) | x_intr (<= 58)
-constexpr int kSlabB = 64;         // per-chunk pass-B record: Z^T u (6) | J_I^T u (<= 58)
 constexpr int kVecReplicas = 32;
-constexpr int kLanesPerPointS = 4;
 
 // Camera-side columns of one observation at a frame, as a row pair:
 // Z (6), intrinsics (focal, center 2, live distortion nd), J_pt (3), corrected r.
@@ -147,6 +145,63 @@ __device__ __forceinline__ void pass_a_obs(const FrameDesc& F, const double* __r
   }
 }
 
+// Last-block finalisation of a grid reduction: every block stores its partial,
+// the last block to arrive sums them into out[0] and re-arms the counter.
+__device__ __forceinline__ void grid_sum_finalize(double v, double* __restrict__ partial,
+                                                  unsigned* __restrict__ counter, double* __restrict__ out) {
+  __shared__ double red[256];
+  __shared__ bool last;
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = red[0];
+    __threadfence();
+    last = (atomicAdd(counter, 1u) == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double acc = 0.0;
+  for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x) acc += __builtin_nontemporal_load(&partial[e]);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = red[0];
+    *counter = 0u;
+  }
+}
+
+// kLanesA lanes per point; each lane keeps its first kCacheA observations' rows
+// (z_o and the two J_pt rows: 8 doubles) in registers, later ones go through zbuf.
+constexpr int kLanesA = 8;
+constexpr int kCacheA = 2;
+
+template <int MODEL, int DEG>
+__device__ __forceinline__ void pass_a_dispatch(const FrameDesc& F, const double* __restrict__ rec,
+                                                const double* __restrict__ params, const double* dirf, double4 X,
+                                                double2 m, int32_t flags, double cauchy_c, double* z, double* P0,
+                                                double* P1) {
+  if constexpr (MODEL >= 0) {
+    pass_a_obs<MODEL, DEG>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+  } else {
+    const int K = F.K;
+    if (K == 0) pass_a_obs<kModelNone, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 1) pass_a_obs<kModelFov, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 4 || K == 5) pass_a_obs<kModelRadtan, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 20) pass_a_obs<kModelRpc, 1>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 44) pass_a_obs<kModelRpc, 2>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else pass_a_obs<kModelRpc, 3>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+  }
+}
+
 template <int MODEL, int DEG>
 __global__ void __launch_bounds__(256) k_pass_a(
     const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
@@ -155,48 +210,47 @@ __global__ void __launch_bounds__(256) k_pass_a(
     const double4* __restrict__ pts, const double* __restrict__ dir,
     const double* __restrict__ tinit, const double* __restrict__ V, const double* __restrict__ dp,
     double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
-    double* __restrict__ sq_partial, int32_t flags, double cauchy_c) {
+    double* __restrict__ sq_partial, unsigned* __restrict__ counter, double* __restrict__ sq_out,
+    int32_t flags, double cauchy_c) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t p = t / kLanesPerPointS;
-  const int sub = (int)(t % kLanesPerPointS);
+  const int64_t p = t / kLanesA;
+  const int sub = (int)(t % kLanesA);
   const bool valid = p < npts;
   double tv[3] = {0.0, 0.0, 0.0};
   double4 X = make_double4(0, 0, 0, 0);
   int64_t jb = 0, je = 0;
+  double zc[kCacheA][8];
   if (valid) {
     X = pts[p];
     jb = pt_begin[p];
     je = pt_begin[p + 1];
-    for (int64_t j = jb + sub; j < je; j += kLanesPerPointS) {
+    int k = 0;
+    for (int64_t j = jb + sub; j < je; j += kLanesA, k++) {
       const int32_t fr = po_frame[j];
-      const FrameDesc& F = fd[fr];
-      const double* rec = frec + (int64_t)fr * kFrameRecDoubles;
       double z[2], P0[3], P1[3];
-      const double* dirf = dir ? dir + (int64_t)fr * kDirStride : nullptr;
-      const double2 m = po_meas[j];
-      if constexpr (MODEL >= 0) {
-        pass_a_obs<MODEL, DEG>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-      } else {
-        const int K = F.K;
-        if (K == 0) pass_a_obs<kModelNone, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-        else if (K == 1) pass_a_obs<kModelFov, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-        else if (K == 4 || K == 5) pass_a_obs<kModelRadtan, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-        else if (K == 20) pass_a_obs<kModelRpc, 1>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-        else if (K == 44) pass_a_obs<kModelRpc, 2>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-        else pass_a_obs<kModelRpc, 3>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-      }
-      double* zr = zbuf + 8 * j;
-      zr[0] = z[0]; zr[1] = z[1];
+      pass_a_dispatch<MODEL, DEG>(fd[fr], frec + (int64_t)fr * kFrameRecDoubles, params,
+                                  dir ? dir + (int64_t)fr * kDirStride : nullptr, X, po_meas[j], flags, cauchy_c,
+                                  z, P0, P1);
 #pragma unroll
-      for (int q = 0; q < 3; q++) {
-        zr[2 + q] = P0[q];
-        zr[5 + q] = P1[q];
-        tv[q] += P0[q] * z[0] + P1[q] * z[1];
+      for (int q = 0; q < 3; q++) tv[q] += P0[q] * z[0] + P1[q] * z[1];
+      const double row[8] = {z[0], z[1], P0[0], P0[1], P0[2], P1[0], P1[1], P1[2]};
+      bool cached = false;
+#pragma unroll
+      for (int c = 0; c < kCacheA; c++)
+        if (k == c) {
+#pragma unroll
+          for (int q = 0; q < 8; q++) zc[c][q] = row[q];
+          cached = true;
+        }
+      if (!cached) {
+        double* zr = zbuf + 8 * j;
+#pragma unroll
+        for (int q = 0; q < 8; q++) zr[q] = row[q];
       }
     }
   }
 #pragma unroll
-  for (int off = 1; off < kLanesPerPointS; off <<= 1)
+  for (int off = 1; off < kLanesA; off <<= 1)
 #pragma unroll
     for (int q = 0; q < 3; q++) tv[q] += __shfl_xor(tv[q], off, 64);
   double w[3] = {0.0, 0.0, 0.0};
@@ -209,40 +263,44 @@ __global__ void __launch_bounds__(256) k_pass_a(
   if (valid) {
     if (wout && sub == 0)
       for (int q = 0; q < 3; q++) wout[3 * p + q] = w[q];
-    for (int64_t j = jb + sub; j < je; j += kLanesPerPointS) {
-      const double* zr = zbuf + 8 * j;
-      const double u0 = zr[0] - (zr[2] * w[0] + zr[3] * w[1] + zr[4] * w[2]);
-      const double u1 = zr[1] - (zr[5] * w[0] + zr[6] * w[1] + zr[7] * w[2]);
-      if (ubuf) {
-        ubuf[2 * j] = u0;
-        ubuf[2 * j + 1] = u1;
+    int k = 0;
+    for (int64_t j = jb + sub; j < je; j += kLanesA, k++) {
+      double row[8];
+      bool cached = false;
+#pragma unroll
+      for (int c = 0; c < kCacheA; c++)
+        if (k == c) {
+#pragma unroll
+          for (int q = 0; q < 8; q++) row[q] = zc[c][q];
+          cached = true;
+        }
+      if (!cached) {
+        const double* zr = zbuf + 8 * j;
+#pragma unroll
+        for (int q = 0; q < 8; q++) row[q] = zr[q];
       }
+      const double u0 = row[0] - (row[2] * w[0] + row[3] * w[1] + row[4] * w[2]);
+      const double u1 = row[1] - (row[5] * w[0] + row[6] * w[1] + row[7] * w[2]);
+      if (ubuf) *reinterpret_cast<double2*>(ubuf + 2 * j) = make_double2(u0, u1);
       sq += u0 * u0 + u1 * u1;
     }
   }
-  if (sq_partial) {
-    __shared__ double red[256];
-    red[threadIdx.x] = sq;
-    __syncthreads();
-    for (int s2 = 128; s2 > 0; s2 >>= 1) {
-      if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) sq_partial[blockIdx.x] = red[0];
-  }
+  if (sq_partial) grid_sum_finalize(sq, sq_partial, counter, sq_out);
 }
 
 // ------------------------------------------------------------ pass B (frame order)
 // One wave per frame chunk: sum over its observations of Z^T u_o and J_I^T u_o,
-// wave-reduced, written to the chunk's slab record (no atomics).
+// wave-reduced; the lanes then map the 6 frame-local sums through the generators
+// w_k to the pose columns (y_k = w_k . (Z^T u)) and add pose + intrinsic columns
+// into replica (chunk mod kVecReplicas) of the camera-side vector.
 template <int MODEL, int DEG>
 __global__ void __launch_bounds__(64) k_pass_b(
     const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
-    const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd,
+    const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
     const double2* __restrict__ obs_meas, const int32_t* __restrict__ slot_po,
-    const double* __restrict__ ubuf, double* __restrict__ slabb, int32_t flags, double cauchy_c) {
+    const double* __restrict__ ubuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   const int lane = threadIdx.x;
@@ -267,11 +325,11 @@ __global__ void __launch_bounds__(64) k_pass_b(
       obs_rows<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, obs_meas[i], flags, cauchy_c, Z0, Z1, I0, I1, P0,
                            P1, r, &hr);
       const int64_t j = slot_po[i];  // point-order index of this observation
-      const double u0 = ubuf[2 * j], u1 = ubuf[2 * j + 1];
+      const double2 u = *reinterpret_cast<const double2*>(ubuf + 2 * j);
 #pragma unroll
-      for (int a = 0; a < 6; a++) acc[a] += Z0[a] * u0 + Z1[a] * u1;
+      for (int a = 0; a < 6; a++) acc[a] += Z0[a] * u.x + Z1[a] * u.y;
 #pragma unroll
-      for (int q = 0; q < RS::kIntr; q++) acc[6 + q] += I0[q] * u0 + I1[q] * u1;
+      for (int q = 0; q < RS::kIntr; q++) acc[6 + q] += I0[q] * u.x + I1[q] * u.y;
     }
   }
 #pragma unroll
@@ -281,73 +339,119 @@ __global__ void __launch_bounds__(64) k_pass_b(
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     acc[q] = v;
   }
-  if (lane == 0) {
-    double* out = slabb + (int64_t)(chunk_base + ch) * kSlabB;
-#pragma unroll
-    for (int q = 0; q < NA; q++) out[q] = acc[q];
-  }
-}
-
-// Per frame: sum chunk records, map through w to the pose columns, add into
-// replica (f mod kVecReplicas) of the camera-side vector.
-__global__ void __launch_bounds__(64) k_dir_expand(const FrameLin* __restrict__ fl, int32_t nframes,
-                                                   const FrameDesc* __restrict__ fd,
-                                                   const double* __restrict__ frec,
-                                                   const double* __restrict__ slabb,
-                                                   double* __restrict__ yrep, int64_t ng) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nframes) return;
-  const FrameLin L = fl[f];
-  const int NA = L.width - 1;  // 6 + intrinsics (the Gram width minus the residual column)
-  double acc[kSlabB];
-  for (int q = 0; q < NA; q++) acc[q] = 0.0;
-  for (int c = 0; c < L.chunk_count; c++) {
-    const double* s = slabb + (int64_t)(L.first_chunk + c) * kSlabB;
-    for (int q = 0; q < NA; q++) acc[q] += s[q];
-  }
-  double* y = yrep + (int64_t)(f & (kVecReplicas - 1)) * ng;
-  const double* w = frec + (int64_t)f * kFrameRecDoubles + 12;
-  for (int blk = 0; blk < 4; blk++) {
+  // every lane holds the totals; lane k < 22 -> pose column k, 22.. -> intrinsics
+  const FrameLin& L = fl[frame];
+  double* y = yrep + (int64_t)((chunk_base + ch) & (kVecReplicas - 1)) * ng;
+  int64_t dst = -1;
+  double v = 0.0;
+  if (lane < kPoseCols) {
+    const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
-    if (L.goff[b] < 0) continue;
-    const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
-    for (int cc = 0; cc < ncol; cc++) {
-      const double* wk = w + 6 * (k0 + cc);
-      double v = 0.0;
+    if (L.goff[b] >= 0) {
+      const double* wk = rec + 12 + 6 * lane;
+#pragma unroll
       for (int a = 0; a < 6; a++) v += wk[a] * acc[a];
-      atomicAdd(&y[L.goff[b] + cc], v);
+      dst = L.goff[b] + (lane - 7 * blk);
+    }
+  } else {
+    const int q = lane - kPoseCols;  // 0 focal, 1..2 center, 3.. distortion
+    if (q < RS::kIntr) {
+#pragma unroll
+      for (int e = 0; e < RS::kIntr; e++)
+        if (e == q) v = acc[6 + e];
+      if (q == 0) dst = L.goff[MVBA_BLK_FOCAL];
+      else if (q < 3) dst = L.goff[MVBA_BLK_CENTER] >= 0 ? L.goff[MVBA_BLK_CENTER] + (q - 1) : -1;
+      else if (q - 3 < F.K) dst = L.goff[MVBA_BLK_DIST] >= 0 ? L.goff[MVBA_BLK_DIST] + (q - 3) : -1;
     }
   }
-  if (L.goff[MVBA_BLK_FOCAL] >= 0) atomicAdd(&y[L.goff[MVBA_BLK_FOCAL]], acc[6]);
-  if (L.goff[MVBA_BLK_CENTER] >= 0) {
-    atomicAdd(&y[L.goff[MVBA_BLK_CENTER]], acc[7]);
-    atomicAdd(&y[L.goff[MVBA_BLK_CENTER] + 1], acc[8]);
-  }
-  const int nd = NA - 9;
-  const int K = fd[f].K;
-  if (L.goff[MVBA_BLK_DIST] >= 0)
-    for (int q = 0; q < nd && q < K; q++) atomicAdd(&y[L.goff[MVBA_BLK_DIST] + q], acc[9 + q]);
+  if (dst >= 0) atomicAdd(&y[dst], v);
 }
 
-// y = sum_r yrep[r]; replicas re-zeroed.
+// y = sum_r yrep[r] (replicas re-zeroed); with diag: y += diag .* x; with dot_out
+// the grid also reduces x.y into dot_out (p'q when no cross-rank exchange follows).
 __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yrep, int64_t n,
-                                                        double* __restrict__ y) {
+                                                        const double* __restrict__ diag,
+                                                        const double* __restrict__ x, double* __restrict__ y,
+                                                        double* __restrict__ partial, unsigned* __restrict__ counter,
+                                                        double* __restrict__ dot_out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  double acc = 0.0;
+  double d = 0.0;
+  if (e < n) {
+    double acc = 0.0;
 #pragma unroll 8
-  for (int r = 0; r < kVecReplicas; r++) {
-    acc += yrep[r * n + e];
-    yrep[r * n + e] = 0.0;
+    for (int r = 0; r < kVecReplicas; r++) {
+      acc += yrep[r * n + e];
+      yrep[r * n + e] = 0.0;
+    }
+    if (diag) acc += diag[e] * x[e];
+    y[e] = acc;
+    d = x ? x[e] * acc : 0.0;
   }
-  y[e] = acc;
+  if (dot_out) grid_sum_finalize(d, partial, counter, dot_out);
 }
 
-// y += diag .* x (LM damping; applied after the cross-rank sum so it counts once)
-__global__ void k_add_diag(int64_t n, const double* __restrict__ diag, const double* __restrict__ x,
-                           double* __restrict__ y) {
+// y += diag .* x; dot_out = x.y (after a cross-rank sum of y)
+__global__ void __launch_bounds__(256) k_add_diag(int64_t n, const double* __restrict__ diag,
+                                                  const double* __restrict__ x, double* __restrict__ y,
+                                                  double* __restrict__ partial, unsigned* __restrict__ counter,
+                                                  double* __restrict__ dot_out) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < n) y[e] += diag[e] * x[e];
+  double d = 0.0;
+  if (e < n) {
+    const double v = y[e] + diag[e] * x[e];
+    y[e] = v;
+    d = x[e] * v;
+  }
+  if (dot_out) grid_sum_finalize(d, partial, counter, dot_out);
+}
+
+// One CG step on the camera side, one thread per camera entry
+// (conjugate_gradients_solver.cc [ext]); r is double-buffered (r_in -> r_out):
+//   mode & 1: x += alpha p;  & 2: r = r_in - alpha q;  & 4: r = b - q (q null: r = b);
+//   mode & 8: z = M^-1 r (explicit block inverses) and out = [x.b, x.r, r.z].
+__global__ void __launch_bounds__(256) k_cg_update(int64_t n, const int32_t* __restrict__ emap,
+                                                   const int64_t* __restrict__ goff, const int64_t* __restrict__ hoff,
+                                                   const int32_t* __restrict__ bsize, const double* __restrict__ minv,
+                                                   int32_t mode, double alpha, const double* __restrict__ p,
+                                                   const double* __restrict__ q, const double* __restrict__ b,
+                                                   double* __restrict__ x, const double* __restrict__ r_in,
+                                                   double* __restrict__ r_out, double* __restrict__ z,
+                                                   double* __restrict__ partial, unsigned* __restrict__ counters,
+                                                   double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double xb = 0.0, xr = 0.0, rz = 0.0;
+  if (i < n) {
+    const int blk = emap[i];
+    const int64_t o = goff[blk];
+    const int nb = bsize[blk];
+    const int row = (int)(i - o);
+    auto rnew = [&](int64_t k) -> double {
+      if (mode & 2) return r_in[k] - alpha * q[k];
+      if (mode & 4) return q ? b[k] - q[k] : b[k];
+      return r_in[k];
+    };
+    double xi = x[i];
+    if (mode & 1) {
+      xi += alpha * p[i];
+      x[i] = xi;
+    }
+    const double ri = rnew(i);
+    r_out[i] = ri;
+    if (mode & 8) {
+      const double* M = minv + hoff[blk] + (int64_t)row * nb;
+      double zi = 0.0;
+      for (int k = 0; k < nb; k++) zi += M[k] * rnew(o + k);
+      z[i] = zi;
+      xb = xi * b[i];
+      xr = xi * ri;
+      rz = ri * zi;
+    }
+  }
+  if (mode & 8) {
+    grid_sum_finalize(xb, partial, counters + 0, out + 0);
+    grid_sum_finalize(xr, partial + 1024, counters + 1, out + 1);
+    grid_sum_finalize(rz, partial + 2048, counters + 2, out + 2);
+  }
 }
 
 // ------------------------------------------------------------ vectors / blocks
@@ -389,54 +493,62 @@ __global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict
   if (threadIdx.x == 0) out[0] = red[0];
 }
 
-// Block-Jacobi preconditioner: Cholesky factor (in place, lower) of H_bb + diag(d)
-// per camera block (one thread per block; blocks are <= 76 wide).
-__global__ void k_block_chol(int32_t nblocks, const int64_t* __restrict__ goff,
-                             const int64_t* __restrict__ hoff, const int32_t* __restrict__ bsize,
-                             const double* __restrict__ hess, const double* __restrict__ d,
-                             double* __restrict__ fac) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+// Block-Jacobi preconditioner (Ceres' JACOBI for ITERATIVE_SCHUR [ext]:
+// blocks of F'F + D^2): one workgroup (one wave) per camera block factors
+// H_bb + diag(d) in LDS (column-parallel Cholesky) and writes the explicit
+// inverse (lane j solves for column j), so applying it is a block mat-vec.
+__global__ void __launch_bounds__(64) k_block_prec(int32_t nblocks, const int64_t* __restrict__ goff,
+                                                   const int64_t* __restrict__ hoff,
+                                                   const int32_t* __restrict__ bsize,
+                                                   const double* __restrict__ hess, const double* __restrict__ d,
+                                                   double* __restrict__ minv) {
+  extern __shared__ double Ls[];  // [n * n]
+  const int b = blockIdx.x;
   if (b >= nblocks) return;
   const int n = bsize[b];
+  const int lane = threadIdx.x;
   const double* H = hess + hoff[b];
-  double* Lm = fac + hoff[b];
   const double* db = d + goff[b];
-  for (int i = 0; i < n; i++)
-    for (int j = 0; j < n; j++) Lm[i * n + j] = (j <= i) ? H[i * n + j] + (i == j ? db[i] : 0.0) : 0.0;
+  for (int e = lane; e < n * n; e += 64) {
+    const int i = e / n, j = e % n;
+    Ls[e] = (j <= i) ? H[e] + (i == j ? db[i] : 0.0) : 0.0;
+  }
+  __syncthreads();
+  __shared__ double djs;
+  __shared__ int ok;
   for (int j = 0; j < n; j++) {
-    double s = Lm[j * n + j];
-    for (int k = 0; k < j; k++) s -= Lm[j * n + k] * Lm[j * n + k];
-    // singular directions (e.g. constant-zero columns) fall back to identity
-    const double dj = (s > 1e-300) ? sqrt(s) : 1.0;
-    Lm[j * n + j] = dj;
-    for (int i = j + 1; i < n; i++) {
-      double v = Lm[i * n + j];
-      for (int k = 0; k < j; k++) v -= Lm[i * n + k] * Lm[j * n + k];
-      Lm[i * n + j] = (s > 1e-300) ? v / dj : 0.0;
+    if (lane == 0) {
+      double sj = Ls[j * n + j];
+      for (int k = 0; k < j; k++) sj -= Ls[j * n + k] * Ls[j * n + k];
+      // singular directions (e.g. all-zero columns) fall back to identity
+      ok = sj > 1e-300;
+      djs = ok ? sqrt(sj) : 1.0;
+      Ls[j * n + j] = djs;
     }
+    __syncthreads();
+    for (int i = j + 1 + lane; i < n; i += 64) {
+      double v = Ls[i * n + j];
+      for (int k = 0; k < j; k++) v -= Ls[i * n + k] * Ls[j * n + k];
+      Ls[i * n + j] = ok ? v / djs : 0.0;
+    }
+    __syncthreads();
   }
-}
-
-// z = (L L^T)^-1 r per block
-__global__ void k_block_solve(int32_t nblocks, const int64_t* __restrict__ goff,
-                              const int64_t* __restrict__ hoff, const int32_t* __restrict__ bsize,
-                              const double* __restrict__ fac, const double* __restrict__ r,
-                              double* __restrict__ z) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
-  const int n = bsize[b];
-  const double* Lm = fac + hoff[b];
-  const double* rb = r + goff[b];
-  double* zb = z + goff[b];
-  for (int i = 0; i < n; i++) {
-    double v = rb[i];
-    for (int k = 0; k < i; k++) v -= Lm[i * n + k] * zb[k];
-    zb[i] = v / Lm[i * n + i];
-  }
-  for (int i = n - 1; i >= 0; i--) {
-    double v = zb[i];
-    for (int k = i + 1; k < n; k++) v -= Lm[k * n + i] * zb[k];
-    zb[i] = v / Lm[i * n + i];
+  double* M = minv + hoff[b];
+  double y[96];
+  for (int j = lane; j < n; j += 64) {
+    // L y = e_j
+    for (int i = 0; i < n; i++) {
+      double v = (i == j) ? 1.0 : 0.0;
+      for (int k = j; k < i; k++) v -= Ls[i * n + k] * y[k];
+      y[i] = (i < j) ? 0.0 : v / Ls[i * n + i];
+    }
+    // L^T x = y
+    for (int i = n - 1; i >= 0; i--) {
+      double v = y[i];
+      for (int k = i + 1; k < n; k++) v -= Ls[k * n + i] * y[k];
+      y[i] = v / Ls[i * n + i];
+    }
+    for (int i = 0; i < n; i++) M[i * n + j] = y[i];
   }
 }
 
@@ -608,7 +720,6 @@ __global__ void __launch_bounds__(256) k_cost(const Segment* __restrict__ segs, 
 extern "C" {
 
 int mvba_solver_dir_stride(void) { return mvba::kDirStride; }
-int mvba_solver_slabb_stride(void) { return mvba::kSlabB; }
 int mvba_solver_vec_replicas(void) { return mvba::kVecReplicas; }
 
 hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
@@ -619,57 +730,75 @@ hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::Fr
   return hipGetLastError();
 }
 
-// model < 0: mixed camera models (runtime dispatch per observation)
+// model < 0: mixed camera models (runtime dispatch per observation).
+// sq_partial/counter/sq_out: optional grid reduction of sum |u_o|^2 into sq_out[0].
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const mvba::FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
                               const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
-                              double* sq_partial, int32_t flags, double cauchy_c, hipStream_t s,
-                              int64_t* nblocks_out) {
-  const unsigned blocks = (unsigned)((npts * mvba::kLanesPerPointS + 255) / 256);
-  if (nblocks_out) *nblocks_out = blocks;
+                              double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
+                              hipStream_t s) {
+  const unsigned blocks = (unsigned)((npts * mvba::kLanesA + 255) / 256);
   if (npts <= 0) return hipSuccess;
   if (model < 0) {
     hipLaunchKernelGGL((mvba::k_pass_a<-1, 0>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, fd,
-                       frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, flags, cauchy_c);
+                       frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out, flags,
+                       cauchy_c);
     return hipGetLastError();
   }
 #define MVBA_PA(M, D)                                                                                      \
   hipLaunchKernelGGL((mvba::k_pass_a<M, D>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, \
-                     fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, flags, cauchy_c)
+                     fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out,  \
+                     flags, cauchy_c)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PA)
 #undef MVBA_PA
   return hipGetLastError();
 }
 
+int64_t mvba_pass_a_blocks(int64_t npts) { return (npts * mvba::kLanesA + 255) / 256; }
+
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
-                              const mvba::Segment* segs, const mvba::FrameDesc* fd, const double* frec,
-                              const double* params, const double4* pts, const int32_t* obs_pid,
-                              const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* slabb,
-                              int32_t flags, double cauchy_c, hipStream_t s) {
+                              const mvba::Segment* segs, const mvba::FrameDesc* fd, const void* fl,
+                              const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
+                              const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* yrep,
+                              int64_t ng, int32_t flags, double cauchy_c, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
-#define MVBA_PB(M, D)                                                                                      \
-  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks,       \
-                     chunk_base, segs, fd, frec, params, pts, obs_pid, obs_meas, slot_po, ubuf, slabb, flags, \
-                     cauchy_c)
+#define MVBA_PB(M, D)                                                                                       \
+  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks,        \
+                     chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
+                     slot_po, ubuf, yrep, ng, flags, cauchy_c)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)
 #undef MVBA_PB
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_dir_expand(const void* fl, int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
-                                  const double* slabb, double* yrep, int64_t ng, double* y, hipStream_t s) {
-  if (nframes > 0)
-    hipLaunchKernelGGL(mvba::k_dir_expand, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s,
-                       (const mvba::FrameLin*)fl, nframes, fd, frec, slabb, yrep, ng);
-  if (ng > 0)
-    hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, y);
+// y = sum of replicas (+ diag .* x, and x.y -> dot_out when dot_out != null)
+hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
+                                      double* partial, unsigned* counter, double* dot_out, hipStream_t s) {
+  if (ng <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, diag, x,
+                     y, partial, counter, dot_out);
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, hipStream_t s) {
+hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
+                                unsigned* counter, double* dot_out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_add_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, diag, x, y);
+  hipLaunchKernelGGL(mvba::k_add_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, diag, x, y, partial,
+                     counter, dot_out);
+  return hipGetLastError();
+}
+
+// partial needs 3 x 1024 doubles, counters 3 (zero-initialised, re-armed by the kernel)
+hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* goff, const int64_t* hoff,
+                                 const int32_t* bsize, const double* minv, int32_t mode, double alpha, const double* p,
+                                 const double* q, const double* b, double* x, const double* r_in, double* r_out,
+                                 double* z, double* partial, unsigned* counters, double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  if (blocks > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks), dim3(256), 0, s, n, emap, goff, hoff, bsize, minv, mode, alpha,
+                     p, q, b, x, r_in, r_out, z, partial, counters, out);
   return hipGetLastError();
 }
 
@@ -694,19 +823,13 @@ hipError_t mvba_launch_sum(int64_t n, const double* partial, double* out, hipStr
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_block_chol(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
-                                  const double* hess, const double* d, double* fac, hipStream_t s) {
+hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int64_t* goff, const int64_t* hoff,
+                                  const int32_t* bsize, const double* hess, const double* d, double* minv,
+                                  hipStream_t s) {
   if (nblocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_block_chol, dim3((unsigned)((nblocks + 63) / 64)), dim3(64), 0, s, nblocks, goff,
-                     hoff, bsize, hess, d, fac);
-  return hipGetLastError();
-}
-
-hipError_t mvba_launch_block_solve(int32_t nblocks, const int64_t* goff, const int64_t* hoff, const int32_t* bsize,
-                                   const double* fac, const double* r, double* z, hipStream_t s) {
-  if (nblocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_block_solve, dim3((unsigned)((nblocks + 63) / 64)), dim3(64), 0, s, nblocks, goff,
-                     hoff, bsize, fac, r, z);
+  if (max_bsize > 96) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(64),
+                     (size_t)max_bsize * max_bsize * sizeof(double), s, nblocks, goff, hoff, bsize, hess, d, minv);
   return hipGetLastError();
 }
 

@@ -12,6 +12,19 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, "tests", "golden", "cam_error_golden.json")
 
 
+def pytest_sessionstart(session):
+    # Bring up torch's HIP runtime before any test spawns worker processes: a
+    # parent that used the GPU only through libmvba could not initialise torch's
+    # runtime after mp.spawn children had run (seen on the MI355X box).
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:  # noqa: BLE001 - CPU container: nothing to do
+        pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libmvba.so)")
 
