@@ -189,7 +189,7 @@ class BracketedCamBatch {
     // Every block is evaluated (the adapter cannot see SetParameterBlockConstant);
     // Evaluate() copies only the non-NULL jacobians Ceres asks for.
     std::vector<uint8_t> constant(block_ptr_.size(), 0);
-    mvba_problem_desc d;
+    mvba_problem_desc d{};
     std::memset(&d, 0, sizeof(d));
     d.num_blocks = (int32_t)block_ptr_.size();
     d.block_size = block_size_.data();

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MVBA_ABI_VERSION 1
+#define MVBA_ABI_VERSION 2
 
 /* Status codes. Non-zero codes mirror the reference's fatal checks. */
 typedef enum mvba_status {
@@ -117,7 +117,41 @@ typedef struct mvba_problem_desc {
   const int32_t* residual_camera; /* [num_residuals] camera model index */
   const double* residual_meas;    /* [2*num_residuals] meas_dist_pix */
   const double* residual_stamps;  /* [3*num_residuals] left_ref, right_ref, cam stamp */
+
+  /* Optional BracketedDepthError residual blocks (rig_calibrator.cc:522-609),
+   * added by rig_calibrator.cc:1755-1791 when --depth_tri_weight > 0. Each must
+   * share (beg, end, ref_to_cam, offset, stamps) with at least one
+   * BracketedCamError block (the image the depth cloud belongs to). Zero-fill
+   * these fields when there are none. */
+  int64_t num_depth_residuals;
+  const int32_t* depth_blocks;   /* [7*n] beg, end, ref_to_cam, depth_to_image (7 rigid | 12 affine),
+                                    scale (1), xyz (3), offset (1): MVBA_DBLK_* order */
+  const double* depth_meas;      /* [3*n] meas_depth_xyz (depth-cloud point) */
+  const double* depth_weight;    /* [n] weight (FLAGS_depth_tri_weight) */
+  const double* depth_stamps;    /* [3*n] left_ref, right_ref, cam stamp */
 } mvba_problem_desc;
+
+/* Depth block order (BracketedDepthError) and its Jacobian layout: rows
+ * MVBA_DJAC_BASE_b + i*size_b + j = entry (residual row i, column j) of block b,
+ * i.e. Ceres' row-major 3 x size_b block concatenated, with depth_to_image always
+ * given 12 columns of room (a rigid 7-parameter block uses the first 21 rows). */
+enum {
+  MVBA_DBLK_BEG = 0,
+  MVBA_DBLK_END = 1,
+  MVBA_DBLK_REF_TO_CAM = 2,
+  MVBA_DBLK_DEPTH_TO_IMAGE = 3,
+  MVBA_DBLK_SCALE = 4,
+  MVBA_DBLK_XYZ = 5,
+  MVBA_DBLK_OFFSET = 6
+};
+#define MVBA_DJAC_BASE_BEG 0
+#define MVBA_DJAC_BASE_END 21
+#define MVBA_DJAC_BASE_REF_TO_CAM 42
+#define MVBA_DJAC_BASE_DEPTH_TO_IMAGE 63
+#define MVBA_DJAC_BASE_SCALE 99
+#define MVBA_DJAC_BASE_XYZ 102
+#define MVBA_DJAC_BASE_OFFSET 111
+#define MVBA_DJAC_ROWS 114
 
 typedef struct mvba_options {
   int32_t device;        /* HIP device ordinal */
@@ -228,6 +262,21 @@ mvba_status mvba_point_block_map(const struct mvba_handle* h, int32_t* block_ids
 mvba_status mvba_linearize_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                                   double* d_cam_grad, double* d_cam_hess, double* d_pt_grad,
                                   double* d_pt_hess, double* d_cost, void* hip_stream);
+
+/* ---- Depth residuals (BracketedDepthError) -------------------------------
+ * Host: residuals [3n] and Jacobian [n * MVBA_DJAC_ROWS] (nullable) in depth
+ * insertion order, Cauchy corrector applied with MVBA_EVAL_APPLY_LOSS, cost =
+ * sum of 0.5*rho over depth blocks. Device: column planes res[3][ld],
+ * J[MVBA_DJAC_ROWS][ld] in device order (mvba_depth_order), ld >=
+ * mvba_num_depth_slots(), multiple of 16. mvba_evaluate / mvba_linearize_device
+ * / mvba_solve include the depth blocks' cost and normal equations. */
+int64_t mvba_num_depth_residuals(const struct mvba_handle* h);
+int64_t mvba_num_depth_slots(const struct mvba_handle* h);
+mvba_status mvba_depth_order(const struct mvba_handle* h, int64_t* out /* [num_depth_slots] */);
+mvba_status mvba_evaluate_depth(struct mvba_handle* h, int32_t flags, double cauchy_threshold, double* cost,
+                                double* residuals, double* jacobian);
+mvba_status mvba_evaluate_depth_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                       double* d_res, double* d_J, int64_t ld, void* hip_stream);
 
 /* Counts for reporting. */
 int64_t mvba_num_residuals(const struct mvba_handle* h);

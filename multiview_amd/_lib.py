@@ -61,6 +61,11 @@ class ProblemDesc(C.Structure):
         ("residual_camera", C.c_void_p),
         ("residual_meas", C.c_void_p),
         ("residual_stamps", C.c_void_p),
+        ("num_depth_residuals", C.c_int64),
+        ("depth_blocks", C.c_void_p),
+        ("depth_meas", C.c_void_p),
+        ("depth_weight", C.c_void_p),
+        ("depth_stamps", C.c_void_p),
     ]
 
 
@@ -91,6 +96,11 @@ class LinLayout(C.Structure):
         ("supported", C.c_int32),
     ]
 
+
+# BracketedDepthError Jacobian layout (MVBA_DJAC_BASE_*): rows per block,
+# depth_to_image given 12 columns of room.
+DJAC_BASE = (0, 21, 42, 63, 99, 102, 111)
+DJAC_ROWS = 114
 
 REDUCE_SUM, REDUCE_MAX = 0, 1
 CONVERGENCE, NO_CONVERGENCE, FAILURE = 0, 1, 2
@@ -171,6 +181,12 @@ SIGNATURES = {
     "mvba_point_block_map": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mvba_linearize_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_num_depth_residuals": (C.c_int64, [C.c_void_p]),
+    "mvba_num_depth_slots": (C.c_int64, [C.c_void_p]),
+    "mvba_depth_order": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mvba_evaluate_depth": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_evaluate_depth_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
+                                             C.c_int64, C.c_void_p]),
     "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
     "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),
     "mvba_get_params": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -1,0 +1,430 @@
+// mvba_depth.hip — BracketedDepthError residual blocks on gfx950
+// (rig_calibrator.cc:522-609, added at :1755-1791 when --depth_tri_weight > 0).
+//
+//   M  = (depth_to_image with linear *= scale) * meas_depth_xyz     (:558-569)
+//   Mw = world_to_cam.inverse() * M                                 (:572)
+//   r  = weight * (X - Mw)                                          (:578-580)
+//
+// world_to_cam is the K0 frame record of the image the depth cloud belongs to
+// (same beg/end/ref_to_cam/offset blocks and stamps), so the pose columns reuse
+// the frame's generators: with Mw = R^-1 (M - t) and dXc/dp_k = w_k x Xc + v_k,
+//   dr_i/dp_k = weight * [ M x Rinv_i ; Rinv_i ] . [w_k ; v_k]
+// depth_to_image / scale columns: dr/dtheta = -weight Rinv dM/dtheta; xyz: weight I.
+// Device order: depth blocks sorted by frame, line-aligned frame ranges, segments
+// of <= 64 blocks of one frame (one wave each), like the reprojection blocks.
+#include "mvba_device.h"
+
+namespace mvba {
+
+// Eigen Matrix3d::inverse (cofactors / determinant) as restated in oracle.cpp's
+// affine_inverse (Affine3d::inverse in Affine mode [ext]).
+__device__ __forceinline__ void inverse3(const double* m, double* o) {
+  const double c00 = m[4] * m[8] - m[5] * m[7];
+  const double c10 = m[5] * m[6] - m[3] * m[8];
+  const double c20 = m[3] * m[7] - m[4] * m[6];
+  const double det = c00 * m[0] + c10 * m[1] + c20 * m[2];
+  const double inv = 1.0 / det;
+  o[0] = c00 * inv;
+  o[1] = (m[2] * m[7] - m[1] * m[8]) * inv;
+  o[2] = (m[1] * m[5] - m[2] * m[4]) * inv;
+  o[3] = c10 * inv;
+  o[4] = (m[0] * m[8] - m[2] * m[6]) * inv;
+  o[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
+  o[6] = c20 * inv;
+  o[7] = (m[1] * m[6] - m[0] * m[7]) * inv;
+  o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
+}
+
+__device__ __forceinline__ double loss_scale3(double r0, double r1, double r2, int32_t flags, double cauchy_c,
+                                              double* half_rho) {
+  const double s = r0 * r0 + r1 * r1 + r2 * r2;
+  if (flags & MVBA_EVAL_APPLY_LOSS) {
+    const double sum = 1.0 + s * cauchy_c;
+    *half_rho = 0.5 * (log(sum) / cauchy_c);
+    return sqrt(fmax(DBL_MIN, 1.0 / sum));
+  }
+  *half_rho = 0.5 * s;
+  return 1.0;
+}
+
+// Residual and Jacobian rows of one depth block, all multiplied by the loss
+// scale sr (Ceres' corrector for Cauchy, alpha = 0).
+struct DepthRows {
+  double r[3];       // corrected residual
+  double rr[3];      // raw residual (host corrector path)
+  double Z[3][6];    // pose rows: J_pose(i, k) = Z[i] . w_k
+  double D[3][12];   // depth_to_image rows (dti_n used)
+  double S[3];       // scale column
+  double P;          // xyz: P * identity
+  double sr, half_rho;
+};
+
+__device__ __forceinline__ void depth_rows(const DepthDesc& d, const double* __restrict__ rec,
+                                           const double* __restrict__ params, double4 m, double X0, double X1,
+                                           double X2, int32_t flags, double cauchy_c, DepthRows& o) {
+  const double* p = params + d.dti_off;
+  double A[9], b[3], qh[4] = {0, 0, 0, 1}, in = 1.0;
+  if (d.dti_n == 12) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+#pragma unroll
+      for (int c = 0; c < 3; c++) A[3 * r + c] = p[4 * r + c];
+      b[r] = p[4 * r + 3];
+    }
+  } else {
+    rigid(p, A, qh, &in);
+    b[0] = p[0]; b[1] = p[1]; b[2] = p[2];
+  }
+  const double s = params[d.scale_off];
+  const double w = m.w;
+  double Am[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) Am[r] = A[3 * r] * m.x + A[3 * r + 1] * m.y + A[3 * r + 2] * m.z;
+  // (linear * scale) * meas + translation, in Eigen's order: ((s A) m) + b
+  double M[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) M[r] = (s * A[3 * r]) * m.x + (s * A[3 * r + 1]) * m.y + (s * A[3 * r + 2]) * m.z + b[r];
+  double Ri[9];
+  inverse3(rec, Ri);
+  const double ti[3] = {-(Ri[0] * rec[9] + Ri[1] * rec[10] + Ri[2] * rec[11]),
+                        -(Ri[3] * rec[9] + Ri[4] * rec[10] + Ri[5] * rec[11]),
+                        -(Ri[6] * rec[9] + Ri[7] * rec[10] + Ri[8] * rec[11])};
+  const double X[3] = {X0, X1, X2};
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const double Mw = Ri[3 * i] * M[0] + Ri[3 * i + 1] * M[1] + Ri[3 * i + 2] * M[2] + ti[i];
+    o.rr[i] = w * (X[i] - Mw);
+  }
+  const double sr = loss_scale3(o.rr[0], o.rr[1], o.rr[2], flags, cauchy_c, &o.half_rho);
+  o.sr = sr;
+  const double ws = w * sr;
+  o.P = ws;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    o.r[i] = o.rr[i] * sr;
+    const double ri[3] = {Ri[3 * i], Ri[3 * i + 1], Ri[3 * i + 2]};
+    double mx[3];
+    cross(M, ri, mx);
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      o.Z[i][q] = ws * mx[q];
+      o.Z[i][3 + q] = ws * ri[q];
+    }
+    o.S[i] = -ws * (ri[0] * Am[0] + ri[1] * Am[1] + ri[2] * Am[2]);
+#pragma unroll
+    for (int q = 0; q < 12; q++) o.D[i][q] = 0.0;
+    if (d.dti_n == 12) {
+#pragma unroll
+      for (int rr = 0; rr < 3; rr++) {
+        const double g = -ws * ri[rr];
+        o.D[i][4 * rr] = g * s * m.x;
+        o.D[i][4 * rr + 1] = g * s * m.y;
+        o.D[i][4 * rr + 2] = g * s * m.z;
+        o.D[i][4 * rr + 3] = g;
+      }
+    } else {
+      // translation
+#pragma unroll
+      for (int j = 0; j < 3; j++) o.D[i][j] = -ws * ri[j];
+      // quaternion: dM/dq_k = s (om_k x Am)  ->  dr_i/dq_k = -ws s om_k . (Am x ri)
+      double axr[3];
+      cross(Am, ri, axr);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        double om[3];
+        quat_generator(qh, 2.0 * in, k, om);
+        o.D[i][3 + k] = -ws * s * (om[0] * axr[0] + om[1] * axr[1] + om[2] * axr[2]);
+      }
+    }
+  }
+}
+
+constexpr int kDJacBase[7] = {MVBA_DJAC_BASE_BEG, MVBA_DJAC_BASE_END, MVBA_DJAC_BASE_REF_TO_CAM,
+                              MVBA_DJAC_BASE_DEPTH_TO_IMAGE, MVBA_DJAC_BASE_SCALE, MVBA_DJAC_BASE_XYZ,
+                              MVBA_DJAC_BASE_OFFSET};
+
+// ------------------------------------------------------------ evaluation (K1-depth)
+// One lane per depth block, one wave per segment. res[3][ld], J[MVBA_DJAC_ROWS][ld]
+// column planes; constant blocks are not written. flags & APPLY_LOSS applies the
+// corrector in-kernel.
+__global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ segs, int32_t nseg,
+                                                  const DepthDesc* __restrict__ dd, const double4* __restrict__ dmeas,
+                                                  const FrameDesc* __restrict__ fd, const double* __restrict__ frec,
+                                                  const double* __restrict__ params, const double4* __restrict__ pts,
+                                                  double* __restrict__ res, double* __restrict__ J, int64_t ld,
+                                                  int32_t flags, double cauchy_c) {
+  const int seg = blockIdx.x;
+  if (seg >= nseg) return;
+  const Segment sg = segs[seg];
+  const int lane = threadIdx.x;
+  if (lane >= sg.count) return;
+  const int64_t i = (int64_t)sg.begin + lane;
+  const DepthDesc d = dd[i];
+  const double* rec = frec + (int64_t)d.frame * kFrameRecDoubles;
+  const double4 X = pts[d.pid];
+  DepthRows o;
+  depth_rows(d, rec, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
+  const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
+  if (res) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) __builtin_nontemporal_store(loss ? o.r[q] : o.rr[q], &res[q * ld + i]);
+  }
+  if (!J) return;
+  // raw (uncorrected) Jacobian unless APPLY_LOSS: divide the corrected rows back
+  const double un = loss ? 1.0 : 1.0 / o.sr;
+  const int mask = d.free_mask;
+  const double* wv = rec + 12;
+  for (int blk = 0; blk < 4; blk++) {
+    const int db = (blk == 3) ? MVBA_DBLK_OFFSET : blk;
+    if (!(mask & (1 << db))) continue;
+    const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
+    for (int i3 = 0; i3 < 3; i3++)
+      for (int c = 0; c < ncol; c++) {
+        const double* wk = wv + 6 * (k0 + c);
+        double v = 0.0;
+#pragma unroll
+        for (int a = 0; a < 6; a++) v += o.Z[i3][a] * wk[a];
+        __builtin_nontemporal_store(v * un, &J[(int64_t)(kDJacBase[db] + i3 * ncol + c) * ld + i]);
+      }
+  }
+  if (mask & (1 << MVBA_DBLK_DEPTH_TO_IMAGE)) {
+    const int n = d.dti_n;
+    for (int i3 = 0; i3 < 3; i3++)
+      for (int c = 0; c < n; c++)
+        __builtin_nontemporal_store(o.D[i3][c] * un, &J[(int64_t)(MVBA_DJAC_BASE_DEPTH_TO_IMAGE + i3 * n + c) * ld + i]);
+  }
+  if (mask & (1 << MVBA_DBLK_SCALE))
+    for (int i3 = 0; i3 < 3; i3++)
+      __builtin_nontemporal_store(o.S[i3] * un, &J[(int64_t)(MVBA_DJAC_BASE_SCALE + i3) * ld + i]);
+  if (mask & (1 << MVBA_DBLK_XYZ))
+    for (int i3 = 0; i3 < 3; i3++)
+      for (int c = 0; c < 3; c++)
+        __builtin_nontemporal_store(i3 == c ? o.P * un : 0.0, &J[(int64_t)(MVBA_DJAC_BASE_XYZ + i3 * 3 + c) * ld + i]);
+}
+
+// ------------------------------------------------------------ normal equations
+// One wave per segment: Gram of B = [Z (6) | D (12) | S | r] over its 3*64 rows
+// with fp64 MFMA (rows staged in LDS [column][row]), then the wave expands it:
+// pose blocks through the frame's generators, depth_to_image and scale blocks
+// directly, into replica (segment mod 32) of [cam_grad | cam_hess | cost].
+constexpr int kDW = 20;          // Gram width
+constexpr int kDT = 2;           // 16-wide tiles
+constexpr int kDRows = 192;      // 3 rows x 64 lanes
+constexpr int kDLd = kDRows + 2; // LDS leading dimension (doubles)
+constexpr int kDReplicas = 32;
+
+__global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ segs, int32_t nseg,
+                                                   const DepthDesc* __restrict__ dd,
+                                                   const double4* __restrict__ dmeas, const double* __restrict__ frec,
+                                                   const double* __restrict__ params,
+                                                   const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
+                                                   double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags,
+                                                   double cauchy_c) {
+  __shared__ double lds[kDT * 16 * kDLd];
+  __shared__ double G[kDW * kDW];
+  const int seg = blockIdx.x;
+  if (seg >= nseg) return;
+  const Segment sg = segs[seg];
+  const int lane = threadIdx.x;
+  const int frame = __builtin_amdgcn_readfirstlane(sg.frame);
+  const double* rec = frec + (int64_t)frame * kFrameRecDoubles;
+  double cost = 0.0;
+  double row[3][kDW];
+#pragma unroll
+  for (int i3 = 0; i3 < 3; i3++)
+#pragma unroll
+    for (int q = 0; q < kDW; q++) row[i3][q] = 0.0;
+  DepthDesc d0 = dd[sg.begin];
+  if (lane < sg.count) {
+    const int64_t i = (int64_t)sg.begin + lane;
+    const DepthDesc d = dd[i];
+    const double4 X = pts[d.pid];
+    DepthRows o;
+    depth_rows(d, rec, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
+    cost = o.half_rho;
+#pragma unroll
+    for (int i3 = 0; i3 < 3; i3++) {
+#pragma unroll
+      for (int a = 0; a < 6; a++) row[i3][a] = o.Z[i3][a];
+#pragma unroll
+      for (int q = 0; q < 12; q++) row[i3][6 + q] = o.D[i3][q];
+      row[i3][18] = o.S[i3];
+      row[i3][19] = o.r[i3];
+    }
+  }
+  // stage [column][row]; padding columns 20..31 zero
+#pragma unroll
+  for (int i3 = 0; i3 < 3; i3++)
+#pragma unroll
+    for (int q = 0; q < kDT * 16; q++) lds[q * kDLd + 3 * lane + i3] = q < kDW ? row[i3][q] : 0.0;
+  __syncthreads();
+  dbl4 acc[3] = {dbl4{0, 0, 0, 0}, dbl4{0, 0, 0, 0}, dbl4{0, 0, 0, 0}};
+  const int col = lane & 15, rsub = lane >> 4;
+#pragma unroll 4
+  for (int st = 0; st < kDRows / 4; st++) {
+    const int r = 4 * st + rsub;
+    const double v0 = lds[col * kDLd + r], v1 = lds[(16 + col) * kDLd + r];
+    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v0, acc[0], 0, 0, 0);
+    acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v1, acc[1], 0, 0, 0);
+    acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, v1, acc[2], 0, 0, 0);
+  }
+  // lane holds G[(lane>>4) + 4r][lane & 15] of tile pairs (0,0), (0,1), (1,1)
+  const int pairs[3][2] = {{0, 0}, {0, 1}, {1, 1}};
+#pragma unroll
+  for (int pidx = 0; pidx < 3; pidx++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int a = pairs[pidx][0] * 16 + (lane >> 4) + 4 * r, b = pairs[pidx][1] * 16 + (lane & 15);
+      if (a < kDW && b < kDW) {
+        G[a * kDW + b] = acc[pidx][r];
+        G[b * kDW + a] = acc[pidx][r];
+      }
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) cost += __shfl_xor(cost, off, 64);
+  __syncthreads();
+  // expand (frame-uniform blocks)
+  const FrameLin& L = fl[frame];
+  double* grad = rep + (int64_t)(seg & (kDReplicas - 1)) * (ng + nh + 1);
+  double* hess = grad + ng;
+  const double* wv = rec + 12;
+  for (int blk = 0; blk < 4; blk++) {
+    const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+    if (L.goff[b] < 0) continue;
+    const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
+    for (int e = lane; e < ncol; e += 64) {
+      const double* wk = wv + 6 * (k0 + e);
+      double g = 0.0;
+      for (int a = 0; a < 6; a++) g += wk[a] * G[a * kDW + 19];
+      atomicAdd(&grad[L.goff[b] + e], g);
+    }
+    for (int e = lane; e < ncol * ncol; e += 64) {
+      const int kk = e / ncol, kc = e % ncol;
+      const double* wa = wv + 6 * (k0 + kk);
+      const double* wb = wv + 6 * (k0 + kc);
+      double h = 0.0;
+      for (int a = 0; a < 6; a++) {
+        double t = 0.0;
+        for (int c = 0; c < 6; c++) t += G[a * kDW + c] * wb[c];
+        h += wa[a] * t;
+      }
+      atomicAdd(&hess[L.hoff[b] + e], h);
+    }
+  }
+  // depth_to_image and scale: sensor blocks, the same for the whole segment
+  // (one image = one sensor), so take them from the first block's record.
+  if (d0.goff_dti >= 0) {
+    const int n = d0.dti_n;
+    for (int e = lane; e < n; e += 64) atomicAdd(&grad[d0.goff_dti + e], G[(6 + e) * kDW + 19]);
+    for (int e = lane; e < n * n; e += 64) {
+      const int a = e / n, c = e % n;
+      atomicAdd(&hess[d0.hoff_dti + e], G[(6 + a) * kDW + 6 + c]);
+    }
+  }
+  if (d0.goff_scale >= 0 && lane == 0) {
+    atomicAdd(&grad[d0.goff_scale], G[18 * kDW + 19]);
+    atomicAdd(&hess[d0.hoff_scale], G[18 * kDW + 18]);
+  }
+  if (lane == 0) atomicAdd(&grad[ng + nh], cost);
+}
+
+// Point side: V_p += (w sr)^2 I, g_p += (w sr) r~ (after k_points_lin wrote them).
+__global__ void __launch_bounds__(256) k_depth_points(int64_t nslots, const DepthDesc* __restrict__ dd,
+                                                      const int64_t* __restrict__ dorder,
+                                                      const double4* __restrict__ dmeas,
+                                                      const double* __restrict__ frec,
+                                                      const double* __restrict__ params,
+                                                      const double4* __restrict__ pts, double* __restrict__ pgrad,
+                                                      double* __restrict__ phess, int32_t flags, double cauchy_c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots || dorder[i] < 0) return;
+  const DepthDesc d = dd[i];
+  const double4 X = pts[d.pid];
+  if (X.w == 0.0) return;
+  DepthRows o;
+  depth_rows(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
+  const double P2 = o.P * o.P;
+  atomicAdd(&phess[6 * d.pid + 0], P2);
+  atomicAdd(&phess[6 * d.pid + 3], P2);
+  atomicAdd(&phess[6 * d.pid + 5], P2);
+#pragma unroll
+  for (int q = 0; q < 3; q++) atomicAdd(&pgrad[3 * d.pid + q], o.P * o.r[q]);
+}
+
+// Cost partials (sum 0.5 rho) per 256-thread block over the depth slots.
+__global__ void __launch_bounds__(256) k_depth_cost(int64_t nslots, const DepthDesc* __restrict__ dd,
+                                                    const int64_t* __restrict__ dorder,
+                                                    const double4* __restrict__ dmeas,
+                                                    const double* __restrict__ frec,
+                                                    const double* __restrict__ params,
+                                                    const double4* __restrict__ pts, int32_t flags, double cauchy_c,
+                                                    double* __restrict__ partial) {
+  __shared__ double red[256];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double c = 0.0;
+  if (i < nslots && dorder[i] >= 0) {
+    const DepthDesc d = dd[i];
+    const double4 X = pts[d.pid];
+    DepthRows o;
+    depth_rows(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c,
+               o);
+    c = o.half_rho;
+  }
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+}  // namespace mvba
+
+extern "C" {
+
+size_t mvba_depth_desc_size(void) { return sizeof(mvba::DepthDesc); }
+
+hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
+                                 const double4* dmeas, const mvba::FrameDesc* fd, const double* frec,
+                                 const double* params, const double4* pts, double* res, double* J, int64_t ld,
+                                 int32_t flags, double cauchy_c, hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_depth_obs, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, fd, frec, params,
+                     pts, res, J, ld, flags, cauchy_c);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
+                                  const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                  const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
+                                  hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_depth_gram, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params,
+                     pts, (const mvba::FrameLin*)fl, rep, ng, nh, flags, cauchy_c);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_depth_points(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
+                                    const double4* dmeas, const double* frec, const double* params,
+                                    const double4* pts, double* pgrad, double* phess, int32_t flags, double cauchy_c,
+                                    hipStream_t s) {
+  if (nslots <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_depth_points, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s, nslots, dd, dorder,
+                     dmeas, frec, params, pts, pgrad, phess, flags, cauchy_c);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
+                                  const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                  int32_t flags, double cauchy_c, double* partial, hipStream_t s,
+                                  int64_t* nblocks_out) {
+  const int64_t blocks = (nslots + 255) / 256;
+  if (nblocks_out) *nblocks_out = blocks;
+  if (nslots <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_depth_cost, dim3((unsigned)blocks), dim3(256), 0, s, nslots, dd, dorder, dmeas, frec,
+                     params, pts, flags, cauchy_c, partial);
+  return hipGetLastError();
+}
+
+}  // extern "C"

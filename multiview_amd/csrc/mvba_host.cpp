@@ -34,7 +34,8 @@ static void free_all(mvba_handle* h) {
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
-                  h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po};
+                  h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
+                  h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ};
   solver_state_free(h->solver);
   h->solver = nullptr;
   for (void* p : ptrs)
@@ -118,6 +119,38 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     if (d->block_offset[b] < 0 || d->block_offset[b] + d->block_size[b] > d->num_param_doubles)
       return bad(MVBA_E_INVALID, "parameter block outside the packed vector");
 
+  // BracketedDepthError blocks: constructor checks (rig_calibrator.cc:534-543) and
+  // the image they belong to (a BracketedCamError block with the same pose
+  // blocks and stamps, whose world_to_cam they use).
+  const int64_t ND = d->num_depth_residuals;
+  if (ND < 0) return bad(MVBA_E_INVALID, "negative sizes in problem description");
+  if (ND > 0 && (!d->depth_blocks || !d->depth_meas || !d->depth_weight || !d->depth_stamps))
+    return bad(MVBA_E_INVALID, "null array in problem description");
+  if (ND > std::numeric_limits<int32_t>::max() - 64)
+    return bad(MVBA_E_INVALID, "too many depth residual blocks for one handle (shard the problem)");
+  std::unordered_map<PoseKey, int64_t, PoseKeyHash> pose_first;  // pose key -> first residual using it
+  if (ND > 0) {
+    pose_first.reserve(1024);
+    for (int64_t i = 0; i < N; i++) {
+      const int32_t* blk = d->residual_blocks + 8 * i;
+      pose_first.emplace(PoseKey::make(blk[0], blk[1], blk[2], blk[4], d->residual_stamps + 3 * i), i);
+    }
+  }
+  for (int64_t j = 0; j < ND; j++) {
+    const int32_t* blk = d->depth_blocks + 7 * j;
+    for (int b = 0; b < 7; b++)
+      if (blk[b] < 0 || blk[b] >= d->num_blocks) return bad(MVBA_E_INVALID, "parameter block index out of range");
+    static const int kDepthSize[7] = {7, 7, 7, 7, 1, 3, 1};
+    for (int b = 0; b < 7; b++) {
+      const int sz = d->block_size[blk[b]];
+      const bool ok = (b == MVBA_DBLK_DEPTH_TO_IMAGE) ? (sz == 7 || sz == 12) : (sz == kDepthSize[b]);
+      if (!ok) return bad(MVBA_E_DEPTH_BLOCK_SIZES, "BracketedDepthError: The block sizes were not set up properly.\n");
+    }
+    if (pose_first.find(PoseKey::make(blk[0], blk[1], blk[2], blk[6], d->depth_stamps + 3 * j)) == pose_first.end())
+      return bad(MVBA_E_INVALID,
+                 "depth residual block without a BracketedCamError block sharing its pose blocks and stamps");
+  }
+
   // The product path computes on the GPU only: no device, no handle.
   int32_t ndev = 0;
   if (mvba_device_count(&ndev) != MVBA_OK) return bad(MVBA_E_NO_DEVICE, "no HIP device available");
@@ -149,6 +182,20 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       res_pt[i] = id;
     } else {
       res_pt[i] = it->second;
+    }
+  }
+  std::vector<int32_t> dep_pt(ND);
+  for (int64_t j = 0; j < ND; j++) {
+    const int32_t b = d->depth_blocks[7 * j + MVBA_DBLK_XYZ];
+    auto it = pt_index.find(b);
+    if (it == pt_index.end()) {
+      const int32_t id = (int32_t)pt_off.size();
+      pt_index.emplace(b, id);
+      pt_off.push_back(d->block_offset[b]);
+      pt_free.push_back(d->block_constant[b] ? 0 : 1);
+      dep_pt[j] = id;
+    } else {
+      dep_pt[j] = it->second;
     }
   }
   h->npts = (int64_t)pt_off.size();
@@ -322,6 +369,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   std::vector<int32_t> po_frame;
   std::vector<double2> po_meas;
   std::vector<int32_t> slot_po;
+  std::vector<int64_t> goff_of(d->num_blocks, -1), hoff_of(d->num_blocks, -1);
   {
     h->lin_ok = true;
     for (const Group& G : h->groups)
@@ -334,7 +382,6 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     for (auto& kv : pt_index) is_point[kv.first] = 1;
     h->pt_block_ids.resize(h->npts);
     for (auto& kv : pt_index) h->pt_block_ids[kv.second] = kv.first;
-    std::vector<int64_t> goff_of(d->num_blocks, -1), hoff_of(d->num_blocks, -1);
     for (int b = 0; b < d->num_blocks; b++) {
       if (is_point[b] || d->block_constant[b]) continue;
       const int64_t sz = d->block_size[b];
@@ -410,6 +457,84 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     h->nchunks = (int32_t)chunks.size();
   }
 
+  // ---- depth blocks: device order by frame, line-aligned frame ranges, segments
+  std::vector<mvba::DepthDesc> ddesc;
+  std::vector<double4> dmeas;
+  std::vector<Segment> dsegs;
+  if (ND > 0) {
+    std::unordered_map<PoseKey, int32_t, PoseKeyHash> frame_of_key;
+    frame_of_key.reserve(frames.size() * 2);
+    for (int64_t i = 0; i < N; i++) {
+      const int32_t* blk = d->residual_blocks + 8 * i;
+      frame_of_key.emplace(PoseKey::make(blk[0], blk[1], blk[2], blk[4], d->residual_stamps + 3 * i), res_frame[i]);
+    }
+    std::vector<int32_t> dep_frame(ND);
+    for (int64_t j = 0; j < ND; j++) {
+      const int32_t* blk = d->depth_blocks + 7 * j;
+      dep_frame[j] = frame_of_key.at(PoseKey::make(blk[0], blk[1], blk[2], blk[6], d->depth_stamps + 3 * j));
+    }
+    std::vector<int64_t> didx(ND);
+    for (int64_t j = 0; j < ND; j++) didx[j] = j;
+    std::stable_sort(didx.begin(), didx.end(), [&](int64_t a, int64_t b) { return dep_frame[a] < dep_frame[b]; });
+    constexpr int64_t kAlign = 16;
+    int64_t slot = 0;
+    int32_t prev = -1;
+    std::vector<int64_t> slot_of(ND);
+    for (int64_t q = 0; q < ND; q++) {
+      const int64_t j = didx[q];
+      if (dep_frame[j] != prev) slot = (slot + kAlign - 1) / kAlign * kAlign;
+      if (dep_frame[j] != prev || dsegs.back().count == 64) {
+        Segment sg;
+        sg.begin = (int32_t)slot;
+        sg.count = 0;
+        sg.frame = dep_frame[j];
+        sg.pad = 0;
+        dsegs.push_back(sg);
+      }
+      prev = dep_frame[j];
+      dsegs.back().count++;
+      slot_of[j] = slot++;
+    }
+    h->ndep_slots = (slot + kAlign - 1) / kAlign * kAlign;
+    h->dep_order.assign(h->ndep_slots, -1);
+    ddesc.assign(h->ndep_slots, mvba::DepthDesc{});
+    dmeas.assign(h->ndep_slots, make_double4(0, 0, 0, 0));
+    for (int64_t j = 0; j < ND; j++) {
+      const int32_t* blk = d->depth_blocks + 7 * j;
+      const int64_t p = slot_of[j];
+      h->dep_order[p] = j;
+      mvba::DepthDesc& D = ddesc[p];
+      D.dti_off = d->block_offset[blk[MVBA_DBLK_DEPTH_TO_IMAGE]];
+      D.scale_off = d->block_offset[blk[MVBA_DBLK_SCALE]];
+      D.goff_dti = goff_of[blk[MVBA_DBLK_DEPTH_TO_IMAGE]];
+      D.hoff_dti = hoff_of[blk[MVBA_DBLK_DEPTH_TO_IMAGE]];
+      D.goff_scale = goff_of[blk[MVBA_DBLK_SCALE]];
+      D.hoff_scale = hoff_of[blk[MVBA_DBLK_SCALE]];
+      D.frame = dep_frame[j];
+      D.pid = dep_pt[j];
+      D.dti_n = d->block_size[blk[MVBA_DBLK_DEPTH_TO_IMAGE]];
+      const int fm = frames[dep_frame[j]].free_mask;
+      int m = 0;
+      if (fm & (1 << MVBA_BLK_BEG)) m |= 1 << MVBA_DBLK_BEG;
+      if (fm & (1 << MVBA_BLK_END)) m |= 1 << MVBA_DBLK_END;
+      if (fm & (1 << MVBA_BLK_REF_TO_CAM)) m |= 1 << MVBA_DBLK_REF_TO_CAM;
+      if (fm & (1 << MVBA_BLK_OFFSET)) m |= 1 << MVBA_DBLK_OFFSET;
+      if (!d->block_constant[blk[MVBA_DBLK_DEPTH_TO_IMAGE]]) m |= 1 << MVBA_DBLK_DEPTH_TO_IMAGE;
+      if (!d->block_constant[blk[MVBA_DBLK_SCALE]]) m |= 1 << MVBA_DBLK_SCALE;
+      if (pt_free[dep_pt[j]]) m |= 1 << MVBA_DBLK_XYZ;
+      D.free_mask = m;
+      dmeas[p] = make_double4(d->depth_meas[3 * j], d->depth_meas[3 * j + 1], d->depth_meas[3 * j + 2],
+                              d->depth_weight[j]);
+      int cols = 0;
+      for (int b = 0; b < 7; b++)
+        if (m & (1 << b)) cols += (b == MVBA_DBLK_DEPTH_TO_IMAGE) ? D.dti_n : (b == MVBA_DBLK_SCALE || b == MVBA_DBLK_OFFSET) ? 1 : (b == MVBA_DBLK_XYZ ? 3 : 7);
+      // Algorithmic bytes: meas + weight 32 + point 24 + residual 24 + 24 per written column.
+      h->bytes_dep += 32.0 + 24.0 + 24.0 + 24.0 * cols;
+    }
+  }
+  h->ndep = ND;
+  h->ndep_segs = (int32_t)dsegs.size();
+
   // ---- upload
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) {
@@ -446,6 +571,10 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_po_frame, po_frame));
   chk(upload(&h->d_po_meas, po_meas));
   chk(upload(&h->d_slot_po, slot_po));
+  chk(upload(&h->d_dep_desc, ddesc));
+  chk(upload(&h->d_dep_meas, dmeas));
+  chk(upload(&h->d_dep_segs, dsegs));
+  chk(upload(&h->d_dep_order, h->dep_order));
   if (e != hipSuccess) {
     g_create_error = std::string("HIP error during mvba_create: ") + hipGetErrorString(e);
     free_all(h);
@@ -614,8 +743,8 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
   if ((h->cam_grad_size && (!d_cam_grad || !d_cam_hess)) || (h->npts && (!d_pt_grad || !d_pt_hess)))
     return h->fail(MVBA_E_INVALID, "null output buffer");
   if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
-  if (mvba_frame_lin_size() != sizeof(mvba::FrameLinHost))
-    return h->fail(MVBA_E_INVALID, "FrameLin layout mismatch between host and device code");
+  if (mvba_frame_lin_size() != sizeof(mvba::FrameLinHost) || mvba_depth_desc_size() != sizeof(mvba::DepthDesc))
+    return h->fail(MVBA_E_INVALID, "record layout mismatch between host and device code");
   hipStream_t s = (hipStream_t)stream;
   double cauchy_c = 0.0;
   if (flags & MVBA_EVAL_APPLY_LOSS) {
@@ -638,6 +767,10 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
                          h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
                          h->d_slab + G.slab_base, lflags, cauchy_c, s);
   }
+  if (e == hipSuccess && h->ndep_segs > 0)
+    e = mvba_launch_depth_gram(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_frec, h->d_params,
+                               h->d_pts, h->d_frame_lin, h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags,
+                               cauchy_c, s);
   if (e == hipSuccess)
     e = mvba_launch_expand(h->d_frame_lin, (int32_t)h->nframes, h->max_w16, h->d_fd, h->d_frec, h->d_slab,
                            h->d_rep, h->cam_grad_size, h->cam_hess_size, d_cam_grad, d_cam_hess, d_cost, s);
@@ -646,6 +779,9 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
                                h->groups.size() == 1 ? h->groups[0].deg : 0, h->d_pt_begin, h->npts,
                                h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
                                d_pt_grad, d_pt_hess, lflags, cauchy_c, s);
+  if (e == hipSuccess && h->ndep > 0)
+    e = mvba_launch_depth_points(h->ndep_slots, h->d_dep_desc, h->d_dep_order, h->d_dep_meas, h->d_frec, h->d_params,
+                                 h->d_pts, d_pt_grad, d_pt_hess, lflags, cauchy_c, s);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_linearize_device launch");
   return MVBA_OK;
 }
@@ -718,6 +854,130 @@ mvba_status mvba_evaluate(mvba_handle* h, int32_t flags, double cauchy_threshold
     // Summed in AddResidualBlock order (Problem::Evaluate with num_threads = 1).
     double total = 0.0;
     for (int64_t i = 0; i < N; i++) total += cost_ins[i];
+    *cost = total;
+  }
+  return MVBA_OK;
+}
+
+int64_t mvba_num_depth_residuals(const mvba_handle* h) { return h ? h->ndep : 0; }
+int64_t mvba_num_depth_slots(const mvba_handle* h) { return h ? h->ndep_slots : 0; }
+
+mvba_status mvba_depth_order(const mvba_handle* h, int64_t* out) {
+  if (!h || !out) return MVBA_E_INVALID;
+  if (!h->dep_order.empty()) std::memcpy(out, h->dep_order.data(), h->dep_order.size() * sizeof(int64_t));
+  return MVBA_OK;
+}
+
+mvba_status mvba_evaluate_depth_device(mvba_handle* h, int32_t flags, double cauchy_threshold, double* d_res,
+                                       double* d_J, int64_t ld, void* stream) {
+  if (!h) return MVBA_E_INVALID;
+  if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  if (mvba_depth_desc_size() != sizeof(mvba::DepthDesc))
+    return h->fail(MVBA_E_INVALID, "record layout mismatch between host and device code");
+  if (ld < h->ndep_slots || (ld % 16) != 0)
+    return h->fail(MVBA_E_INVALID, "leading dimension must be >= mvba_num_depth_slots() and a multiple of 16");
+  if ((flags & MVBA_EVAL_JACOBIAN) && !d_J) return h->fail(MVBA_E_INVALID, "Jacobian requested without a Jacobian buffer");
+  if (!(flags & MVBA_EVAL_JACOBIAN)) d_J = nullptr;
+  double cauchy_c = 0.0;
+  if (flags & MVBA_EVAL_APPLY_LOSS) {
+    if (!(cauchy_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
+    cauchy_c = 1.0 / (cauchy_threshold * cauchy_threshold);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipSuccess;
+  if (!(flags & MVBA_EVAL_SKIP_PREP)) {
+    h->gen++;
+    e = mvba_launch_prep(h->d_fd, h->nframes, h->d_params, h->d_frec, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,
+                         h->gen, h->d_err, s);
+    h->prep_done = true;
+  } else if (!h->prep_done) {
+    return h->fail(MVBA_E_INVALID, "MVBA_EVAL_SKIP_PREP before any full evaluation");
+  }
+  if (e == hipSuccess && !(flags & MVBA_EVAL_PREP_ONLY))
+    e = mvba_launch_depth_obs(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_fd, h->d_frec,
+                              h->d_params, h->d_pts, d_res, d_J, ld, flags & (MVBA_EVAL_APPLY_LOSS), cauchy_c, s);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth_device launch");
+  return MVBA_OK;
+}
+
+mvba_status mvba_evaluate_depth(mvba_handle* h, int32_t flags, double cauchy_threshold, double* cost,
+                                double* residuals, double* jacobian) {
+  if (!h) return MVBA_E_INVALID;
+  const bool want_jac = jacobian != nullptr && (flags & MVBA_EVAL_JACOBIAN);
+  const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
+  if (loss && !(cauchy_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
+  const int64_t ND = h->ndep, S = h->ndep_slots;
+  if (ND == 0) {
+    if (cost) *cost = 0.0;
+    return MVBA_OK;
+  }
+  if (!h->d_dres) {
+    h->dld = (S + 63) / 64 * 64;
+    hipError_t e = dalloc(&h->d_dres, (size_t)(3 * h->dld));
+    if (e == hipSuccess) e = dalloc(&h->d_dJ, (size_t)MVBA_DJAC_ROWS * (size_t)h->dld);
+    if (e != hipSuccess) return h->hip_fail(e, "allocating depth outputs");
+  }
+  const int64_t ld = h->dld;
+  // raw residuals / Jacobian on the device; Ceres' corrector applied here
+  mvba_status st = mvba_evaluate_depth_device(h, MVBA_EVAL_RESIDUALS | (want_jac ? MVBA_EVAL_JACOBIAN : 0), 0.0,
+                                              h->d_dres, want_jac ? h->d_dJ : nullptr, ld, nullptr);
+  if (st != MVBA_OK) return st;
+  st = mvba_sync_status(h, nullptr);
+  if (st != MVBA_OK) return st;
+  h->h_dres.resize((size_t)(3 * ld));
+  hipError_t e = hipMemcpy(h->h_dres.data(), h->d_dres, (size_t)(3 * ld) * sizeof(double), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth residual copy");
+  std::vector<mvba::DepthDesc> desc;
+  if (want_jac) {
+    h->h_dJ.resize((size_t)MVBA_DJAC_ROWS * (size_t)ld);
+    e = hipMemcpy(h->h_dJ.data(), h->d_dJ, h->h_dJ.size() * sizeof(double), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth Jacobian copy");
+    desc.resize((size_t)S);
+    e = hipMemcpy(desc.data(), h->d_dep_desc, (size_t)S * sizeof(mvba::DepthDesc), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth record copy");
+  }
+  const double b = cauchy_threshold * cauchy_threshold;
+  const double c = loss ? 1.0 / b : 0.0;
+  std::vector<double> cost_ins(cost ? (size_t)ND : 0);
+  static const int kBase[7] = {MVBA_DJAC_BASE_BEG, MVBA_DJAC_BASE_END, MVBA_DJAC_BASE_REF_TO_CAM,
+                               MVBA_DJAC_BASE_DEPTH_TO_IMAGE, MVBA_DJAC_BASE_SCALE, MVBA_DJAC_BASE_XYZ,
+                               MVBA_DJAC_BASE_OFFSET};
+#pragma omp parallel for schedule(static)
+  for (int64_t p = 0; p < S; p++) {
+    const int64_t j = h->dep_order[p];
+    if (j < 0) continue;
+    const double r0 = h->h_dres[p], r1 = h->h_dres[ld + p], r2 = h->h_dres[2 * ld + p];
+    const double s2 = r0 * r0 + r1 * r1 + r2 * r2;
+    double sr = 1.0, cj;
+    if (!loss) {
+      cj = 0.5 * s2;
+    } else {
+      const double sum = 1.0 + s2 * c;
+      cj = 0.5 * (b * std::log(sum));
+      sr = std::sqrt(std::max(std::numeric_limits<double>::min(), 1.0 / sum));
+    }
+    if (cost) cost_ins[(size_t)j] = cj;
+    if (residuals) {
+      residuals[3 * j] = r0 * sr;
+      residuals[3 * j + 1] = r1 * sr;
+      residuals[3 * j + 2] = r2 * sr;
+    }
+    if (want_jac) {
+      double* Jo = jacobian + j * MVBA_DJAC_ROWS;
+      for (int row = 0; row < MVBA_DJAC_ROWS; row++) Jo[row] = 0.0;
+      const int mask = desc[(size_t)p].free_mask;
+      for (int bb = 0; bb < 7; bb++) {
+        if (!(mask & (1 << bb))) continue;
+        const int size = (bb == MVBA_DBLK_DEPTH_TO_IMAGE) ? desc[(size_t)p].dti_n
+                         : (bb == MVBA_DBLK_SCALE || bb == MVBA_DBLK_OFFSET) ? 1 : (bb == MVBA_DBLK_XYZ ? 3 : 7);
+        for (int q = 0; q < 3 * size; q++) Jo[kBase[bb] + q] = h->h_dJ[(size_t)(kBase[bb] + q) * ld + p] * sr;
+      }
+    }
+  }
+  if (cost) {
+    double total = 0.0;
+    for (int64_t j = 0; j < ND; j++) total += cost_ins[(size_t)j];
     *cost = total;
   }
   return MVBA_OK;

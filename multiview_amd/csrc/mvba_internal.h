@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstring>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -47,7 +48,52 @@ hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg
                            hipStream_t s);
 }
 
+extern "C" {
+size_t mvba_depth_desc_size(void);
+hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
+                                 const double4* dmeas, const mvba::FrameDesc* fd, const double* frec,
+                                 const double* params, const double4* pts, double* res, double* J, int64_t ld,
+                                 int32_t flags, double cauchy_c, hipStream_t s);
+hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
+                                  const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                  const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
+                                  hipStream_t s);
+hipError_t mvba_launch_depth_points(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
+                                    const double4* dmeas, const double* frec, const double* params,
+                                    const double4* pts, double* pgrad, double* phess, int32_t flags, double cauchy_c,
+                                    hipStream_t s);
+hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
+                                  const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                  int32_t flags, double cauchy_c, double* partial, hipStream_t s,
+                                  int64_t* nblocks_out);
+}
+
 namespace mvba_internal {
+
+// (beg, end, ref_to_cam, offset) block ids + the three stamps: what
+// calc_world_to_cam_trans depends on (rig_calibrator.cc:362-390).
+struct PoseKey {
+  int32_t b[4];
+  uint64_t s[3];
+  static PoseKey make(int32_t b0, int32_t b1, int32_t b2, int32_t b4, const double* st) {
+    PoseKey k;
+    k.b[0] = b0; k.b[1] = b1; k.b[2] = b2; k.b[3] = b4;
+    std::memcpy(k.s, st, 24);
+    return k;
+  }
+  bool operator==(const PoseKey& o) const {
+    return std::memcmp(b, o.b, sizeof(b)) == 0 && s[0] == o.s[0] && s[1] == o.s[1] && s[2] == o.s[2];
+  }
+};
+struct PoseKeyHash {
+  size_t operator()(const PoseKey& k) const {
+    uint64_t x = 1469598103934665603ull;
+    auto mix = [&](uint64_t v) { x = (x ^ v) * 1099511628211ull; };
+    for (int q = 0; q < 4; q++) mix((uint64_t)(uint32_t)k.b[q]);
+    mix(k.s[0]); mix(k.s[1]); mix(k.s[2]);
+    return (size_t)x;
+  }
+};
 
 constexpr int kFixedSize[7] = {7, 7, 7, 3, 1, 1, 2};
 
@@ -148,6 +194,20 @@ struct mvba_handle {
   int32_t* d_slot_po = nullptr;          // device slot -> point-order index (-1 = padding)
   std::vector<int64_t> cam_poff;         // camera-side entry -> packed parameter offset
   int32_t nchunks = 0;
+
+  // BracketedDepthError blocks (device order by frame)
+  int64_t ndep = 0, ndep_slots = 0;
+  int32_t ndep_segs = 0;
+  double bytes_dep = 0.0;
+  std::vector<int64_t> dep_order;         // depth slot -> depth insertion index (-1 = padding)
+  mvba::DepthDesc* d_dep_desc = nullptr;
+  double4* d_dep_meas = nullptr;          // (x, y, z, weight)
+  Segment* d_dep_segs = nullptr;
+  int64_t* d_dep_order = nullptr;
+  double* d_dres = nullptr;               // library-owned depth outputs (lazy)
+  double* d_dJ = nullptr;
+  int64_t dld = 0;
+  std::vector<double> h_dres, h_dJ;
 
   SolverState* solver = nullptr;         // LM state, allocated by the first mvba_solve
 

@@ -60,6 +60,18 @@ struct FrameLinHost {
   int64_t hoff[8];
 };
 
+// Per BracketedDepthError residual (device order: sorted by frame), 64 bytes.
+// The frame is the image whose pose blocks and stamps it shares (its world_to_cam
+// and generators are the frame's K0 record).
+struct DepthDesc {
+  int64_t dti_off, scale_off;    // packed offsets of depth_to_image and scale
+  int64_t goff_dti, goff_scale;  // camera-side gradient offsets (-1: constant)
+  int64_t hoff_dti, hoff_scale;  // camera-side Hessian offsets
+  int32_t frame, pid;            // frame record, point index
+  int32_t dti_n;                 // 7 (rigid) or 12 (affine)
+  int32_t free_mask;             // bits MVBA_DBLK_*: block is free (Jacobian written)
+};
+
 }  // namespace mvba
 
 #endif  // MVBA_TYPES_H_

@@ -32,6 +32,8 @@ class Evaluator:
         self.ld = ((self.num_slots + 63) // 64) * 64
         self.num_frames = int(self.lib.mvba_num_frames(self.h))
         self.num_points = int(self.lib.mvba_num_points(self.h))
+        self.num_depth = int(self.lib.mvba_num_depth_residuals(self.h))
+        self.num_depth_slots = int(self.lib.mvba_num_depth_slots(self.h))
 
     # ---------------------------------------------------------------- params
     def set_params(self, params: np.ndarray | None = None):
@@ -61,6 +63,20 @@ class Evaluator:
             (_lib.EVAL_APPLY_LOSS if apply_loss else 0)
         st = self.lib.mvba_evaluate(self.h, flags, float(robust_threshold), C.byref(cost),
                                     r.ctypes.data, J.ctypes.data if J is not None else None)
+        _lib.check(st, self.h)
+        return cost.value, r, J
+
+    def evaluate_depth(self, jacobian: bool = True, apply_loss: bool = False, robust_threshold: float = 3.0):
+        """BracketedDepthError blocks, host, depth insertion order: (cost,
+        residuals [N_d, 3], Jacobian [N_d, DJAC_ROWS] or None)."""
+        n = self.num_depth
+        r = np.empty((n, 3), dtype=np.float64)
+        J = np.empty((n, _lib.DJAC_ROWS), dtype=np.float64) if jacobian else None
+        cost = C.c_double(0.0)
+        flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0) | \
+            (_lib.EVAL_APPLY_LOSS if apply_loss else 0)
+        st = self.lib.mvba_evaluate_depth(self.h, flags, float(robust_threshold), C.byref(cost), r.ctypes.data,
+                                          J.ctypes.data if J is not None else None)
         _lib.check(st, self.h)
         return cost.value, r, J
 

@@ -64,11 +64,21 @@ class CamProblem:
     residual_meas: np.ndarray         # float64 [N, 2]
     residual_stamps: np.ndarray       # float64 [N, 3]
     residual_names: list = field(default_factory=list)  # per residual block: sensor name
+    # BracketedDepthError blocks (optional): 7 block ids each (MVBA_DBLK_* order)
+    depth_blocks: np.ndarray = field(default_factory=lambda: np.zeros((0, 7), dtype=np.int32))
+    depth_meas: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
+    depth_weight: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    depth_stamps: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
+    depth_after: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int64))  # preceding cam block
     _keep: list = field(default_factory=list, repr=False)
 
     @property
     def num_residuals(self) -> int:
         return int(self.residual_blocks.shape[0])
+
+    @property
+    def num_depth_residuals(self) -> int:
+        return int(self.depth_blocks.shape[0])
 
     def jacobian_stride(self) -> int:
         kmax = int(self.camera_dist_size.max()) if len(self.camera_dist_size) else 0
@@ -86,6 +96,10 @@ class CamProblem:
             np.ascontiguousarray(self.residual_camera, dtype=np.int32),
             np.ascontiguousarray(self.residual_meas, dtype=np.float64).reshape(-1),
             np.ascontiguousarray(self.residual_stamps, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.depth_blocks, dtype=np.int32).reshape(-1),
+            np.ascontiguousarray(self.depth_meas, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.depth_weight, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.depth_stamps, dtype=np.float64).reshape(-1),
         ]
         self._keep = arrs
         d = _lib.ProblemDesc()
@@ -102,10 +116,16 @@ class CamProblem:
         d.residual_camera = arrs[6].ctypes.data
         d.residual_meas = arrs[7].ctypes.data
         d.residual_stamps = arrs[8].ctypes.data
+        d.num_depth_residuals = self.num_depth_residuals
+        d.depth_blocks = arrs[9].ctypes.data
+        d.depth_meas = arrs[10].ctypes.data
+        d.depth_weight = arrs[11].ctypes.data
+        d.depth_stamps = arrs[12].ctypes.data
         return d
 
     def subset(self, idx: np.ndarray) -> "CamProblem":
-        """Problem made of the residual blocks ``idx`` (same parameter blocks)."""
+        """Problem made of the residual blocks ``idx`` (same parameter blocks, no
+        depth blocks)."""
         idx = np.asarray(idx)
         return CamProblem(
             block_size=self.block_size, block_offset=self.block_offset,

@@ -233,6 +233,10 @@ class Rig:
     obs_pix: np.ndarray               # [N_obs, 2] float32-rounded measurements
     init: dict = field(default_factory=dict)  # perturbed initial values
     sensor_names: list = field(default_factory=list)
+    # depth clouds (config c5): per observation of a depth sensor, the cloud point
+    depth_obs: np.ndarray = None      # [N_d] indices into obs_* (observations with depth)
+    depth_meas: np.ndarray = None     # [N_d, 3] float32-rounded depth-cloud points
+    depth_to_image: np.ndarray = None  # [N_s, 7 | 12] true depth_to_image per sensor
 
     @property
     def num_sensors(self):
@@ -251,10 +255,15 @@ def _sensor_yaw_deg(s: int, n_s: int) -> float:
 
 
 def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, models=None,
-             seed=1001, point_range=None, window=20, noise_px=0.5) -> Rig:
+             seed=1001, point_range=None, window=20, noise_px=0.5, depth_sensors=(),
+             depth_noise=0.01, affine_depth=False) -> Rig:
     """Build a synthetic rig. ``point_range=(lo, hi)`` generates only points
     [lo, hi) of a larger problem (landmark-range sharding): the
-    cameras are identical on every shard, points use a per-shard stream."""
+    cameras are identical on every shard, points use a per-shard stream.
+    ``depth_sensors``: sensors that also carry a depth cloud (config c5); every
+    observation of such a sensor gets the cloud point of its landmark,
+    depth_to_image^-1 (X_cam) + N(0, depth_noise^2), rounded to float32 (clouds
+    are float32, dense_map_utils.cc:1382)."""
     models = list(models or ["radtan"] * num_sensors)
     assert len(models) == num_sensors
     rng = np.random.default_rng(seed)
@@ -409,12 +418,39 @@ def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, mode
     init["dist"] = [d.copy() for d in dist]
     init["offsets"] = offsets.copy()
 
+    # depth clouds: true depth_to_image per sensor (small rotation + offset), scale 1
+    drng = np.random.default_rng([seed, 13])
+    nd_par = 12 if affine_depth else 7
+    dti_true = np.zeros((ns, nd_par))
+    dti_init = np.zeros((ns, nd_par))
+    Rd = small_rot(drng, ns, np.deg2rad(2.0))
+    td = np.array([0.05, -0.02, 0.01]) + drng.normal(0, 0.01, size=(ns, 3))
+    dRd = small_rot(irng, ns, np.deg2rad(0.1))
+    tdi = td + irng.normal(0, 0.01, size=(ns, 3))
+    for s_ in range(ns):
+        if affine_depth:
+            dti_true[s_] = np.concatenate([Rd[s_], td[s_][:, None]], axis=1).reshape(-1)
+            dti_init[s_] = np.concatenate([dRd[s_] @ Rd[s_], tdi[s_][:, None]], axis=1).reshape(-1)
+        else:
+            dti_true[s_] = np.r_[td[s_], mat_to_quat(Rd[s_][None])[0]]
+            dti_init[s_] = np.r_[tdi[s_], mat_to_quat((dRd[s_] @ Rd[s_])[None])[0]]
+    init["depth_to_image"] = dti_init
+    init["depth_scale"] = np.ones(ns)
+    dsel = np.nonzero(np.isin(cam_type[obs_cid], np.asarray(depth_sensors, dtype=np.int64)))[0]
+    dt = cam_type[obs_cid[dsel]]
+    Xc_d = Xo[dsel]
+    # meas = dti^-1 (X_cam) = R_d^T (X_cam - t_d)
+    dmeas = np.einsum("nji,nj->ni", Rd[dt], Xc_d - td[dt])
+    dmeas += np.random.default_rng([seed, 17, lo, hi]).normal(0, depth_noise, size=dmeas.shape)
+    dmeas = dmeas.astype(np.float32).astype(np.float64)
+
     names = ["ref_cam"] + [f"cam{s}" for s in range(1, ns)]
     return Rig(sensor_models=models, ref_stamps=ref_stamps, offsets=offsets,
                world_to_ref=world_to_ref, ref_to_cam=ref_to_cam, focal=focal, center=center,
                dist=dist, cam_type=cam_type, cam_beg=cam_beg, cam_end=cam_end,
                cam_stamp=cam_stamp, world_to_cam=world_to_cam, xyz=xyz, obs_pid=obs_pid,
-               obs_cid=obs_cid, obs_pix=obs_pix, init=init, sensor_names=names)
+               obs_cid=obs_cid, obs_pix=obs_pix, init=init, sensor_names=names,
+               depth_obs=dsel, depth_meas=dmeas, depth_to_image=dti_true)
 
 
 # ------------------------------------------------------------ problem assembly
@@ -426,6 +462,11 @@ class FloatFlags:
     intrinsics_to_float: tuple = ("focal_length", "optical_center", "distortion")
     float_timestamp_offsets: bool = True
     no_rig: bool = False
+    # depth (rig_calibrator.cc:1755-1791)
+    depth_tri_weight: float = 0.0
+    depth_to_image_transforms_to_float: tuple = ()
+    float_scale: bool = False
+    affine_depth_to_image: bool = False
 
 
 def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = True) -> CamProblem:
@@ -493,6 +534,19 @@ def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = Tr
             dist_b.append(-1)
     ph_b = add([0.0], True)  # distortion_placeholder (rig_calibrator.cc:1608)
     dist_b = [b if b >= 0 else ph_b for b in dist_b]
+    use_depth = flags.depth_tri_weight > 0 and rig.depth_obs is not None and rig.depth_obs.size > 0
+    if use_depth:
+        dti_src = src.get("depth_to_image", rig.depth_to_image) if use_init else rig.depth_to_image
+        want = 12 if flags.affine_depth_to_image else 7
+        if dti_src.shape[1] != want:
+            raise ValueError("rig depth_to_image kind does not match affine_depth_to_image")
+        dti_b0 = len(sizes)
+        for s in range(ns):
+            add(dti_src[s], names[s] not in flags.depth_to_image_transforms_to_float)
+        scl_b0 = len(sizes)
+        for s in range(ns):
+            add([src.get("depth_scale", np.ones(ns))[s] if use_init else 1.0],
+                (not flags.float_scale) or flags.affine_depth_to_image)
 
     sizes = np.array(sizes, dtype=np.int32)
     offs = np.zeros(len(sizes), dtype=np.int64)
@@ -527,11 +581,30 @@ def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = Tr
 
     dsize = np.array([len(d) for d in src["dist"]], dtype=np.int32)
     half = np.tile(np.array(IMAGE_SIZE, dtype=np.float64) / 2.0, (ns, 1))
-    return CamProblem(block_size=sizes, block_offset=offs, block_constant=const, params=params,
-                      camera_dist_size=dsize, camera_half_size=half, residual_blocks=blocks,
-                      residual_camera=ct.astype(np.int32), residual_meas=rig.obs_pix.copy(),
-                      residual_stamps=stamps,
-                      residual_names=None if n > 100000 else [names[t] for t in ct])
+    P = CamProblem(block_size=sizes, block_offset=offs, block_constant=const, params=params,
+                   camera_dist_size=dsize, camera_half_size=half, residual_blocks=blocks,
+                   residual_camera=ct.astype(np.int32), residual_meas=rig.obs_pix.copy(),
+                   residual_stamps=stamps,
+                   residual_names=None if n > 100000 else [names[t] for t in ct])
+    if use_depth:
+        # one BracketedDepthError right after the observation's BracketedCamError
+        # (rig_calibrator.cc:1755-1791): same beg/end/ref_to_cam/offset/stamps
+        k = rig.depth_obs
+        dct = ct[k]
+        db = np.empty((k.size, 7), dtype=np.int32)
+        db[:, 0] = blocks[k, 0]
+        db[:, 1] = blocks[k, 1]
+        db[:, 2] = blocks[k, 2]
+        db[:, 3] = dti_b0 + dct
+        db[:, 4] = scl_b0 + dct
+        db[:, 5] = blocks[k, 3]
+        db[:, 6] = blocks[k, 4]
+        P.depth_blocks = db
+        P.depth_meas = rig.depth_meas.copy()
+        P.depth_weight = np.full(k.size, float(flags.depth_tri_weight))
+        P.depth_stamps = stamps[k].copy()
+        P.depth_after = k.astype(np.int64)
+    return P
 
 
 # Workload presets.

@@ -155,3 +155,39 @@ def residual_stats(residuals, name_ids, num_names):
     lib.oracle_residual_stats(r.ctypes.data, ids.ctypes.data, r.size, num_names, out.ctypes.data,
                               cnt.ctypes.data)
     return out.reshape(num_names, 4), cnt
+
+
+DJAC_BASE = (0, 21, 42, 63, 99, 102, 111)
+DJAC_ROWS = 114
+
+
+def evaluate_depth(problem, mode=ANALYTIC, apply_loss=False, robust_threshold=3.0):
+    """All BracketedDepthError blocks of a CamProblem (rig_calibrator.cc:547-583),
+    depth insertion order. Returns (cost, r [n,3], J [n,DJAC_ROWS] or None) with
+    Ceres' Cauchy corrector applied when apply_loss (as Problem::Evaluate)."""
+    n = problem.num_depth_residuals
+    r = np.zeros((n, 3))
+    J = np.zeros((n, DJAC_ROWS)) if mode != RESIDUAL else None
+    b = robust_threshold * robust_threshold
+    cost = 0.0
+    for j in range(n):
+        blk = problem.depth_blocks[j]
+        blocks = [problem.block_values(int(x)) for x in blk]
+        const = problem.block_constant[blk]
+        rj, Jj = depth_error(blocks, const, problem.depth_weight[j], problem.depth_meas[j],
+                             *problem.depth_stamps[j], mode=mode)
+        s2 = float(rj @ rj)
+        sr = 1.0
+        if apply_loss:
+            cost += 0.5 * (b * np.log(1.0 + s2 / b))
+            sr = np.sqrt(max(np.finfo(float).tiny, 1.0 / (1.0 + s2 / b)))
+        else:
+            cost += 0.5 * s2
+        r[j] = rj * sr
+        if J is not None:
+            off = 0
+            for bb in range(7):
+                size = blocks[bb].size
+                J[j, DJAC_BASE[bb]:DJAC_BASE[bb] + 3 * size] = Jj[off:off + 3 * size] * sr
+                off += 3 * size
+    return cost, r, J
