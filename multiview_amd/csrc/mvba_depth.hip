@@ -379,6 +379,124 @@ __global__ void __launch_bounds__(256) k_depth_cost(int64_t nslots, const DepthD
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
+// ------------------------------------------------------------ solver passes
+// Depth blocks in the implicit Schur product (mvba_solver.hip has the
+// reprojection passes). With J_pt = P I (P = weight * sr):
+//   sa (before pass A): z_d = J_cam,d x (pose part via the frame's u_f = w x),
+//      tadd_p += P z_d  (consumed by pass A together with the reprojection terms);
+//   sb (after pass A):  u_d = z_d - P w_p; y += J_cam,d^T u_d (wave-reduced per
+//      segment, mapped through the generators, added into replica seg mod 32);
+//      optionally sum |u_d|^2 (model cost of the step).
+__global__ void __launch_bounds__(256) k_depth_sa(int64_t nslots, const DepthDesc* __restrict__ dd,
+                                                  const int64_t* __restrict__ dorder,
+                                                  const double4* __restrict__ dmeas, const double* __restrict__ frec,
+                                                  const double* __restrict__ params, const double4* __restrict__ pts,
+                                                  const double* __restrict__ dir, const double* __restrict__ x,
+                                                  double* __restrict__ dz, double* __restrict__ tadd, int32_t flags,
+                                                  double cauchy_c, int32_t dir_stride) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nslots || dorder[i] < 0) return;
+  const DepthDesc d = dd[i];
+  const double4 X = pts[d.pid];
+  DepthRows o;
+  depth_rows(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
+  const double* u = dir + (int64_t)d.frame * dir_stride;
+  double z[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    double v = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; a++) v += o.Z[r][a] * u[a];
+    if (d.goff_dti >= 0)
+      for (int q = 0; q < d.dti_n; q++) v += o.D[r][q] * x[d.goff_dti + q];
+    if (d.goff_scale >= 0) v += o.S[r] * x[d.goff_scale];
+    z[r] = v;
+    dz[3 * i + r] = v;
+  }
+  if (X.w != 0.0)
+#pragma unroll
+    for (int r = 0; r < 3; r++) atomicAdd(&tadd[3 * d.pid + r], o.P * z[r]);
+}
+
+__global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ segs, int32_t nseg,
+                                                 const DepthDesc* __restrict__ dd, const double4* __restrict__ dmeas,
+                                                 const double* __restrict__ frec, const double* __restrict__ params,
+                                                 const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
+                                                 const double* __restrict__ dz, const double* __restrict__ wp,
+                                                 double* __restrict__ yrep, int64_t ng, double* __restrict__ sq_partial,
+                                                 unsigned* __restrict__ counter, double* __restrict__ sq_out,
+                                                 int32_t flags, double cauchy_c) {
+  constexpr int NA = 6 + 12 + 1;
+  const int seg = blockIdx.x;
+  const Segment sg = segs[seg];
+  const int lane = threadIdx.x;
+  const int frame = __builtin_amdgcn_readfirstlane(sg.frame);
+  const double* rec = frec + (int64_t)frame * kFrameRecDoubles;
+  double acc[NA];
+#pragma unroll
+  for (int q = 0; q < NA; q++) acc[q] = 0.0;
+  double sq = 0.0;
+  const DepthDesc d0 = dd[sg.begin];
+  if (lane < sg.count) {
+    const int64_t i = (int64_t)sg.begin + lane;
+    const DepthDesc d = dd[i];
+    const double4 X = pts[d.pid];
+    DepthRows o;
+    depth_rows(d, rec, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
+    double u[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      u[r] = dz ? dz[3 * i + r] : 0.0;
+      if (X.w != 0.0) u[r] -= o.P * wp[3 * d.pid + r];
+      sq += u[r] * u[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+#pragma unroll
+      for (int a = 0; a < 6; a++) acc[a] += o.Z[r][a] * u[r];
+#pragma unroll
+      for (int q = 0; q < 12; q++) acc[6 + q] += o.D[r][q] * u[r];
+      acc[18] += o.S[r] * u[r];
+    }
+  }
+  if (yrep) {
+#pragma unroll
+    for (int q = 0; q < NA; q++) {
+      double v = acc[q];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      acc[q] = v;
+    }
+    const FrameLin& L = fl[frame];
+    double* y = yrep + (int64_t)(seg & (kDReplicas - 1)) * ng;
+    int64_t dst = -1;
+    double v = 0.0;
+    if (lane < kPoseCols) {
+      const int blk = lane / 7;
+      const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+      if (L.goff[b] >= 0) {
+        const double* wk = rec + 12 + 6 * lane;
+#pragma unroll
+        for (int a = 0; a < 6; a++) v += wk[a] * acc[a];
+        dst = L.goff[b] + (lane - 7 * blk);
+      }
+    } else if (lane < kPoseCols + 12) {
+      const int q = lane - kPoseCols;
+      if (d0.goff_dti >= 0 && q < d0.dti_n) {
+#pragma unroll
+        for (int e = 0; e < 12; e++)
+          if (e == q) v = acc[6 + e];
+        dst = d0.goff_dti + q;
+      }
+    } else if (lane == kPoseCols + 12 && d0.goff_scale >= 0) {
+      v = acc[18];
+      dst = d0.goff_scale;
+    }
+    if (dst >= 0) atomicAdd(&y[dst], v);
+  }
+  if (sq_partial) grid_sum_finalize(sq, sq_partial, counter, sq_out);
+}
+
 }  // namespace mvba
 
 extern "C" {
@@ -424,6 +542,28 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
   if (nslots <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_depth_cost, dim3((unsigned)blocks), dim3(256), 0, s, nslots, dd, dorder, dmeas, frec,
                      params, pts, flags, cauchy_c, partial);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_depth_sa(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
+                                const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                const double* dir, const double* x, double* dz, double* tadd, int32_t flags,
+                                double cauchy_c, int32_t dir_stride, hipStream_t s) {
+  if (nslots <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_depth_sa, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s, nslots, dd, dorder,
+                     dmeas, frec, params, pts, dir, x, dz, tadd, flags, cauchy_c, dir_stride);
+  return hipGetLastError();
+}
+
+// sq_partial needs nseg doubles
+hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
+                                const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                const void* fl, const double* dz, const double* wp, double* yrep, int64_t ng,
+                                double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
+                                hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params, pts,
+                     (const mvba::FrameLin*)fl, dz, wp, yrep, ng, sq_partial, counter, sq_out, flags, cauchy_c);
   return hipGetLastError();
 }
 

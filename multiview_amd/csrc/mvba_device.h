@@ -321,6 +321,40 @@ struct FrameLin {
   int64_t hoff[8];                   // camera-side Hessian offsets per block
 };
 
+// Last-block finalisation of a grid reduction: every block stores its partial,
+// the last block to arrive sums them into out[0] and re-arms the counter.
+__device__ __forceinline__ void grid_sum_finalize(double v, double* __restrict__ partial,
+                                                  unsigned* __restrict__ counter, double* __restrict__ out) {
+  __shared__ double red[256];
+  __shared__ bool last;
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = red[0];
+    __threadfence();
+    last = (atomicAdd(counter, 1u) == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  double acc = 0.0;
+  for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x) acc += __builtin_nontemporal_load(&partial[e]);
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = red[0];
+    *counter = 0u;
+  }
+}
+
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef double dbl2v __attribute__((ext_vector_type(2)));
 

@@ -145,40 +145,6 @@ __device__ __forceinline__ void pass_a_obs(const FrameDesc& F, const double* __r
   }
 }
 
-// Last-block finalisation of a grid reduction: every block stores its partial,
-// the last block to arrive sums them into out[0] and re-arms the counter.
-__device__ __forceinline__ void grid_sum_finalize(double v, double* __restrict__ partial,
-                                                  unsigned* __restrict__ counter, double* __restrict__ out) {
-  __shared__ double red[256];
-  __shared__ bool last;
-  red[threadIdx.x] = v;
-  __syncthreads();
-  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
-    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    partial[blockIdx.x] = red[0];
-    __threadfence();
-    last = (atomicAdd(counter, 1u) == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  double acc = 0.0;
-  for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x) acc += __builtin_nontemporal_load(&partial[e]);
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
-    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    out[0] = red[0];
-    *counter = 0u;
-  }
-}
-
 // kLanesA lanes per point; each lane keeps its first kCacheA observations' rows
 // (z_o and the two J_pt rows: 8 doubles) in registers, later ones go through zbuf.
 constexpr int kLanesA = 8;
@@ -208,8 +174,8 @@ __global__ void __launch_bounds__(256) k_pass_a(
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const double* __restrict__ dir,
-    const double* __restrict__ tinit, const double* __restrict__ V, const double* __restrict__ dp,
-    double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
+    const double* __restrict__ tinit, double* __restrict__ tadd, const double* __restrict__ V,
+    const double* __restrict__ dp, double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
     double* __restrict__ sq_partial, unsigned* __restrict__ counter, double* __restrict__ sq_out,
     int32_t flags, double cauchy_c) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -255,6 +221,13 @@ __global__ void __launch_bounds__(256) k_pass_a(
     for (int q = 0; q < 3; q++) tv[q] += __shfl_xor(tv[q], off, 64);
   double w[3] = {0.0, 0.0, 0.0};
   double sq = 0.0;
+  if (valid && tadd) {
+    // depth-block contributions J_pt^T z (k_depth_sa), consumed and re-zeroed; the
+    // point's lanes share a wave, so every lane reads before lane 0 writes
+    for (int q = 0; q < 3; q++) tv[q] += tadd[3 * p + q];
+    if (sub == 0)
+      for (int q = 0; q < 3; q++) tadd[3 * p + q] = 0.0;
+  }
   if (valid && X.w != 0.0) {
     if (tinit)
       for (int q = 0; q < 3; q++) tv[q] += tinit[3 * p + q];
@@ -735,21 +708,21 @@ hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::Fr
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const mvba::FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
-                              const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
-                              double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
-                              hipStream_t s) {
+                              double* tadd, const double* V, const double* dp, double* zbuf, double* ubuf,
+                              double* wout, double* sq_partial, unsigned* counter, double* sq_out, int32_t flags,
+                              double cauchy_c, hipStream_t s) {
   const unsigned blocks = (unsigned)((npts * mvba::kLanesA + 255) / 256);
   if (npts <= 0) return hipSuccess;
   if (model < 0) {
     hipLaunchKernelGGL((mvba::k_pass_a<-1, 0>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, fd,
-                       frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out, flags,
-                       cauchy_c);
+                       frec, params, pts, dir, tinit, tadd, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out,
+                       flags, cauchy_c);
     return hipGetLastError();
   }
 #define MVBA_PA(M, D)                                                                                      \
   hipLaunchKernelGGL((mvba::k_pass_a<M, D>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, \
-                     fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out,  \
-                     flags, cauchy_c)
+                     fd, frec, params, pts, dir, tinit, tadd, V, dp, zbuf, ubuf, wout, sq_partial, counter,    \
+                     sq_out, flags, cauchy_c)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PA)
 #undef MVBA_PA
   return hipGetLastError();

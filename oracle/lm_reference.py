@@ -27,6 +27,8 @@ def _columns(P):
     for b in range(7):
         used[P.residual_blocks[:, b]] = True
     used[P.residual_blocks[K_of > 0, 7]] = True
+    if P.num_depth_residuals:
+        used[P.depth_blocks.reshape(-1)] = True
     free = np.nonzero(used & (P.block_constant == 0))[0]
     col = np.full(len(P.block_size), -1, dtype=np.int64)
     pos = 0
@@ -60,12 +62,32 @@ def _jacobian(P, params, col, ncols, use_loss, thr):
             for k in range(n):
                 for comp in range(2):
                     np.add.at(D, (2 * sel[ok] + comp, c0[ok] + k), Jb[ok, comp, k])
-    return cost, r.reshape(-1), D
+    r = r.reshape(-1)
+    if P.num_depth_residuals:
+        # BracketedDepthError rows (rig_calibrator.cc:547-583), 3 per block
+        cd, rd, Jd = oracle_py.evaluate_depth(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
+        nd = P.num_depth_residuals
+        Dd = np.zeros((3 * nd, ncols))
+        for j in range(nd):
+            for b in range(7):
+                bid = int(P.depth_blocks[j, b])
+                c0 = col[bid]
+                if c0 < 0:
+                    continue
+                size = int(P.block_size[bid])
+                base = oracle_py.DJAC_BASE[b]
+                Dd[3 * j:3 * j + 3, c0:c0 + size] += Jd[j, base:base + 3 * size].reshape(3, size)
+        cost += cd
+        r = np.concatenate([r, rd.reshape(-1)])
+        D = np.vstack([D, Dd])
+    return cost, r, D
 
 
 def _cost(P, params, use_loss, thr):
     Q = dataclasses.replace(P, params=params)
     c, _, _ = oracle_py.evaluate(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
+    if P.num_depth_residuals:
+        c += oracle_py.evaluate_depth(Q, oracle_py.RESIDUAL, apply_loss=use_loss, robust_threshold=thr)[0]
     return c
 
 

@@ -134,6 +134,49 @@ def test_ill_conditioned_rpc_reaches_same_cost():
     assert np.all(np.isfinite(x))
 
 
+DEPTH_FLAGS = dict(camera_poses_to_float=(), depth_tri_weight=10.0, depth_to_image_transforms_to_float=("cam2",),
+                   float_scale=True)
+
+
+@pytest.mark.parametrize("affine", [False, True])
+def test_depth_one_exact_step_matches_dense_lm(affine):
+    """BracketedDepthError blocks in the implicit Schur product, right-hand side
+    and back-substitution: one exact-CG LM step equals the dense step."""
+    from oracle import lm_reference
+
+    R = rig.make_rig(num_sensors=3, num_ref=12, num_points=200, obs_per_point=5, models=["radtan", "fov", "none"],
+                     seed=81, depth_sensors=(2,), affine_depth=affine)
+    P = rig.build_problem(R, rig.FloatFlags(affine_depth_to_image=affine, **DEPTH_FLAGS))
+    assert P.num_depth_residuals > 0
+    for use_loss in (False, True):
+        x_ref, s_ref = lm_reference.solve(P, max_num_iterations=1, use_loss=use_loss, **TOL)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=2000, use_loss=int(use_loss),
+                         robust_threshold=3.0, **TOL)
+            x = ev.get_params()
+        assert np.isclose(s["initial_cost"], s_ref["initial_cost"], rtol=1e-11)
+        m = _free_mask(P)
+        assert _close(x[m], x_ref[m], 1e-8), (use_loss, np.abs(x[m] - x_ref[m]).max())
+
+
+def test_depth_converged_params_match_cpu_lm():
+    from oracle import lm_reference
+
+    R = rig.make_rig(num_sensors=3, num_ref=12, num_points=200, obs_per_point=5, models=["radtan", "fov", "none"],
+                     seed=82, depth_sensors=(2,))
+    P = rig.build_problem(R, rig.FloatFlags(**DEPTH_FLAGS))
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, **TOL)
+        x = ev.get_params()
+    assert s["termination_type"] == 0, s["message"]
+    assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-9)
+    assert np.abs(_poses(P, x) - _poses(P, x_ref)).max() <= 1e-6
+    assert _close(_others(P, x), _others(P, x_ref), 1e-6)
+
+
 def test_bounded_offsets_and_callback_path():
     """Floated timestamp offsets carry the reference's bracket bounds; a no-op
     allreduce callback (single rank) must not change the result."""
