@@ -22,6 +22,7 @@ timed on this host.
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -107,7 +108,7 @@ def main():
     cfg["point_range"] = (rank * npts, (rank + 1) * npts)
     t0 = time.perf_counter()
     R = rig.make_rig(**cfg)
-    P = rig.build_problem(R)
+    P = rig.build_problem(R, rig.FloatFlags(**rig.CONFIG_FLAGS.get(args.config, {})))
     t_gen = time.perf_counter() - t0
 
     ev = Evaluator(P, device=dev)
@@ -195,6 +196,38 @@ def main():
         },
         "gen_s": t_gen,
     }
+    # ---- depth blocks (c5): K1-depth evaluation, materialised
+    if ev.num_depth > 0:
+        dld = (ev.num_depth_slots + 63) // 64 * 64
+        dres = torch.empty((3, dld), dtype=torch.float64, device="cuda")
+        dJ = torch.empty((_lib.DJAC_ROWS, dld), dtype=torch.float64, device="cuda")
+
+        def dstep():
+            _lib.check(ev.lib.mvba_evaluate_depth_device(
+                ev.h, _lib.EVAL_RESIDUALS | _lib.EVAL_JACOBIAN | _lib.EVAL_SKIP_PREP, 0.0,
+                C.c_void_p(dres.data_ptr()), C.c_void_p(dJ.data_ptr()), dld, C.c_void_p(sh)), ev.h)
+
+        for _ in range(args.warmup):
+            dstep()
+        torch.cuda.synchronize()
+        de = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        de[0].record(stream)
+        for _ in range(args.steps):
+            dstep()
+        de[1].record(stream)
+        torch.cuda.synchronize()
+        d_ms = de[0].elapsed_time(de[1]) / args.steps
+        dbytes = float(ev.lib.mvba_eval_bytes(ev.h, _lib.EVAL_DEPTH))
+        line["depth"] = {
+            "what": "BracketedDepthError residual+Jacobian (K1-depth, materialised, column planes)",
+            "num_depth_residuals": ev.num_depth,
+            "evals_per_s": ev.num_depth / (d_ms * 1e-3),
+            "kernel_ms": d_ms,
+            "bytes_per_launch": dbytes,
+            "achieved_GBps": dbytes / (d_ms * 1e-3) / 1e9,
+            "frac_of_hbm_peak": dbytes / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        }
+
     # ---- phase B: normal equations (K2) + the per-iteration exchange (§8e)
     from multiview_amd.dist import NormalEquationBuffer, check_layouts_agree
 

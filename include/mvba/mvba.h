@@ -278,6 +278,11 @@ mvba_status mvba_evaluate_depth(struct mvba_handle* h, int32_t flags, double cau
 mvba_status mvba_evaluate_depth_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                                        double* d_res, double* d_J, int64_t ld, void* hip_stream);
 
+/* mvba_eval_bytes(h, MVBA_EVAL_DEPTH): algorithmic bytes of one materialised
+ * depth evaluation (per block 32 meas+weight, 24 landmark, 24 residual, 24 per
+ * written Jacobian column). */
+#define MVBA_EVAL_DEPTH 0x100
+
 /* Counts for reporting. */
 int64_t mvba_num_residuals(const struct mvba_handle* h);
 /* Device slots = residuals + padding that line-aligns every frame's range; device

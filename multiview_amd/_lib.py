@@ -33,6 +33,7 @@ EVAL_JACOBIAN = 0x2
 EVAL_APPLY_LOSS = 0x4
 EVAL_PREP_ONLY = 0x8
 EVAL_SKIP_PREP = 0x10
+EVAL_DEPTH = 0x100
 
 # Jacobian row bases (MVBA_JAC_BASE_*), block order of rig_calibrator.cc:1695-1699.
 JAC_BASE = (0, 14, 28, 42, 48, 50, 52, 56)

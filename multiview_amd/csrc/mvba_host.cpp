@@ -620,6 +620,7 @@ int64_t mvba_num_points(const mvba_handle* h) { return h ? h->npts : 0; }
 
 double mvba_eval_bytes(const mvba_handle* h, int32_t flags) {
   if (!h) return 0.0;
+  if (flags & MVBA_EVAL_DEPTH) return h->bytes_dep;
   return h->bytes_res + ((flags & MVBA_EVAL_JACOBIAN) ? h->bytes_jac : 0.0);
 }
 

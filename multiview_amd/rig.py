@@ -607,12 +607,15 @@ def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = Tr
     return P
 
 
-# Workload presets.
+# Workload presets. c5 runs with CONFIG_FLAGS["c5"].
 CONFIGS = {
     "c1": dict(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, models=["none"] * 3, seed=1001),
     "c2": dict(num_sensors=3, num_ref=1000, num_points=100000, obs_per_point=10.0, models=["radtan"] * 3, seed=1002),
     "c3": dict(num_sensors=3, num_ref=3000, num_points=1000000, obs_per_point=10.0, models=["rpc2"] * 3, seed=1003),
     "c4": dict(num_sensors=8, num_ref=2500, num_points=5000000, obs_per_point=10.0, models=["radtan"] * 8, seed=1004),
+    # 3 image sensors + 1 image+depth sensor: ~1M reprojection + ~250k depth blocks
+    "c5": dict(num_sensors=4, num_ref=1000, num_points=100000, obs_per_point=10.0, models=["radtan"] * 4, seed=1005,
+               depth_sensors=(3,)),
 }
 
 
@@ -646,3 +649,9 @@ def offset_bounds(rig: Rig, problem: CamProblem, flags: FloatFlags | None = None
         lower[o] = max(lo[s], cur - max_change) + 1.0e-5
         upper[o] = min(hi[s], cur + max_change) - 1.0e-5
     return lower, upper
+
+
+# FloatFlags of the presets beyond the default "everything floats"
+CONFIG_FLAGS = {
+    "c5": dict(depth_tri_weight=10.0, depth_to_image_transforms_to_float=("cam3",), float_scale=True),
+}
