@@ -12,132 +12,9 @@
 // depth_to_image / scale columns: dr/dtheta = -weight Rinv dM/dtheta; xyz: weight I.
 // Device order: depth blocks sorted by frame, line-aligned frame ranges, segments
 // of <= 64 blocks of one frame (one wave each), like the reprojection blocks.
-#include "mvba_device.h"
+#include "mvba_depth.h"
 
 namespace mvba {
-
-// Eigen Matrix3d::inverse (cofactors / determinant) as restated in oracle.cpp's
-// affine_inverse (Affine3d::inverse in Affine mode [ext]).
-__device__ __forceinline__ void inverse3(const double* m, double* o) {
-  const double c00 = m[4] * m[8] - m[5] * m[7];
-  const double c10 = m[5] * m[6] - m[3] * m[8];
-  const double c20 = m[3] * m[7] - m[4] * m[6];
-  const double det = c00 * m[0] + c10 * m[1] + c20 * m[2];
-  const double inv = 1.0 / det;
-  o[0] = c00 * inv;
-  o[1] = (m[2] * m[7] - m[1] * m[8]) * inv;
-  o[2] = (m[1] * m[5] - m[2] * m[4]) * inv;
-  o[3] = c10 * inv;
-  o[4] = (m[0] * m[8] - m[2] * m[6]) * inv;
-  o[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
-  o[6] = c20 * inv;
-  o[7] = (m[1] * m[6] - m[0] * m[7]) * inv;
-  o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
-}
-
-__device__ __forceinline__ double loss_scale3(double r0, double r1, double r2, int32_t flags, double cauchy_c,
-                                              double* half_rho) {
-  const double s = r0 * r0 + r1 * r1 + r2 * r2;
-  if (flags & MVBA_EVAL_APPLY_LOSS) {
-    const double sum = 1.0 + s * cauchy_c;
-    *half_rho = 0.5 * (log(sum) / cauchy_c);
-    return sqrt(fmax(DBL_MIN, 1.0 / sum));
-  }
-  *half_rho = 0.5 * s;
-  return 1.0;
-}
-
-// Residual and Jacobian rows of one depth block, all multiplied by the loss
-// scale sr (Ceres' corrector for Cauchy, alpha = 0).
-struct DepthRows {
-  double r[3];       // corrected residual
-  double rr[3];      // raw residual (host corrector path)
-  double Z[3][6];    // pose rows: J_pose(i, k) = Z[i] . w_k
-  double D[3][12];   // depth_to_image rows (dti_n used)
-  double S[3];       // scale column
-  double P;          // xyz: P * identity
-  double sr, half_rho;
-};
-
-__device__ __forceinline__ void depth_rows(const DepthDesc& d, const double* __restrict__ rec,
-                                           const double* __restrict__ params, double4 m, double X0, double X1,
-                                           double X2, int32_t flags, double cauchy_c, DepthRows& o) {
-  const double* p = params + d.dti_off;
-  double A[9], b[3], qh[4] = {0, 0, 0, 1}, in = 1.0;
-  if (d.dti_n == 12) {
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-#pragma unroll
-      for (int c = 0; c < 3; c++) A[3 * r + c] = p[4 * r + c];
-      b[r] = p[4 * r + 3];
-    }
-  } else {
-    rigid(p, A, qh, &in);
-    b[0] = p[0]; b[1] = p[1]; b[2] = p[2];
-  }
-  const double s = params[d.scale_off];
-  const double w = m.w;
-  double Am[3];
-#pragma unroll
-  for (int r = 0; r < 3; r++) Am[r] = A[3 * r] * m.x + A[3 * r + 1] * m.y + A[3 * r + 2] * m.z;
-  // (linear * scale) * meas + translation, in Eigen's order: ((s A) m) + b
-  double M[3];
-#pragma unroll
-  for (int r = 0; r < 3; r++) M[r] = (s * A[3 * r]) * m.x + (s * A[3 * r + 1]) * m.y + (s * A[3 * r + 2]) * m.z + b[r];
-  double Ri[9];
-  inverse3(rec, Ri);
-  const double ti[3] = {-(Ri[0] * rec[9] + Ri[1] * rec[10] + Ri[2] * rec[11]),
-                        -(Ri[3] * rec[9] + Ri[4] * rec[10] + Ri[5] * rec[11]),
-                        -(Ri[6] * rec[9] + Ri[7] * rec[10] + Ri[8] * rec[11])};
-  const double X[3] = {X0, X1, X2};
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    const double Mw = Ri[3 * i] * M[0] + Ri[3 * i + 1] * M[1] + Ri[3 * i + 2] * M[2] + ti[i];
-    o.rr[i] = w * (X[i] - Mw);
-  }
-  const double sr = loss_scale3(o.rr[0], o.rr[1], o.rr[2], flags, cauchy_c, &o.half_rho);
-  o.sr = sr;
-  const double ws = w * sr;
-  o.P = ws;
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    o.r[i] = o.rr[i] * sr;
-    const double ri[3] = {Ri[3 * i], Ri[3 * i + 1], Ri[3 * i + 2]};
-    double mx[3];
-    cross(M, ri, mx);
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-      o.Z[i][q] = ws * mx[q];
-      o.Z[i][3 + q] = ws * ri[q];
-    }
-    o.S[i] = -ws * (ri[0] * Am[0] + ri[1] * Am[1] + ri[2] * Am[2]);
-#pragma unroll
-    for (int q = 0; q < 12; q++) o.D[i][q] = 0.0;
-    if (d.dti_n == 12) {
-#pragma unroll
-      for (int rr = 0; rr < 3; rr++) {
-        const double g = -ws * ri[rr];
-        o.D[i][4 * rr] = g * s * m.x;
-        o.D[i][4 * rr + 1] = g * s * m.y;
-        o.D[i][4 * rr + 2] = g * s * m.z;
-        o.D[i][4 * rr + 3] = g;
-      }
-    } else {
-      // translation
-#pragma unroll
-      for (int j = 0; j < 3; j++) o.D[i][j] = -ws * ri[j];
-      // quaternion: dM/dq_k = s (om_k x Am)  ->  dr_i/dq_k = -ws s om_k . (Am x ri)
-      double axr[3];
-      cross(Am, ri, axr);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        double om[3];
-        quat_generator(qh, 2.0 * in, k, om);
-        o.D[i][3 + k] = -ws * s * (om[0] * axr[0] + om[1] * axr[1] + om[2] * axr[2]);
-      }
-    }
-  }
-}
 
 constexpr int kDJacBase[7] = {MVBA_DJAC_BASE_BEG, MVBA_DJAC_BASE_END, MVBA_DJAC_BASE_REF_TO_CAM,
                               MVBA_DJAC_BASE_DEPTH_TO_IMAGE, MVBA_DJAC_BASE_SCALE, MVBA_DJAC_BASE_XYZ,
@@ -174,30 +51,42 @@ __global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ se
   const double un = loss ? 1.0 : 1.0 / o.sr;
   const int mask = d.free_mask;
   const double* wv = rec + 12;
+#pragma unroll
   for (int blk = 0; blk < 4; blk++) {
     const int db = (blk == 3) ? MVBA_DBLK_OFFSET : blk;
-    if (!(mask & (1 << db))) continue;
     const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
-    for (int i3 = 0; i3 < 3; i3++)
-      for (int c = 0; c < ncol; c++) {
-        const double* wk = wv + 6 * (k0 + c);
+    if (!(mask & (1 << db))) continue;
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+      if (c >= ncol) break;
+      const double* wk = wv + 6 * (k0 + c);
+#pragma unroll
+      for (int i3 = 0; i3 < 3; i3++) {
         double v = 0.0;
 #pragma unroll
         for (int a = 0; a < 6; a++) v += o.Z[i3][a] * wk[a];
         __builtin_nontemporal_store(v * un, &J[(int64_t)(kDJacBase[db] + i3 * ncol + c) * ld + i]);
       }
+    }
   }
   if (mask & (1 << MVBA_DBLK_DEPTH_TO_IMAGE)) {
     const int n = d.dti_n;
+#pragma unroll
     for (int i3 = 0; i3 < 3; i3++)
-      for (int c = 0; c < n; c++)
-        __builtin_nontemporal_store(o.D[i3][c] * un, &J[(int64_t)(MVBA_DJAC_BASE_DEPTH_TO_IMAGE + i3 * n + c) * ld + i]);
+#pragma unroll
+      for (int c = 0; c < 12; c++)
+        if (c < n)
+          __builtin_nontemporal_store(o.D[i3][c] * un,
+                                      &J[(int64_t)(MVBA_DJAC_BASE_DEPTH_TO_IMAGE + i3 * n + c) * ld + i]);
   }
   if (mask & (1 << MVBA_DBLK_SCALE))
+#pragma unroll
     for (int i3 = 0; i3 < 3; i3++)
       __builtin_nontemporal_store(o.S[i3] * un, &J[(int64_t)(MVBA_DJAC_BASE_SCALE + i3) * ld + i]);
   if (mask & (1 << MVBA_DBLK_XYZ))
+#pragma unroll
     for (int i3 = 0; i3 < 3; i3++)
+#pragma unroll
       for (int c = 0; c < 3; c++)
         __builtin_nontemporal_store(i3 == c ? o.P * un : 0.0, &J[(int64_t)(MVBA_DJAC_BASE_XYZ + i3 * 3 + c) * ld + i]);
 }
@@ -328,29 +217,6 @@ __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ s
   if (lane == 0) atomicAdd(&grad[ng + nh], cost);
 }
 
-// Point side: V_p += (w sr)^2 I, g_p += (w sr) r~ (after k_points_lin wrote them).
-__global__ void __launch_bounds__(256) k_depth_points(int64_t nslots, const DepthDesc* __restrict__ dd,
-                                                      const int64_t* __restrict__ dorder,
-                                                      const double4* __restrict__ dmeas,
-                                                      const double* __restrict__ frec,
-                                                      const double* __restrict__ params,
-                                                      const double4* __restrict__ pts, double* __restrict__ pgrad,
-                                                      double* __restrict__ phess, int32_t flags, double cauchy_c) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nslots || dorder[i] < 0) return;
-  const DepthDesc d = dd[i];
-  const double4 X = pts[d.pid];
-  if (X.w == 0.0) return;
-  DepthRows o;
-  depth_rows(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
-  const double P2 = o.P * o.P;
-  atomicAdd(&phess[6 * d.pid + 0], P2);
-  atomicAdd(&phess[6 * d.pid + 3], P2);
-  atomicAdd(&phess[6 * d.pid + 5], P2);
-#pragma unroll
-  for (int q = 0; q < 3; q++) atomicAdd(&pgrad[3 * d.pid + q], o.P * o.r[q]);
-}
-
 // Cost partials (sum 0.5 rho) per 256-thread block over the depth slots.
 __global__ void __launch_bounds__(256) k_depth_cost(int64_t nslots, const DepthDesc* __restrict__ dd,
                                                     const int64_t* __restrict__ dorder,
@@ -379,52 +245,16 @@ __global__ void __launch_bounds__(256) k_depth_cost(int64_t nslots, const DepthD
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-// ------------------------------------------------------------ solver passes
-// Depth blocks in the implicit Schur product (mvba_solver.hip has the
-// reprojection passes). With J_pt = P I (P = weight * sr):
-//   sa (before pass A): z_d = J_cam,d x (pose part via the frame's u_f = w x),
-//      tadd_p += P z_d  (consumed by pass A together with the reprojection terms);
-//   sb (after pass A):  u_d = z_d - P w_p; y += J_cam,d^T u_d (wave-reduced per
-//      segment, mapped through the generators, added into replica seg mod 32);
-//      optionally sum |u_d|^2 (model cost of the step).
-__global__ void __launch_bounds__(256) k_depth_sa(int64_t nslots, const DepthDesc* __restrict__ dd,
-                                                  const int64_t* __restrict__ dorder,
-                                                  const double4* __restrict__ dmeas, const double* __restrict__ frec,
-                                                  const double* __restrict__ params, const double4* __restrict__ pts,
-                                                  const double* __restrict__ dir, const double* __restrict__ x,
-                                                  double* __restrict__ dz, double* __restrict__ tadd, int32_t flags,
-                                                  double cauchy_c, int32_t dir_stride) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nslots || dorder[i] < 0) return;
-  const DepthDesc d = dd[i];
-  const double4 X = pts[d.pid];
-  DepthRows o;
-  depth_rows(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
-  const double* u = dir + (int64_t)d.frame * dir_stride;
-  double z[3];
-#pragma unroll
-  for (int r = 0; r < 3; r++) {
-    double v = 0.0;
-#pragma unroll
-    for (int a = 0; a < 6; a++) v += o.Z[r][a] * u[a];
-    if (d.goff_dti >= 0)
-      for (int q = 0; q < d.dti_n; q++) v += o.D[r][q] * x[d.goff_dti + q];
-    if (d.goff_scale >= 0) v += o.S[r] * x[d.goff_scale];
-    z[r] = v;
-    dz[3 * i + r] = v;
-  }
-  if (X.w != 0.0)
-#pragma unroll
-    for (int r = 0; r < 3; r++) atomicAdd(&tadd[3 * d.pid + r], o.P * z[r]);
-}
-
+// ------------------------------------------------------------ solver pass
+// Depth blocks in the implicit Schur product after pass A (which computed, in
+// point order, u_d = J_cam,d x - P w_p for every depth block into du):
+// y += J_cam,d^T u_d, wave-reduced per segment, mapped through the generators,
+// added into replica (segment mod 32) of the camera-side vector.
 __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ segs, int32_t nseg,
                                                  const DepthDesc* __restrict__ dd, const double4* __restrict__ dmeas,
                                                  const double* __restrict__ frec, const double* __restrict__ params,
                                                  const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
-                                                 const double* __restrict__ dz, const double* __restrict__ wp,
-                                                 double* __restrict__ yrep, int64_t ng, double* __restrict__ sq_partial,
-                                                 unsigned* __restrict__ counter, double* __restrict__ sq_out,
+                                                 const double* __restrict__ du, double* __restrict__ yrep, int64_t ng,
                                                  int32_t flags, double cauchy_c) {
   constexpr int NA = 6 + 12 + 1;
   const int seg = blockIdx.x;
@@ -435,31 +265,18 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
   double acc[NA];
 #pragma unroll
   for (int q = 0; q < NA; q++) acc[q] = 0.0;
-  double sq = 0.0;
   const DepthDesc d0 = dd[sg.begin];
   if (lane < sg.count) {
     const int64_t i = (int64_t)sg.begin + lane;
     const DepthDesc d = dd[i];
     const double4 X = pts[d.pid];
-    DepthRows o;
-    depth_rows(d, rec, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
-    double u[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-      u[r] = dz ? dz[3 * i + r] : 0.0;
-      if (X.w != 0.0) u[r] -= o.P * wp[3 * d.pid + r];
-      sq += u[r] * u[r];
-    }
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-#pragma unroll
-      for (int a = 0; a < 6; a++) acc[a] += o.Z[r][a] * u[r];
-#pragma unroll
-      for (int q = 0; q < 12; q++) acc[6 + q] += o.D[r][q] * u[r];
-      acc[18] += o.S[r] * u[r];
-    }
+    const double4 m = dmeas[i];
+    DepthCore c;
+    depth_core(d, rec, params, m, X.x, X.y, X.z, flags, cauchy_c, c);
+    const double u[3] = {du[3 * i], du[3 * i + 1], du[3 * i + 2]};
+    depth_jtu(c, m, u, acc, acc + 6, acc + 18);
   }
-  if (yrep) {
+  {
 #pragma unroll
     for (int q = 0; q < NA; q++) {
       double v = acc[q];
@@ -494,7 +311,6 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
     }
     if (dst >= 0) atomicAdd(&y[dst], v);
   }
-  if (sq_partial) grid_sum_finalize(sq, sq_partial, counter, sq_out);
 }
 
 }  // namespace mvba
@@ -523,16 +339,6 @@ hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_depth_points(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
-                                    const double4* dmeas, const double* frec, const double* params,
-                                    const double4* pts, double* pgrad, double* phess, int32_t flags, double cauchy_c,
-                                    hipStream_t s) {
-  if (nslots <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_depth_points, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s, nslots, dd, dorder,
-                     dmeas, frec, params, pts, pgrad, phess, flags, cauchy_c);
-  return hipGetLastError();
-}
-
 hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   int32_t flags, double cauchy_c, double* partial, hipStream_t s,
@@ -545,25 +351,13 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_depth_sa(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
-                                const double4* dmeas, const double* frec, const double* params, const double4* pts,
-                                const double* dir, const double* x, double* dz, double* tadd, int32_t flags,
-                                double cauchy_c, int32_t dir_stride, hipStream_t s) {
-  if (nslots <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_depth_sa, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s, nslots, dd, dorder,
-                     dmeas, frec, params, pts, dir, x, dz, tadd, flags, cauchy_c, dir_stride);
-  return hipGetLastError();
-}
-
-// sq_partial needs nseg doubles
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
-                                const void* fl, const double* dz, const double* wp, double* yrep, int64_t ng,
-                                double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
-                                hipStream_t s) {
+                                const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
+                                double cauchy_c, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params, pts,
-                     (const mvba::FrameLin*)fl, dz, wp, yrep, ng, sq_partial, counter, sq_out, flags, cauchy_c);
+                     (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c);
   return hipGetLastError();
 }
 

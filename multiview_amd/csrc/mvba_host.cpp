@@ -35,7 +35,8 @@ static void free_all(mvba_handle* h) {
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
                   h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
-                  h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ};
+                  h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
+                  h->d_dpt_begin, h->d_dpo_slot};
   solver_state_free(h->solver);
   h->solver = nullptr;
   for (void* p : ptrs)
@@ -534,6 +535,19 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   }
   h->ndep = ND;
   h->ndep_segs = (int32_t)dsegs.size();
+  std::vector<int64_t> dpt_begin;
+  std::vector<int32_t> dpo_slot;
+  if (ND > 0) {
+    dpt_begin.assign(h->npts + 1, 0);
+    for (int64_t j = 0; j < ND; j++) dpt_begin[dep_pt[j] + 1]++;
+    for (int64_t p = 0; p < h->npts; p++) dpt_begin[p + 1] += dpt_begin[p];
+    std::vector<int64_t> fill(dpt_begin.begin(), dpt_begin.end() - 1);
+    dpo_slot.resize(ND);
+    for (int64_t q = 0; q < h->ndep_slots; q++) {
+      const int64_t j = h->dep_order[q];
+      if (j >= 0) dpo_slot[fill[dep_pt[j]]++] = (int32_t)q;
+    }
+  }
 
   // ---- upload
   hipError_t e = hipSuccess;
@@ -575,6 +589,8 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_dep_meas, dmeas));
   chk(upload(&h->d_dep_segs, dsegs));
   chk(upload(&h->d_dep_order, h->dep_order));
+  chk(upload(&h->d_dpt_begin, dpt_begin));
+  chk(upload(&h->d_dpo_slot, dpo_slot));
   if (e != hipSuccess) {
     g_create_error = std::string("HIP error during mvba_create: ") + hipGetErrorString(e);
     free_all(h);
@@ -779,10 +795,7 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
     e = mvba_launch_points_lin(h->groups.size() == 1 ? h->groups[0].model : -1,
                                h->groups.size() == 1 ? h->groups[0].deg : 0, h->d_pt_begin, h->npts,
                                h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
-                               d_pt_grad, d_pt_hess, lflags, cauchy_c, s);
-  if (e == hipSuccess && h->ndep > 0)
-    e = mvba_launch_depth_points(h->ndep_slots, h->d_dep_desc, h->d_dep_order, h->d_dep_meas, h->d_frec, h->d_params,
-                                 h->d_pts, d_pt_grad, d_pt_hess, lflags, cauchy_c, s);
+                               d_pt_grad, d_pt_hess, lflags, cauchy_c, h->depth_csr(), s);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_linearize_device launch");
   return MVBA_OK;
 }

@@ -40,7 +40,7 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
                                   const int32_t* po_frame, const double2* po_meas, const FrameDesc* fd,
                                   const double* frec, const double* params, const double4* pts,
                                   double* pgrad, double* phess, int32_t flags, double cauchy_c,
-                                  hipStream_t s);
+                                  mvba::DepthCsr dc, hipStream_t s);
 hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
                            const FrameDesc* fd, const double* frec, const double* params,
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
@@ -58,10 +58,6 @@ hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
                                   hipStream_t s);
-hipError_t mvba_launch_depth_points(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
-                                    const double4* dmeas, const double* frec, const double* params,
-                                    const double4* pts, double* pgrad, double* phess, int32_t flags, double cauchy_c,
-                                    hipStream_t s);
 hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   int32_t flags, double cauchy_c, double* partial, hipStream_t s,
@@ -204,6 +200,16 @@ struct mvba_handle {
   double4* d_dep_meas = nullptr;          // (x, y, z, weight)
   Segment* d_dep_segs = nullptr;
   int64_t* d_dep_order = nullptr;
+  int64_t* d_dpt_begin = nullptr;         // CSR point -> depth slots
+  int32_t* d_dpo_slot = nullptr;
+  mvba::DepthCsr depth_csr() const {
+    mvba::DepthCsr c;
+    c.begin = ndep > 0 ? d_dpt_begin : nullptr;
+    c.slot = d_dpo_slot;
+    c.dd = d_dep_desc;
+    c.meas = d_dep_meas;
+    return c;
+  }
   double* d_dres = nullptr;               // library-owned depth outputs (lazy)
   double* d_dJ = nullptr;
   int64_t dld = 0;

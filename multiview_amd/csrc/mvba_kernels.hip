@@ -19,7 +19,7 @@
 //     dR_wc/dp_k = [w_k]x R_wc,   d(Xc)/dp_k = w_k x Xc + v_k,
 // so per observation the 22 pose columns are  J_ik = (Xc x G_i).w_k + G_i.v_k
 // with G = d(pixel)/d(Xc) (2x3). w_k, v_k depend only on the frame (K0).
-#include "mvba_device.h"
+#include "mvba_depth.h"
 
 namespace mvba {
 
@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(256) k_points_lin(
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, double* __restrict__ pgrad, double* __restrict__ phess,
-    int32_t flags, double cauchy_c) {
+    int32_t flags, double cauchy_c, DepthCsr dc) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = t / kLanesPerPoint;
   const int sub = (int)(t % kLanesPerPoint);
@@ -612,6 +612,23 @@ __global__ void __launch_bounds__(256) k_points_lin(
         else if (K == 44) point_obs<kModelRpc, 2>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
         else if (K == 76) point_obs<kModelRpc, 3>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
       }
+    }
+  }
+  if (dc.begin && valid && X.w != 0.0) {
+    // BracketedDepthError blocks of this point: J_pt = P I (P = weight * sr)
+    const double4* dmeas = reinterpret_cast<const double4*>(dc.meas);
+    for (int64_t j = dc.begin[p] + sub; j < dc.begin[p + 1]; j += kLanesPerPoint) {
+      const int32_t sl = dc.slot[j];
+      const DepthDesc d = dc.dd[sl];
+      DepthRows o;
+      depth_rows(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, dmeas[sl], X.x, X.y, X.z, flags, cauchy_c,
+                 o);
+      const double P2 = o.P * o.P;
+      V[0] += P2;
+      V[3] += P2;
+      V[5] += P2;
+#pragma unroll
+      for (int c = 0; c < 3; c++) g[c] += o.P * o.r[c];
     }
   }
 #pragma unroll
@@ -749,12 +766,12 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
                                   const int32_t* po_frame, const double2* po_meas,
                                   const mvba::FrameDesc* fd, const double* frec, const double* params,
                                   const double4* pts, double* pgrad, double* phess, int32_t flags,
-                                  double cauchy_c, hipStream_t s) {
+                                  double cauchy_c, mvba::DepthCsr dc, hipStream_t s) {
   if (npts <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((npts * mvba::kLanesPerPoint + 255) / 256);
 #define MVBA_PTS(M, D)                                                                                \
   hipLaunchKernelGGL((mvba::k_points_lin<M, D>), dim3(blocks), dim3(256), 0, s, pt_begin, npts,      \
-                     po_frame, po_meas, fd, frec, params, pts, pgrad, phess, flags, cauchy_c)
+                     po_frame, po_meas, fd, frec, params, pts, pgrad, phess, flags, cauchy_c, dc)
   if (model < 0) {
     MVBA_PTS(-1, 0);
   } else {

@@ -33,18 +33,13 @@ hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const FrameDes
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
-                              double* tadd, const double* V, const double* dp, double* zbuf, double* ubuf,
-                              double* wout, double* sq_partial, unsigned* counter, double* sq_out, int32_t flags,
-                              double cauchy_c, hipStream_t s);
-hipError_t mvba_launch_depth_sa(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
-                                const double4* dmeas, const double* frec, const double* params, const double4* pts,
-                                const double* dir, const double* x, double* dz, double* tadd, int32_t flags,
-                                double cauchy_c, int32_t dir_stride, hipStream_t s);
+                              const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
+                              double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
+                              mvba::DepthCsr dc, const double* xcam, double* du, hipStream_t s);
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
-                                const void* fl, const double* dz, const double* wp, double* yrep, int64_t ng,
-                                double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
-                                hipStream_t s);
+                                const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
+                                double cauchy_c, hipStream_t s);
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
                               const Segment* segs, const FrameDesc* fd, const void* fl, const double* frec,
                               const double* params, const double4* pts, const int32_t* obs_pid,
@@ -108,9 +103,7 @@ struct SolverState {
   double* dir = nullptr;      // [nframes * dir stride]
   double* zbuf = nullptr;     // [8 N] point-order z_o | J_pt rows
   double* ubuf = nullptr;     // [2 N]
-  double* dz = nullptr;       // [3 depth slots] z_d of the depth blocks
-  double* tadd = nullptr;     // [3 np] depth contributions to t_p (zero between products)
-  double* wbuf = nullptr;     // [3 np] w_p of the last pass A (depth blocks need it)
+  double* du = nullptr;       // [3 depth slots] u_d of the depth blocks (pass A -> k_depth_sb)
   double* partial = nullptr;  // [npartial]
   double* scal = nullptr;     // [32] device scalars
   unsigned* cnt = nullptr;    // [8] grid-reduction counters (kept zero between kernels)
@@ -125,7 +118,7 @@ struct SolverState {
 void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
-                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->ubuf, S->dz, S->tadd, S->wbuf,
+                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->ubuf, S->du,
                   S->cnt, S->partial, S->scal, S->bsize, S->emap, S->goff, S->hoff, S->cam_poff};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -177,10 +170,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->dir, (size_t)(h->nframes * mvba_solver_dir_stride())));
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
     HCHK(dalloc(&S->ubuf, (size_t)(2 * N)));
-    HCHK(dalloc(&S->dz, (size_t)(3 * h->ndep_slots)));
-    HCHK(dalloc(&S->tadd, (size_t)(3 * S->np)));
-    HCHK(hipMemset(S->tadd, 0, (size_t)std::max<int64_t>(3 * S->np, 1) * sizeof(double)));
-    HCHK(dalloc(&S->wbuf, (size_t)(3 * S->np)));
+    HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
     HCHK(dalloc(&S->cnt, 8));
     HCHK(hipMemset(S->cnt, 0, 8 * sizeof(unsigned)));
     int64_t ncost = 0;
@@ -316,7 +306,7 @@ class Solver {
   // pass B over every model group into the replicas, then y = sum of replicas.
   // Single rank: damping and the x.y dot are fused into the replica reduction
   // (dot -> scal[dot_slot]); sharded: cross-rank sum of y first.
-  void reduce_frames(double* y, const double* xv, int dot_slot, const double* dz) {
+  void reduce_frames(double* y, const double* xv, int dot_slot) {
     for (const Group& G : h_->groups)
       HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
                               h_->d_segs, h_->d_fd, h_->d_frame_lin, h_->d_frec, h_->d_params, h_->d_pts,
@@ -324,8 +314,8 @@ class Solver {
                               cauchy_c_, s_));
     if (h_->ndep > 0)
       HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
-                                h_->d_params, h_->d_pts, h_->d_frame_lin, dz, S_->wbuf, S_->yrep, S_->ng, nullptr,
-                                nullptr, nullptr, flags_, cauchy_c_, s_));
+                                h_->d_params, h_->d_pts, h_->d_frame_lin, S_->du, S_->yrep, S_->ng, flags_, cauchy_c_,
+                                s_));
     const bool fuse = xv && !o_.allreduce;
     HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr, y, S_->partial,
                                     S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, s_));
@@ -337,29 +327,20 @@ class Solver {
   // y = S x (implicit Schur complement with damping); x.y -> scal[dot_slot]
   void apply_schur(const double* xv, double* y, int dot_slot) {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, s_));
-    const bool dep = h_->ndep > 0;
-    if (dep) depth_sa(xv);
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
-                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, nullptr, dep ? S_->tadd : nullptr,
-                            S_->phess, S_->dmp + S_->ng, S_->zbuf, S_->ubuf, dep ? S_->wbuf : nullptr, nullptr,
-                            nullptr, nullptr, flags_, cauchy_c_, s_));
-    reduce_frames(y, xv, dot_slot, S_->dz);
-  }
-
-  // z_d = J_cam,d x for the depth blocks, J_pt^T z_d into tadd
-  void depth_sa(const double* xv) {
-    HCHK(mvba_launch_depth_sa(h_->ndep_slots, h_->d_dep_desc, h_->d_dep_order, h_->d_dep_meas, h_->d_frec,
-                              h_->d_params, h_->d_pts, S_->dir, xv, S_->dz, S_->tadd, flags_, cauchy_c_,
-                              mvba_solver_dir_stride(), s_));
+                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, nullptr, S_->phess, S_->dmp + S_->ng,
+                            S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_, cauchy_c_,
+                            h_->depth_csr(), xv, S_->du, s_));
+    reduce_frames(y, xv, dot_slot);
   }
 
   // b = -(g_c - W (V+D)^-1 g_p)
   void schur_rhs() {
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
-                            h_->d_frec, h_->d_params, h_->d_pts, nullptr, S_->G + S_->ng, nullptr, S_->phess,
-                            S_->dmp + S_->ng, S_->zbuf, S_->ubuf, h_->ndep > 0 ? S_->wbuf : nullptr, nullptr,
-                            nullptr, nullptr, flags_, cauchy_c_, s_));
-    reduce_frames(S_->tmp, nullptr, 0, nullptr);  // = -W w
+                            h_->d_frec, h_->d_params, h_->d_pts, nullptr, S_->G + S_->ng, S_->phess,
+                            S_->dmp + S_->ng, S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_,
+                            cauchy_c_, h_->depth_csr(), nullptr, S_->du, s_));
+    reduce_frames(S_->tmp, nullptr, 0);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
   }
 
@@ -444,18 +425,11 @@ class Solver {
   double back_substitute() {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
                                s_));
-    const bool dep = h_->ndep > 0;
-    if (dep) depth_sa(S_->delta);
+    // |J delta|^2 over the local reprojection and depth blocks -> scal[0]
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
-                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, dep ? S_->tadd : nullptr,
-                            S_->phess, S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial,
-                            S_->cnt + 5, S_->scal + 0, flags_, cauchy_c_, s_));  // |J delta|^2 (local observations)
-    HCHK(hipMemsetAsync(S_->scal + 3, 0, sizeof(double), s_));
-    if (dep)  // depth rows of J delta: u_d = z_d - P w_p (w_p = -delta_p, not yet negated)
-      HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
-                                h_->d_params, h_->d_pts, h_->d_frame_lin, S_->dz, S_->delta + S_->ng, nullptr,
-                                S_->ng, S_->partial, S_->cnt + 6, S_->scal + 3, flags_, cauchy_c_, s_));
-    HCHK(mvba_launch_axpby(1, 1.0, S_->scal + 0, 1.0, S_->scal + 3, S_->scal + 0, s_));
+                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
+                            S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial, S_->cnt + 5,
+                            S_->scal + 0, flags_, cauchy_c_, h_->depth_csr(), S_->delta, S_->du, s_));
     HCHK(mvba_launch_axpby(3 * S_->np, -1.0, S_->delta + S_->ng, 0.0, nullptr, S_->delta + S_->ng, s_));
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);

@@ -10,7 +10,7 @@
 //          sum J_intr^T u_o, mapped through w to the pose columns in the same
 //          kernel: S x = J_cam^T u (+ LM damping).
 // Same two passes give the reduced right-hand side and the point back-substitution.
-#include "mvba_device.h"
+#include "mvba_depth.h"
 
 namespace mvba {
 
@@ -174,10 +174,10 @@ __global__ void __launch_bounds__(256) k_pass_a(
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const double* __restrict__ dir,
-    const double* __restrict__ tinit, double* __restrict__ tadd, const double* __restrict__ V,
+    const double* __restrict__ tinit, const double* __restrict__ V,
     const double* __restrict__ dp, double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
     double* __restrict__ sq_partial, unsigned* __restrict__ counter, double* __restrict__ sq_out,
-    int32_t flags, double cauchy_c) {
+    int32_t flags, double cauchy_c, DepthCsr dc, const double* __restrict__ xcam, double* __restrict__ du) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = t / kLanesA;
   const int sub = (int)(t % kLanesA);
@@ -215,19 +215,36 @@ __global__ void __launch_bounds__(256) k_pass_a(
       }
     }
   }
+  const double4* dmeas = reinterpret_cast<const double4*>(dc.meas);
+  int64_t db = 0, de = 0;
+  double dP0 = 0.0;
+  if (dc.begin && valid) {
+    // BracketedDepthError blocks: z_d = J_cam,d x, t_p += P z_d (J_pt = P I);
+    // z_d parked in du until w_p is known
+    db = dc.begin[p];
+    de = dc.begin[p + 1];
+    for (int64_t j = db + sub; j < de; j += kLanesA) {
+      const int32_t sl = dc.slot[j];
+      const DepthDesc d = dc.dd[sl];
+      const double4 m = dmeas[sl];
+      DepthCore c;
+      depth_core(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, m, X.x, X.y, X.z, flags, cauchy_c, c);
+      double z[3] = {0.0, 0.0, 0.0};
+      if (dir) depth_jx(d, c, m, dir + (int64_t)d.frame * kDirStride, xcam, z);
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        du[3 * (int64_t)sl + r] = z[r];
+        if (X.w != 0.0) tv[r] += c.P * z[r];
+      }
+      if (j == db + sub) dP0 = c.P;  // first entry of this lane: keep P for the second loop
+    }
+  }
 #pragma unroll
   for (int off = 1; off < kLanesA; off <<= 1)
 #pragma unroll
     for (int q = 0; q < 3; q++) tv[q] += __shfl_xor(tv[q], off, 64);
   double w[3] = {0.0, 0.0, 0.0};
   double sq = 0.0;
-  if (valid && tadd) {
-    // depth-block contributions J_pt^T z (k_depth_sa), consumed and re-zeroed; the
-    // point's lanes share a wave, so every lane reads before lane 0 writes
-    for (int q = 0; q < 3; q++) tv[q] += tadd[3 * p + q];
-    if (sub == 0)
-      for (int q = 0; q < 3; q++) tadd[3 * p + q] = 0.0;
-  }
   if (valid && X.w != 0.0) {
     if (tinit)
       for (int q = 0; q < 3; q++) tv[q] += tinit[3 * p + q];
@@ -256,6 +273,24 @@ __global__ void __launch_bounds__(256) k_pass_a(
       const double u1 = row[1] - (row[5] * w[0] + row[6] * w[1] + row[7] * w[2]);
       if (ubuf) *reinterpret_cast<double2*>(ubuf + 2 * j) = make_double2(u0, u1);
       sq += u0 * u0 + u1 * u1;
+    }
+  }
+  if (valid && de > db) {
+    // u_d = z_d - P w_p  (P = weight * sr depends only on the residual: recompute)
+    for (int64_t j = db + sub; j < de; j += kLanesA) {
+      const int32_t sl = dc.slot[j];
+      double P = dP0;
+      if (j != db + sub) {
+        const DepthDesc d = dc.dd[sl];
+        P = depth_p(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, dmeas[sl], X.x, X.y, X.z, flags,
+                    cauchy_c);
+      }
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const double u = du[3 * (int64_t)sl + r] - P * w[r];
+        du[3 * (int64_t)sl + r] = u;
+        sq += u * u;
+      }
     }
   }
   if (sq_partial) grid_sum_finalize(sq, sq_partial, counter, sq_out);
@@ -708,21 +743,21 @@ hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::Fr
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const mvba::FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
-                              double* tadd, const double* V, const double* dp, double* zbuf, double* ubuf,
-                              double* wout, double* sq_partial, unsigned* counter, double* sq_out, int32_t flags,
-                              double cauchy_c, hipStream_t s) {
+                              const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
+                              double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
+                              mvba::DepthCsr dc, const double* xcam, double* du, hipStream_t s) {
   const unsigned blocks = (unsigned)((npts * mvba::kLanesA + 255) / 256);
   if (npts <= 0) return hipSuccess;
   if (model < 0) {
     hipLaunchKernelGGL((mvba::k_pass_a<-1, 0>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, fd,
-                       frec, params, pts, dir, tinit, tadd, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out,
-                       flags, cauchy_c);
+                       frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out, flags,
+                       cauchy_c, dc, xcam, du);
     return hipGetLastError();
   }
 #define MVBA_PA(M, D)                                                                                      \
   hipLaunchKernelGGL((mvba::k_pass_a<M, D>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, \
-                     fd, frec, params, pts, dir, tinit, tadd, V, dp, zbuf, ubuf, wout, sq_partial, counter,    \
-                     sq_out, flags, cauchy_c)
+                     fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out,  \
+                     flags, cauchy_c, dc, xcam, du)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PA)
 #undef MVBA_PA
   return hipGetLastError();

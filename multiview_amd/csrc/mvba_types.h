@@ -72,6 +72,15 @@ struct DepthDesc {
   int32_t free_mask;             // bits MVBA_DBLK_*: block is free (Jacobian written)
 };
 
+// Point-ordered view of the depth blocks (CSR point -> depth slots), passed by
+// value to the point-order kernels; begin == nullptr: no depth blocks.
+struct DepthCsr {
+  const int64_t* begin;    // [num_points + 1]
+  const int32_t* slot;     // [num_depth] depth slot of each entry
+  const DepthDesc* dd;     // [depth slots]
+  const void* meas;        // double4 [depth slots] (x, y, z, weight)
+};
+
 }  // namespace mvba
 
 #endif  // MVBA_TYPES_H_
