@@ -278,6 +278,17 @@ mvba_status mvba_evaluate_depth(struct mvba_handle* h, int32_t flags, double cau
 mvba_status mvba_evaluate_depth_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                                        double* d_res, double* d_J, int64_t ld, void* hip_stream);
 
+/* ---- Residual statistics (evalResiduals + calc_residuals_stats,
+ * rig_calibrator.cc:1157-1180, :753-789) ------------------------------------
+ * Raw residuals (no loss) divided by their scale (1 for pixels, the depth weight
+ * for depth blocks), |r| grouped by residual name, and per group the values at
+ * sorted positions int(0.25 len), int(0.5 len), int(0.75 len), len-1.
+ * Groups (num_cameras*2 + 3): 2c + k = camera c, pixel component k
+ * ("<sensor>_pix_x", "<sensor>_pix_y"); 2*num_cameras + k = depth component k
+ * ("depth_tri_{x,y,z}_m"). out [4*groups] (NaN for empty groups), counts [groups].
+ * Synchronous. */
+mvba_status mvba_residual_stats(struct mvba_handle* h, double* out, int64_t* counts, void* hip_stream);
+
 /* mvba_eval_bytes(h, MVBA_EVAL_DEPTH): algorithmic bytes of one materialised
  * depth evaluation (per block 32 meas+weight, 24 landmark, 24 residual, 24 per
  * written Jacobian column). */

@@ -188,6 +188,7 @@ SIGNATURES = {
     "mvba_evaluate_depth": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_evaluate_depth_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                                              C.c_int64, C.c_void_p]),
+    "mvba_residual_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
     "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),
     "mvba_get_params": (C.c_int, [C.c_void_p, C.c_void_p]),

@@ -163,6 +163,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   h->device = dev;
   h->nres = N;
   h->nparams = d->num_param_doubles;
+  h->ncams = d->num_cameras;
   h->kmax = kmax;
   h->jac_rows = MVBA_JAC_BASE_DIST + 2 * kmax;
 
@@ -361,6 +362,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   }
   if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
   h->bytes_res = bytes_res;
+  h->nsegs = (int64_t)segs.size();
   h->bytes_jac = bytes_jac;
 
   // ---- linearization structures (K2)

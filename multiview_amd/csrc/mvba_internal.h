@@ -144,6 +144,8 @@ struct mvba_handle {
   int device = 0;
   std::string err;
   int64_t nres = 0, nslots = 0, nframes = 0, npts = 0, nparams = 0;
+  int64_t nsegs = 0;
+  int32_t ncams = 0;
   int kmax = 0, jac_rows = 0;
   std::vector<int64_t> order;        // device slot -> insertion index (-1 = padding)
   std::vector<uint8_t> row_written;  // device position -> block bitmask

@@ -139,6 +139,31 @@ class Evaluator:
                                             C.c_void_p(stream or 0))
         _lib.check(st, self.h)
 
+    # ------------------------------------------------------- residual stats
+    def residual_stats(self, sensor_names=None) -> list:
+        """evalResiduals + calc_residuals_stats (rig_calibrator.cc:1157-1180,
+        :753-789) on the GPU. Returns [(name, p25, p50, p75, p100, count)] in the
+        reference's print order (std::map: names sorted), only names that have
+        residual blocks."""
+        ncam = len(self.problem.camera_dist_size)
+        names = list(sensor_names or [f"cam{c}" for c in range(ncam)])
+        ng = 2 * ncam + 3
+        out = np.empty(4 * ng)
+        counts = np.empty(ng, dtype=np.int64)
+        _lib.check(self.lib.mvba_residual_stats(self.h, out.ctypes.data, counts.ctypes.data, None), self.h)
+        labels = [f"{names[c]}_pix_{xy}" for c in range(ncam) for xy in "xy"] + \
+            [f"depth_tri_{a}_m" for a in "xyz"]
+        rows = [(labels[g], *out[4 * g:4 * g + 4], int(counts[g])) for g in range(ng) if counts[g] > 0]
+        return sorted(rows, key=lambda r: r[0])
+
+    @staticmethod
+    def format_residual_stats(rows, tag: str) -> str:
+        """The reference's stdout block (calc_residuals_stats, setprecision(5))."""
+        lines = [f"The 25, 50, 75, and 100th percentile residual stats {tag}"]
+        for name, a, b, c, d, n in rows:
+            lines.append(f"{name}: {a:.5g} {b:.5g} {c:.5g} {d:.5g} ({n} residuals)")
+        return "\n".join(lines)
+
     # ---------------------------------------------------------------- solver
     def get_params(self) -> np.ndarray:
         out = np.empty(self.problem.params.size, dtype=np.float64)

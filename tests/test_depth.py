@@ -167,3 +167,32 @@ def test_depth_linearize_parity(oracle, name, apply_loss):
         scale = np.maximum(np.abs(ref).max(axis=1, keepdims=True), 1e-300)
         assert (np.abs(got - ref) <= 1e-9 * scale).all()
     assert np.isclose(cost.item(), c_o + cd, rtol=1e-11)
+
+
+@pytest.mark.gpu
+def test_residual_stats_match_oracle(oracle):
+    """mvba_residual_stats = evalResiduals + calc_residuals_stats: raw residuals
+    divided by their scale, grouped by name, percentiles by index; against the
+    oracle's residuals fed to the oracle's restatement of calc_residuals_stats."""
+    R = _rig(False, seed=23)
+    P = rig.build_problem(R, _flags(False))
+    names = R.sensor_names
+    with Evaluator(P) as ev:
+        ev.set_params()
+        rows = ev.residual_stats(names)
+    _, r, _ = oracle.evaluate(P, oracle.RESIDUAL)
+    _, rd, _ = oracle.evaluate_depth(P, oracle.RESIDUAL)
+    ncam = len(P.camera_dist_size)
+    vals = np.concatenate([r.reshape(-1), (rd / P.depth_weight[:, None]).reshape(-1)])
+    ids = np.concatenate([(2 * P.residual_camera[:, None] + np.arange(2)).reshape(-1),
+                          (2 * ncam + np.tile(np.arange(3), rd.shape[0]))]).astype(np.int32)
+    ref, counts = oracle.residual_stats(vals, ids, 2 * ncam + 3)
+    labels = [f"{names[c]}_pix_{xy}" for c in range(ncam) for xy in "xy"] + [f"depth_tri_{a}_m" for a in "xyz"]
+    expect = sorted([(labels[g], *ref[g], int(counts[g])) for g in range(2 * ncam + 3) if counts[g] > 0],
+                    key=lambda t: t[0])
+    assert [e[0] for e in expect] == [g[0] for g in rows]
+    for g, e in zip(rows, expect):
+        assert g[5] == e[5]
+        assert np.allclose(g[1:5], e[1:5], rtol=1e-9, atol=1e-12), (g, e)
+    text = Evaluator.format_residual_stats(rows, "before opt")
+    assert text.splitlines()[0] == "The 25, 50, 75, and 100th percentile residual stats before opt"
