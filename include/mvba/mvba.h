@@ -64,7 +64,9 @@ typedef enum mvba_status {
   /* No usable GPU (the product path has no CPU fallback). */
   MVBA_E_NO_DEVICE = 6,
   /* "BracketedDepthError: The block sizes were not set up properly." rig_calibrator.cc:534-543 */
-  MVBA_E_DEPTH_BLOCK_SIZES = 7
+  MVBA_E_DEPTH_BLOCK_SIZES = 7,
+  /* "XYZError: The block sizes were not set up properly." rig_calibrator.cc:714-715 */
+  MVBA_E_XYZ_BLOCK_SIZES = 8
 } mvba_status;
 
 /* Parameter-block order of one BracketedCamError residual block, exactly the
@@ -129,6 +131,16 @@ typedef struct mvba_problem_desc {
   const double* depth_meas;      /* [3*n] meas_depth_xyz (depth-cloud point) */
   const double* depth_weight;    /* [n] weight (FLAGS_depth_tri_weight) */
   const double* depth_stamps;    /* [3*n] left_ref, right_ref, cam stamp */
+
+  /* Optional XYZError residual blocks (rig_calibrator.cc:709-751): r = weight *
+   * (xyz - ref_xyz) on one point block, with their own Cauchy threshold:
+   * --tri_weight / --tri_robust_threshold (:1889-1898) or --mesh_tri_weight /
+   * --robust_threshold (:1866-1877). Zero-fill when there are none. */
+  int64_t num_xyz_residuals;
+  const int32_t* xyz_block;      /* [n] point block id (size 3) */
+  const double* xyz_ref;         /* [3*n] reference xyz */
+  const double* xyz_weight;      /* [n] weight */
+  const double* xyz_threshold;   /* [n] Cauchy threshold used with MVBA_EVAL_APPLY_LOSS (> 0) */
 } mvba_problem_desc;
 
 /* Depth block order (BracketedDepthError) and its Jacobian layout: rows
@@ -277,6 +289,14 @@ mvba_status mvba_evaluate_depth(struct mvba_handle* h, int32_t flags, double cau
                                 double* residuals, double* jacobian);
 mvba_status mvba_evaluate_depth_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                                        double* d_res, double* d_J, int64_t ld, void* hip_stream);
+
+/* ---- XYZ priors (XYZError) ---------------------------------------------
+ * Host, insertion order: residuals [3n], Jacobian [9n] (row-major 3x3, nullable),
+ * cost = sum 0.5*rho (each block's own threshold with MVBA_EVAL_APPLY_LOSS).
+ * mvba_linearize_device and mvba_solve include them (point blocks only). */
+int64_t mvba_num_xyz_residuals(const struct mvba_handle* h);
+mvba_status mvba_evaluate_xyz(struct mvba_handle* h, int32_t flags, double* cost, double* residuals,
+                              double* jacobian);
 
 /* ---- Residual statistics (evalResiduals + calc_residuals_stats,
  * rig_calibrator.cc:1157-1180, :753-789) ------------------------------------

@@ -21,11 +21,12 @@ MVBA_E_HIP = 4
 MVBA_E_INVALID = 5
 MVBA_E_NO_DEVICE = 6
 MVBA_E_DEPTH_BLOCK_SIZES = 7
+MVBA_E_XYZ_BLOCK_SIZES = 8
 
 STATUS_NAMES = {
     0: "MVBA_OK", 1: "MVBA_E_ALPHA_RANGE", 2: "MVBA_E_BLOCK_SIZES",
     3: "MVBA_E_BAD_DISTORTION", 4: "MVBA_E_HIP", 5: "MVBA_E_INVALID",
-    6: "MVBA_E_NO_DEVICE", 7: "MVBA_E_DEPTH_BLOCK_SIZES",
+    6: "MVBA_E_NO_DEVICE", 7: "MVBA_E_DEPTH_BLOCK_SIZES", 8: "MVBA_E_XYZ_BLOCK_SIZES",
 }
 
 EVAL_RESIDUALS = 0x1
@@ -67,6 +68,11 @@ class ProblemDesc(C.Structure):
         ("depth_meas", C.c_void_p),
         ("depth_weight", C.c_void_p),
         ("depth_stamps", C.c_void_p),
+        ("num_xyz_residuals", C.c_int64),
+        ("xyz_block", C.c_void_p),
+        ("xyz_ref", C.c_void_p),
+        ("xyz_weight", C.c_void_p),
+        ("xyz_threshold", C.c_void_p),
     ]
 
 
@@ -189,6 +195,8 @@ SIGNATURES = {
     "mvba_evaluate_depth_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                                              C.c_int64, C.c_void_p]),
     "mvba_residual_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_num_xyz_residuals": (C.c_int64, [C.c_void_p]),
+    "mvba_evaluate_xyz": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
     "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),
     "mvba_get_params": (C.c_int, [C.c_void_p, C.c_void_p]),

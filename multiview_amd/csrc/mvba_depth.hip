@@ -313,6 +313,40 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
   }
 }
 
+// ------------------------------------------------------------ XYZError priors
+// r = weight (X - ref) (rig_calibrator.cc:720-724), own Cauchy threshold.
+// Cost (sum 0.5 rho) over the entries, grid-reduced into out[0].
+__global__ void __launch_bounds__(256) k_xyz_cost(int64_t n, const int32_t* __restrict__ xpid,
+                                                  const double4* __restrict__ xref, const double* __restrict__ xcc,
+                                                  const double4* __restrict__ pts, int32_t flags,
+                                                  double* __restrict__ partial, unsigned* __restrict__ counter,
+                                                  double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double c = 0.0;
+  if (j < n) {
+    const double4 X = pts[xpid[j]];
+    const double4 R = xref[j];
+    double hr;
+    loss_scale3(R.w * (X.x - R.x), R.w * (X.y - R.y), R.w * (X.z - R.z), flags, xcc[j], &hr);
+    c = hr;
+  }
+  grid_sum_finalize(c, partial, counter, out);
+}
+
+// raw residuals into out[3 * insertion index]
+__global__ void k_xyz_eval(int64_t n, const int32_t* __restrict__ xpid, const int64_t* __restrict__ xorder,
+                           const double4* __restrict__ xref, const double4* __restrict__ pts,
+                           double* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double4 X = pts[xpid[j]];
+  const double4 R = xref[j];
+  const int64_t o = xorder[j];
+  out[3 * o] = R.w * (X.x - R.x);
+  out[3 * o + 1] = R.w * (X.y - R.y);
+  out[3 * o + 2] = R.w * (X.z - R.z);
+}
+
 }  // namespace mvba
 
 extern "C" {
@@ -358,6 +392,23 @@ hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const m
   if (nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params, pts,
                      (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_xyz_cost(int64_t n, const int32_t* xpid, const double4* xref, const double* xcc,
+                                const double4* pts, int32_t flags, double* partial, unsigned* counter,
+                                double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_xyz_cost, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, xpid, xref, xcc, pts,
+                     flags, partial, counter, out);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_xyz_eval(int64_t n, const int32_t* xpid, const int64_t* xorder, const double4* xref,
+                                const double4* pts, double* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_xyz_eval, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, xpid, xorder, xref,
+                     pts, out);
   return hipGetLastError();
 }
 

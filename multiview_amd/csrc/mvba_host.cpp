@@ -36,7 +36,8 @@ static void free_all(mvba_handle* h) {
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
                   h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
-                  h->d_dpt_begin, h->d_dpo_slot};
+                  h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xpid,
+                  h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt};
   solver_state_free(h->solver);
   h->solver = nullptr;
   for (void* p : ptrs)
@@ -152,6 +153,17 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
                  "depth residual block without a BracketedCamError block sharing its pose blocks and stamps");
   }
 
+  // XYZError priors: constructor check (rig_calibrator.cc:714-715).
+  const int64_t NX = d->num_xyz_residuals;
+  if (NX < 0) return bad(MVBA_E_INVALID, "negative sizes in problem description");
+  if (NX > 0 && (!d->xyz_block || !d->xyz_ref || !d->xyz_weight || !d->xyz_threshold))
+    return bad(MVBA_E_INVALID, "null array in problem description");
+  for (int64_t j = 0; j < NX; j++) {
+    const int32_t b = d->xyz_block[j];
+    if (b < 0 || b >= d->num_blocks) return bad(MVBA_E_INVALID, "parameter block index out of range");
+    if (d->block_size[b] != 3) return bad(MVBA_E_XYZ_BLOCK_SIZES, "XYZError: The block sizes were not set up properly.\n");
+  }
+
   // The product path computes on the GPU only: no device, no handle.
   int32_t ndev = 0;
   if (mvba_device_count(&ndev) != MVBA_OK) return bad(MVBA_E_NO_DEVICE, "no HIP device available");
@@ -198,6 +210,20 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       dep_pt[j] = id;
     } else {
       dep_pt[j] = it->second;
+    }
+  }
+  std::vector<int32_t> xyz_pt(NX);
+  for (int64_t j = 0; j < NX; j++) {
+    const int32_t b = d->xyz_block[j];
+    auto it = pt_index.find(b);
+    if (it == pt_index.end()) {
+      const int32_t id = (int32_t)pt_off.size();
+      pt_index.emplace(b, id);
+      pt_off.push_back(d->block_offset[b]);
+      pt_free.push_back(d->block_constant[b] ? 0 : 1);
+      xyz_pt[j] = id;
+    } else {
+      xyz_pt[j] = it->second;
     }
   }
   h->npts = (int64_t)pt_off.size();
@@ -551,6 +577,33 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     }
   }
 
+  // ---- XYZ priors in point order
+  std::vector<int64_t> xpt_begin, xorder;
+  std::vector<double4> xref;
+  std::vector<double> xcc;
+  std::vector<int32_t> xpid;
+  h->nxyz = NX;
+  h->xfree.assign((size_t)NX, 0);
+  for (int64_t j = 0; j < NX; j++) h->xfree[(size_t)j] = pt_free[xyz_pt[j]];
+  if (NX > 0) {
+    xpt_begin.assign(h->npts + 1, 0);
+    for (int64_t j = 0; j < NX; j++) xpt_begin[xyz_pt[j] + 1]++;
+    for (int64_t p = 0; p < h->npts; p++) xpt_begin[p + 1] += xpt_begin[p];
+    std::vector<int64_t> fill(xpt_begin.begin(), xpt_begin.end() - 1);
+    xref.resize(NX);
+    xcc.resize(NX);
+    xpid.resize(NX);
+    xorder.resize(NX);
+    for (int64_t j = 0; j < NX; j++) {
+      const int64_t q = fill[xyz_pt[j]]++;
+      xref[q] = make_double4(d->xyz_ref[3 * j], d->xyz_ref[3 * j + 1], d->xyz_ref[3 * j + 2], d->xyz_weight[j]);
+      const double t = d->xyz_threshold[j];
+      xcc[q] = t > 0.0 ? 1.0 / (t * t) : 0.0;
+      xpid[q] = xyz_pt[j];
+      xorder[q] = j;
+    }
+  }
+
   // ---- upload
   hipError_t e = hipSuccess;
   auto chk = [&](hipError_t x) {
@@ -593,6 +646,14 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_dep_order, h->dep_order));
   chk(upload(&h->d_dpt_begin, dpt_begin));
   chk(upload(&h->d_dpo_slot, dpo_slot));
+  chk(upload(&h->d_xpt_begin, xpt_begin));
+  chk(upload(&h->d_xref, xref));
+  chk(upload(&h->d_xcc, xcc));
+  chk(upload(&h->d_xpid, xpid));
+  chk(upload(&h->d_xorder, xorder));
+  chk(dalloc(&h->d_xscal, (size_t)(1 + std::max<int64_t>((NX + 255) / 256, 1))));
+  chk(dalloc(&h->d_xcnt, 1));
+  if (e == hipSuccess) chk(hipMemset(h->d_xcnt, 0, sizeof(unsigned)));
   if (e != hipSuccess) {
     g_create_error = std::string("HIP error during mvba_create: ") + hipGetErrorString(e);
     free_all(h);
@@ -797,7 +858,12 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
     e = mvba_launch_points_lin(h->groups.size() == 1 ? h->groups[0].model : -1,
                                h->groups.size() == 1 ? h->groups[0].deg : 0, h->d_pt_begin, h->npts,
                                h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
-                               d_pt_grad, d_pt_hess, lflags, cauchy_c, h->depth_csr(), s);
+                               d_pt_grad, d_pt_hess, lflags, cauchy_c, h->point_extra(), s);
+  if (e == hipSuccess && h->nxyz > 0 && d_cost) {
+    e = mvba_launch_xyz_cost(h->nxyz, h->d_xpid, h->d_xref, h->d_xcc, h->d_pts, lflags, h->d_xscal + 1, h->d_xcnt,
+                             h->d_xscal, s);
+    if (e == hipSuccess) e = mvba_launch_axpby(1, 1.0, d_cost, 1.0, h->d_xscal, d_cost, s);
+  }
   if (e != hipSuccess) return h->hip_fail(e, "mvba_linearize_device launch");
   return MVBA_OK;
 }
@@ -997,6 +1063,66 @@ mvba_status mvba_evaluate_depth(mvba_handle* h, int32_t flags, double cauchy_thr
     *cost = total;
   }
   return MVBA_OK;
+}
+
+int64_t mvba_num_xyz_residuals(const mvba_handle* h) { return h ? h->nxyz : 0; }
+
+mvba_status mvba_evaluate_xyz(mvba_handle* h, int32_t flags, double* cost, double* residuals, double* jacobian) {
+  if (!h) return MVBA_E_INVALID;
+  if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
+  const int64_t NX = h->nxyz;
+  if (NX == 0) {
+    if (cost) *cost = 0.0;
+    return MVBA_OK;
+  }
+  if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  hipError_t e = hipSuccess;
+  if (!h->d_xout) e = dalloc(&h->d_xout, (size_t)(3 * NX));
+  // points gathered by the prep kernel (K0), then raw residuals in insertion order
+  h->gen++;
+  if (e == hipSuccess)
+    e = mvba_launch_prep(h->d_fd, h->nframes, h->d_params, h->d_frec, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,
+                         h->gen, h->d_err, nullptr);
+  h->prep_done = true;
+  if (e == hipSuccess) e = mvba_launch_xyz_eval(NX, h->d_xpid, h->d_xorder, h->d_xref, h->d_pts, h->d_xout, nullptr);
+  std::vector<double> raw((size_t)(3 * NX)), w((size_t)NX), thr((size_t)NX);
+  if (e == hipSuccess) e = hipMemcpy(raw.data(), h->d_xout, raw.size() * sizeof(double), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_xyz");
+  // weights / thresholds in insertion order (for the Jacobian and the corrector)
+  std::vector<double4> xref((size_t)NX);
+  std::vector<double> xcc((size_t)NX);
+  std::vector<int64_t> xorder((size_t)NX);
+  e = hipMemcpy(xref.data(), h->d_xref, xref.size() * sizeof(double4), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(xcc.data(), h->d_xcc, xcc.size() * sizeof(double), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(xorder.data(), h->d_xorder, xorder.size() * sizeof(int64_t), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_xyz");
+  const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
+  double total = 0.0;
+  std::vector<double> cj((size_t)NX);
+  for (int64_t q = 0; q < NX; q++) {
+    const int64_t j = xorder[q];
+    const double c = xcc[q];
+    const double* r = &raw[(size_t)(3 * j)];
+    const double s2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+    double sr = 1.0;
+    if (loss) {
+      if (!(c > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
+      const double sum = 1.0 + s2 * c;
+      cj[(size_t)j] = 0.5 * (std::log(sum) / c);
+      sr = std::sqrt(std::max(std::numeric_limits<double>::min(), 1.0 / sum));
+    } else {
+      cj[(size_t)j] = 0.5 * s2;
+    }
+    if (residuals)
+      for (int k = 0; k < 3; k++) residuals[3 * j + k] = r[k] * sr;
+    if (jacobian && (flags & MVBA_EVAL_JACOBIAN))  // constant point: NULL jacobian in Ceres -> zeros
+      for (int a = 0; a < 3; a++)
+        for (int k = 0; k < 3; k++)
+          jacobian[9 * j + 3 * a + k] = (a == k && h->xfree[(size_t)j]) ? xref[q].w * sr : 0.0;
+  }
+  for (int64_t j = 0; j < NX; j++) total += cj[(size_t)j];
+  if (cost) *cost = total;
+  return mvba_sync_status(h, nullptr);
 }
 
 }  // extern "C"

@@ -40,7 +40,7 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
                                   const int32_t* po_frame, const double2* po_meas, const FrameDesc* fd,
                                   const double* frec, const double* params, const double4* pts,
                                   double* pgrad, double* phess, int32_t flags, double cauchy_c,
-                                  mvba::DepthCsr dc, hipStream_t s);
+                                  mvba::PointExtra dc, hipStream_t s);
 hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
                            const FrameDesc* fd, const double* frec, const double* params,
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
@@ -58,6 +58,13 @@ hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
                                   hipStream_t s);
+hipError_t mvba_launch_xyz_cost(int64_t n, const int32_t* xpid, const double4* xref, const double* xcc,
+                                const double4* pts, int32_t flags, double* partial, unsigned* counter,
+                                double* out, hipStream_t s);
+hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
+                             hipStream_t s);
+hipError_t mvba_launch_xyz_eval(int64_t n, const int32_t* xpid, const int64_t* xorder, const double4* xref,
+                                const double4* pts, double* out, hipStream_t s);
 hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, const int64_t* dorder,
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   int32_t flags, double cauchy_c, double* partial, hipStream_t s,
@@ -204,14 +211,28 @@ struct mvba_handle {
   int64_t* d_dep_order = nullptr;
   int64_t* d_dpt_begin = nullptr;         // CSR point -> depth slots
   int32_t* d_dpo_slot = nullptr;
-  mvba::DepthCsr depth_csr() const {
-    mvba::DepthCsr c;
+  mvba::PointExtra point_extra() const {
+    mvba::PointExtra c;
     c.begin = ndep > 0 ? d_dpt_begin : nullptr;
     c.slot = d_dpo_slot;
     c.dd = d_dep_desc;
     c.meas = d_dep_meas;
+    c.xbegin = nxyz > 0 ? d_xpt_begin : nullptr;
+    c.xref = d_xref;
+    c.xcc = d_xcc;
     return c;
   }
+  // XYZError priors (point order)
+  int64_t nxyz = 0;
+  std::vector<uint8_t> xfree;             // insertion order: point block free
+  int64_t* d_xpt_begin = nullptr;         // CSR point -> prior entries
+  double4* d_xref = nullptr;              // (x, y, z, weight)
+  double* d_xcc = nullptr;                // Cauchy c = 1/threshold^2
+  int32_t* d_xpid = nullptr;              // point of each entry
+  int64_t* d_xorder = nullptr;            // entry -> insertion index
+  double* d_xout = nullptr;               // [3 nxyz] raw residuals (insertion order), lazy
+  double* d_xscal = nullptr;              // [1 + partials] prior cost scratch
+  unsigned* d_xcnt = nullptr;             // grid-reduction counter (kept zero)
   double* d_dres = nullptr;               // library-owned depth outputs (lazy)
   double* d_dJ = nullptr;
   int64_t dld = 0;

@@ -587,7 +587,7 @@ __global__ void __launch_bounds__(256) k_points_lin(
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, double* __restrict__ pgrad, double* __restrict__ phess,
-    int32_t flags, double cauchy_c, DepthCsr dc) {
+    int32_t flags, double cauchy_c, PointExtra dc) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = t / kLanesPerPoint;
   const int sub = (int)(t % kLanesPerPoint);
@@ -629,6 +629,23 @@ __global__ void __launch_bounds__(256) k_points_lin(
       V[5] += P2;
 #pragma unroll
       for (int c = 0; c < 3; c++) g[c] += o.P * o.r[c];
+    }
+  }
+  if (dc.xbegin && valid && X.w != 0.0) {
+    // XYZError priors (rig_calibrator.cc:720-724): J_pt = weight * sr * I
+    const double4* xref = reinterpret_cast<const double4*>(dc.xref);
+    for (int64_t j = dc.xbegin[p] + sub; j < dc.xbegin[p + 1]; j += kLanesPerPoint) {
+      const double4 R = xref[j];
+      const double r0 = R.w * (X.x - R.x), r1 = R.w * (X.y - R.y), r2 = R.w * (X.z - R.z);
+      double hr;
+      const double sr = loss_scale3(r0, r1, r2, flags, dc.xcc[j], &hr);
+      const double P = R.w * sr;
+      V[0] += P * P;
+      V[3] += P * P;
+      V[5] += P * P;
+      g[0] += P * r0 * sr;
+      g[1] += P * r1 * sr;
+      g[2] += P * r2 * sr;
     }
   }
 #pragma unroll
@@ -766,7 +783,7 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
                                   const int32_t* po_frame, const double2* po_meas,
                                   const mvba::FrameDesc* fd, const double* frec, const double* params,
                                   const double4* pts, double* pgrad, double* phess, int32_t flags,
-                                  double cauchy_c, mvba::DepthCsr dc, hipStream_t s) {
+                                  double cauchy_c, mvba::PointExtra dc, hipStream_t s) {
   if (npts <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((npts * mvba::kLanesPerPoint + 255) / 256);
 #define MVBA_PTS(M, D)                                                                                \

@@ -35,7 +35,7 @@ hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64
                               const double* params, const double4* pts, const double* dir, const double* tinit,
                               const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
                               double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
-                              mvba::DepthCsr dc, const double* xcam, double* du, hipStream_t s);
+                              mvba::PointExtra dc, const double* xcam, double* du, hipStream_t s);
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
@@ -296,6 +296,11 @@ class Solver {
       HCHK(mvba_launch_sum(nb, S_->partial, S_->scal + 17, s_));
       HCHK(mvba_launch_axpby(1, 1.0, acc, 1.0, S_->scal + 17, acc, s_));
     }
+    if (h_->nxyz > 0) {
+      HCHK(mvba_launch_xyz_cost(h_->nxyz, h_->d_xpid, h_->d_xref, h_->d_xcc, h_->d_pts, flags_, h_->d_xscal + 1,
+                                h_->d_xcnt, h_->d_xscal, s_));
+      HCHK(mvba_launch_axpby(1, 1.0, acc, 1.0, h_->d_xscal, acc, s_));
+    }
     check_alpha();
     exchange(acc, 1, MVBA_REDUCE_SUM);
     HCHK(hipMemcpyAsync(S_->hscal + 16, acc, sizeof(double), hipMemcpyDeviceToHost, s_));
@@ -330,7 +335,7 @@ class Solver {
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, nullptr, S_->phess, S_->dmp + S_->ng,
                             S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_, cauchy_c_,
-                            h_->depth_csr(), xv, S_->du, s_));
+                            h_->point_extra(), xv, S_->du, s_));
     reduce_frames(y, xv, dot_slot);
   }
 
@@ -339,7 +344,7 @@ class Solver {
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, nullptr, S_->G + S_->ng, S_->phess,
                             S_->dmp + S_->ng, S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_,
-                            cauchy_c_, h_->depth_csr(), nullptr, S_->du, s_));
+                            cauchy_c_, h_->point_extra(), nullptr, S_->du, s_));
     reduce_frames(S_->tmp, nullptr, 0);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
   }
@@ -429,7 +434,7 @@ class Solver {
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
                             S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial, S_->cnt + 5,
-                            S_->scal + 0, flags_, cauchy_c_, h_->depth_csr(), S_->delta, S_->du, s_));
+                            S_->scal + 0, flags_, cauchy_c_, h_->point_extra(), S_->delta, S_->du, s_));
     HCHK(mvba_launch_axpby(3 * S_->np, -1.0, S_->delta + S_->ng, 0.0, nullptr, S_->delta + S_->ng, s_));
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);

@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256) k_pass_a(
     const double* __restrict__ tinit, const double* __restrict__ V,
     const double* __restrict__ dp, double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
     double* __restrict__ sq_partial, unsigned* __restrict__ counter, double* __restrict__ sq_out,
-    int32_t flags, double cauchy_c, DepthCsr dc, const double* __restrict__ xcam, double* __restrict__ du) {
+    int32_t flags, double cauchy_c, PointExtra dc, const double* __restrict__ xcam, double* __restrict__ du) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = t / kLanesA;
   const int sub = (int)(t % kLanesA);
@@ -291,6 +291,17 @@ __global__ void __launch_bounds__(256) k_pass_a(
         du[3 * (int64_t)sl + r] = u;
         sq += u * u;
       }
+    }
+  }
+  if (sq_partial && valid && dc.xbegin && X.w != 0.0) {
+    // XYZError priors: no camera columns, u = -P w_p
+    const double4* xref = reinterpret_cast<const double4*>(dc.xref);
+    for (int64_t j = dc.xbegin[p] + sub; j < dc.xbegin[p + 1]; j += kLanesA) {
+      const double4 R = xref[j];
+      double hr;
+      const double sr = loss_scale3(R.w * (X.x - R.x), R.w * (X.y - R.y), R.w * (X.z - R.z), flags, dc.xcc[j], &hr);
+      const double P = R.w * sr;
+      sq += P * P * (w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
     }
   }
   if (sq_partial) grid_sum_finalize(sq, sq_partial, counter, sq_out);
@@ -745,7 +756,7 @@ hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64
                               const double* params, const double4* pts, const double* dir, const double* tinit,
                               const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
                               double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
-                              mvba::DepthCsr dc, const double* xcam, double* du, hipStream_t s) {
+                              mvba::PointExtra dc, const double* xcam, double* du, hipStream_t s) {
   const unsigned blocks = (unsigned)((npts * mvba::kLanesA + 255) / 256);
   if (npts <= 0) return hipSuccess;
   if (model < 0) {

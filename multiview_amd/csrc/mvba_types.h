@@ -72,13 +72,19 @@ struct DepthDesc {
   int32_t free_mask;             // bits MVBA_DBLK_*: block is free (Jacobian written)
 };
 
-// Point-ordered view of the depth blocks (CSR point -> depth slots), passed by
-// value to the point-order kernels; begin == nullptr: no depth blocks.
-struct DepthCsr {
+// Point-ordered views of the point-side residual blocks beyond BracketedCamError,
+// passed by value to the point-order kernels:
+//  * depth blocks: CSR point -> depth slots (begin == nullptr: none);
+//  * XYZError priors: CSR point -> prior entries (xbegin == nullptr: none), entry
+//    = (ref xyz, weight) + Cauchy c = 1/threshold^2.
+struct PointExtra {
   const int64_t* begin;    // [num_points + 1]
   const int32_t* slot;     // [num_depth] depth slot of each entry
   const DepthDesc* dd;     // [depth slots]
   const void* meas;        // double4 [depth slots] (x, y, z, weight)
+  const int64_t* xbegin;   // [num_points + 1]
+  const void* xref;        // double4 [num_xyz] (x, y, z, weight), point order
+  const double* xcc;       // [num_xyz] Cauchy c of each prior
 };
 
 }  // namespace mvba

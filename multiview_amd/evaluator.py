@@ -80,6 +80,19 @@ class Evaluator:
         _lib.check(st, self.h)
         return cost.value, r, J
 
+    def evaluate_xyz(self, jacobian: bool = True, apply_loss: bool = False):
+        """XYZError priors, insertion order: (cost, residuals [n, 3], Jacobian [n, 9])."""
+        n = self.problem.num_xyz_residuals
+        r = np.empty((n, 3))
+        J = np.empty((n, 9)) if jacobian else None
+        cost = C.c_double(0.0)
+        flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0) | \
+            (_lib.EVAL_APPLY_LOSS if apply_loss else 0)
+        st = self.lib.mvba_evaluate_xyz(self.h, flags, C.byref(cost), r.ctypes.data,
+                                        J.ctypes.data if J is not None else None)
+        _lib.check(st, self.h)
+        return cost.value, r, J
+
     def evaluate_device(self, jacobian: bool = True, apply_loss: bool = False,
                         robust_threshold: float = 3.0, residuals=None, jac=None, ld: int = 0,
                         stream=None, phase: int = 0):

@@ -70,6 +70,11 @@ class CamProblem:
     depth_weight: np.ndarray = field(default_factory=lambda: np.zeros(0))
     depth_stamps: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
     depth_after: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int64))  # preceding cam block
+    # XYZError priors (optional): point block, reference xyz, weight, Cauchy threshold
+    xyz_block: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int32))
+    xyz_ref: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
+    xyz_weight: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    xyz_threshold: np.ndarray = field(default_factory=lambda: np.zeros(0))
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -79,6 +84,10 @@ class CamProblem:
     @property
     def num_depth_residuals(self) -> int:
         return int(self.depth_blocks.shape[0])
+
+    @property
+    def num_xyz_residuals(self) -> int:
+        return int(self.xyz_block.shape[0])
 
     def jacobian_stride(self) -> int:
         kmax = int(self.camera_dist_size.max()) if len(self.camera_dist_size) else 0
@@ -100,6 +109,10 @@ class CamProblem:
             np.ascontiguousarray(self.depth_meas, dtype=np.float64).reshape(-1),
             np.ascontiguousarray(self.depth_weight, dtype=np.float64).reshape(-1),
             np.ascontiguousarray(self.depth_stamps, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.xyz_block, dtype=np.int32).reshape(-1),
+            np.ascontiguousarray(self.xyz_ref, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.xyz_weight, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.xyz_threshold, dtype=np.float64).reshape(-1),
         ]
         self._keep = arrs
         d = _lib.ProblemDesc()
@@ -121,6 +134,11 @@ class CamProblem:
         d.depth_meas = arrs[10].ctypes.data
         d.depth_weight = arrs[11].ctypes.data
         d.depth_stamps = arrs[12].ctypes.data
+        d.num_xyz_residuals = self.num_xyz_residuals
+        d.xyz_block = arrs[13].ctypes.data
+        d.xyz_ref = arrs[14].ctypes.data
+        d.xyz_weight = arrs[15].ctypes.data
+        d.xyz_threshold = arrs[16].ctypes.data
         return d
 
     def subset(self, idx: np.ndarray) -> "CamProblem":

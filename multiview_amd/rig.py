@@ -467,6 +467,9 @@ class FloatFlags:
     depth_to_image_transforms_to_float: tuple = ()
     float_scale: bool = False
     affine_depth_to_image: bool = False
+    # XYZError prior on every point (rig_calibrator.cc:1889-1898)
+    tri_weight: float = 0.0
+    tri_robust_threshold: float = 0.0
 
 
 def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = True) -> CamProblem:
@@ -604,6 +607,15 @@ def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = Tr
         P.depth_weight = np.full(k.size, float(flags.depth_tri_weight))
         P.depth_stamps = stamps[k].copy()
         P.depth_after = k.astype(np.int64)
+    if flags.tri_weight > 0:
+        # --tri_weight: keep points near their values before the optimisation
+        # (xyz_vec_orig, :1571-1578), Cauchy(--tri_robust_threshold)
+        if not flags.tri_robust_threshold > 0:
+            raise ValueError("a positive --tri_robust_threshold is needed with --tri_weight")
+        P.xyz_block = (xyz_b0 + np.arange(npts)).astype(np.int32)
+        P.xyz_ref = np.asarray(src["xyz"], dtype=np.float64).reshape(-1, 3).copy()
+        P.xyz_weight = np.full(npts, float(flags.tri_weight))
+        P.xyz_threshold = np.full(npts, float(flags.tri_robust_threshold))
     return P
 
 

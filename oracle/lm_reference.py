@@ -29,6 +29,8 @@ def _columns(P):
     used[P.residual_blocks[K_of > 0, 7]] = True
     if P.num_depth_residuals:
         used[P.depth_blocks.reshape(-1)] = True
+    if P.num_xyz_residuals:
+        used[P.xyz_block] = True
     free = np.nonzero(used & (P.block_constant == 0))[0]
     col = np.full(len(P.block_size), -1, dtype=np.int64)
     pos = 0
@@ -80,6 +82,17 @@ def _jacobian(P, params, col, ncols, use_loss, thr):
         cost += cd
         r = np.concatenate([r, rd.reshape(-1)])
         D = np.vstack([D, Dd])
+    if P.num_xyz_residuals:
+        cx, rx, Jx = oracle_py.evaluate_xyz(Q, apply_loss=use_loss)
+        nx = P.num_xyz_residuals
+        Dx = np.zeros((3 * nx, ncols))
+        for j in range(nx):
+            c0 = col[int(P.xyz_block[j])]
+            if c0 >= 0:
+                Dx[3 * j:3 * j + 3, c0:c0 + 3] = Jx[j].reshape(3, 3)
+        cost += cx
+        r = np.concatenate([r, rx.reshape(-1)])
+        D = np.vstack([D, Dx])
     return cost, r, D
 
 
@@ -88,6 +101,8 @@ def _cost(P, params, use_loss, thr):
     c, _, _ = oracle_py.evaluate(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
     if P.num_depth_residuals:
         c += oracle_py.evaluate_depth(Q, oracle_py.RESIDUAL, apply_loss=use_loss, robust_threshold=thr)[0]
+    if P.num_xyz_residuals:
+        c += oracle_py.evaluate_xyz(Q, apply_loss=use_loss)[0]
     return c
 
 

@@ -191,3 +191,30 @@ def evaluate_depth(problem, mode=ANALYTIC, apply_loss=False, robust_threshold=3.
                 J[j, DJAC_BASE[bb]:DJAC_BASE[bb] + 3 * size] = Jj[off:off + 3 * size] * sr
                 off += 3 * size
     return cost, r, J
+
+
+def evaluate_xyz(problem, apply_loss=False):
+    """XYZError (rig_calibrator.cc:720-724): r = weight (xyz - ref), Jacobian
+    weight * I (3x3 row-major, zero for constant points), each block with its
+    own Cauchy threshold. Returns (cost, r [n,3], J [n,9])."""
+    n = problem.num_xyz_residuals
+    r = np.zeros((n, 3))
+    J = np.zeros((n, 9))
+    cost = 0.0
+    for j in range(n):
+        b = int(problem.xyz_block[j])
+        x = problem.block_values(b)
+        w = problem.xyz_weight[j]
+        rj = w * (x - problem.xyz_ref[j])
+        s2 = float(rj @ rj)
+        sr = 1.0
+        if apply_loss:
+            bb = problem.xyz_threshold[j] ** 2
+            cost += 0.5 * (bb * np.log(1.0 + s2 / bb))
+            sr = np.sqrt(max(np.finfo(float).tiny, 1.0 / (1.0 + s2 / bb)))
+        else:
+            cost += 0.5 * s2
+        r[j] = rj * sr
+        if not problem.block_constant[b]:
+            J[j] = (w * sr * np.eye(3)).reshape(-1)
+    return cost, r, J
