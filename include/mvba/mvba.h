@@ -298,6 +298,51 @@ int64_t mvba_num_xyz_residuals(const struct mvba_handle* h);
 mvba_status mvba_evaluate_xyz(struct mvba_handle* h, int32_t flags, double* cost, double* residuals,
                               double* jacobian);
 
+/* ---- Tracks: triangulation and outlier flagging --------
+ * Per optimisation pass rig_calibrator re-triangulates every track from the
+ * current cameras (multiViewTriangulation, interest_point.cc:649-722:
+ * undistort each inlier keypoint with Convert<DISTORTED, UNDISTORTED_C>, then
+ * openMVG::Triangulation::compute(3), triangulation_nview.cc:87-150, with
+ * P = diag(f, f, 1) [R | t]) and afterwards flags outliers by triangulation
+ * angle and reprojection error (flagOutliersByTriAngleAndReprojErr,
+ * rig_calibrator.cc:1045-1154). Both are one GPU thread per track. */
+typedef struct mvba_tracks_desc {
+  int32_t num_images;
+  const double* world_to_cam;    /* [12*num_images]: R row-major (9), then t (3) */
+  const int32_t* image_camera;   /* [num_images] camera model index */
+  int32_t num_cameras;
+  const double* focal;           /* [num_cameras] */
+  const double* center;          /* [2*num_cameras] optical offset */
+  const int32_t* dist_size;      /* [num_cameras] K (RPC: [dist | undist], 2x the coefficients) */
+  const int64_t* dist_offset;    /* [num_cameras] into dist */
+  const double* dist;            /* packed distortion vectors */
+  const double* dist_half;       /* [2*num_cameras] distorted half size */
+  const double* undist_half;     /* [2*num_cameras] undistorted half size */
+  int64_t num_points;
+  const int64_t* track_begin;    /* [num_points+1] */
+  const int32_t* track_image;    /* [num_obs] image of each feature (increasing within a track) */
+  const double* track_pix;       /* [2*num_obs] keypoint (distorted pixel) */
+} mvba_tracks_desc;
+
+/* inlier [num_obs] in/out (0/1); xyz [3*num_points] out. Tracks with < 2 inlier
+ * rays, or a non-finite solution, get all their features flagged outliers; their
+ * xyz is left as in the reference (0 for < 2 rays, the non-finite value otherwise). */
+mvba_status mvba_triangulate(const mvba_tracks_desc* d, int32_t device, uint8_t* inlier, double* xyz);
+/* residuals [2*num_obs]: the pixel residual of each feature (evalResiduals after
+ * the solve; only read for inliers). counts[4] out: outliers by angle, features
+ * seen by the angle pass, outliers by reprojection error, features seen by the
+ * reprojection pass. */
+mvba_status mvba_flag_outliers(const mvba_tracks_desc* d, int32_t device, const double* xyz,
+                               const double* residuals, double min_triangulation_angle,
+                               double max_reprojection_error, uint8_t* inlier, int64_t* counts);
+/* world_to_cam of every frame (image) at the handle's current parameters, from
+ * the K0 frame records: out [12*num_frames] (R row-major, t); frame_of_residual
+ * [num_residuals] (nullable): the frame of each BracketedCamError block in
+ * AddResidualBlock order. Synchronous. */
+mvba_status mvba_frame_poses(struct mvba_handle* h, double* out, int32_t* frame_of_residual);
+/* Message of the last failed mvba_triangulate / mvba_flag_outliers on this thread. */
+const char* mvba_tracks_error(void);
+
 /* ---- Residual statistics (evalResiduals + calc_residuals_stats,
  * rig_calibrator.cc:1157-1180, :753-789) ------------------------------------
  * Raw residuals (no loss) divided by their scale (1 for pixels, the depth weight

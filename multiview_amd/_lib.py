@@ -161,6 +161,26 @@ class SolverSummary(C.Structure):
     ]
 
 
+class TracksDesc(C.Structure):
+    _fields_ = [
+        ("num_images", C.c_int32),
+        ("world_to_cam", C.c_void_p),
+        ("image_camera", C.c_void_p),
+        ("num_cameras", C.c_int32),
+        ("focal", C.c_void_p),
+        ("center", C.c_void_p),
+        ("dist_size", C.c_void_p),
+        ("dist_offset", C.c_void_p),
+        ("dist", C.c_void_p),
+        ("dist_half", C.c_void_p),
+        ("undist_half", C.c_void_p),
+        ("num_points", C.c_int64),
+        ("track_begin", C.c_void_p),
+        ("track_image", C.c_void_p),
+        ("track_pix", C.c_void_p),
+    ]
+
+
 # Every symbol include/mvba/mvba.h declares, with (restype, argtypes).
 SIGNATURES = {
     "mvba_abi_version": (C.c_int, []),
@@ -196,6 +216,11 @@ SIGNATURES = {
                                              C.c_int64, C.c_void_p]),
     "mvba_residual_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_num_xyz_residuals": (C.c_int64, [C.c_void_p]),
+    "mvba_triangulate": (C.c_int, [C.POINTER(TracksDesc), C.c_int32, C.c_void_p, C.c_void_p]),
+    "mvba_flag_outliers": (C.c_int, [C.POINTER(TracksDesc), C.c_int32, C.c_void_p, C.c_void_p, C.c_double,
+                                     C.c_double, C.c_void_p, C.c_void_p]),
+    "mvba_frame_poses": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_tracks_error": (C.c_char_p, []),
     "mvba_evaluate_xyz": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
     "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),

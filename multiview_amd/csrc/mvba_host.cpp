@@ -290,6 +290,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     res_frame[i] = id;
   }
   h->nframes = (int64_t)frames.size();
+  h->res_frame = res_frame;
 
   // ---- groups by (model, degree), then device order
   std::vector<int> gkey_of_cam(d->num_cameras);
@@ -1123,6 +1124,22 @@ mvba_status mvba_evaluate_xyz(mvba_handle* h, int32_t flags, double* cost, doubl
   for (int64_t j = 0; j < NX; j++) total += cj[(size_t)j];
   if (cost) *cost = total;
   return mvba_sync_status(h, nullptr);
+}
+
+mvba_status mvba_frame_poses(mvba_handle* h, double* out, int32_t* frame_of_residual) {
+  if (!h || !out) return MVBA_E_INVALID;
+  if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
+  mvba_status st = mvba_evaluate_device(h, MVBA_EVAL_PREP_ONLY, 0.0, nullptr, nullptr, 0, nullptr);
+  if (st != MVBA_OK) return st;
+  st = mvba_sync_status(h, nullptr);
+  if (st != MVBA_OK) return st;
+  if (h->nframes > 0) {
+    hipError_t e = hipMemcpy2D(out, 12 * sizeof(double), h->d_frec, mvba::kFrameRecDoubles * sizeof(double),
+                               12 * sizeof(double), (size_t)h->nframes, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return h->hip_fail(e, "mvba_frame_poses");
+  }
+  if (frame_of_residual) std::memcpy(frame_of_residual, h->res_frame.data(), h->res_frame.size() * sizeof(int32_t));
+  return MVBA_OK;
 }
 
 }  // extern "C"

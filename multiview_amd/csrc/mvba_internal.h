@@ -158,6 +158,7 @@ struct mvba_handle {
   std::vector<uint8_t> row_written;  // device position -> block bitmask
   std::vector<int16_t> pos_K;        // device position -> distortion length
   std::vector<Group> groups;
+  std::vector<int32_t> res_frame;   // AddResidualBlock index -> frame
   double bytes_res = 0.0, bytes_jac = 0.0;
 
   double* d_params = nullptr;

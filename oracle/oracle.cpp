@@ -38,6 +38,7 @@
 //                      exact derivative of the same formulas, independent of the
 //                      hand-derived chain rule used by the HIP kernels.
 // ============================================================================
+#include <array>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -665,6 +666,200 @@ void oracle_residual_stats(const double* residuals, const int32_t* name_ids, int
     out[4 * k + 2] = v[(int)(0.75 * len)];
     out[4 * k + 3] = v[len - 1];
   }
+}
+
+// ---------------------------------------------------------------- tracks
+// Convert<DISTORTED, UNDISTORTED_C> (camera_params.cc:316-355, :408-410) with
+// OpenCV 3.2 cv::undistortPoints [ext] restated for RADTAN (5 iterations, R = I,
+// P = undistorted intrinsics) and compute_rpc on the undistortion half for RPC.
+static void rpc_eval_cpu(const double* c, int n, double x, double y, double* ox, double* oy) {
+  const int d = rpc_degree(n);
+  std::vector<double> px(d + 1), py(d + 1);
+  double vx = 1.0, vy = 1.0;
+  for (int k = 0; k <= d; k++) {
+    px[k] = vx; vx *= x;
+    py[k] = vy; vy *= y;
+  }
+  double vals[4] = {0.0, 1.0, 0.0, 1.0};
+  int ci = 0;
+  for (int count = 0; count < 4; count++) {
+    const int start = (count == 1 || count == 3) ? 1 : 0;
+    for (int dg = start; dg <= d; dg++)
+      for (int i = 0; i <= dg; i++) vals[count] += c[ci++] * px[dg - i] * py[i];
+  }
+  *ox = vals[0] / vals[1];
+  *oy = vals[2] / vals[3];
+}
+
+int oracle_undistort(double f, const double* c, const double* k, int K, const double* dhalf, const double* uhalf,
+                     const double* pix, double* out) {
+  const double dx = pix[0] - dhalf[0], dy = pix[1] - dhalf[1];
+  if (K == 0) {
+    out[0] = dx - (c[0] - dhalf[0]);
+    out[1] = dy - (c[1] - dhalf[1]);
+  } else if (K == 1) {
+    const double nx = (dx - (c[0] - dhalf[0])) / f, ny = (dy - (c[1] - dhalf[1])) / f;
+    const double rd = std::sqrt(nx * nx + ny * ny);
+    const double ru = std::tan(rd * k[0]) / (2 * std::tan(k[0] / 2));
+    const double conv = rd > 1e-5 ? ru / rd : 1.0;
+    out[0] = conv * (nx * f);
+    out[1] = conv * (ny * f);
+  } else if (K == 4 || K == 5) {
+    const double sx = dx + dhalf[0], sy = dy + dhalf[1];
+    double x = (sx - c[0]) * (1.0 / f), y = (sy - c[1]) * (1.0 / f);
+    const double kk[5] = {k[0], k[1], k[2], k[3], K == 5 ? k[4] : 0.0};
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+      const double r2 = x * x + y * y;
+      const double icdist = 1.0 / (1 + ((kk[4] * r2 + kk[1]) * r2 + kk[0]) * r2);
+      const double deltaX = 2 * kk[2] * x * y + kk[3] * (r2 + 2 * x * x);
+      const double deltaY = kk[2] * (r2 + 2 * y * y) + 2 * kk[3] * x * y;
+      x = (x0 - deltaX) * icdist;
+      y = (y0 - deltaY) * icdist;
+    }
+    out[0] = (f * x + 0.0 * y + uhalf[0]) - uhalf[0];
+    out[1] = (0.0 * x + f * y + uhalf[1]) - uhalf[1];
+  } else {
+    if (!distortion_size_valid(K)) return MVBA_E_BAD_DISTORTION;
+    rpc_eval_cpu(k + K / 2, K / 2, dx, dy, &out[0], &out[1]);
+  }
+  return MVBA_OK;
+}
+
+// Eigen Matrix3d::inverse [ext]: adjugate from cofactors, det along column 0.
+static void eigen_inverse3_cpu(const double* m, double* o) {
+  auto M = [&](int r, int cc) { return m[3 * r + cc]; };
+  auto cof = [&](int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return M(i1, j1) * M(i2, j2) - M(i1, j2) * M(i2, j1);
+  };
+  const double c0[3] = {cof(0, 0), cof(1, 0), cof(2, 0)};
+  const double det = c0[0] * M(0, 0) + c0[1] * M(1, 0) + c0[2] * M(2, 0);
+  const double inv = 1.0 / det;
+  for (int j = 0; j < 3; j++) o[j] = c0[j] * inv;
+  o[3] = cof(0, 1) * inv; o[4] = cof(1, 1) * inv; o[5] = cof(2, 1) * inv;
+  o[6] = cof(0, 2) * inv; o[7] = cof(1, 2) * inv; o[8] = cof(2, 2) * inv;
+}
+
+// multiViewTriangulation (interest_point.cc:649-722) over tracks; same layout as
+// mvba_tracks_desc. wc: [12*num_images] R (9) + t (3).
+int oracle_triangulate(int64_t npts, const int64_t* tb, const int32_t* img, const int32_t* image_cam,
+                       const double* wc, const double* focal, const double* center, const int32_t* Ks,
+                       const int64_t* doff, const double* dist, const double* dhalf, const double* uhalf,
+                       const double* pix, uint8_t* inlier, double* xyz) {
+  for (int64_t p = 0; p < npts; p++) {
+    xyz[3 * p] = xyz[3 * p + 1] = xyz[3 * p + 2] = 0.0;
+    std::vector<std::array<double, 12>> Ps;
+    std::vector<std::array<double, 2>> uv;
+    for (int64_t o = tb[p]; o < tb[p + 1]; o++) {
+      if (!inlier[o]) continue;
+      const int im = img[o], cam = image_cam[im];
+      std::array<double, 2> u;
+      const int st = oracle_undistort(focal[cam], center + 2 * cam, dist + doff[cam], Ks[cam], dhalf + 2 * cam,
+                                      uhalf + 2 * cam, pix + 2 * o, u.data());
+      if (st != MVBA_OK) return st;
+      std::array<double, 12> P;
+      const double* w = wc + 12 * im;
+      for (int r = 0; r < 3; r++) {  // P_From_KRt: K [R | t], K = diag(f, f, 1)
+        const double s = r < 2 ? focal[cam] : 1.0;
+        for (int cc = 0; cc < 3; cc++) P[4 * r + cc] = s * w[3 * r + cc];
+        P[4 * r + 3] = s * w[9 + r];
+      }
+      Ps.push_back(P);
+      uv.push_back(u);
+    }
+    if (Ps.size() < 2) {
+      for (int64_t o = tb[p]; o < tb[p + 1]; o++) inlier[o] = 0;
+      continue;
+    }
+    // openMVG Triangulation::compute(3) (triangulation_nview.cc:87-150)
+    std::vector<double> weights(Ps.size(), 1.0);
+    double X[3] = {0, 0, 0};
+    for (int it = 0; it < 3; it++) {
+      double AtA[9] = {0}, Atb[3] = {0};
+      for (size_t i = 0; i < Ps.size(); i++) {
+        const double* P = Ps[i].data();
+        const double w = weights[i];
+        double v1[3], v2[3];
+        for (int j = 0; j < 3; j++) {
+          v1[j] = w * (P[j] - uv[i][0] * P[8 + j]);
+          v2[j] = w * (P[4 + j] - uv[i][1] * P[8 + j]);
+          Atb[j] += w * (v1[j] * (uv[i][0] * P[11] - P[3]) + v2[j] * (uv[i][1] * P[11] - P[7]));
+        }
+        for (int k = 0; k < 3; k++)
+          for (int j = 0; j <= k; j++) {
+            const double v = v1[j] * v1[k] + v2[j] * v2[k];
+            AtA[3 * j + k] += v;
+            if (j < k) AtA[3 * k + j] += v;
+          }
+      }
+      double Ai[9];
+      eigen_inverse3_cpu(AtA, Ai);
+      for (int r = 0; r < 3; r++) X[r] = Ai[3 * r] * Atb[0] + Ai[3 * r + 1] * Atb[1] + Ai[3 * r + 2] * Atb[2];
+      for (size_t i = 0; i < Ps.size(); i++) {
+        const double* P = Ps[i].data();
+        const double z = P[8] * X[0] + P[9] * X[1] + P[10] * X[2] + P[11];
+        weights[i] = 1.0 / z;
+      }
+    }
+    for (int r = 0; r < 3; r++) xyz[3 * p + r] = X[r];
+    if (!std::isfinite(X[0]) || !std::isfinite(X[1]) || !std::isfinite(X[2]))
+      for (int64_t o = tb[p]; o < tb[p + 1]; o++) inlier[o] = 0;
+  }
+  return MVBA_OK;
+}
+
+// flagOutliersByTriAngleAndReprojErr (rig_calibrator.cc:1045-1154). counts[4]:
+// angle outliers, angle total, reprojection outliers, reprojection total.
+void oracle_flag_outliers(int64_t npts, const int64_t* tb, const int32_t* img, const double* wc, const double* xyz,
+                          const double* res, double min_angle, double max_err, uint8_t* inlier, int64_t* counts) {
+  for (int q = 0; q < 4; q++) counts[q] = 0;
+  auto center = [&](int im, double* C) {
+    Aff<double> a;
+    for (int q = 0; q < 9; q++) a.R[q] = wc[12 * im + q];
+    for (int q = 0; q < 3; q++) a.t[q] = wc[12 * im + 9 + q];
+    Aff<double> inv = affine_inverse(a);
+    for (int q = 0; q < 3; q++) C[q] = inv.t[q];
+  };
+  for (int64_t p = 0; p < npts; p++) {
+    double max_angle = 0.0;
+    for (int64_t o1 = tb[p]; o1 < tb[p + 1]; o1++) {
+      if (!inlier[o1]) continue;
+      counts[1]++;
+      double C1[3], r1[3];
+      center(img[o1], C1);
+      for (int q = 0; q < 3; q++) r1[q] = xyz[3 * p + q] - C1[q];
+      const double n1 = std::sqrt(r1[0] * r1[0] + r1[1] * r1[1] + r1[2] * r1[2]);
+      if (n1 > 0) for (int q = 0; q < 3; q++) r1[q] /= n1;
+      for (int64_t o2 = tb[p]; o2 < tb[p + 1]; o2++) {
+        if (img[o2] <= img[o1] || !inlier[o2]) continue;
+        double C2[3], r2[3];
+        center(img[o2], C2);
+        for (int q = 0; q < 3; q++) r2[q] = xyz[3 * p + q] - C2[q];
+        const double n2 = std::sqrt(r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2]);
+        if (n2 > 0) for (int q = 0; q < 3; q++) r2[q] /= n2;
+        const double ang = (180.0 / M_PI) * std::acos(r1[0] * r2[0] + r1[1] * r2[1] + r1[2] * r2[2]);
+        if (std::isnan(ang) || std::isinf(ang)) continue;
+        max_angle = std::max(max_angle, ang);
+      }
+    }
+    if (max_angle >= min_angle) continue;
+    for (int64_t o = tb[p]; o < tb[p + 1]; o++)
+      if (inlier[o]) {
+        counts[0]++;
+        inlier[o] = 0;
+      }
+  }
+  for (int64_t p = 0; p < npts; p++)
+    for (int64_t o = tb[p]; o < tb[p + 1]; o++) {
+      if (!inlier[o]) continue;
+      counts[3]++;
+      const double rx = res[2 * o], ry = res[2 * o + 1];
+      if (!(std::sqrt(rx * rx + ry * ry) <= max_err)) {
+        counts[2]++;
+        inlier[o] = 0;
+      }
+    }
 }
 
 }  // extern "C"

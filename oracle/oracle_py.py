@@ -30,6 +30,11 @@ def load():
     if not os.path.exists(LIB):
         build()
     lib = C.CDLL(LIB)
+    lib.oracle_triangulate.restype = C.c_int
+    lib.oracle_triangulate.argtypes = [C.c_int64] + [C.c_void_p] * 14
+    lib.oracle_flag_outliers.restype = None
+    lib.oracle_flag_outliers.argtypes = [C.c_int64] + [C.c_void_p] * 5 + [C.c_double, C.c_double] + \
+        [C.c_void_p] * 2
     lib.oracle_evaluate.restype = C.c_int
     lib.oracle_evaluate.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_double,
                                     C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -218,3 +223,36 @@ def evaluate_xyz(problem, apply_loss=False):
         if not problem.block_constant[b]:
             J[j] = (w * sr * np.eye(3)).reshape(-1)
     return cost, r, J
+
+
+def triangulate(tracks, inlier=None):
+    """multiViewTriangulation restated (oracle.cpp). tracks: multiview_amd.tracks.Tracks."""
+    lib = load()
+    d = tracks.desc()
+    ar = tracks._keep
+    inl = np.ones(tracks.num_obs, dtype=np.uint8) if inlier is None else np.array(inlier, dtype=np.uint8)
+    xyz = np.zeros((tracks.num_points, 3))
+    st = lib.oracle_triangulate(C.c_int64(tracks.num_points), ar[9].ctypes.data, ar[10].ctypes.data,
+                                ar[1].ctypes.data, ar[0].ctypes.data, ar[2].ctypes.data, ar[3].ctypes.data,
+                                ar[4].ctypes.data, ar[5].ctypes.data, ar[6].ctypes.data, ar[7].ctypes.data,
+                                ar[8].ctypes.data, ar[11].ctypes.data, inl.ctypes.data, xyz.ctypes.data)
+    if st != 0:
+        raise OracleError(st, "triangulate")
+    del d
+    return inl, xyz
+
+
+def flag_outliers(tracks, xyz, residuals, min_angle, max_err, inlier):
+    """flagOutliersByTriAngleAndReprojErr restated (oracle.cpp)."""
+    lib = load()
+    d = tracks.desc()
+    ar = tracks._keep
+    inl = np.array(inlier, dtype=np.uint8)
+    x = np.ascontiguousarray(xyz, dtype=np.float64)
+    r = np.ascontiguousarray(residuals, dtype=np.float64)
+    counts = np.zeros(4, dtype=np.int64)
+    lib.oracle_flag_outliers(C.c_int64(tracks.num_points), ar[9].ctypes.data, ar[10].ctypes.data, ar[0].ctypes.data,
+                             x.ctypes.data, r.ctypes.data, C.c_double(min_angle), C.c_double(max_err),
+                             inl.ctypes.data, counts.ctypes.data)
+    del d
+    return inl, counts
