@@ -78,6 +78,19 @@ def cpu_baseline(problem, sample: int, min_seconds: float = 10.0):
                       f"{dt:.1f} s"}
 
 
+def _pmc_traffic(config):
+    """HBM bytes per K1 launch from the committed PMC summary of this config
+    (tools/pmc_summary.py over separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes of this same command; profiles/), or None."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    path = os.path.join(here, "profiles", "r01", f"pmc_k1_{config}.json")
+    try:
+        with open(path) as f:
+            return float(json.load(f)["traffic_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main():
     args = parse()
     import torch
@@ -189,7 +202,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": _pmc_traffic(args.config),
             "bytes_per_launch": bytes_eval,
             "kernel_ms": obs_ms,
             "prep_ms": prep_ms,

@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU session producing the round's evidence: GPU tests, default bench (with the
+# CPU baseline), rocprof kernel stats for c2 and c5, and two PMC passes
+# (FETCH_SIZE, WRITE_SIZE: they cannot share a pass on gfx950) for K1's HBM traffic.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p $OUT
+TAG=${1:-r01}
+run() {
+  local name=$1 secs=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/steps.log
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name exit $rc" | tee -a $OUT/steps.log
+  tail -3 "$OUT/$name.log" | cut -c1-400
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return $rc
+}
+run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
+run bench_$TAG 600 python bench.py
+run prof_c2_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2_$TAG -o run --output-format csv -- python3 bench.py --steps 10 --no-cpu-baseline
+run prof_c5_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c5_$TAG -o run --output-format csv -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline
+run pmc_fetch_$TAG 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --ba-iters 0
+run pmc_write_$TAG 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --ba-iters 0
+exit 0
