@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MVBA_ABI_VERSION 2
+#define MVBA_ABI_VERSION 3
 
 /* Status codes. Non-zero codes mirror the reference's fatal checks. */
 typedef enum mvba_status {
@@ -348,9 +348,11 @@ const char* mvba_tracks_error(void);
  * Raw residuals (no loss) divided by their scale (1 for pixels, the depth weight
  * for depth blocks), |r| grouped by residual name, and per group the values at
  * sorted positions int(0.25 len), int(0.5 len), int(0.75 len), len-1.
- * Groups (num_cameras*2 + 3): 2c + k = camera c, pixel component k
+ * Groups (num_cameras*2 + 6): 2c + k = camera c, pixel component k
  * ("<sensor>_pix_x", "<sensor>_pix_y"); 2*num_cameras + k = depth component k
- * ("depth_tri_{x,y,z}_m"). out [4*groups] (NaN for empty groups), counts [groups].
+ * ("depth_tri_{x,y,z}_m"); 2*num_cameras + 3 + k = XYZ prior component k
+ * ("tri_{x,y,z}_m", scale = its weight). out [4*groups] (NaN for empty groups),
+ * counts [groups].
  * Synchronous. */
 mvba_status mvba_residual_stats(struct mvba_handle* h, double* out, int64_t* counts, void* hip_stream);
 

@@ -17,6 +17,7 @@
 namespace mvba {
 
 // Reprojection slots: group 2*cam + component; padding slots -> sentinel group.
+// Depth blocks: groups 2*ncam + k; XYZ priors (--tri_weight): 2*ncam + 3 + k.
 __global__ void k_stats_keys_cam(const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
                                  const double* __restrict__ res, int64_t ld, int64_t nslots,
                                  uint64_t* __restrict__ keys, uint32_t* __restrict__ groups) {
@@ -47,6 +48,24 @@ __global__ void k_stats_keys_depth(int64_t nslots, const int64_t* __restrict__ d
     const double v = fabs(dres[k * ld + i] / w);
     keys[k * nslots + i] = __double_as_longlong(v);
     groups[k * nslots + i] = g0 + k;
+  }
+}
+
+// XYZError prior blocks: group g0 + component, value |w (X - ref)| / w (the
+// reference divides the raw residual by its scale, rig_calibrator.cc:1172-1173).
+__global__ void k_stats_keys_xyz(int64_t n, const int32_t* __restrict__ xpid, const double4* __restrict__ xref,
+                                 const double4* __restrict__ pts, uint32_t g0, uint64_t* __restrict__ keys,
+                                 uint32_t* __restrict__ groups) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double4 X = pts[xpid[j]];
+  const double4 R = xref[j];
+  const double d[3] = {X.x - R.x, X.y - R.y, X.z - R.z};
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const double v = fabs((R.w * d[k]) / R.w);
+    keys[k * n + j] = __double_as_longlong(v);
+    groups[k * n + j] = g0 + k;
   }
 }
 
@@ -104,9 +123,9 @@ mvba_status mvba_residual_stats(mvba_handle* h, double* out, int64_t* counts, vo
     if (st != MVBA_OK) return st;
   }
   const int32_t ncam_groups = 2 * h->ncams;
-  const int32_t ngroups = ncam_groups + 3;
+  const int32_t ngroups = ncam_groups + 6;
   const uint32_t sentinel = (uint32_t)ngroups;
-  const int64_t n_cam = 2 * h->nslots, n_dep = 3 * h->ndep_slots, n = n_cam + n_dep;
+  const int64_t n_cam = 2 * h->nslots, n_dep = 3 * h->ndep_slots, n_xyz = 3 * h->nxyz, n = n_cam + n_dep + n_xyz;
   hipError_t e = hipSuccess;
   uint64_t *k0 = nullptr, *k1 = nullptr;
   uint32_t *g0 = nullptr, *g1 = nullptr;
@@ -141,6 +160,10 @@ mvba_status mvba_residual_stats(mvba_handle* h, double* out, int64_t* counts, vo
       hipLaunchKernelGGL(mvba::k_stats_keys_depth, dim3((unsigned)((h->ndep_slots + 255) / 256)), dim3(256), 0, s,
                          h->ndep_slots, h->d_dep_order, h->d_dep_meas, h->d_dres, h->dld, (uint32_t)ncam_groups,
                          k0 + n_cam, g0 + n_cam);
+    if (h->nxyz > 0)
+      hipLaunchKernelGGL(mvba::k_stats_keys_xyz, dim3((unsigned)((h->nxyz + 255) / 256)), dim3(256), 0, s, h->nxyz,
+                         h->d_xpid, h->d_xref, h->d_pts, (uint32_t)(ncam_groups + 3), k0 + n_cam + n_dep,
+                         g0 + n_cam + n_dep);
     size_t t1 = tb1, t2 = tb2;
     chk(hipcub::DeviceRadixSort::SortPairs(temp, t1, k0, k1, g0, g1, (int)n, 0, 64, s));   // by value
     chk(hipcub::DeviceRadixSort::SortPairs(temp, t2, g1, g0, k1, k0, (int)n, 0, gbits, s)); // stable by group

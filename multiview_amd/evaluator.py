@@ -160,12 +160,12 @@ class Evaluator:
         residual blocks."""
         ncam = len(self.problem.camera_dist_size)
         names = list(sensor_names or [f"cam{c}" for c in range(ncam)])
-        ng = 2 * ncam + 3
+        ng = 2 * ncam + 6
         out = np.empty(4 * ng)
         counts = np.empty(ng, dtype=np.int64)
         _lib.check(self.lib.mvba_residual_stats(self.h, out.ctypes.data, counts.ctypes.data, None), self.h)
         labels = [f"{names[c]}_pix_{xy}" for c in range(ncam) for xy in "xy"] + \
-            [f"depth_tri_{a}_m" for a in "xyz"]
+            [f"depth_tri_{a}_m" for a in "xyz"] + [f"tri_{a}_m" for a in "xyz"]
         rows = [(labels[g], *out[4 * g:4 * g + 4], int(counts[g])) for g in range(ng) if counts[g] > 0]
         return sorted(rows, key=lambda r: r[0])
 

@@ -1,0 +1,456 @@
+"""CPU restatement of rig_calibrator's main() (rig_calibrator/bin/rig_calibrator.cc
+:1268-2041) for end-to-end parity of the CLI (multiview_amd/cli/rig_calibrator).
+
+TEST INFRASTRUCTURE (oracle/): only tests/ may call this. It reads the same
+input files as the CLI with its own parsers and runs the reference's pass loop
+on the CPU pieces of the oracle:
+    triangulation        oracle_py.triangulate   (multiViewTriangulation)
+    solve                lm_reference.solve      (Ceres LM, dense exact steps)
+    residual statistics  oracle_py.residual_stats (calc_residuals_stats)
+    outlier flagging     oracle_py.flag_outliers (flagOutliersByTriAngleAndReprojErr)
+Parity is pinned the same way as those pieces; the orchestration
+here follows:
+    readRigConfig                 dense_map_utils.cc:940-1057
+    ReadNVM / readImageEntry      interest_point.cc:1248-1331, :1611-1671
+    lookupImagesAndBrackets       dense_map_utils.cc:1441-1657 (+ NoBrackets :1664-1741)
+    calc_rig_using_word_to_cam    rig_calibrator.cc:1186-1266
+    appendMatchesFromNvm          interest_point.cc:1788-1845
+    flagOutlierByExclusionDist    rig_calibrator.cc:1003-1039
+    problem assembly              rig_calibrator.cc:1614-1898
+    copy back / outputs           rig_calibrator.cc:1924-2038
+Only the flags the tests use are modelled (no bounds: float_timestamp_offsets off).
+"""
+from __future__ import annotations
+
+import math
+import os
+import re
+
+import numpy as np
+
+from multiview_amd.problem import CamProblem
+from multiview_amd.rig import mat_to_quat, quat_to_mat
+from multiview_amd.tracks import Tracks
+
+from . import lm_reference, oracle_py
+
+
+def _read_config(path):
+    """Tag/value lines of rig_config.txt; comments after '#'."""
+    lines = []
+    for ln in open(path):
+        ln = ln.split("#", 1)[0].strip()
+        if ln:
+            lines.append(ln.split())
+    sensors = []
+    it = iter(lines[1:])
+    for tok in it:
+        assert tok[0] == "sensor_name:"
+        s = {"name": tok[1]}
+        for _ in range(10):
+            t = next(it)
+            s[t[0].rstrip(":")] = t[1:]
+        sensors.append(s)
+    out = []
+    for s in sensors:
+        T = np.array([float(v) for v in s["ref_to_sensor_transform"]])
+        D = np.array([float(v) for v in s["depth_to_image_transform"]])
+        out.append(dict(name=s["name"], focal=float(s["focal_length"][0]),
+                        center=np.array([float(v) for v in s["optical_center"]]),
+                        dist=np.array([float(v) for v in s["distortion_coeffs"]]),
+                        image_size=[int(float(v)) for v in s["image_size"]],
+                        crop=[int(float(v)) for v in s["distorted_crop_size"]],
+                        undist=[int(float(v)) for v in s["undistorted_image_size"]],
+                        ref_to_cam=(T[:9].reshape(3, 3), T[9:]), depth_to_image=(D[:9].reshape(3, 3), D[9:]),
+                        offset=float(s["ref_to_sensor_timestamp_offset"][0])))
+    return out
+
+
+def _read_nvm(path):
+    tok = open(path).read().split()
+    assert tok[0] == "NVM_V3"
+    k = 1
+    n = int(tok[k]); k += 1
+    files, w2c = [], []
+    kp = []
+    for _ in range(n):
+        files.append(tok[k])
+        w, x, y, z = (float(v) for v in tok[k + 2:k + 6])
+        c = np.array([float(v) for v in tok[k + 6:k + 9]])
+        k += 11
+        # Quaterniond(w, x, y, z).matrix(): no normalisation
+        tx, ty, tz = 2 * x, 2 * y, 2 * z
+        R = np.array([[1 - (ty * y + tz * z), tx * y - tz * w, tx * z + ty * w],
+                      [tx * y + tz * w, 1 - (tx * x + tz * z), ty * z - tx * w],
+                      [tx * z - ty * w, ty * z + tx * w, 1 - (tx * x + ty * y)]])
+        w2c.append((R, -R @ c))
+        kp.append({})
+    npid = int(tok[k]); k += 1
+    tracks = []
+    for _ in range(npid):
+        k += 6
+        m = int(tok[k]); k += 1
+        t = {}
+        for _ in range(m):
+            cid, fid = int(tok[k]), int(tok[k + 1])
+            kp[cid][fid] = (float(tok[k + 2]), float(tok[k + 3]))
+            t[cid] = fid
+            k += 4
+        tracks.append(t)
+    return files, w2c, kp, tracks
+
+
+_NUM = re.compile(r"^[0-9]*\.?[0-9]*([eE][-+]?[0-9]+)?")
+
+
+def _rigid_to_array(R, t):
+    return np.r_[t, mat_to_quat(np.asarray(R)[None])[0]]
+
+
+def _array_to_rigid(a):
+    q = np.asarray(a[3:], dtype=np.float64)
+    q = q / math.sqrt(float(q @ q))
+    x, y, z, w = q
+    tx, ty, tz = 2 * x, 2 * y, 2 * z
+    R = np.array([[1 - (ty * y + tz * z), tx * y - tz * w, tx * z + ty * w],
+                  [tx * y + tz * w, 1 - (tx * x + tz * z), ty * z - tx * w],
+                  [tx * z - ty * w, ty * z + tx * w, 1 - (tx * x + ty * y)]])
+    return R, np.asarray(a[:3], dtype=np.float64)
+
+
+def _load_cloud(path):
+    with open(path, "rb") as f:
+        rows, cols, ch = np.fromfile(f, dtype=np.int32, count=3)
+        data = np.fromfile(f, dtype=np.float32, count=int(rows) * int(cols) * int(ch))
+    return data.reshape(int(rows), int(cols), int(ch))
+
+
+def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_threshold=3.0, bracket_len=0.6,
+        intrinsics_to_float="", rig_transforms_to_float="", camera_poses_to_float="", no_rig=False,
+        depth_tri_weight=0.0, depth_to_image_transforms_to_float="", float_scale=False, tri_weight=0.0,
+        tri_robust_threshold=0.0, min_triangulation_angle=0.5, max_reprojection_error=25.0,
+        parameter_tolerance=1e-12, timestamp_offsets_max_change=1.0):
+    sensors = _read_config(rig_config)
+    names = [s["name"] for s in sensors]
+    ns = len(sensors)
+    files, file_w2c, nvm_kp, nvm_tracks = _read_nvm(nvm)
+
+    def split(s):
+        return re.sub(r"[\\:, \t\r\n]", " ", s).split()
+
+    # readImageEntry + ImageDataToVectors
+    images = [dict() for _ in range(ns)]
+    depths = [dict() for _ in range(ns)]
+    for f, (R, t) in zip(files, file_w2c):
+        st = float(_NUM.match(os.path.basename(f)).group(0))
+        typ = names.index(os.path.basename(os.path.dirname(f)))
+        images[typ][st] = dict(name=f, w2c=(R, t))
+        pc = os.path.splitext(f)[0] + ".pc"
+        if os.path.exists(pc):
+            depths[typ][st] = dict(name=pc, cloud=_load_cloud(pc))
+    img = [[dict(stamp=s, **images[t][s]) for s in sorted(images[t])] for t in range(ns)]
+    dep = [[dict(stamp=s, **depths[t][s]) for s in sorted(depths[t])] for t in range(ns)]
+    ref_stamps = [m["stamp"] for m in img[0]]
+    world_to_ref = [m["w2c"] for m in img[0]]
+    offsets = np.array([s["offset"] for s in sensors])
+
+    # lookupImages
+    cams = []
+    if not no_rig:
+        nref = len(ref_stamps)
+        for beg in range(nref):
+            end = beg + 1
+            last = end == nref
+            if last:
+                end = beg
+            for t in range(ns):
+                if t == 0:
+                    m = next(x for x in img[0] if x["stamp"] >= ref_stamps[beg])
+                    cam = dict(type=0, stamp=ref_stamps[beg], ref_stamp=ref_stamps[beg], beg=beg, end=beg,
+                               name=m["name"])
+                else:
+                    bt = ref_stamps[beg] + offsets[t]
+                    et = ref_stamps[end] + offsets[t]
+                    if et == bt and last:
+                        et = np.nextafter(et, et + 1.0)
+                    mid = (bt + et) / 2.0
+                    best, bd = None, 1e100
+                    for m in img[t]:  # candidates at or after bt, stop once past et
+                        if m["stamp"] < bt:
+                            continue
+                        if bt <= m["stamp"] < et and abs(m["stamp"] - mid) < bd:
+                            best, bd = m, abs(m["stamp"] - mid)
+                        if m["stamp"] > et:
+                            break
+                    if best is None:
+                        continue
+                    if best["stamp"] > bt and et - bt > bracket_len:
+                        continue
+                    cam = dict(type=t, stamp=best["stamp"], ref_stamp=best["stamp"] - offsets[t], beg=beg, end=end,
+                               name=best["name"])
+                cl = next((d for d in dep[t] if d["stamp"] >= cam["stamp"]), None)
+                cam["cloud"] = None if cl is None else cl["cloud"]
+                cams.append(cam)
+    else:
+        for t in range(ns):
+            for k, m in enumerate(img[t]):
+                cl = next((d for d in dep[t] if d["stamp"] >= m["stamp"]), None)
+                cams.append(dict(type=t, stamp=m["stamp"], ref_stamp=m["stamp"], beg=k, end=k, name=m["name"],
+                                 cloud=None if cl is None else cl["cloud"]))
+    cams.sort(key=lambda c: c["ref_stamp"])  # stable, as the CLI
+    nc = len(cams)
+
+    w2r_vec = np.array([_rigid_to_array(*a) for a in world_to_ref])
+    by_name = {m["name"]: m for t in range(ns) for m in img[t]}
+    w2c0 = [by_name[c["name"]]["w2c"] for c in cams]
+    # calc_rig_using_word_to_cam: entry-wise vals[size/2] (unsorted), det^(1/3)
+    tr = {}
+    for k, c in enumerate(cams):
+        if c["type"] == 0:
+            tr.setdefault(0, []).append(np.eye(4))
+            continue
+        Ri, ti = oracle_py.world_to_cam(w2r_vec[c["beg"]], w2r_vec[c["end"]], [0, 0, 0, 0, 0, 0, 1],
+                                        ref_stamps[c["beg"]], ref_stamps[c["end"]], offsets[c["type"]], c["stamp"])
+        Mi = np.eye(4)
+        Mi[:3, :3], Mi[:3, 3] = Ri, ti
+        Mc = np.eye(4)
+        Mc[:3, :3], Mc[:3, 3] = w2c0[k]
+        tr.setdefault(c["type"], []).append(Mc @ np.linalg.inv(Mi))
+    r2c_vec = np.zeros((ns, 7))
+    for t in range(ns):
+        v = tr[t][len(tr[t]) // 2]
+        L = v[:3, :3] / np.cbrt(np.linalg.det(v[:3, :3]))
+        r2c_vec[t] = _rigid_to_array(L, v[:3, 3])
+    ident = np.array([0, 0, 0, 0, 0, 0, 1.0])
+    focal = np.array([s["focal"] for s in sensors])
+    center = np.array([s["center"] for s in sensors])
+    dist = [s["dist"].copy() for s in sensors]
+    dscale = np.zeros(ns)
+    dti_vec = np.zeros((ns, 7))
+    for t, s in enumerate(sensors):
+        L, tt = s["depth_to_image"]
+        dscale[t] = np.cbrt(np.linalg.det(L))
+        dti_vec[t] = _rigid_to_array(L / dscale[t], tt)
+    w2c_vec = np.array([_rigid_to_array(*a) for a in w2c0]) if no_rig else None
+
+    itf = {n: set() for n in names}
+    cur = ""
+    for v in split(intrinsics_to_float):
+        if v in names:
+            cur = v
+        else:
+            itf[cur].add(v)
+    rtf = set(split(rig_transforms_to_float))
+    cpf = set(split(camera_poses_to_float))
+    dtf = set(split(depth_to_image_transforms_to_float))
+
+    # appendMatchesFromNvm
+    nvm_index = {f: i for i, f in enumerate(files)}
+    nvm_to_cams = {nvm_index[c["name"]]: k for k, c in enumerate(cams)}
+    keypoints = [[] for _ in range(nc)]
+    tracks = []
+    for t in nvm_tracks:
+        out = {}
+        for ncid, fid in sorted(t.items()):
+            if ncid not in nvm_to_cams:
+                continue
+            cid = nvm_to_cams[ncid]
+            x, y = nvm_kp[ncid][fid]
+            ctr = center[cams[cid]["type"]]
+            out[cid] = len(keypoints[cid])
+            keypoints[cid].append(np.float32([x + ctr[0], y + ctr[1]]).astype(np.float64))
+        if len(out) > 1:
+            tracks.append(out)
+    npid = len(tracks)
+    tb = np.zeros(npid + 1, dtype=np.int64)
+    timg, tpix = [], []
+    for p, t in enumerate(tracks):
+        for cid in sorted(t):
+            timg.append(cid)
+            tpix.append(keypoints[cid][t[cid]])
+        tb[p + 1] = len(timg)
+    timg = np.array(timg, dtype=np.int32)
+    tpix = np.array(tpix)
+    inlier = np.ones(len(timg), dtype=np.uint8)
+    for o in range(len(timg)):
+        s = sensors[cams[timg[o]]["type"]]
+        if (abs(tpix[o, 0] - s["image_size"][0] / 2.0) > s["crop"][0] / 2.0
+                or abs(tpix[o, 1] - s["image_size"][1] / 2.0) > s["crop"][1] / 2.0):
+            inlier[o] = 0
+    image_type = np.array([c["type"] for c in cams], dtype=np.int32)
+
+    def world_to_cam_all():
+        out = np.zeros((nc, 12))
+        for k, c in enumerate(cams):
+            if no_rig:
+                R, t = _array_to_rigid(w2c_vec[k])
+            else:
+                R, t = oracle_py.world_to_cam(w2r_vec[c["beg"]], w2r_vec[c["end"]], r2c_vec[c["type"]],
+                                              ref_stamps[c["beg"]], ref_stamps[c["end"]], offsets[c["type"]],
+                                              c["stamp"])
+            out[k] = np.r_[R.reshape(-1), t]
+        return out
+
+    def tracks_obj(w2c):
+        return Tracks(world_to_cam=w2c, image_camera=image_type, focal=focal.copy(), center=center.copy(),
+                      dist=[d.copy() for d in dist],
+                      dist_half=np.array([[s["image_size"][0] / 2.0, s["image_size"][1] / 2.0] for s in sensors]),
+                      undist_half=np.array([[s["undist"][0] / 2.0, s["undist"][1] / 2.0] for s in sensors]),
+                      track_begin=tb, track_image=timg, track_pix=tpix)
+
+    stats_log = []
+    xyz = np.zeros((npid, 3))
+    for _ in range(calibrator_num_passes):
+        w2c = world_to_cam_all()
+        inlier, xyz = oracle_py.triangulate(tracks_obj(w2c), inlier)
+        xyz_orig = xyz.copy()
+        # problem assembly with lazily registered blocks (Ceres Problem semantics)
+        reg, sizes, vals, const = {}, [], [], set()
+
+        def blk(key, v):
+            if key not in reg:
+                reg[key] = len(sizes)
+                sizes.append(len(v))
+                vals.append(np.asarray(v, dtype=np.float64).copy())
+            return reg[key]
+
+        def get(key):
+            kind, i = key
+            return {"w2r": lambda: w2r_vec[i], "w2c": lambda: w2c_vec[i], "id": lambda: ident,
+                    "r2c": lambda: r2c_vec[i], "xyz": lambda: xyz[i], "off": lambda: [offsets[i]],
+                    "f": lambda: [focal[i]], "c": lambda: center[i], "d": lambda: dist[i] if len(dist[i]) else [0.0],
+                    "dti": lambda: dti_vec[i], "sc": lambda: [dscale[i]]}[kind]()
+
+        res, dres, xres = [], [], []
+        for p in range(npid):
+            tri_inl = False
+            for o in range(tb[p], tb[p + 1]):
+                if not inlier[o]:
+                    continue
+                tri_inl = True
+                cid = int(timg[o])
+                c = cams[cid]
+                t = c["type"]
+                if not no_rig:
+                    kb = ("w2r", c["beg"])
+                    ke = ("id", 0) if (t == 0 or c["beg"] == c["end"]) else ("w2r", c["end"])
+                    stamps = [ref_stamps[c["beg"]], ref_stamps[c["end"]], c["stamp"]]
+                else:
+                    kb, ke = ("w2c", cid), ("id", 0)
+                    stamps = [c["stamp"]] * 3
+                kd = ("d", t) if len(dist[t]) else ("d", -1)
+                keys = [kb, ke, ("r2c", t), ("xyz", p), ("off", t), ("f", t), ("c", t), kd]
+                ids = [blk(k, get(k) if k != ("d", -1) else [0.0]) for k in keys]
+                res.append((ids, t, tpix[o], stamps, o))
+                if "focal_length" not in itf[names[t]]:
+                    const.add(("f", t))
+                if "optical_center" not in itf[names[t]]:
+                    const.add(("c", t))
+                if "distortion" not in itf[names[t]] or not len(dist[t]):
+                    const.add(kd)
+                if not no_rig:
+                    if names[0] not in cpf:
+                        const.add(kb)
+                elif names[t] not in cpf:
+                    const.add(kb)
+                if names[0] not in cpf or t == 0 or no_rig:
+                    const.add(ke)
+                const.add(("off", t))  # float_timestamp_offsets is not modelled here
+                if names[t] not in rtf or t == 0 or no_rig:
+                    const.add(("r2c", t))
+                if depth_tri_weight > 0 and c["cloud"] is not None:
+                    cl = c["cloud"]
+                    col, row = int(round(tpix[o, 0])), int(round(tpix[o, 1]))
+                    if col < cl.shape[1] and row < cl.shape[0] and np.any(cl[row, col] != 0):
+                        dk = [kb, ke, ("r2c", t), ("dti", t), ("sc", t), ("xyz", p), ("off", t)]
+                        dres.append(([blk(k, get(k)) for k in dk], cl[row, col].astype(np.float64), stamps))
+                        if not float_scale:
+                            const.add(("sc", t))
+                        if names[t] not in dtf:
+                            const.add(("dti", t))
+            if tri_weight > 0 and tri_inl:
+                xres.append((blk(("xyz", p), get(("xyz", p))), xyz_orig[p]))
+        sizes_a = np.array(sizes, dtype=np.int32)
+        offs = np.zeros(len(sizes), dtype=np.int64)
+        offs[1:] = np.cumsum(sizes_a[:-1])
+        cst = np.zeros(len(sizes), dtype=np.uint8)
+        for k in const:
+            if k in reg:
+                cst[reg[k]] = 1
+        P = CamProblem(block_size=sizes_a, block_offset=offs, block_constant=cst, params=np.concatenate(vals),
+                       camera_dist_size=np.array([len(d) for d in dist], dtype=np.int32),
+                       camera_half_size=np.array([[s["image_size"][0] / 2.0, s["image_size"][1] / 2.0]
+                                                  for s in sensors]),
+                       residual_blocks=np.array([r[0] for r in res], dtype=np.int32),
+                       residual_camera=np.array([r[1] for r in res], dtype=np.int32),
+                       residual_meas=np.array([r[2] for r in res]), residual_stamps=np.array([r[3] for r in res]))
+        if dres:
+            P.depth_blocks = np.array([d[0] for d in dres], dtype=np.int32)
+            P.depth_meas = np.array([d[1] for d in dres])
+            P.depth_weight = np.full(len(dres), float(depth_tri_weight))
+            P.depth_stamps = np.array([d[2] for d in dres])
+        if xres:
+            P.xyz_block = np.array([x[0] for x in xres], dtype=np.int32)
+            P.xyz_ref = np.array([x[1] for x in xres])
+            P.xyz_weight = np.full(len(xres), float(tri_weight))
+            P.xyz_threshold = np.full(len(xres), float(tri_robust_threshold))
+
+        def stats():
+            _, r, _ = oracle_py.evaluate(P, oracle_py.RESIDUAL)
+            ids = [(2 * P.residual_camera[:, None] + np.arange(2)).reshape(-1)]
+            v = [r.reshape(-1)]
+            if dres:
+                _, rd, _ = oracle_py.evaluate_depth(P, oracle_py.RESIDUAL)
+                v.append((rd / P.depth_weight[:, None]).reshape(-1))
+                ids.append(2 * ns + np.tile(np.arange(3), len(dres)))
+            if xres:
+                _, rx, _ = oracle_py.evaluate_xyz(P)
+                v.append((rx.reshape(-1, 3) / P.xyz_weight[:, None]).reshape(-1))
+                ids.append(2 * ns + 3 + np.tile(np.arange(3), len(xres)))
+            ng = 2 * ns + 6
+            out, cnt = oracle_py.residual_stats(np.concatenate(v), np.concatenate(ids).astype(np.int32), ng)
+            labels = [f"{n}_pix_{a}" for n in names for a in "xy"] + [f"depth_tri_{a}_m" for a in "xyz"] + \
+                [f"tri_{a}_m" for a in "xyz"]
+            return sorted([(labels[g], *out[g], int(cnt[g])) for g in range(ng) if cnt[g] > 0])
+
+        before = stats()
+        x, summary = lm_reference.solve(P, max_num_iterations=num_iterations, function_tolerance=1e-16,
+                                        gradient_tolerance=1e-16, parameter_tolerance=parameter_tolerance,
+                                        use_loss=True, robust_threshold=robust_threshold)
+        P.params = x
+        for key, b in reg.items():
+            v = x[offs[b]:offs[b] + sizes[b]]
+            kind, i = key
+            if kind == "w2r":
+                w2r_vec[i] = v
+            elif kind == "w2c":
+                w2c_vec[i] = v
+            elif kind == "r2c":
+                r2c_vec[i] = v
+            elif kind == "xyz":
+                xyz[i] = v
+            elif kind == "off":
+                offsets[i] = v[0]
+            elif kind == "f":
+                focal[i] = v[0]
+            elif kind == "c":
+                center[i] = v
+            elif kind == "d" and i >= 0:
+                dist[i] = v.copy()
+            elif kind == "dti":
+                dti_vec[i] = v
+            elif kind == "sc":
+                dscale[i] = v[0]
+        after = stats()
+        stats_log.append((before, after, summary))
+        _, r, _ = oracle_py.evaluate(P, oracle_py.RESIDUAL)
+        resid = np.zeros((len(timg), 2))
+        for j, rr in enumerate(res):
+            resid[rr[4]] = r[j]
+        w2c = world_to_cam_all()
+        inlier, counts = oracle_py.flag_outliers(tracks_obj(w2c), xyz, resid.reshape(-1), min_triangulation_angle,
+                                                 max_reprojection_error, inlier)
+    w2c = world_to_cam_all()
+    return dict(image_names=[c["name"] for c in cams], world_to_cam=w2c, focal=focal, center=center, dist=dist,
+                ref_to_cam=r2c_vec, offsets=offsets, xyz=xyz, inlier=inlier, stats=stats_log, names=names,
+                depth_to_image=[(_array_to_rigid(dti_vec[t])[0] * dscale[t], dti_vec[t][:3]) for t in range(ns)])

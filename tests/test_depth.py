@@ -173,24 +173,33 @@ def test_depth_linearize_parity(oracle, name, apply_loss):
 def test_residual_stats_match_oracle(oracle):
     """mvba_residual_stats = evalResiduals + calc_residuals_stats: raw residuals
     divided by their scale, grouped by name, percentiles by index; against the
-    oracle's residuals fed to the oracle's restatement of calc_residuals_stats."""
+    oracle's residuals fed to the oracle's restatement of calc_residuals_stats.
+    Pixel, depth (scale depth_tri_weight) and XYZ prior (scale tri_weight) groups."""
     R = _rig(False, seed=23)
-    P = rig.build_problem(R, _flags(False))
+    P = rig.build_problem(R, _flags(False, tri_weight=0.5, tri_robust_threshold=0.1))
+    P.params = P.params.copy()
+    P.params[P.block_offset[P.xyz_block]] += np.linspace(-0.05, 0.05, P.num_xyz_residuals)
     names = R.sensor_names
     with Evaluator(P) as ev:
         ev.set_params()
         rows = ev.residual_stats(names)
     _, r, _ = oracle.evaluate(P, oracle.RESIDUAL)
     _, rd, _ = oracle.evaluate_depth(P, oracle.RESIDUAL)
+    _, rx, _ = oracle.evaluate_xyz(P)
     ncam = len(P.camera_dist_size)
-    vals = np.concatenate([r.reshape(-1), (rd / P.depth_weight[:, None]).reshape(-1)])
+    vals = np.concatenate([r.reshape(-1), (rd / P.depth_weight[:, None]).reshape(-1),
+                           (rx.reshape(-1, 3) / P.xyz_weight[:, None]).reshape(-1)])
     ids = np.concatenate([(2 * P.residual_camera[:, None] + np.arange(2)).reshape(-1),
-                          (2 * ncam + np.tile(np.arange(3), rd.shape[0]))]).astype(np.int32)
-    ref, counts = oracle.residual_stats(vals, ids, 2 * ncam + 3)
-    labels = [f"{names[c]}_pix_{xy}" for c in range(ncam) for xy in "xy"] + [f"depth_tri_{a}_m" for a in "xyz"]
-    expect = sorted([(labels[g], *ref[g], int(counts[g])) for g in range(2 * ncam + 3) if counts[g] > 0],
+                          (2 * ncam + np.tile(np.arange(3), rd.shape[0])),
+                          (2 * ncam + 3 + np.tile(np.arange(3), P.num_xyz_residuals))]).astype(np.int32)
+    ng = 2 * ncam + 6
+    ref, counts = oracle.residual_stats(vals, ids, ng)
+    labels = [f"{names[c]}_pix_{xy}" for c in range(ncam) for xy in "xy"] + \
+        [f"depth_tri_{a}_m" for a in "xyz"] + [f"tri_{a}_m" for a in "xyz"]
+    expect = sorted([(labels[g], *ref[g], int(counts[g])) for g in range(ng) if counts[g] > 0],
                     key=lambda t: t[0])
     assert [e[0] for e in expect] == [g[0] for g in rows]
+    assert "tri_x_m" in [g[0] for g in rows]
     for g, e in zip(rows, expect):
         assert g[5] == e[5]
         assert np.allclose(g[1:5], e[1:5], rtol=1e-9, atol=1e-12), (g, e)
