@@ -37,6 +37,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include <hip/hip_runtime_api.h>
@@ -562,6 +563,7 @@ struct BlockSet {
 struct CamRes {
   double* blk[8];
   int bsize[8];
+  int32_t id[8];  // camera-side block ids in the template block set (id[XYZ] unused)
   int cam_type;
   double meas[2];
   double stamps[3];
@@ -571,6 +573,7 @@ struct CamRes {
 struct DepthRes {
   double* blk[7];
   int bsize[7];
+  int32_t id[7];
   double meas[3];
   double stamps[3];
   int pid;
@@ -584,7 +587,7 @@ struct Plan {
   std::vector<CamRes> cam;
   std::vector<DepthRes> depth;
   std::vector<XyzRes> xyz;
-  std::set<const double*> constant;
+  std::unordered_set<const double*> constant;
   std::map<const double*, std::pair<double, double>> bounds;
 };
 
@@ -978,8 +981,11 @@ static int run(int argc, char** argv) {
   };
 
   const int ngpu = F.num_gpus;
+  int32_t ndev = 0;
+  if (F.calibrator_num_passes > 0 && (mvba_device_count(&ndev) != MVBA_OK || ndev < 1))
+    fatal("No HIP device is available (this build has no CPU compute path).");
   double placeholder = 0.0;  // distortion_placeholder (:1608)
-  double t_tri = 0, t_build = 0, t_stats = 0, t_solve = 0, t_flag = 0;
+  double t_tri = 0, t_build = 0, t_create = 0, t_stats = 0, t_solve = 0, t_flag = 0;
   std::vector<double> residuals_after;  // per feature, [2*nobs]
   for (int pass = 0; pass < F.calibrator_num_passes; pass++) {
     std::cout << "\nOptimization pass " << pass + 1 << " / " << F.calibrator_num_passes << "\n";
@@ -1087,23 +1093,48 @@ static int run(int argc, char** argv) {
         while (hi < npid && (per_pid[(size_t)hi + 1] <= target || s == ngpu - 1)) hi++;
         shards[(size_t)s].pid_lo = lo;
         shards[(size_t)s].pid_hi = hi;
-        shards[(size_t)s].device = device0 + s;
+        shards[(size_t)s].device = (device0 + s) % ndev;  // shards share GPUs when there are fewer
         lo = hi;
       }
     }
+    // camera-side blocks first, in the order the whole problem references them,
+    // so every shard has the same camera layout; constancy and bounds are
+    // properties of the block
+    BlockSet tmpl;
+    tmpl.ids.reserve(4096);
+    for (auto& r : plan.cam)
+      for (int b = 0; b < 8; b++)
+        if (b != MVBA_BLK_XYZ) r.id[b] = tmpl.get(r.blk[b], r.bsize[b]);
+    for (auto& r : plan.depth)
+      for (int b = 0; b < 7; b++)
+        if (b != MVBA_DBLK_XYZ) r.id[b] = tmpl.get(r.blk[b], r.bsize[b]);
+    for (const double* p : plan.constant) {
+      auto it = tmpl.ids.find(p);
+      if (it != tmpl.ids.end()) tmpl.cst[(size_t)it->second] = 1;
+    }
+    for (const auto& kv : plan.bounds) {
+      auto it = tmpl.ids.find(kv.first);
+      if (it == tmpl.ids.end()) continue;
+      tmpl.lo[(size_t)tmpl.off[(size_t)it->second]] = kv.second.first;
+      tmpl.hi[(size_t)tmpl.off[(size_t)it->second]] = kv.second.second;
+    }
+    std::vector<int32_t> point_id((size_t)npid);
     for (auto& S : shards) {
+      S.blocks = tmpl;
       BlockSet& B = S.blocks;
-      // camera-side blocks first, in the order the whole problem references
-      // them, so every shard has the same camera layout
-      for (const auto& r : plan.cam)
-        for (int b = 0; b < 8; b++)
-          if (b != MVBA_BLK_XYZ) B.get(r.blk[b], r.bsize[b]);
-      for (const auto& r : plan.depth)
-        for (int b = 0; b < 7; b++)
-          if (b != MVBA_DBLK_XYZ) B.get(r.blk[b], r.bsize[b]);
+      std::fill(point_id.begin(), point_id.end(), -1);
+      auto point = [&](int pid) {  // point blocks: first use, never constant
+        int32_t& id = point_id[(size_t)pid];
+        if (id < 0) id = B.get(&xyz_vec[3 * (size_t)pid], 3);
+        return id;
+      };
+      const size_t nres_hint = plan.cam.size() / shards.size() + 16;
+      S.res_blocks.reserve(8 * nres_hint);
+      S.res_meas.reserve(2 * nres_hint);
+      S.res_stamps.reserve(3 * nres_hint);
       for (const auto& r : plan.cam) {
         if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
-        for (int b = 0; b < 8; b++) S.res_blocks.push_back(B.get(r.blk[b], r.bsize[b]));
+        for (int b = 0; b < 8; b++) S.res_blocks.push_back(b == MVBA_BLK_XYZ ? point(r.pid) : r.id[b]);
         S.res_cam.push_back(r.cam_type);
         S.res_meas.insert(S.res_meas.end(), r.meas, r.meas + 2);
         S.res_stamps.insert(S.res_stamps.end(), r.stamps, r.stamps + 3);
@@ -1111,27 +1142,17 @@ static int run(int argc, char** argv) {
       }
       for (const auto& r : plan.depth) {
         if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
-        for (int b = 0; b < 7; b++) S.dep_blocks.push_back(B.get(r.blk[b], r.bsize[b]));
+        for (int b = 0; b < 7; b++) S.dep_blocks.push_back(b == MVBA_DBLK_XYZ ? point(r.pid) : r.id[b]);
         S.dep_meas.insert(S.dep_meas.end(), r.meas, r.meas + 3);
         S.dep_weight.push_back(F.depth_tri_weight);
         S.dep_stamps.insert(S.dep_stamps.end(), r.stamps, r.stamps + 3);
       }
       for (const auto& r : plan.xyz) {
         if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
-        S.xyz_block.push_back(B.get(&xyz_vec[3 * (size_t)r.pid], 3));
+        S.xyz_block.push_back(point(r.pid));
         S.xyz_ref.insert(S.xyz_ref.end(), r.ref, r.ref + 3);
         S.xyz_weight.push_back(F.tri_weight);
         S.xyz_thr.push_back(F.tri_robust_threshold);
-      }
-      for (const double* p : plan.constant) {
-        auto it = B.ids.find(p);
-        if (it != B.ids.end()) B.cst[(size_t)it->second] = 1;
-      }
-      for (const auto& kv : plan.bounds) {
-        auto it = B.ids.find(kv.first);
-        if (it == B.ids.end()) continue;
-        B.lo[(size_t)B.off[(size_t)it->second]] = kv.second.first;
-        B.hi[(size_t)B.off[(size_t)it->second]] = kv.second.second;
       }
       for (int t = 0; t < ncam; t++) {
         S.cam_dist_size.push_back((int32_t)dist[(size_t)t].size());
@@ -1164,8 +1185,10 @@ static int run(int argc, char** argv) {
       d.xyz_threshold = S.xyz_thr.data();
       mvba_options o{};
       o.device = S.device;
+      const auto tc = Clock::now();
       check(nullptr, mvba_create(&d, &o, &S.h));
       check(S.h, mvba_set_params(S.h, B.x.data()));
+      t_create += secs(tc);
     }
     t_build += secs(t0);
     t0 = Clock::now();
@@ -1317,7 +1340,7 @@ static int run(int argc, char** argv) {
   }
   if (F.profile)
     std::cout << std::setprecision(4) << "Timings (s): triangulation " << t_tri << ", problem setup " << t_build
-              << ", residual stats " << t_stats << ", solve " << t_solve << ", outlier flagging " << t_flag
+              << " (mvba_create " << t_create << "), residual stats " << t_stats << ", solve " << t_solve << ", outlier flagging " << t_flag
               << std::endl;
   return 0;
 }

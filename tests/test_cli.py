@@ -38,7 +38,14 @@ def _run(cli, *args, cwd=None, timeout=600):
 def _dataset(tmp_path, models=("radtan", "fov", "none"), num_ref=8, num_points=150, seed=3, **kw):
     R = rig.make_rig(num_sensors=len(models), num_ref=num_ref, num_points=num_points, obs_per_point=4,
                      models=list(models), seed=seed, **kw)
-    return R, rig_files.write_dataset(R, str(tmp_path / "data"))
+    dti = None
+    if kw.get("depth_sensors"):
+        dti = np.tile(np.eye(4), (len(models), 1, 1))
+        for s in range(len(models)):  # init depth_to_image (rigid 7-array) as 4x4
+            a = R.init["depth_to_image"][s]
+            dti[s, :3, :3] = rig.quat_to_mat(a[3:][None])[0]
+            dti[s, :3, 3] = a[:3]
+    return R, rig_files.write_dataset(R, str(tmp_path / "data"), depth_to_image=dti)
 
 
 # ---------------------------------------------------------------- CPU
@@ -120,8 +127,8 @@ def test_image_lookup_and_bracketing(cli, tmp_path):
 
 
 def test_rig_config_round_trip(cli, tmp_path):
-    """With no passes the written rig_config.txt holds the configuration read in,
-    the rig transforms derived from the poses (calc_rig_using_word_to_cam)."""
+    """With no passes and --use_initial_rig_transforms the written rig_config.txt
+    holds the configuration read in."""
     R, info = _dataset(tmp_path)
     code, out, err = _run(cli, "--rig_config", info["rig_config"], "--nvm", info["nvm"], "--out_dir",
                           str(tmp_path / "o"), "--calibrator_num_passes", "0", "--use_initial_rig_transforms")
@@ -136,6 +143,28 @@ def test_rig_config_round_trip(cli, tmp_path):
             assert tx == ty
         elif tx:
             assert np.allclose([float(v) for v in tx[1:]], [float(v) for v in ty[1:]], rtol=1e-12, atol=1e-15), (x, y)
+
+
+def test_rig_from_camera_poses(cli, tmp_path):
+    """calc_rig_using_word_to_cam (rig_calibrator.cc:1186-1266): the rig
+    transforms written after zero passes equal the oracle restatement's, and the
+    camera poses are the rig-derived ones (calc_world_to_cam_using_rig)."""
+    from oracle import rig_calibrator_ref
+    from oracle.rig_calibrator_ref import _array_to_rigid
+
+    R, info = _dataset(tmp_path)
+    code, out, err = _run(cli, "--rig_config", info["rig_config"], "--nvm", info["nvm"], "--out_dir",
+                          str(tmp_path / "o"), "--calibrator_num_passes", "0")
+    assert code == 0, err
+    ref = rig_calibrator_ref.run(info["rig_config"], info["nvm"], calibrator_num_passes=0)
+    rows = _read_rig(tmp_path / "o" / "rig_config.txt")
+    for t, r in enumerate(rows):
+        Rr, tr = _array_to_rigid(ref["ref_to_cam"][t])
+        T = np.array(r["ref_to_sensor_transform"])
+        assert np.allclose(T[:9], Rr.reshape(-1), rtol=0, atol=1e-13) and np.allclose(T[9:], tr, atol=1e-13)
+    cams = _read_cameras(tmp_path / "o" / "cameras.txt")
+    for k, nm in enumerate(ref["image_names"]):
+        assert np.allclose(cams[nm], ref["world_to_cam"][k], rtol=0, atol=1e-12)
 
 
 # ---------------------------------------------------------------- GPU
@@ -186,6 +215,9 @@ CASES = {
                               intrinsics_to_float="cam1:focal_length,optical_center")),
     "tri_weight": dict(flags=dict(rig_transforms_to_float="cam2", tri_weight=0.5, tri_robust_threshold=0.1,
                                   intrinsics_to_float="cam2:distortion")),
+    "depth": dict(rig=dict(depth_sensors=(2,)),
+                  flags=dict(rig_transforms_to_float="cam1 cam2", depth_tri_weight=10.0,
+                             depth_to_image_transforms_to_float="cam2", float_scale=True)),
 }
 
 
@@ -200,16 +232,20 @@ def _cli_args(flags):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", list(CASES))
+@pytest.mark.parametrize("name", list(CASES) + ["rig_2shards"])
 def test_cli_matches_oracle_pipeline(cli, tmp_path, name):
+    """rig_2shards: the "rig" case with --num_gpus 2 (landmark shards, host
+    all-reduce between the solver threads; on a one-GPU box both shards share it)."""
     from oracle import rig_calibrator_ref
 
+    shards = 2 if name.endswith("_2shards") else 1
+    name = name.replace("_2shards", "")
     flags = dict(CASES[name]["flags"])
-    R, info = _dataset(tmp_path, seed=11 + len(name))
+    R, info = _dataset(tmp_path, seed=11 + len(name), **CASES[name].get("rig", {}))
     out_dir = tmp_path / "out"
     common = dict(num_iterations=100, parameter_tolerance=1e-12)
     code, out, err = _run(cli, "--rig_config", info["rig_config"], "--nvm", info["nvm"], "--out_dir", str(out_dir),
-                          *_cli_args({**flags, **common}), "--save_nvm")
+                          *_cli_args({**flags, **common}), "--save_nvm", "--num_gpus", str(shards))
     assert code == 0, err + out[-3000:]
     ref = rig_calibrator_ref.run(info["rig_config"], info["nvm"], **flags, **common)
 
@@ -241,6 +277,12 @@ def test_cli_matches_oracle_pipeline(cli, tmp_path, name):
             Rr, tr = _array_to_rigid(ref["ref_to_cam"][t])
             T = np.array(r["ref_to_sensor_transform"])
             assert np.allclose(T[:9], Rr.reshape(-1), atol=1e-6) and np.allclose(T[9:], tr, atol=1e-6)
+    if flags.get("depth_tri_weight"):
+        assert info["num_clouds"] > 0 and "depth_tri_x_m" in before0
+        for t, r in enumerate(rows):
+            Rd, td = ref["depth_to_image"][t]
+            T = np.array(r["depth_to_image_transform"])
+            assert np.allclose(T[:9], Rd.reshape(-1), atol=1e-6) and np.allclose(T[9:], td, atol=1e-6)
     # NVM output: inlier tracks with more than two features
     nvm = open(out_dir / "cameras.nvm").read().split()
     assert nvm[0] == "NVM_V3" and int(nvm[1]) == len(ref["image_names"])
