@@ -445,6 +445,49 @@ mvba_status mvba_solve(struct mvba_handle* h, const mvba_solver_options* o, mvba
 /* Copy the handle's current packed parameter vector to host memory. */
 mvba_status mvba_get_params(struct mvba_handle* h, double* packed);
 
+/* ---- RPC lens-model fitting -----------------------
+ * fitRpcUndist (rpc_distortion.cc:658-721), as run by
+ * CameraParameters::updateRpcUndistortion (camera_params.cc:214-253) after a
+ * pass that floated RPC distortion (rig_calibrator.cc:1946-1948), and
+ * fitRpcDist (:622-656, the fit_rpc tool). Samples the undistorted image on a
+ * num_samples^2 grid (genUndistDistPairs, :519-557; samples whose distorted
+ * pixel leaves the distorted crop box are dropped), then fits RPC coefficients
+ * of degree 1, 2, ..., rpc_degree, each degree starting from the previous fit
+ * (identity at degree 1), by Levenberg-Marquardt with Ceres 1.14's step
+ * control, gradient/function tolerance 1e-16, the given parameter tolerance and
+ * iteration cap per degree.
+ *   MVBA_RPC_FIT_UNDISTORTION: fits undist with undist(rpc(u, dist)) ~ u, where
+ *     dist = rpc_dist_coeffs (2 (d+1)(d+2) - 2 values, degree rpc_degree);
+ *   MVBA_RPC_FIT_DISTORTION: fits rpc(u) ~ the camera's distorted pixel
+ *     (any distortion model of the camera).
+ * coeffs_out: 2 (d+1)(d+2) - 2 values (RPCLensDistortion layout). Synchronous. */
+enum { MVBA_RPC_FIT_DISTORTION = 0, MVBA_RPC_FIT_UNDISTORTION = 1 };
+typedef struct mvba_rpc_camera {
+  double focal;
+  double center[2];            /* optical offset */
+  int32_t dist_size;           /* GetDistortion().size() (RPC: [dist | undist]) */
+  const double* dist;
+  int32_t image_size[2];       /* distorted size */
+  int32_t crop_size[2];        /* distorted crop size */
+  int32_t undist_size[2];      /* undistorted size */
+} mvba_rpc_camera;
+typedef struct mvba_rpc_fit_report {
+  int64_t num_samples_used;
+  double undist_box[4];        /* centred undistorted pixels: min x, min y, max x, max y */
+  double dist_box[4];          /* centred distorted pixels */
+  double initial_cost[6];      /* per degree 1..6 */
+  double final_cost[6];
+  int32_t iterations[6];
+  int32_t termination[6];      /* MVBA_CONVERGENCE / NO_CONVERGENCE / FAILURE */
+  double max_dist_undist_error; /* evalRpcDistUndist (:723-737), UNDISTORTION mode; -1 otherwise */
+} mvba_rpc_fit_report;
+mvba_status mvba_rpc_fit(const mvba_rpc_camera* cam, int32_t mode, int32_t rpc_degree,
+                         const double* rpc_dist_coeffs, int32_t num_samples, int32_t num_iterations,
+                         double parameter_tolerance, int32_t device, double* coeffs_out,
+                         mvba_rpc_fit_report* report);
+/* Message of the last failed mvba_rpc_fit on this thread. */
+const char* mvba_rpc_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -181,6 +181,35 @@ class TracksDesc(C.Structure):
     ]
 
 
+RPC_FIT_DISTORTION = 0
+RPC_FIT_UNDISTORTION = 1
+
+
+class RpcCamera(C.Structure):
+    _fields_ = [
+        ("focal", C.c_double),
+        ("center", C.c_double * 2),
+        ("dist_size", C.c_int32),
+        ("dist", C.c_void_p),
+        ("image_size", C.c_int32 * 2),
+        ("crop_size", C.c_int32 * 2),
+        ("undist_size", C.c_int32 * 2),
+    ]
+
+
+class RpcFitReport(C.Structure):
+    _fields_ = [
+        ("num_samples_used", C.c_int64),
+        ("undist_box", C.c_double * 4),
+        ("dist_box", C.c_double * 4),
+        ("initial_cost", C.c_double * 6),
+        ("final_cost", C.c_double * 6),
+        ("iterations", C.c_int32 * 6),
+        ("termination", C.c_int32 * 6),
+        ("max_dist_undist_error", C.c_double),
+    ]
+
+
 # Every symbol include/mvba/mvba.h declares, with (restype, argtypes).
 SIGNATURES = {
     "mvba_abi_version": (C.c_int, []),
@@ -221,6 +250,9 @@ SIGNATURES = {
                                      C.c_double, C.c_void_p, C.c_void_p]),
     "mvba_frame_poses": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_tracks_error": (C.c_char_p, []),
+    "mvba_rpc_fit": (C.c_int, [C.POINTER(RpcCamera), C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
+                               C.c_double, C.c_int32, C.c_void_p, C.POINTER(RpcFitReport)]),
+    "mvba_rpc_error": (C.c_char_p, []),
     "mvba_evaluate_xyz": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
     "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),

@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmvba.so")
-SOURCES = ["mvba_kernels.hip", "mvba_solver.hip", "mvba_depth.hip", "mvba_stats.hip", "mvba_tracks.hip",
+SOURCES = ["mvba_kernels.hip", "mvba_solver.hip", "mvba_depth.hip", "mvba_stats.hip", "mvba_tracks.hip", "mvba_rpc.hip",
            "mvba_host.cpp", "mvba_solve.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wall",

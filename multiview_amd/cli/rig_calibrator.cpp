@@ -850,9 +850,6 @@ static int run(int argc, char** argv) {
     focal[(size_t)t] = rig.params[(size_t)t].focal;
     center[(size_t)t] = {rig.params[(size_t)t].center[0], rig.params[(size_t)t].center[1]};
     dist[(size_t)t] = rig.params[(size_t)t].dist;
-    if (intrinsics_to_float[(size_t)t].count("distortion") && dist[(size_t)t].size() > 5)
-      fatal("Floating RPC distortion needs the undistortion refit (updateRpcUndistortion, camera_params.cc:214-253), "
-            "which this build does not implement yet.");
   }
   std::vector<double> offsets = rig.offsets;
   std::vector<double> world_to_cam_vec;
@@ -1256,6 +1253,36 @@ static int run(int argc, char** argv) {
         if (is_point || s == 0)
           std::memcpy(S.blocks.owner[b], x.data() + S.blocks.off[b], sizeof(double) * (size_t)S.blocks.size[b]);
       }
+    }
+    // RPC: refit the undistortion half to the optimized distortion half
+    // (updateRpcUndistortion, rig_calibrator.cc:1946-1948 -> camera_params.cc:214-253)
+    for (int t = 0; t < ncam; t++) {
+      auto& D = dist[(size_t)t];
+      if (!intrinsics_to_float[(size_t)t].count("distortion") || D.size() <= 5) continue;
+      const int num_samples = 400, num_iter = 100;
+      std::cout << "Finding RPC undistortion. Using " << num_samples << " samples in width and height, " << num_iter
+                << " iterations, and " << F.num_opt_threads << " threads." << std::endl;
+      const size_t half = D.size() / 2;
+      mvba_rpc_camera rc{};
+      rc.focal = focal[(size_t)t];
+      rc.center[0] = center[(size_t)t][0];
+      rc.center[1] = center[(size_t)t][1];
+      rc.dist_size = (int32_t)D.size();
+      rc.dist = D.data();
+      const auto& cp = rig.params[(size_t)t];
+      for (int k = 0; k < 2; k++) {
+        rc.image_size[k] = cp.image_size[k];
+        rc.crop_size[k] = cp.crop_size[k];
+        rc.undist_size[k] = cp.undist_size[k];
+      }
+      const int deg = (int)std::lround(std::sqrt(2.0 * (double)half + 5.0) / 2.0 - 1.5);
+      std::vector<double> undist(half);
+      mvba_rpc_fit_report rep{};
+      if (mvba_rpc_fit(&rc, MVBA_RPC_FIT_UNDISTORTION, deg, D.data(), num_samples, num_iter, 1e-12, device0,
+                       undist.data(), &rep) != MVBA_OK)
+        fatal(std::string("RPC undistortion fit: ") + mvba_rpc_error());
+      std::copy(undist.begin(), undist.end(), D.begin() + (std::ptrdiff_t)half);
+      std::cout << "Max distort_undistort error: " << rep.max_dist_undist_error << std::endl;
     }
     t0 = Clock::now();
     residual_stats(shards, cam_names, "after opt");

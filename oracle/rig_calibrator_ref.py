@@ -441,6 +441,16 @@ def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_thre
                 dti_vec[i] = v
             elif kind == "sc":
                 dscale[i] = v[0]
+        # updateRpcUndistortion (rig_calibrator.cc:1946-1948) for floated RPC distortion
+        from . import rpc_fit_reference
+
+        for t in range(ns):
+            if "distortion" in itf[names[t]] and len(dist[t]) > 5:
+                half = len(dist[t]) // 2
+                cam = dict(focal=focal[t], center=center[t], dist=dist[t], image_size=sensors[t]["image_size"],
+                           crop_size=sensors[t]["crop"], undist_size=sensors[t]["undist"])
+                und, _, _, _ = rpc_fit_reference.fit_rpc_undist(cam, dist[t][:half], 400)
+                dist[t] = np.concatenate([dist[t][:half], und])
         after = stats()
         stats_log.append((before, after, summary))
         _, r, _ = oracle_py.evaluate(P, oracle_py.RESIDUAL)

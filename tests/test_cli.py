@@ -215,6 +215,8 @@ CASES = {
                               intrinsics_to_float="cam1:focal_length,optical_center")),
     "tri_weight": dict(flags=dict(rig_transforms_to_float="cam2", tri_weight=0.5, tri_robust_threshold=0.1,
                                   intrinsics_to_float="cam2:distortion")),
+    "rpc": dict(rig=dict(models=("radtan", "rpc2", "fov")),
+                flags=dict(rig_transforms_to_float="cam1 cam2", intrinsics_to_float="cam1:focal_length,distortion")),
     "depth": dict(rig=dict(depth_sensors=(2,)),
                   flags=dict(rig_transforms_to_float="cam1 cam2", depth_tri_weight=10.0,
                              depth_to_image_transforms_to_float="cam2", float_scale=True)),
