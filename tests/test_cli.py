@@ -215,8 +215,11 @@ CASES = {
                               intrinsics_to_float="cam1:focal_length,optical_center")),
     "tri_weight": dict(flags=dict(rig_transforms_to_float="cam2", tri_weight=0.5, tri_robust_threshold=0.1,
                                   intrinsics_to_float="cam2:distortion")),
-    "rpc": dict(rig=dict(models=("radtan", "rpc2", "fov")),
-                flags=dict(rig_transforms_to_float="cam1 cam2", intrinsics_to_float="cam1:focal_length,distortion")),
+    # floating RPC distortion (undistortion refit after each pass); the RPC's
+    # linear terms trade off with focal length and rig rotation, so only the
+    # distortion of cam1 floats (a unique minimum to compare)
+    "rpc": dict(rig=dict(models=("radtan", "rpc1", "fov"), num_points=400),
+                flags=dict(rig_transforms_to_float="cam2", intrinsics_to_float="cam1:distortion")),
     "depth": dict(rig=dict(depth_sensors=(2,)),
                   flags=dict(rig_transforms_to_float="cam1 cam2", depth_tri_weight=10.0,
                              depth_to_image_transforms_to_float="cam2", float_scale=True)),
@@ -272,7 +275,19 @@ def test_cli_matches_oracle_pipeline(cli, tmp_path, name):
     for t, r in enumerate(rows):
         assert abs(r["focal_length"][0] - ref["focal"][t]) <= 1e-6 * ref["focal"][t]
         assert np.allclose(r["optical_center"], ref["center"][t], rtol=1e-6)
-        assert np.allclose(r["distortion_coeffs"], ref["dist"][t], rtol=1e-6, atol=1e-8)
+        got_d, want_d = np.array(r["distortion_coeffs"]), np.asarray(ref["dist"][t])
+        if got_d.size > 5:
+            # RPC: compare both halves as models on the image (coefficients of
+            # high-degree terms are poorly determined individually; the image
+            # corners are barely observed in this small rig): 1e-5 of the half size
+            from oracle.rpc_fit_reference import compute_rpc
+
+            g = np.stack(np.meshgrid(np.linspace(-500, 500, 21), np.linspace(-380, 380, 17)), -1).reshape(-1, 2)
+            h = got_d.size // 2
+            for a, b in ((got_d[:h], want_d[:h]), (got_d[h:], want_d[h:])):
+                assert np.abs(compute_rpc(g, a) - compute_rpc(g, b)).max() < 1e-5 * 512
+        else:
+            assert np.allclose(got_d, want_d, rtol=1e-6, atol=1e-8)
         if not flags.get("no_rig"):
             from oracle.rig_calibrator_ref import _array_to_rigid
 
