@@ -255,7 +255,8 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
                                                  const double* __restrict__ frec, const double* __restrict__ params,
                                                  const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
                                                  const double* __restrict__ du, double* __restrict__ yrep, int64_t ng,
-                                                 int32_t flags, double cauchy_c) {
+                                                 int32_t flags, double cauchy_c, const int32_t* __restrict__ gate) {
+  if (gate && *gate) return;
   constexpr int NA = 6 + 12 + 1;
   const int seg = blockIdx.x;
   const Segment sg = segs[seg];
@@ -388,10 +389,10 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
-                                double cauchy_c, hipStream_t s) {
+                                double cauchy_c, const int32_t* gate, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params, pts,
-                     (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c);
+                     (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c, gate);
   return hipGetLastError();
 }
 

@@ -323,7 +323,7 @@ struct FrameLin {
 
 // Last-block finalisation of a grid reduction: every block stores its partial,
 // the last block to arrive sums them into out[0] and re-arms the counter.
-__device__ __forceinline__ void grid_sum_finalize(double v, double* __restrict__ partial,
+__device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__ partial,
                                                   unsigned* __restrict__ counter, double* __restrict__ out) {
   __shared__ double red[256];
   __shared__ bool last;
@@ -339,7 +339,7 @@ __device__ __forceinline__ void grid_sum_finalize(double v, double* __restrict__
     last = (atomicAdd(counter, 1u) == gridDim.x - 1);
   }
   __syncthreads();
-  if (!last) return;
+  if (!last) return false;
   __threadfence();
   double acc = 0.0;
   for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x) acc += __builtin_nontemporal_load(&partial[e]);
@@ -353,6 +353,49 @@ __device__ __forceinline__ void grid_sum_finalize(double v, double* __restrict__
     out[0] = red[0];
     *counter = 0u;
   }
+  return true;
+}
+
+// Three sums in one last-block finalisation (block partials interleaved as
+// partial[3 b + k]); the last block also returns the sums in res[0..2].
+__device__ __forceinline__ bool grid_sum3_finalize(double a, double b, double c, double* __restrict__ partial,
+                                                   unsigned* __restrict__ counter, double* __restrict__ out,
+                                                   double* res) {
+  __shared__ double red[3][256];
+  __shared__ bool last;
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  red[2][threadIdx.x] = c;
+  __syncthreads();
+  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2)
+      for (int k = 0; k < 3; k++) red[k][threadIdx.x] += red[k][threadIdx.x + s2];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 3; k++) partial[3 * blockIdx.x + k] = red[k][0];
+    __threadfence();
+    last = (atomicAdd(counter, 1u) == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!last) return false;
+  __threadfence();
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x)
+    for (int k = 0; k < 3; k++) acc[k] += __builtin_nontemporal_load(&partial[3 * e + k]);
+  for (int k = 0; k < 3; k++) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
+    if ((int)threadIdx.x < s2)
+      for (int k = 0; k < 3; k++) red[k][threadIdx.x] += red[k][threadIdx.x + s2];
+    __syncthreads();
+  }
+  for (int k = 0; k < 3; k++) res[k] = red[k][0];
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 3; k++) out[k] = red[k][0];
+    *counter = 0u;
+  }
+  return true;
 }
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));

@@ -29,30 +29,37 @@ int mvba_solver_dir_stride(void);
 int mvba_solver_vec_replicas(void);
 int64_t mvba_pass_a_blocks(int64_t npts);
 hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const FrameDesc* fd, const double* frec,
-                                 const double* x, double* dir, hipStream_t s);
+                                 const double* x, double* dir, const int32_t* gate, hipStream_t s);
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
                               const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
                               double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
-                              mvba::PointExtra dc, const double* xcam, double* du, hipStream_t s);
+                              mvba::PointExtra dc, const double* xcam, double* du, const int32_t* gate,
+                              const double* prec, hipStream_t s);
+hipError_t mvba_launch_frame_proj(int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
+                                  const double* params, double* prec, hipStream_t s);
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
-                                double cauchy_c, hipStream_t s);
+                                double cauchy_c, const int32_t* gate, hipStream_t s);
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
                               const Segment* segs, const FrameDesc* fd, const void* fl, const double* frec,
                               const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* yrep,
-                              int64_t ng, int32_t flags, double cauchy_c, hipStream_t s);
+                              int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
-                                      double* partial, unsigned* counter, double* dot_out, hipStream_t s);
+                                      double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
+                                      mvba::CgCtl* ctl, hipStream_t s);
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
                                 unsigned* counter, double* dot_out, hipStream_t s);
 hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* goff, const int64_t* hoff,
                                  const int32_t* bsize, const double* minv, int32_t mode, double alpha, const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
-                                 double* z, double* partial, unsigned* counters, double* out, hipStream_t s);
+                                 double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
+                                 int32_t iter, hipStream_t s);
+hipError_t mvba_launch_cg_p(int64_t n, const mvba::CgCtl* ctl, int32_t first, double beta, const double* z, double* p,
+                            hipStream_t s);
 hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
                              hipStream_t s);
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, double* out,
@@ -108,6 +115,9 @@ struct SolverState {
   double* scal = nullptr;     // [32] device scalars
   unsigned* cnt = nullptr;    // [8] grid-reduction counters (kept zero between kernels)
   double* hscal = nullptr;    // [32] pinned host mirror
+  mvba::CgCtl* ctl = nullptr; // device CG control (single-rank solves)
+  double* prec = nullptr;     // [nframes * kProjDoubles] projection records
+  mvba::CgCtl* hctl = nullptr; // pinned host mirror
   int64_t npartial = 0;
   int32_t* bsize = nullptr;
   int32_t* emap = nullptr;    // camera entry -> camera block
@@ -119,10 +129,11 @@ void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
                   S->hi, S->b, S->r, S->r2, S->z, S->p, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->ubuf, S->du,
-                  S->cnt, S->partial, S->scal, S->bsize, S->emap, S->goff, S->hoff, S->cam_poff};
+                  S->cnt, S->partial, S->scal, S->bsize, S->emap, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (S->hscal) (void)hipHostFree(S->hscal);
+  if (S->hctl) (void)hipHostFree(S->hctl);
   delete S;
 }
 
@@ -168,6 +179,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->yrep, nrep));
     HCHK(hipMemset(S->yrep, 0, nrep * sizeof(double)));
     HCHK(dalloc(&S->dir, (size_t)(h->nframes * mvba_solver_dir_stride())));
+    HCHK(dalloc(&S->prec, (size_t)(h->nframes * mvba::kProjDoubles)));
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
     HCHK(dalloc(&S->ubuf, (size_t)(2 * N)));
     HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
@@ -180,6 +192,8 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->partial, (size_t)S->npartial));
     HCHK(dalloc(&S->scal, 32));
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hscal), 32 * sizeof(double)));
+    HCHK(hipMalloc(reinterpret_cast<void**>(&S->ctl), sizeof(mvba::CgCtl)));
+    HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hctl), sizeof(mvba::CgCtl)));
     std::vector<int32_t> bs(S->nblocks);
     for (int32_t k = 0; k < S->nblocks; k++) {
       const int32_t bid = h->cam_block_ids[k];
@@ -311,40 +325,47 @@ class Solver {
   // pass B over every model group into the replicas, then y = sum of replicas.
   // Single rank: damping and the x.y dot are fused into the replica reduction
   // (dot -> scal[dot_slot]); sharded: cross-rank sum of y first.
-  void reduce_frames(double* y, const double* xv, int dot_slot) {
+  // gate: device CG stop flag (nullptr: always run); ctl: CG step-length logic
+  // in the finalising block of the x.y reduction (single rank only)
+  void reduce_frames(double* y, const double* xv, int dot_slot, const int32_t* gate = nullptr,
+                     mvba::CgCtl* ctl = nullptr) {
     for (const Group& G : h_->groups)
       HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
                               h_->d_segs, h_->d_fd, h_->d_frame_lin, h_->d_frec, h_->d_params, h_->d_pts,
                               h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, S_->ubuf, S_->yrep, S_->ng, flags_,
-                              cauchy_c_, s_));
+                              cauchy_c_, gate, s_));
     if (h_->ndep > 0)
       HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
                                 h_->d_params, h_->d_pts, h_->d_frame_lin, S_->du, S_->yrep, S_->ng, flags_, cauchy_c_,
-                                s_));
+                                gate, s_));
     const bool fuse = xv && !o_.allreduce;
     HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr, y, S_->partial,
-                                    S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, s_));
+                                    S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate, fuse ? ctl : nullptr,
+                                    s_));
     exchange(y, S_->ng, MVBA_REDUCE_SUM);
     if (xv && !fuse)
       HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, s_));
   }
 
   // y = S x (implicit Schur complement with damping); x.y -> scal[dot_slot]
-  void apply_schur(const double* xv, double* y, int dot_slot) {
-    HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, s_));
+  void apply_schur(const double* xv, double* y, int dot_slot, const int32_t* gate = nullptr,
+                   mvba::CgCtl* ctl = nullptr) {
+    HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, gate, s_));
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, nullptr, S_->phess, S_->dmp + S_->ng,
                             S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_, cauchy_c_,
-                            h_->point_extra(), xv, S_->du, s_));
-    reduce_frames(y, xv, dot_slot);
+                            h_->point_extra(), xv, S_->du, gate, S_->prec, s_));
+    reduce_frames(y, xv, dot_slot, gate, ctl);
   }
 
-  // b = -(g_c - W (V+D)^-1 g_p)
+  // b = -(g_c - W (V+D)^-1 g_p). Starts every linear solve: the projection
+  // records for pass A are built here (parameters fixed until the next step).
   void schur_rhs() {
+    HCHK(mvba_launch_frame_proj((int32_t)h_->nframes, h_->d_fd, h_->d_frec, h_->d_params, S_->prec, s_));
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, nullptr, S_->G + S_->ng, S_->phess,
                             S_->dmp + S_->ng, S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_,
-                            cauchy_c_, h_->point_extra(), nullptr, S_->du, s_));
+                            cauchy_c_, h_->point_extra(), nullptr, S_->du, nullptr, S_->prec, s_));
     reduce_frames(S_->tmp, nullptr, 0);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
   }
@@ -368,7 +389,7 @@ class Solver {
     // r is double-buffered: each update reads S_->r and writes S_->r2, then they swap
     auto upd = [&](int32_t mode, double alpha, const double* q) {
       HCHK(mvba_launch_cg_update(n, S_->emap, S_->goff, S_->hoff, S_->bsize, S_->fac, mode, alpha, S_->p, q, S_->b, xv,
-                                 S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, s_));
+                                 S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, nullptr, 0, s_));
       std::swap(S_->r, S_->r2);
     };
     // r = b (x = 0); z = M^-1 r; rho = r'z. Q0 = -x'(b + r) = 0
@@ -385,14 +406,14 @@ class Solver {
         break;
       }
       if (i == 1) {
-        HCHK(hipMemcpyAsync(S_->p, S_->z, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s_));
+        HCHK(mvba_launch_cg_p(n, nullptr, 1, 0.0, S_->z, S_->p, s_));
       } else {
         const double beta = rho / last_rho;
         if (bad(beta)) {
           R.status = 2;
           break;
         }
-        HCHK(mvba_launch_axpby(n, 1.0, S_->z, beta, S_->p, S_->p, s_));
+        HCHK(mvba_launch_cg_p(n, nullptr, 0, beta, S_->z, S_->p, s_));
       }
       apply_schur(S_->p, S_->q, 0);
       const double pq = fetch(1)[0];
@@ -426,15 +447,65 @@ class Solver {
     return R;
   }
 
+  // The same PCG with every scalar step on the device (CgCtl): iterations are
+  // enqueued in batches and gated by ctl->done, one host read per batch
+  // instead of two per iteration. Single rank only (the all-reduce callback
+  // needs the host between kernels).
+  CgResult cg_device() {
+    CgResult R;
+    const int64_t n = S_->ng;
+    double* xv = S_->delta;
+    HCHK(hipMemsetAsync(xv, 0, (size_t)std::max<int64_t>(n, 1) * sizeof(double), s_));
+    if (n == 0) return R;
+    dot(n, S_->b, S_->b, 0);
+    const double norm_b = std::sqrt(fetch(1)[0]);
+    if (norm_b == 0.0) return R;
+    mvba::CgCtl c{};
+    c.eta = o_.eta;
+    c.min_iter = o_.min_linear_solver_iterations;
+    c.max_iter = o_.max_linear_solver_iterations;
+    *S_->hctl = c;
+    HCHK(hipMemcpyAsync(S_->ctl, S_->hctl, sizeof(mvba::CgCtl), hipMemcpyHostToDevice, s_));
+    const int32_t* gate = &S_->ctl->done;
+    auto upd = [&](int32_t mode, const double* q, int32_t iter, bool end_logic) {
+      HCHK(mvba_launch_cg_update(n, S_->emap, S_->goff, S_->hoff, S_->bsize, S_->fac, mode, 0.0, S_->p, q, S_->b, xv,
+                                 S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl,
+                                 end_logic ? iter : -1, s_));
+      std::swap(S_->r, S_->r2);
+    };
+    upd(4 | 8, nullptr, 0, true);  // r = b, z = M^-1 r, rho
+    int i = 1;
+    for (int batch = 4;; batch = 8) {
+      for (int k = 0; k < batch && i <= std::max(o_.max_linear_solver_iterations, 1); k++, i++) {
+        HCHK(mvba_launch_cg_p(n, S_->ctl, 0, 0.0, S_->z, S_->p, s_));
+        apply_schur(S_->p, S_->q, 0, gate, S_->ctl);
+        if (i % 10 == 0) {  // residual reset: r = b - A x
+          upd(1, S_->q, i, false);
+          apply_schur(xv, S_->tmp, 1, gate, nullptr);
+          upd(4 | 8, S_->tmp, i, true);
+        } else {
+          upd(1 | 2 | 8, S_->q, i, true);
+        }
+      }
+      HCHK(hipMemcpyAsync(S_->hctl, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
+      HCHK(hipStreamSynchronize(s_));
+      if (S_->hctl->done) break;
+      if (i > std::max(o_.max_linear_solver_iterations, 1)) break;  // not reached: the device stops at max_iter
+    }
+    R.iters = S_->hctl->iters;
+    R.status = S_->hctl->status;
+    return R;
+  }
+
   // delta_p = -(V+D)^-1 (g_p + W' delta_c); returns model cost change -(g'delta + |J delta|^2 / 2)
   double back_substitute() {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
-                               s_));
+                               nullptr, s_));
     // |J delta|^2 over the local reprojection and depth blocks -> scal[0]
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
                             S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial, S_->cnt + 5,
-                            S_->scal + 0, flags_, cauchy_c_, h_->point_extra(), S_->delta, S_->du, s_));
+                            S_->scal + 0, flags_, cauchy_c_, h_->point_extra(), S_->delta, S_->du, nullptr, S_->prec, s_));
     HCHK(mvba_launch_axpby(3 * S_->np, -1.0, S_->delta + S_->ng, 0.0, nullptr, S_->delta + S_->ng, s_));
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);
@@ -751,7 +822,7 @@ void Solver::run(mvba_solver_summary* sum) {
     HCHK(mvba_launch_block_prec(S_->nblocks, S_->max_bsize, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->dmp,
                                 S_->fac, s_));
     schur_rhs();
-    const CgResult cgr = cg();
+    const CgResult cgr = o_.allreduce ? cg() : cg_device();
     sum->num_linear_iterations += cgr.iters;
     bool valid = cgr.status != 2;
     double mcc = 0.0;

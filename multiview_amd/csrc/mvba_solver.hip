@@ -70,7 +70,9 @@ struct RowShape {
 __global__ void __launch_bounds__(64) k_frame_dir(const FrameLin* __restrict__ fl, int32_t nframes,
                                                   const FrameDesc* __restrict__ fd,
                                                   const double* __restrict__ frec,
-                                                  const double* __restrict__ x, double* __restrict__ dir) {
+                                                  const double* __restrict__ x, double* __restrict__ dir,
+                                                  const int32_t* __restrict__ gate) {
+  if (gate && *gate) return;
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= nframes) return;
   const FrameLin L = fl[f];
@@ -120,55 +122,98 @@ __device__ __forceinline__ void solve3(const double* V, const double* dp, const 
   w[2] = (C * t[0] + E * t[1] + Fv * t[2]) * id;
 }
 
+// z_o = J_cam,o x and the point rows P = G R, with the camera-side columns
+// folded into z as they are produced (never held as a row pair): the pose part
+// (Xc x G_i).d + G_i.d' = G_i.(d x Xc + d'), then focal, centre and distortion
+// columns times their direction entries. Keeps pass A's register footprint to
+// the projection itself.
 template <int MODEL, int DEG>
-__device__ __forceinline__ void pass_a_obs(const FrameDesc& F, const double* __restrict__ rec,
-                                           const double* __restrict__ params, const double* dirf,
+__device__ __forceinline__ void pass_a_obs(const double* __restrict__ rec, const double* dirf,
                                            double4 X, double2 m, int32_t flags, double cauchy_c,
                                            double* z, double* P0, double* P1) {
-  using RS = RowShape<MODEL, DEG>;
-  double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], r[2], hr;
+  const double f = rec[12];
+  const int K = (int)rec[17];
+  Proj o;
+  project<MODEL, DEG>(rec, X.x, X.y, X.z, f, rec[13], rec[14], rec + 18, K, rec[15], rec[16], o);
+  double hr;
+  const double sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
+  const double fz = f / o.Xc[2] * sr;
+  const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+  const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
 #pragma unroll
-  for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;
-  obs_rows<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, Z0, Z1, I0, I1, P0, P1, r, &hr);
-  z[0] = z[1] = 0.0;
-  if (dirf) {
-#pragma unroll
-    for (int a = 0; a < 6; a++) {
-      z[0] += Z0[a] * dirf[a];
-      z[1] += Z1[a] * dirf[a];
-    }
-#pragma unroll
-    for (int q = 0; q < RS::kIntr; q++) {
-      z[0] += I0[q] * dirf[6 + q];
-      z[1] += I1[q] * dirf[6 + q];
-    }
+  for (int q = 0; q < 3; q++) {
+    P0[q] = G0[0] * rec[q] + G0[1] * rec[3 + q] + G0[2] * rec[6 + q];
+    P1[q] = G1[0] * rec[q] + G1[1] * rec[3 + q] + G1[2] * rec[6 + q];
   }
+  z[0] = z[1] = 0.0;
+  if (!dirf) return;
+  double v[3];
+  cross(dirf, o.Xc, v);
+#pragma unroll
+  for (int q = 0; q < 3; q++) v[q] += dirf[3 + q];
+  double z0 = G0[0] * v[0] + G0[1] * v[1] + G0[2] * v[2];
+  double z1 = G1[0] * v[0] + G1[1] * v[1] + G1[2] * v[2];
+  z0 += o.df0 * sr * dirf[6];
+  z1 += o.df1 * sr * dirf[6];
+  if constexpr (MODEL != kModelRpc) {  // centre columns (RPC: structurally zero)
+    z0 += sr * dirf[7];
+    z1 += sr * dirf[8];
+  }
+  dist_columns<MODEL, DEG>(o, f, K, sr, [&](int q, double a0, double a1) {
+    z0 += a0 * dirf[9 + q];
+    z1 += a1 * dirf[9 + q];
+  });
+  z[0] = z0;
+  z[1] = z1;
 }
 
 // kLanesA lanes per point; each lane keeps its first kCacheA observations' rows
 // (z_o and the two J_pt rows: 8 doubles) in registers, later ones go through zbuf.
-constexpr int kLanesA = 8;
-constexpr int kCacheA = 2;
+constexpr int kLanesA = 4;
+constexpr int kCacheA = 3;
 
 template <int MODEL, int DEG>
-__device__ __forceinline__ void pass_a_dispatch(const FrameDesc& F, const double* __restrict__ rec,
-                                                const double* __restrict__ params, const double* dirf, double4 X,
+__device__ __forceinline__ void pass_a_dispatch(const double* __restrict__ rec, const double* dirf, double4 X,
                                                 double2 m, int32_t flags, double cauchy_c, double* z, double* P0,
                                                 double* P1) {
   if constexpr (MODEL >= 0) {
-    pass_a_obs<MODEL, DEG>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    pass_a_obs<MODEL, DEG>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
   } else {
-    const int K = F.K;
-    if (K == 0) pass_a_obs<kModelNone, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-    else if (K == 1) pass_a_obs<kModelFov, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-    else if (K == 4 || K == 5) pass_a_obs<kModelRadtan, 0>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-    else if (K == 20) pass_a_obs<kModelRpc, 1>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-    else if (K == 44) pass_a_obs<kModelRpc, 2>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
-    else pass_a_obs<kModelRpc, 3>(F, rec, params, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    const int K = (int)rec[17];
+    if (K == 0) pass_a_obs<kModelNone, 0>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 1) pass_a_obs<kModelFov, 0>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 4 || K == 5) pass_a_obs<kModelRadtan, 0>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 20) pass_a_obs<kModelRpc, 1>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 44) pass_a_obs<kModelRpc, 2>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else pass_a_obs<kModelRpc, 3>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
   }
 }
 
-template <int MODEL, int DEG>
+// Projection records (kProjDoubles per frame) from the frame records and the
+// current parameters; one thread per (frame, slot).
+__global__ void __launch_bounds__(256) k_frame_proj(int32_t nframes, const FrameDesc* __restrict__ fd,
+                                                    const double* __restrict__ frec,
+                                                    const double* __restrict__ params, double* __restrict__ prec) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t f = t / kProjDoubles;
+  const int q = (int)(t % kProjDoubles);
+  if (f >= nframes) return;
+  const FrameDesc& F = fd[f];
+  double v = 0.0;
+  if (q < 12) v = frec[f * kFrameRecDoubles + q];
+  else if (q == 12) v = params[F.off[MVBA_BLK_FOCAL]];
+  else if (q == 13) v = params[F.off[MVBA_BLK_CENTER]];
+  else if (q == 14) v = params[F.off[MVBA_BLK_CENTER] + 1];
+  else if (q == 15) v = F.h0;
+  else if (q == 16) v = F.h1;
+  else if (q == 17) v = (double)F.K;
+  else if (q - 18 < F.K) v = params[F.off[MVBA_BLK_DIST] + (q - 18)];
+  prec[t] = v;
+}
+
+// DEPTH: the problem has BracketedDepthError blocks (their code path is heavy;
+// compiled out of the reprojection-only variant to keep its registers down).
+template <int MODEL, int DEG, bool DEPTH>
 __global__ void __launch_bounds__(256) k_pass_a(
     const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
@@ -177,7 +222,9 @@ __global__ void __launch_bounds__(256) k_pass_a(
     const double* __restrict__ tinit, const double* __restrict__ V,
     const double* __restrict__ dp, double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
     double* __restrict__ sq_partial, unsigned* __restrict__ counter, double* __restrict__ sq_out,
-    int32_t flags, double cauchy_c, PointExtra dc, const double* __restrict__ xcam, double* __restrict__ du) {
+    int32_t flags, double cauchy_c, PointExtra dc, const double* __restrict__ xcam, double* __restrict__ du,
+    const int32_t* __restrict__ gate, const double* __restrict__ prec) {
+  if (gate && *gate) return;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = t / kLanesA;
   const int sub = (int)(t % kLanesA);
@@ -194,9 +241,8 @@ __global__ void __launch_bounds__(256) k_pass_a(
     for (int64_t j = jb + sub; j < je; j += kLanesA, k++) {
       const int32_t fr = po_frame[j];
       double z[2], P0[3], P1[3];
-      pass_a_dispatch<MODEL, DEG>(fd[fr], frec + (int64_t)fr * kFrameRecDoubles, params,
-                                  dir ? dir + (int64_t)fr * kDirStride : nullptr, X, po_meas[j], flags, cauchy_c,
-                                  z, P0, P1);
+      pass_a_dispatch<MODEL, DEG>(prec + (int64_t)fr * kProjDoubles, dir ? dir + (int64_t)fr * kDirStride : nullptr,
+                                  X, po_meas[j], flags, cauchy_c, z, P0, P1);
 #pragma unroll
       for (int q = 0; q < 3; q++) tv[q] += P0[q] * z[0] + P1[q] * z[1];
       const double row[8] = {z[0], z[1], P0[0], P0[1], P0[2], P1[0], P1[1], P1[2]};
@@ -218,7 +264,7 @@ __global__ void __launch_bounds__(256) k_pass_a(
   const double4* dmeas = reinterpret_cast<const double4*>(dc.meas);
   int64_t db = 0, de = 0;
   double dP0 = 0.0;
-  if (dc.begin && valid) {
+  if (DEPTH && dc.begin && valid) {
     // BracketedDepthError blocks: z_d = J_cam,d x, t_p += P z_d (J_pt = P I);
     // z_d parked in du until w_p is known
     db = dc.begin[p];
@@ -275,7 +321,7 @@ __global__ void __launch_bounds__(256) k_pass_a(
       sq += u0 * u0 + u1 * u1;
     }
   }
-  if (valid && de > db) {
+  if (DEPTH && valid && de > db) {
     // u_d = z_d - P w_p  (P = weight * sr depends only on the residual: recompute)
     for (int64_t j = db + sub; j < de; j += kLanesA) {
       const int32_t sl = dc.slot[j];
@@ -319,12 +365,13 @@ __global__ void __launch_bounds__(64) k_pass_b(
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
     const double2* __restrict__ obs_meas, const int32_t* __restrict__ slot_po,
-    const double* __restrict__ ubuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c) {
+    const double* __restrict__ ubuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c,
+    const int32_t* __restrict__ gate) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   const int lane = threadIdx.x;
   const int ch = blockIdx.x;
-  if (ch >= nchunks) return;
+  if (ch >= nchunks || (gate && *gate)) return;
   const int4 c = chunks[ch];
   const int frame = __builtin_amdgcn_readfirstlane(c.z);
   const FrameDesc& F = fd[frame];
@@ -392,7 +439,9 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
                                                         const double* __restrict__ diag,
                                                         const double* __restrict__ x, double* __restrict__ y,
                                                         double* __restrict__ partial, unsigned* __restrict__ counter,
-                                                        double* __restrict__ dot_out) {
+                                                        double* __restrict__ dot_out, const int32_t* __restrict__ gate,
+                                                        CgCtl* __restrict__ ctl) {
+  if (gate && *gate) return;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double d = 0.0;
   if (e < n) {
@@ -406,7 +455,38 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
     y[e] = acc;
     d = x ? x[e] * acc : 0.0;
   }
-  if (dot_out) grid_sum_finalize(d, partial, counter, dot_out);
+  if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0) {
+    // CG step length (conjugate_gradients_solver.cc [ext]): pq <= 0 -> "Matrix
+    // is indefinite" (NO_CONVERGENCE, x kept); alpha = rho / pq, inf -> failure
+    const double pq = dot_out[0];
+    ctl->first = 0;
+    if (pq <= 0.0 || isinf(pq) || isnan(pq)) {
+      ctl->status = 1;
+      ctl->done = 1;
+    } else {
+      const double alpha = ctl->rho / pq;
+      ctl->alpha = alpha;
+      if (isinf(alpha)) {
+        ctl->status = 2;
+        ctl->done = 1;
+      }
+    }
+  }
+}
+
+// p = z (first iteration) or z + beta p; with ctl, gated by the CG control and
+// first/beta taken from it (both CG drivers use this kernel, so their
+// arithmetic is identical).
+__global__ void __launch_bounds__(256) k_cg_p(int64_t n, const CgCtl* __restrict__ ctl, int32_t first, double beta,
+                                              const double* __restrict__ z, double* __restrict__ p) {
+  if (ctl) {
+    if (ctl->done) return;
+    first = ctl->first;
+    beta = ctl->beta;
+  }
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  p[e] = first ? z[e] : z[e] + beta * p[e];
 }
 
 // y += diag .* x; dot_out = x.y (after a cross-rank sum of y)
@@ -436,7 +516,11 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const int32_t* __r
                                                    double* __restrict__ x, const double* __restrict__ r_in,
                                                    double* __restrict__ r_out, double* __restrict__ z,
                                                    double* __restrict__ partial, unsigned* __restrict__ counters,
-                                                   double* __restrict__ out) {
+                                                   double* __restrict__ out, CgCtl* __restrict__ ctl, int32_t iter) {
+  if (ctl) {
+    if (ctl->done) return;
+    alpha = ctl->alpha;
+  }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double xb = 0.0, xr = 0.0, rz = 0.0;
   if (i < n) {
@@ -467,9 +551,53 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const int32_t* __r
     }
   }
   if (mode & 8) {
-    grid_sum_finalize(xb, partial, counters + 0, out + 0);
-    grid_sum_finalize(xr, partial + 1024, counters + 1, out + 1);
-    grid_sum_finalize(rz, partial + 2048, counters + 2, out + 2);
+    double sums[3];
+    if (grid_sum3_finalize(xb, xr, rz, partial, counters, out, sums) && ctl && threadIdx.x == 0) {
+      const double sxb = sums[0], sxr = sums[1];
+      const double rho_next = sums[2];
+      auto bad = [](double v) { return v == 0.0 || isinf(v) || isnan(v); };
+      if (iter == 0) {  // r = b, z = M^-1 r: initial rho, Q0 = 0
+        ctl->Q0 = 0.0;
+        ctl->first = 1;
+        if (bad(rho_next)) {
+          ctl->status = 2;
+          ctl->iters = 1;
+          ctl->done = 1;
+        }
+        ctl->rho = rho_next;
+        return;
+      }
+      ctl->iters = iter;
+      const double Q1 = -(sxb + sxr);
+      const double zeta = iter * (Q1 - ctl->Q0) / Q1;
+      if (zeta < ctl->eta && iter >= ctl->min_iter) {
+        ctl->status = 0;
+        ctl->done = 1;
+        return;
+      }
+      ctl->Q0 = Q1;
+      if (iter >= ctl->max_iter) {
+        ctl->status = 1;
+        ctl->done = 1;
+        return;
+      }
+      // top of the next iteration: rho, beta
+      const double last_rho = ctl->rho;
+      if (bad(rho_next)) {
+        ctl->status = 2;
+        ctl->iters = iter + 1;
+        ctl->done = 1;
+        return;
+      }
+      const double beta = rho_next / last_rho;
+      ctl->rho = rho_next;
+      ctl->beta = beta;
+      if (bad(beta)) {
+        ctl->status = 2;
+        ctl->iters = iter + 1;
+        ctl->done = 1;
+      }
+    }
   }
 }
 
@@ -742,10 +870,10 @@ int mvba_solver_dir_stride(void) { return mvba::kDirStride; }
 int mvba_solver_vec_replicas(void) { return mvba::kVecReplicas; }
 
 hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
-                                 const double* x, double* dir, hipStream_t s) {
+                                 const double* x, double* dir, const int32_t* gate, hipStream_t s) {
   if (nframes <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_frame_dir, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s,
-                     (const mvba::FrameLin*)fl, nframes, fd, frec, x, dir);
+                     (const mvba::FrameLin*)fl, nframes, fd, frec, x, dir, gate);
   return hipGetLastError();
 }
 
@@ -756,21 +884,42 @@ hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64
                               const double* params, const double4* pts, const double* dir, const double* tinit,
                               const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
                               double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
-                              mvba::PointExtra dc, const double* xcam, double* du, hipStream_t s) {
+                              mvba::PointExtra dc, const double* xcam, double* du, const int32_t* gate,
+                              const double* prec, hipStream_t s) {
   const unsigned blocks = (unsigned)((npts * mvba::kLanesA + 255) / 256);
   if (npts <= 0) return hipSuccess;
+  const bool depth = dc.begin != nullptr;
   if (model < 0) {
-    hipLaunchKernelGGL((mvba::k_pass_a<-1, 0>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, fd,
-                       frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out, flags,
-                       cauchy_c, dc, xcam, du);
+    if (depth)
+      hipLaunchKernelGGL((mvba::k_pass_a<-1, 0, true>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,
+                         po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter,
+                         sq_out, flags, cauchy_c, dc, xcam, du, gate, prec);
+    else
+      hipLaunchKernelGGL((mvba::k_pass_a<-1, 0, false>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,
+                         po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter,
+                         sq_out, flags, cauchy_c, dc, xcam, du, gate, prec);
     return hipGetLastError();
   }
-#define MVBA_PA(M, D)                                                                                      \
-  hipLaunchKernelGGL((mvba::k_pass_a<M, D>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame, po_meas, \
-                     fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, sq_out,  \
-                     flags, cauchy_c, dc, xcam, du)
+#define MVBA_PA(M, D)                                                                                          \
+  if (depth)                                                                                                 \
+    hipLaunchKernelGGL((mvba::k_pass_a<M, D, true>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,   \
+                       po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, \
+                       sq_out, flags, cauchy_c, dc, xcam, du, gate, prec);                                             \
+  else                                                                                                       \
+    hipLaunchKernelGGL((mvba::k_pass_a<M, D, false>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,  \
+                       po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, \
+                       sq_out, flags, cauchy_c, dc, xcam, du, gate, prec)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PA)
 #undef MVBA_PA
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_frame_proj(int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
+                                  const double* params, double* prec, hipStream_t s) {
+  if (nframes <= 0) return hipSuccess;
+  const int64_t n = (int64_t)nframes * mvba::kProjDoubles;
+  hipLaunchKernelGGL(mvba::k_frame_proj, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nframes, fd, frec,
+                     params, prec);
   return hipGetLastError();
 }
 
@@ -780,12 +929,12 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const mvba::Segment* segs, const mvba::FrameDesc* fd, const void* fl,
                               const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* yrep,
-                              int64_t ng, int32_t flags, double cauchy_c, hipStream_t s) {
+                              int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PB(M, D)                                                                                       \
   hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks,        \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
-                     slot_po, ubuf, yrep, ng, flags, cauchy_c)
+                     slot_po, ubuf, yrep, ng, flags, cauchy_c, gate)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)
 #undef MVBA_PB
   return hipGetLastError();
@@ -793,10 +942,11 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
 
 // y = sum of replicas (+ diag .* x, and x.y -> dot_out when dot_out != null)
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
-                                      double* partial, unsigned* counter, double* dot_out, hipStream_t s) {
+                                      double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
+                                      mvba::CgCtl* ctl, hipStream_t s) {
   if (ng <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, diag, x,
-                     y, partial, counter, dot_out);
+                     y, partial, counter, dot_out, gate, ctl);
   return hipGetLastError();
 }
 
@@ -812,12 +962,20 @@ hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, 
 hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* goff, const int64_t* hoff,
                                  const int32_t* bsize, const double* minv, int32_t mode, double alpha, const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
-                                 double* z, double* partial, unsigned* counters, double* out, hipStream_t s) {
+                                 double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
+                                 int32_t iter, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   if (blocks > 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks), dim3(256), 0, s, n, emap, goff, hoff, bsize, minv, mode, alpha,
-                     p, q, b, x, r_in, r_out, z, partial, counters, out);
+                     p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_cg_p(int64_t n, const mvba::CgCtl* ctl, int32_t first, double beta, const double* z, double* p,
+                            hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_cg_p, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, ctl, first, beta, z, p);
   return hipGetLastError();
 }
 

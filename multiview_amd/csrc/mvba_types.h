@@ -26,6 +26,15 @@ struct FrameDesc {
 //        beg tx ty tz qx qy qz qw | end (7) | ref_to_cam (7) | offset (1)):
 //        omega_k (3), v_k (3), with d(Xc)/dp_k = omega_k x Xc + v_k.
 constexpr int kFrameRecDoubles = 144;
+
+// Per-frame projection record for the solver's point-order pass (built once per
+// linear solve, the parameters being fixed during CG), so one observation needs
+// two independent loads (this record and the frame's CG direction) instead of
+// the frame descriptor -> parameter vector chain:
+//   [0..11] R_wc, t_wc | 12 f | 13, 14 optical centre | 15, 16 half size |
+//   17 K (as double) | 18.. live distortion coefficients (<= kProjDist)
+constexpr int kProjDoubles = 64;
+constexpr int kProjDist = kProjDoubles - 18;
 constexpr int kPoseCols = 22;
 
 // A segment = up to 64 consecutive device-order residuals of ONE frame,
@@ -85,6 +94,25 @@ struct PointExtra {
   const int64_t* xbegin;   // [num_points + 1]
   const void* xref;        // double4 [num_xyz] (x, y, z, weight), point order
   const double* xcc;       // [num_xyz] Cauchy c of each prior
+};
+
+// Device-resident control of one preconditioned-CG solve (single-rank solves):
+// the scalar steps of conjugate_gradients_solver.cc [ext] run in the
+// finalising block of the reductions, so the host enqueues iterations in
+// batches without reading scalars back; `done` gates every kernel of the
+// iterations enqueued past the stopping point.
+struct CgCtl {
+  int32_t done;     // 1: stopped (later iterations are no-ops)
+  int32_t status;   // 0 converged, 1 no convergence (x usable), 2 failure
+  int32_t iters;    // CgResult::iters
+  int32_t first;    // next direction update is p = z
+  double rho;       // r.z of the current iteration
+  double beta;      // next direction update p = z + beta p
+  double alpha;     // step of the current iteration
+  double Q0;        // q-criterion state
+  double eta;
+  int32_t min_iter;
+  int32_t max_iter;
 };
 
 }  // namespace mvba

@@ -32,6 +32,33 @@ __global__ void __launch_bounds__(256) k_planes(double* __restrict__ J, long ld,
   }
 }
 
+// Tiled variant: plane p of slot i at J[(i / 64) * planes * 64 + p * 64 + i % 64]
+// (each wave streams one contiguous planes*512-B region).
+__global__ void __launch_bounds__(256) k_tiled(double* __restrict__ J, int planes, long n) {
+  const long wave = (long)(blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const long i = wave * 64 + lane;
+  if (i >= n) return;
+  const double v = (double)(i & 1023);
+  double* dst = J + wave * (long)planes * 64 + lane;
+  for (int p = 0; p < planes; p++) __builtin_nontemporal_store(v + p, dst + (long)p * 64);
+}
+
+float run_tiled(double* J, int planes, long n, int reps) {
+  int blocks = (int)((n + 255) / 256);
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  hipLaunchKernelGGL(k_tiled, dim3(blocks), dim3(256), 0, 0, J, planes, n);
+  CHECK(hipEventRecord(a));
+  for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k_tiled, dim3(blocks), dim3(256), 0, 0, J, planes, n);
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
 template <int E, bool NT>
 float run(double* J, long ld, int planes, long n, int shift, int reps) {
   long waves = (n - shift) / (64 * E);
@@ -57,7 +84,7 @@ int main(int argc, char** argv) {
   double* J;
   CHECK(hipMalloc(&J, sizeof(double) * ld * planes));
   const double bytes = 8.0 * n * planes;
-  struct { const char* name; float ms; } res[8];
+  struct { const char* name; float ms; } res[12];
   int k = 0;
   res[k++] = {"dwordx2 nt   aligned", run<1, true>(J, ld, planes, n, 0, 20)};
   res[k++] = {"dwordx2 plain aligned", run<1, false>(J, ld, planes, n, 0, 20)};
@@ -65,6 +92,20 @@ int main(int argc, char** argv) {
   res[k++] = {"dwordx4 plain aligned", run<2, false>(J, ld, planes, n, 0, 20)};
   res[k++] = {"dwordx2 nt   shift 8B", run<1, true>(J, ld, planes, n, 1, 20)};
   res[k++] = {"dwordx4 nt   shift 16B", run<2, true>(J, ld, planes, n, 2, 20)};
+  res[k++] = {"tiled 64 x planes nt", run_tiled(J, planes, n, 20)};
+  CHECK(hipFree(J));
+  // leading-dimension padding: planes 8 MB apart may share DRAM channels
+  const long pads[5] = {64, 512 + 64, 4096 + 64, 32768 + 192, 1 << 16};
+  std::vector<double*> keep;
+  for (int q = 0; q < 5; q++) {
+    const long ldp = ld + pads[q];
+    double* Jp;
+    CHECK(hipMalloc(&Jp, sizeof(double) * ldp * planes));
+    float ms = run<1, true>(Jp, ldp, planes, n, 0, 20);
+    printf("dwordx2 nt ld+%-8ld    %8.3f ms  %7.1f GB/s\n", pads[q], ms, bytes / (ms * 1e-3) / 1e9);
+    CHECK(hipFree(Jp));
+  }
+  CHECK(hipMalloc(&J, sizeof(double) * ld * planes));
   for (int i = 0; i < k; i++)
     printf("%-24s %8.3f ms  %7.1f GB/s\n", res[i].name, res[i].ms, bytes / (res[i].ms * 1e-3) / 1e9);
   CHECK(hipFree(J));
