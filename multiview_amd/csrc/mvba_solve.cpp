@@ -763,6 +763,31 @@ void Solver::run(mvba_solver_summary* sum) {
     build(o_.upper_bounds, inf, &S_->hi);
   }
 
+  // Nothing to optimize (no residual blocks, or every block constant): Ceres
+  // 1.14 returns CONVERGENCE with the cost evaluated once (solver.cc [ext]).
+  {
+    double nfree = (double)S_->ng;
+    if (nfree == 0.0 && S_->np > 0) {
+      std::vector<uint8_t> pt_free(S_->np);
+      HCHK(hipMemcpy(pt_free.data(), h_->d_pt_free, S_->np, hipMemcpyDeviceToHost));
+      for (uint8_t f : pt_free) nfree += f ? 1.0 : 0.0;
+    }
+    if (o_.allreduce) {
+      HCHK(hipMemcpyAsync(S_->scal, &nfree, sizeof(double), hipMemcpyHostToDevice, s_));
+      exchange(S_->scal, 1, MVBA_REDUCE_MAX);
+      nfree = fetch(1)[0];
+    }
+    if (nfree == 0.0) {
+      const double c = cost();
+      sum->initial_cost = sum->final_cost = c;
+      sum->num_successful_steps = 0;
+      sum->termination_type = MVBA_CONVERGENCE;
+      std::snprintf(sum->message, sizeof(sum->message),
+                    "Function tolerance reached. No non-constant parameter blocks found.");
+      sum->total_time_s = now_s() - t0;
+      return;
+    }
+  }
   HCHK(mvba_launch_gather(S_->ng, S_->cam_poff, S_->np, h_->d_pt_off, h_->d_pt_free, h_->d_params, S_->x, s_));
   double tl = now_s();
   double x_cost = linearize();

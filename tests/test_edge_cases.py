@@ -1,0 +1,158 @@
+"""Edge cases of the boundary: creation-time validation (CPU), empty and
+all-constant problems, single-observation points and frames, the maximum RPC
+degree, and the solver's supported range (GPU).
+
+The reference behaviour these follow: Problem::AddResidualBlock's index and size
+checks (the ABI reports them as MVBA_E_INVALID / MVBA_E_BLOCK_SIZES before the
+device is touched), Ceres 1.14 returning CONVERGENCE with "No non-constant
+parameter blocks found." when nothing floats, and the LM's damped point blocks
+(V_p + D_p) keeping points seen by one camera solvable."""
+import numpy as np
+import pytest
+
+from multiview_amd import _lib, rig
+from multiview_amd.evaluator import Evaluator
+from multiview_amd.problem import CamProblem
+
+
+def _small(models=("radtan", "fov", "none"), seed=3, **kw):
+    R = rig.make_rig(num_sensors=len(models), num_ref=8, num_points=120, obs_per_point=4, models=list(models),
+                     seed=seed)
+    return R, rig.build_problem(R, rig.FloatFlags(**kw))
+
+
+def _status(P):
+    with pytest.raises(_lib.MvbaError) as e:
+        Evaluator(P)
+    return e.value.status, str(e.value)
+
+
+# ---------------------------------------------------------------- CPU
+def test_residual_camera_out_of_range():
+    _, P = _small()
+    P.residual_camera = P.residual_camera.copy()
+    P.residual_camera[3] = 7
+    st, msg = _status(P)
+    assert st == _lib.MVBA_E_INVALID and "camera index out of range" in msg
+
+
+def test_block_index_out_of_range():
+    _, P = _small()
+    P.residual_blocks = P.residual_blocks.copy()
+    P.residual_blocks[5, 3] = len(P.block_size) + 10
+    st, msg = _status(P)
+    assert st == _lib.MVBA_E_INVALID and "block index out of range" in msg
+
+
+def test_block_outside_packed_vector():
+    _, P = _small()
+    P.block_offset = P.block_offset.copy()
+    P.block_offset[-1] = P.params.size  # last block starts past the end
+    st, msg = _status(P)
+    assert st == _lib.MVBA_E_INVALID and "outside the packed vector" in msg
+
+
+def test_wrong_block_size():
+    _, P = _small()
+    P.residual_blocks = P.residual_blocks.copy()
+    P.residual_blocks[0, 3] = P.residual_blocks[0, 0]  # a 7-vector where the 3-vector point belongs
+    st, _ = _status(P)
+    assert st == _lib.MVBA_E_BLOCK_SIZES
+
+
+def _empty_problem():
+    return CamProblem(block_size=np.zeros(0, np.int32), block_offset=np.zeros(0, np.int64),
+                      block_constant=np.zeros(0, np.uint8), params=np.zeros(0),
+                      camera_dist_size=np.zeros(1, np.int32), camera_half_size=np.full((1, 2), 100.0),
+                      residual_blocks=np.zeros((0, 8), np.int32), residual_camera=np.zeros(0, np.int32),
+                      residual_meas=np.zeros((0, 2)), residual_stamps=np.zeros((0, 3)))
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.mark.gpu
+def test_empty_problem():
+    P = _empty_problem()
+    with Evaluator(P) as ev:
+        ev.set_params()
+        cost, r, J = ev.evaluate(jacobian=True)
+        assert cost == 0.0 and r.size == 0
+        s = ev.solve()
+    assert s["termination_type"] == _lib.CONVERGENCE
+    assert "No non-constant parameter blocks" in s["message"]
+    assert s["initial_cost"] == 0.0 == s["final_cost"]
+
+
+@pytest.mark.gpu
+def test_all_constant_problem(oracle):
+    _, P = _small(camera_poses_to_float=(), rig_transforms_to_float=(), intrinsics_to_float=(),
+                  float_timestamp_offsets=False)
+    P.block_constant = np.ones_like(P.block_constant)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(use_loss=1, robust_threshold=3.0)
+        x = ev.get_params()
+    c_o, _, _ = oracle.evaluate(P, oracle.RESIDUAL, apply_loss=True, robust_threshold=3.0)
+    assert s["termination_type"] == _lib.CONVERGENCE and "No non-constant" in s["message"]
+    assert np.isclose(s["final_cost"], c_o, rtol=1e-12)
+    assert np.array_equal(x, P.params)
+
+
+@pytest.mark.gpu
+def test_single_observation_points_and_frames():
+    """Points seen once have a rank-2 block V_p; with LM damping the step is
+    defined and the solve reaches the CPU LM's cost (the points' positions along
+    their rays are a null direction, so only the cost is compared)."""
+    from oracle import lm_reference
+
+    R = rig.make_rig(num_sensors=3, num_ref=8, num_points=150, obs_per_point=2.0, models=["radtan", "fov", "none"],
+                     seed=21)
+    P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=()))
+    # drop every second observation of each point: many points keep a single one
+    keep = np.ones(P.num_residuals, bool)
+    first = np.r_[True, R.obs_pid[1:] != R.obs_pid[:-1]]
+    keep[~first] = np.arange((~first).sum()) % 2 == 0
+    for name in ("residual_blocks", "residual_camera", "residual_meas", "residual_stamps"):
+        setattr(P, name, getattr(P, name)[keep])
+    P.residual_names = None
+    counts = np.bincount(R.obs_pid[keep])
+    assert (counts == 1).sum() > 20
+    TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, **TOL)
+        x = ev.get_params()
+    assert np.isfinite(x).all()
+    assert s["termination_type"] != _lib.FAILURE, s["message"]
+    assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deg", [4, 5, 6])
+def test_high_rpc_degree_evaluation(oracle, deg):
+    """K1 covers RPC degree 1..6 (kMaxRpcDegree): residuals and Jacobian at the
+    maximum degrees against the oracle's exact derivative."""
+    R = rig.make_rig(num_sensors=2, num_ref=6, num_points=60, obs_per_point=3, models=[f"rpc{deg}", "radtan"],
+                     seed=30 + deg)
+    P = rig.build_problem(R)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        cost_g, r_g, J_g = ev.evaluate(jacobian=True)
+    cost_o, r_o, J_o = oracle.evaluate(P, oracle.ANALYTIC)
+    pix = np.maximum(np.abs(P.residual_meas + r_o).max(axis=1), 1.0)
+    assert np.all(np.abs(r_g - r_o) <= 1e-9 * pix[:, None])
+    colmax = np.maximum(np.abs(J_o).max(axis=0), 1e-12)
+    assert (np.abs(J_g - J_o) / colmax).max() <= 1e-9
+
+
+@pytest.mark.gpu
+def test_solver_rejects_rpc_beyond_gram_range():
+    """The normal-equation (MFMA Gram) path covers RPC degree <= 3; the solver
+    says so instead of running."""
+    R = rig.make_rig(num_sensors=2, num_ref=6, num_points=60, obs_per_point=3, models=["rpc4", "radtan"], seed=40)
+    P = rig.build_problem(R)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        with pytest.raises(_lib.MvbaError) as e:
+            ev.solve()
+    assert e.value.status == _lib.MVBA_E_INVALID
