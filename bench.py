@@ -72,11 +72,42 @@ def cpu_baseline(problem, sample: int, min_seconds: float = 10.0):
         dt = time.perf_counter() - t0
         if dt >= min_seconds or passes >= 64:
             break
+    # the oracle's analytic evaluator on the same sample ("also
+    # report the build's analytic CPU evaluator on the same cores"), ~3 s
+    t1 = time.perf_counter()
+    adone = 0
+    while True:
+        oracle_py.evaluate_mt(problem, oracle_py.ANALYTIC, 0, n, threads=CPU_THREADS)
+        adone += n
+        adt = time.perf_counter() - t1
+        if adt >= 3.0 or adone >= 64 * n:
+            break
     return {"value": done / dt, "unit": "evals/s", "cores": CPU_THREADS, "kind": "port",
             "sample": f"{passes} pass(es) over {n} of {problem.num_residuals} residual blocks of the "
                       f"same workload: oracle NUMDIFF = per-block functor + Ceres 1.14 central "
                       f"differences (1 + 2*n_free calls per block), {CPU_THREADS} OpenMP threads, "
-                      f"{dt:.1f} s"}
+                      f"{dt:.1f} s",
+            "analytic_value": adone / adt,
+            "analytic_sample": f"oracle ANALYTIC (exact derivative, dual numbers) over the same {n} blocks, "
+                               f"{CPU_THREADS} threads, {adt:.1f} s"}
+
+
+def _stream_copy_gbs(torch, stream, nbytes=1 << 30, reps=10):
+    """Device-to-device copy of a 1 GiB buffer (read + write bytes / time) on the
+    bench stream, HIP events around `reps` copies: the achievable HBM rate the
+    K1 number is also reported against."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device="cuda").fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
 def _pmc_traffic(config):
@@ -210,6 +241,12 @@ def main():
         },
         "gen_s": t_gen,
     }
+    # achievable HBM bandwidth on this box ("measure achieved peak
+    # with a STREAM-like copy kernel ... and report against both")
+    stream_gbs = _stream_copy_gbs(torch, stream)
+    line["roofline"]["stream_copy_gbs"] = stream_gbs
+    line["roofline"]["frac_of_stream"] = achieved / stream_gbs if stream_gbs else None
+    line["roofline"]["stream_note"] = "1 GiB device-to-device tensor copy (read + write bytes), same stream"
     # ---- depth blocks (c5): K1-depth evaluation, materialised
     if ev.num_depth > 0:
         dld = (ev.num_depth_slots + 63) // 64 * 64

@@ -24,4 +24,6 @@ run prof_c2_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2_$TAG -o ru
 run prof_c5_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c5_$TAG -o run --output-format csv -- python3 bench.py --config c5 --steps 10 --no-cpu-baseline
 run pmc_fetch_$TAG 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --ba-iters 0
 run pmc_write_$TAG 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --ba-iters 0
+# MFMA use of the K2 Gram kernels (fp64 v_mfma_f64_16x16x4f64): busy cycles vs wall
+run pmc_mfma_$TAG 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -d $OUT/pmc_mfma_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --ba-iters 2
 exit 0
