@@ -279,6 +279,54 @@ def main():
             "frac_of_hbm_peak": dbytes / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
         }
 
+    # ---- fp32 evaluation (config c5 is quoted "fp32 eval / fp64 solve"): the same
+    # fp64 arithmetic, outputs rounded to float at the store (half the output bytes)
+    res32 = torch.empty((2, ld), dtype=torch.float32, device="cuda")
+    jac32 = torch.empty((ev.stride, ld), dtype=torch.float32, device="cuda")
+    for _ in range(args.warmup):
+        ev.evaluate_device(True, residuals=res32, jac=jac32, ld=ld, stream=sh, phase=_lib.EVAL_SKIP_PREP)
+    torch.cuda.synchronize()
+    fe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fe[0].record(stream)
+    for _ in range(args.steps):
+        ev.evaluate_device(True, residuals=res32, jac=jac32, ld=ld, stream=sh, phase=_lib.EVAL_SKIP_PREP)
+    fe[1].record(stream)
+    torch.cuda.synchronize()
+    f_ms = fe[0].elapsed_time(fe[1]) / args.steps
+    reads = 44.0 * n  # meas 16 + point index 4 + landmark 24 per observation
+    f32_bytes = reads + (bytes_eval - reads) / 2.0
+    line["eval_f32"] = {
+        "what": "K1 with fp32 outputs (fp64 arithmetic, one rounding at the store)",
+        "evals_per_s": n / (f_ms * 1e-3),
+        "kernel_ms": f_ms,
+        "bytes_per_launch": f32_bytes,
+        "achieved_GBps": f32_bytes / (f_ms * 1e-3) / 1e9,
+    }
+    del res32, jac32
+    if ev.num_depth > 0:
+        dres32 = torch.empty((3, dld), dtype=torch.float32, device="cuda")
+        dJ32 = torch.empty((_lib.DJAC_ROWS, dld), dtype=torch.float32, device="cuda")
+
+        def dstep32():
+            _lib.check(ev.lib.mvba_evaluate_depth_device_f32(
+                ev.h, _lib.EVAL_RESIDUALS | _lib.EVAL_JACOBIAN | _lib.EVAL_SKIP_PREP, 0.0,
+                C.c_void_p(dres32.data_ptr()), C.c_void_p(dJ32.data_ptr()), dld, C.c_void_p(sh)), ev.h)
+
+        for _ in range(args.warmup):
+            dstep32()
+        torch.cuda.synchronize()
+        fe[0].record(stream)
+        for _ in range(args.steps):
+            dstep32()
+        fe[1].record(stream)
+        torch.cuda.synchronize()
+        fd_ms = fe[0].elapsed_time(fe[1]) / args.steps
+        dreads = 56.0 * ev.num_depth
+        line["eval_f32"]["depth_evals_per_s"] = ev.num_depth / (fd_ms * 1e-3)
+        line["eval_f32"]["depth_kernel_ms"] = fd_ms
+        line["eval_f32"]["depth_achieved_GBps"] = (dreads + (dbytes - dreads) / 2.0) / (fd_ms * 1e-3) / 1e9
+        del dres32, dJ32
+
     # ---- phase B: normal equations (K2) + the per-iteration exchange (§8e)
     from multiview_amd.dist import NormalEquationBuffer, check_layouts_agree
 

@@ -239,6 +239,12 @@ mvba_status mvba_evaluate_device(struct mvba_handle* h, int32_t flags, double ca
                                  double* d_residuals, double* d_jacobian, int64_t ld,
                                  void* hip_stream);
 mvba_status mvba_device_buffers(struct mvba_handle* h, mvba_device_view* view);
+/* fp32 output of the same evaluation ("fp32 eval, fp64
+ * solve"): identical fp64 arithmetic, each residual/Jacobian value rounded once
+ * to float at the store, half the output bytes. Caller-owned float planes with
+ * the same layout and ld rules as mvba_evaluate_device. */
+mvba_status mvba_evaluate_device_f32(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                     float* d_residuals, float* d_jacobian, int64_t ld, void* hip_stream);
 /* Host copy of the device order: out[p] = AddResidualBlock index of device
  * slot p, -1 for padding (mvba_num_slots() int64). */
 mvba_status mvba_residual_order(const struct mvba_handle* h, int64_t* out);
@@ -289,6 +295,9 @@ mvba_status mvba_evaluate_depth(struct mvba_handle* h, int32_t flags, double cau
                                 double* residuals, double* jacobian);
 mvba_status mvba_evaluate_depth_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                                        double* d_res, double* d_J, int64_t ld, void* hip_stream);
+/* fp32 output of the depth evaluation (same rules as mvba_evaluate_device_f32). */
+mvba_status mvba_evaluate_depth_device_f32(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                           float* d_res, float* d_J, int64_t ld, void* hip_stream);
 
 /* ---- XYZ priors (XYZError) ---------------------------------------------
  * Host, insertion order: residuals [3n], Jacobian [9n] (row-major 3x3, nullable),

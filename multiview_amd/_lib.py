@@ -224,6 +224,8 @@ SIGNATURES = {
     "mvba_jacobian_stride": (C.c_int32, [C.c_void_p]),
     "mvba_evaluate_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                                        C.c_int64, C.c_void_p]),
+    "mvba_evaluate_device_f32": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
+                                           C.c_int64, C.c_void_p]),
     "mvba_device_buffers": (C.c_int, [C.c_void_p, C.POINTER(DeviceView)]),
     "mvba_sync_status": (C.c_int, [C.c_void_p, C.c_void_p]),
     "mvba_residual_order": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -243,6 +245,8 @@ SIGNATURES = {
     "mvba_evaluate_depth": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_evaluate_depth_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                                              C.c_int64, C.c_void_p]),
+    "mvba_evaluate_depth_device_f32": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
+                                                 C.c_int64, C.c_void_p]),
     "mvba_residual_stats": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_num_xyz_residuals": (C.c_int64, [C.c_void_p]),
     "mvba_triangulate": (C.c_int, [C.POINTER(TracksDesc), C.c_int32, C.c_void_p, C.c_void_p]),

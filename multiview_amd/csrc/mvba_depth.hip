@@ -24,11 +24,13 @@ constexpr int kDJacBase[7] = {MVBA_DJAC_BASE_BEG, MVBA_DJAC_BASE_END, MVBA_DJAC_
 // One lane per depth block, one wave per segment. res[3][ld], J[MVBA_DJAC_ROWS][ld]
 // column planes; constant blocks are not written. flags & APPLY_LOSS applies the
 // corrector in-kernel.
+// OT: double (fp64 output) or float (fp32 output of the same fp64 arithmetic).
+template <class OT>
 __global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ segs, int32_t nseg,
                                                   const DepthDesc* __restrict__ dd, const double4* __restrict__ dmeas,
                                                   const FrameDesc* __restrict__ fd, const double* __restrict__ frec,
                                                   const double* __restrict__ params, const double4* __restrict__ pts,
-                                                  double* __restrict__ res, double* __restrict__ J, int64_t ld,
+                                                  OT* __restrict__ res, OT* __restrict__ J, int64_t ld,
                                                   int32_t flags, double cauchy_c) {
   const int seg = blockIdx.x;
   if (seg >= nseg) return;
@@ -44,7 +46,7 @@ __global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ se
   const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
   if (res) {
 #pragma unroll
-    for (int q = 0; q < 3; q++) __builtin_nontemporal_store(loss ? o.r[q] : o.rr[q], &res[q * ld + i]);
+    for (int q = 0; q < 3; q++) __builtin_nontemporal_store((OT)(loss ? o.r[q] : o.rr[q]), &res[q * ld + i]);
   }
   if (!J) return;
   // raw (uncorrected) Jacobian unless APPLY_LOSS: divide the corrected rows back
@@ -65,7 +67,7 @@ __global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ se
         double v = 0.0;
 #pragma unroll
         for (int a = 0; a < 6; a++) v += o.Z[i3][a] * wk[a];
-        __builtin_nontemporal_store(v * un, &J[(int64_t)(kDJacBase[db] + i3 * ncol + c) * ld + i]);
+        __builtin_nontemporal_store((OT)(v * un), &J[(int64_t)(kDJacBase[db] + i3 * ncol + c) * ld + i]);
       }
     }
   }
@@ -76,19 +78,19 @@ __global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ se
 #pragma unroll
       for (int c = 0; c < 12; c++)
         if (c < n)
-          __builtin_nontemporal_store(o.D[i3][c] * un,
+          __builtin_nontemporal_store((OT)(o.D[i3][c] * un),
                                       &J[(int64_t)(MVBA_DJAC_BASE_DEPTH_TO_IMAGE + i3 * n + c) * ld + i]);
   }
   if (mask & (1 << MVBA_DBLK_SCALE))
 #pragma unroll
     for (int i3 = 0; i3 < 3; i3++)
-      __builtin_nontemporal_store(o.S[i3] * un, &J[(int64_t)(MVBA_DJAC_BASE_SCALE + i3) * ld + i]);
+      __builtin_nontemporal_store((OT)(o.S[i3] * un), &J[(int64_t)(MVBA_DJAC_BASE_SCALE + i3) * ld + i]);
   if (mask & (1 << MVBA_DBLK_XYZ))
 #pragma unroll
     for (int i3 = 0; i3 < 3; i3++)
 #pragma unroll
       for (int c = 0; c < 3; c++)
-        __builtin_nontemporal_store(i3 == c ? o.P * un : 0.0, &J[(int64_t)(MVBA_DJAC_BASE_XYZ + i3 * 3 + c) * ld + i]);
+        __builtin_nontemporal_store((OT)(i3 == c ? o.P * un : 0.0), &J[(int64_t)(MVBA_DJAC_BASE_XYZ + i3 * 3 + c) * ld + i]);
 }
 
 // ------------------------------------------------------------ normal equations
@@ -356,11 +358,15 @@ size_t mvba_depth_desc_size(void) { return sizeof(mvba::DepthDesc); }
 
 hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                  const double4* dmeas, const mvba::FrameDesc* fd, const double* frec,
-                                 const double* params, const double4* pts, double* res, double* J, int64_t ld,
-                                 int32_t flags, double cauchy_c, hipStream_t s) {
+                                 const double* params, const double4* pts, void* res, void* J, int64_t ld,
+                                 int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_depth_obs, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, fd, frec, params,
-                     pts, res, J, ld, flags, cauchy_c);
+  if (out_f32)
+    hipLaunchKernelGGL(mvba::k_depth_obs<float>, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, fd, frec,
+                       params, pts, (float*)res, (float*)J, ld, flags, cauchy_c);
+  else
+    hipLaunchKernelGGL(mvba::k_depth_obs<double>, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, fd,
+                       frec, params, pts, (double*)res, (double*)J, ld, flags, cauchy_c);
   return hipGetLastError();
 }
 

@@ -714,8 +714,23 @@ static mvba_status ensure_outputs(mvba_handle* h) {
   return MVBA_OK;
 }
 
+static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double cauchy_threshold, void* d_res,
+                                        void* d_J, int64_t ld, int32_t out_f32, void* stream);
+
 mvba_status mvba_evaluate_device(mvba_handle* h, int32_t flags, double cauchy_threshold,
                                  double* d_res, double* d_J, int64_t ld, void* stream) {
+  return evaluate_device_impl(h, flags, cauchy_threshold, d_res, d_J, ld, 0, stream);
+}
+
+mvba_status mvba_evaluate_device_f32(mvba_handle* h, int32_t flags, double cauchy_threshold, float* d_res,
+                                     float* d_J, int64_t ld, void* stream) {
+  if (!h) return MVBA_E_INVALID;
+  if (!d_res && !d_J) return h->fail(MVBA_E_INVALID, "fp32 output needs caller-owned buffers");
+  return evaluate_device_impl(h, flags, cauchy_threshold, d_res, d_J, ld, 1, stream);
+}
+
+static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double cauchy_threshold, void* d_res,
+                                        void* d_J, int64_t ld, int32_t out_f32, void* stream) {
   if (!h) return MVBA_E_INVALID;
   if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
   if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
@@ -756,7 +771,7 @@ mvba_status mvba_evaluate_device(mvba_handle* h, int32_t flags, double cauchy_th
     const Group& G = h->groups[g];
     e = mvba_launch_obs(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->d_frec,
                         h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags,
-                        cauchy_c, s);
+                        cauchy_c, out_f32, s);
   }
   if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
   return MVBA_OK;
@@ -951,8 +966,21 @@ mvba_status mvba_depth_order(const mvba_handle* h, int64_t* out) {
   return MVBA_OK;
 }
 
+static mvba_status evaluate_depth_device_impl(mvba_handle* h, int32_t flags, double cauchy_threshold, void* d_res,
+                                              void* d_J, int64_t ld, int32_t out_f32, void* stream);
+
 mvba_status mvba_evaluate_depth_device(mvba_handle* h, int32_t flags, double cauchy_threshold, double* d_res,
                                        double* d_J, int64_t ld, void* stream) {
+  return evaluate_depth_device_impl(h, flags, cauchy_threshold, d_res, d_J, ld, 0, stream);
+}
+
+mvba_status mvba_evaluate_depth_device_f32(mvba_handle* h, int32_t flags, double cauchy_threshold, float* d_res,
+                                           float* d_J, int64_t ld, void* stream) {
+  return evaluate_depth_device_impl(h, flags, cauchy_threshold, d_res, d_J, ld, 1, stream);
+}
+
+static mvba_status evaluate_depth_device_impl(mvba_handle* h, int32_t flags, double cauchy_threshold, void* d_res,
+                                              void* d_J, int64_t ld, int32_t out_f32, void* stream) {
   if (!h) return MVBA_E_INVALID;
   if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
   if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
@@ -979,7 +1007,8 @@ mvba_status mvba_evaluate_depth_device(mvba_handle* h, int32_t flags, double cau
   }
   if (e == hipSuccess && !(flags & MVBA_EVAL_PREP_ONLY))
     e = mvba_launch_depth_obs(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_fd, h->d_frec,
-                              h->d_params, h->d_pts, d_res, d_J, ld, flags & (MVBA_EVAL_APPLY_LOSS), cauchy_c, s);
+                              h->d_params, h->d_pts, d_res, d_J, ld, flags & (MVBA_EVAL_APPLY_LOSS), cauchy_c,
+                              out_f32, s);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth_device launch");
   return MVBA_OK;
 }

@@ -44,7 +44,7 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
 hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
                            const FrameDesc* fd, const double* frec, const double* params,
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
-                           double* res, double* J, int64_t ld, int32_t flags, double cauchy_c,
+                           void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
                            hipStream_t s);
 }
 
@@ -52,8 +52,8 @@ extern "C" {
 size_t mvba_depth_desc_size(void);
 hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                  const double4* dmeas, const mvba::FrameDesc* fd, const double* frec,
-                                 const double* params, const double4* pts, double* res, double* J, int64_t ld,
-                                 int32_t flags, double cauchy_c, hipStream_t s);
+                                 const double* params, const double4* pts, void* res, void* J, int64_t ld,
+                                 int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s);
 hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,

@@ -188,16 +188,19 @@ __global__ void __launch_bounds__(kPrepBlock) k_prep(const FrameDesc* __restrict
 }
 
 // ------------------------------------------------------------ K1: observations
-__device__ __forceinline__ void stj(double* J, int64_t ld, int row, int64_t i, double v) {
-  __builtin_nontemporal_store(v, J + (int64_t)row * ld + i);
+// OT = double (fp64 output) or float (fp32 output: the same fp64 arithmetic,
+// each value rounded once at the store; half the output bytes).
+template <class OT>
+__device__ __forceinline__ void stj(OT* J, int64_t ld, int row, int64_t i, double v) {
+  __builtin_nontemporal_store((OT)v, J + (int64_t)row * ld + i);
 }
 
-template <int MODEL, int DEG>
+template <int MODEL, int DEG, class OT>
 __global__ void __launch_bounds__(256) k_obs(
     const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
-    const double2* __restrict__ obs_meas, double* __restrict__ res, double* __restrict__ J,
+    const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
     int64_t ld, int32_t flags, double cauchy_c) {
   const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
@@ -230,8 +233,8 @@ __global__ void __launch_bounds__(256) k_obs(
   r0 *= sr;
   r1 *= sr;
   if (res) {
-    __builtin_nontemporal_store(r0, res + i);
-    __builtin_nontemporal_store(r1, res + ld + i);
+    __builtin_nontemporal_store((OT)r0, res + i);
+    __builtin_nontemporal_store((OT)r1, res + ld + i);
   }
   if (!(flags & MVBA_EVAL_JACOBIAN)) return;
 
@@ -702,13 +705,17 @@ hipError_t mvba_launch_prep(const mvba::FrameDesc* fd, int64_t nframes, const do
 hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_t nseg,
                            const mvba::FrameDesc* fd, const double* frec, const double* params,
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
-                           double* res, double* J, int64_t ld, int32_t flags, double cauchy_c,
+                           void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
                            hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((nseg + 3) / 4);
-#define MVBA_OBS(M, D)                                                                          \
-  hipLaunchKernelGGL((mvba::k_obs<M, D>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec, \
-                     params, pts, obs_pid, obs_meas, res, J, ld, flags, cauchy_c)
+#define MVBA_OBS(M, D)                                                                                     \
+  if (out_f32)                                                                                           \
+    hipLaunchKernelGGL((mvba::k_obs<M, D, float>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec,    \
+                       params, pts, obs_pid, obs_meas, (float*)res, (float*)J, ld, flags, cauchy_c);       \
+  else                                                                                                   \
+    hipLaunchKernelGGL((mvba::k_obs<M, D, double>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec,   \
+                       params, pts, obs_pid, obs_meas, (double*)res, (double*)J, ld, flags, cauchy_c)
   MVBA_SWITCH_MODEL(model, deg, MVBA_OBS)
 #undef MVBA_OBS
   return hipGetLastError();

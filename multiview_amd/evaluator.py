@@ -97,13 +97,15 @@ class Evaluator:
                         robust_threshold: float = 3.0, residuals=None, jac=None, ld: int = 0,
                         stream=None, phase: int = 0):
         """Asynchronous device evaluation. residuals/jac: optional torch float64
-        CUDA tensors of shape [2, ld] / [stride, ld] (caller-owned outputs)."""
+        CUDA tensors of shape [2, ld] / [stride, ld] (caller-owned outputs);
+        float32 tensors select the fp32-output evaluation."""
         flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0) | \
             (_lib.EVAL_APPLY_LOSS if apply_loss else 0) | phase
         rp = C.c_void_p(residuals.data_ptr()) if residuals is not None else None
         jp = C.c_void_p(jac.data_ptr()) if jac is not None else None
-        st = self.lib.mvba_evaluate_device(self.h, flags, float(robust_threshold), rp, jp,
-                                           int(ld), C.c_void_p(stream or 0))
+        f32 = residuals is not None and str(residuals.dtype) == "torch.float32"
+        fn = self.lib.mvba_evaluate_device_f32 if f32 else self.lib.mvba_evaluate_device
+        st = fn(self.h, flags, float(robust_threshold), rp, jp, int(ld), C.c_void_p(stream or 0))
         _lib.check(st, self.h)
 
     def sync(self, stream=None):

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "mvba", "mvba.h")
 def declared_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"\b(mvba_[a-z_]+)\s*\(", src)
+    names = re.findall(r"\b(mvba_[a-z0-9_]+)\s*\(", src)
     return sorted(set(names))
 
 
