@@ -157,3 +157,38 @@ def test_residual_stats_percentiles(oracle):
     n = len(s)
     assert cnt[0] == n
     assert np.allclose(out[0], [s[int(0.25 * n)], s[int(0.5 * n)], s[int(0.75 * n)], s[n - 1]])
+
+
+# ------------------------------------------------------------ depth golden vectors
+def _depth_golden():
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "depth_error_golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+DEPTH_CASES = _depth_golden()
+
+
+@pytest.mark.parametrize("ci", range(len(DEPTH_CASES)))
+def test_oracle_depth_matches_mpmath_golden(oracle, ci):
+    """BracketedDepthError (rig_calibrator.cc:547-583): the oracle's restatement
+    against the independent 50-digit mpmath one (tests/golden/make_golden_depth.py),
+    rigid and affine depth_to_image, reference / interpolated / no-rig frames,
+    scale != 1. Residuals 1e-12 relative, Jacobian 1e-8 of each block's largest entry."""
+    import numpy as np
+
+    c = DEPTH_CASES[ci]
+    blocks = [np.array(b) for b in c["blocks"]]
+    r, J = oracle.depth_error(blocks, np.zeros(7, np.uint8), c["weight"], c["meas"], *c["stamps"],
+                              mode=oracle.ANALYTIC)
+    rg = np.array(c["residual"])
+    assert np.abs(r - rg).max() <= 1e-12 * max(np.abs(rg).max(), 1.0)
+    off = 0
+    for b, blk in enumerate(blocks):
+        n = 3 * blk.size
+        Jg = np.array(c["jacobian"][b])
+        scale = max(np.abs(Jg).max(), 1e-300)
+        assert np.abs(J[off:off + n] - Jg).max() <= 1e-8 * scale, (b, np.abs(J[off:off + n] - Jg).max() / scale)
+        off += n
