@@ -35,6 +35,7 @@ static void free_all(mvba_handle* h) {
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
                   h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
+                  h->d_po_slot,
                   h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
                   h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xpid,
                   h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt};
@@ -396,7 +397,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   std::vector<int4> chunks;
   std::vector<mvba::FrameLinHost> flin(frames.size());
   std::vector<int64_t> pt_begin;
-  std::vector<int32_t> po_frame;
+  std::vector<int32_t> po_frame, po_slot;
   std::vector<double2> po_meas;
   std::vector<int32_t> slot_po;
   std::vector<int64_t> goff_of(d->num_blocks, -1), hoff_of(d->num_blocks, -1);
@@ -484,6 +485,9 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     slot_po.assign(nslots, -1);
     for (int64_t p = 0; p < nslots; p++)
       if (h->order[p] >= 0) slot_po[p] = po_of[h->order[p]];
+    po_slot.assign(N, -1);
+    for (int64_t p = 0; p < nslots; p++)
+      if (slot_po[p] >= 0) po_slot[slot_po[p]] = (int32_t)p;
     h->nchunks = (int32_t)chunks.size();
   }
 
@@ -641,6 +645,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_po_frame, po_frame));
   chk(upload(&h->d_po_meas, po_meas));
   chk(upload(&h->d_slot_po, slot_po));
+  chk(upload(&h->d_po_slot, po_slot));
   chk(upload(&h->d_dep_desc, ddesc));
   chk(upload(&h->d_dep_meas, dmeas));
   chk(upload(&h->d_dep_segs, dsegs));

@@ -198,6 +198,7 @@ struct mvba_handle {
   int32_t* d_po_frame = nullptr;
   double2* d_po_meas = nullptr;
   int32_t* d_slot_po = nullptr;          // device slot -> point-order index (-1 = padding)
+  int32_t* d_po_slot = nullptr;          // point-order index -> device slot
   std::vector<int64_t> cam_poff;         // camera-side entry -> packed parameter offset
   int32_t nchunks = 0;
 

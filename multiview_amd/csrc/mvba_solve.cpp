@@ -29,14 +29,23 @@ int mvba_solver_dir_stride(void);
 int mvba_solver_vec_replicas(void);
 int64_t mvba_pass_a_blocks(int64_t npts);
 hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const FrameDesc* fd, const double* frec,
-                                 const double* x, double* dir, const int32_t* gate, hipStream_t s);
+                                 const double* x, double* dir, const int32_t* gate, const mvba::LazyDir* lz,
+                                 hipStream_t s);
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
-                              const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
+                              const double* V, const double* dp, double* zbuf, double* wout, int32_t wstride,
                               double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
                               mvba::PointExtra dc, const double* xcam, double* du, const int32_t* gate,
                               const double* prec, hipStream_t s);
+hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int32_t nchunks,
+                                    const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
+                                    const double2* obs_meas, const int32_t* slot_po, const double* dir,
+                                    double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
+                                    const double* prec, hipStream_t s);
+hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
+                               const double* tinit, const double* V, const double* dp, const double4* pts,
+                               double* wout, int32_t wstride, const int32_t* gate, hipStream_t s);
 hipError_t mvba_launch_frame_proj(int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
                                   const double* params, double* prec, hipStream_t s);
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
@@ -46,7 +55,7 @@ hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const m
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
                               const Segment* segs, const FrameDesc* fd, const void* fl, const double* frec,
                               const double* params, const double4* pts, const int32_t* obs_pid,
-                              const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* yrep,
+                              const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
@@ -58,8 +67,6 @@ hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* 
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
                                  int32_t iter, hipStream_t s);
-hipError_t mvba_launch_cg_p(int64_t n, const mvba::CgCtl* ctl, int32_t first, double beta, const double* z, double* p,
-                            hipStream_t s);
 hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
                              hipStream_t s);
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, double* out,
@@ -105,11 +112,13 @@ struct SolverState {
   double* scr = nullptr;      // [nc] scratch
   double* lo = nullptr;       // [nc] bounds (compact) or null
   double* hi = nullptr;
-  double *b = nullptr, *r = nullptr, *r2 = nullptr, *z = nullptr, *p = nullptr, *q = nullptr, *tmp = nullptr;  // [ng]
+  double *b = nullptr, *r = nullptr, *r2 = nullptr, *z = nullptr, *p = nullptr, *p2 = nullptr, *q = nullptr,
+         *tmp = nullptr;  // [ng]; p, p2: the CG direction, double-buffered
   double* yrep = nullptr;     // [replicas * ng], kept zero between products
   double* dir = nullptr;      // [nframes * dir stride]
   double* zbuf = nullptr;     // [8 N] point-order z_o | J_pt rows
-  double* ubuf = nullptr;     // [2 N]
+  double* wbuf = nullptr;     // [4 np] w_p of the last pass A (double4 per point)
+  double* cbuf = nullptr;     // [4 slots] frame-order pass A: J_pt^T z per slot
   double* du = nullptr;       // [3 depth slots] u_d of the depth blocks (pass A -> k_depth_sb)
   double* partial = nullptr;  // [npartial]
   double* scal = nullptr;     // [32] device scalars
@@ -128,7 +137,7 @@ struct SolverState {
 void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
-                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->ubuf, S->du,
+                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->du,
                   S->cnt, S->partial, S->scal, S->bsize, S->emap, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -174,14 +183,15 @@ SolverState* alloc_state(mvba_handle* h) {
     for (double** v : {&S->G, &S->cdiag, &S->sc, &S->dmp, &S->x, &S->xn, &S->delta, &S->scr})
       HCHK(dalloc(v, (size_t)S->nc));
     HCHK(dalloc(&S->fac, (size_t)S->nh));
-    for (double** v : {&S->b, &S->r, &S->r2, &S->z, &S->p, &S->q, &S->tmp}) HCHK(dalloc(v, (size_t)ng1));
+    for (double** v : {&S->b, &S->r, &S->r2, &S->z, &S->p, &S->p2, &S->q, &S->tmp}) HCHK(dalloc(v, (size_t)ng1));
     const size_t nrep = (size_t)mvba_solver_vec_replicas() * (size_t)ng1;
     HCHK(dalloc(&S->yrep, nrep));
     HCHK(hipMemset(S->yrep, 0, nrep * sizeof(double)));
     HCHK(dalloc(&S->dir, (size_t)(h->nframes * mvba_solver_dir_stride())));
     HCHK(dalloc(&S->prec, (size_t)(h->nframes * mvba::kProjDoubles)));
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
-    HCHK(dalloc(&S->ubuf, (size_t)(2 * N)));
+    HCHK(dalloc(&S->wbuf, (size_t)(4 * std::max<int64_t>(S->np, 1))));
+    HCHK(dalloc(&S->cbuf, (size_t)(4 * std::max<int64_t>(N, 1))));
     HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
     HCHK(dalloc(&S->cnt, 8));
     HCHK(hipMemset(S->cnt, 0, 8 * sizeof(unsigned)));
@@ -327,12 +337,13 @@ class Solver {
   // (dot -> scal[dot_slot]); sharded: cross-rank sum of y first.
   // gate: device CG stop flag (nullptr: always run); ctl: CG step-length logic
   // in the finalising block of the x.y reduction (single rank only)
-  void reduce_frames(double* y, const double* xv, int dot_slot, const int32_t* gate = nullptr,
+  // dir: the frame directions of xv (null: pass B with x = 0, u_o = -J_pt w_p)
+  void reduce_frames(double* y, const double* xv, int dot_slot, const double* dir, const int32_t* gate = nullptr,
                      mvba::CgCtl* ctl = nullptr) {
     for (const Group& G : h_->groups)
       HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
                               h_->d_segs, h_->d_fd, h_->d_frame_lin, h_->d_frec, h_->d_params, h_->d_pts,
-                              h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, S_->ubuf, S_->yrep, S_->ng, flags_,
+                              h_->d_obs_pid, h_->d_obs_meas, dir, (const double4*)S_->wbuf, S_->yrep, S_->ng, flags_,
                               cauchy_c_, gate, s_));
     if (h_->ndep > 0)
       HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
@@ -347,26 +358,42 @@ class Solver {
       HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, s_));
   }
 
-  // y = S x (implicit Schur complement with damping); x.y -> scal[dot_slot]
+  // w_p = (V + D)^-1 (tinit + sum J_pt^T J_cam x) into wbuf (dir: frame
+  // directions of x, null for x = 0). Depth blocks need the point-lane kernel
+  // (it also forms their u_d); otherwise the frame-order sweep + point solve.
+  void pass_a_w(const double* dir, const double* tinit, const double* xv, const int32_t* gate) {
+    if (h_->ndep > 0)
+      HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas,
+                              h_->d_fd, h_->d_frec, h_->d_params, h_->d_pts, dir, tinit, S_->phess,
+                              S_->dmp + S_->ng, S_->zbuf, S_->wbuf, 4, nullptr, nullptr, nullptr, flags_, cauchy_c_,
+                              h_->point_extra(), xv, S_->du, gate, S_->prec, s_));
+    else {
+      if (dir)
+        for (const Group& G : h_->groups)
+          HCHK(mvba_launch_pass_a_frame(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, h_->d_segs,
+                                        h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dir, (double4*)S_->cbuf, flags_,
+                                        cauchy_c_, gate, S_->prec, s_));
+      HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, h_->d_po_slot, dir ? (const double4*)S_->cbuf : nullptr,
+                               tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate, s_));
+    }
+  }
+
+  // y = S x (implicit Schur complement with damping); x.y -> scal[dot_slot].
+  // lz: x is the CG direction formed by the frame-direction kernel (into xv)
   void apply_schur(const double* xv, double* y, int dot_slot, const int32_t* gate = nullptr,
-                   mvba::CgCtl* ctl = nullptr) {
-    HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, gate, s_));
-    HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
-                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, nullptr, S_->phess, S_->dmp + S_->ng,
-                            S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_, cauchy_c_,
-                            h_->point_extra(), xv, S_->du, gate, S_->prec, s_));
-    reduce_frames(y, xv, dot_slot, gate, ctl);
+                   mvba::CgCtl* ctl = nullptr, const mvba::LazyDir* lz = nullptr) {
+    HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, gate, lz,
+                               s_));
+    pass_a_w(S_->dir, nullptr, xv, gate);
+    reduce_frames(y, xv, dot_slot, S_->dir, gate, ctl);
   }
 
   // b = -(g_c - W (V+D)^-1 g_p). Starts every linear solve: the projection
   // records for pass A are built here (parameters fixed until the next step).
   void schur_rhs() {
     HCHK(mvba_launch_frame_proj((int32_t)h_->nframes, h_->d_fd, h_->d_frec, h_->d_params, S_->prec, s_));
-    HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
-                            h_->d_frec, h_->d_params, h_->d_pts, nullptr, S_->G + S_->ng, S_->phess,
-                            S_->dmp + S_->ng, S_->zbuf, S_->ubuf, nullptr, nullptr, nullptr, nullptr, flags_,
-                            cauchy_c_, h_->point_extra(), nullptr, S_->du, nullptr, S_->prec, s_));
-    reduce_frames(S_->tmp, nullptr, 0);  // = -W w
+    pass_a_w(nullptr, S_->G + S_->ng, nullptr, nullptr);
+    reduce_frames(S_->tmp, nullptr, 0, nullptr);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
   }
 
@@ -405,17 +432,17 @@ class Solver {
         R.status = 2;
         break;
       }
-      if (i == 1) {
-        HCHK(mvba_launch_cg_p(n, nullptr, 1, 0.0, S_->z, S_->p, s_));
-      } else {
-        const double beta = rho / last_rho;
-        if (bad(beta)) {
+      // p = z (i = 1) or z + beta p, formed by the frame-direction kernel
+      mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, nullptr, i == 1 ? 1 : 0, 0.0};
+      if (i > 1) {
+        lz.beta = rho / last_rho;
+        if (bad(lz.beta)) {
           R.status = 2;
           break;
         }
-        HCHK(mvba_launch_cg_p(n, nullptr, 0, beta, S_->z, S_->p, s_));
       }
-      apply_schur(S_->p, S_->q, 0);
+      std::swap(S_->p, S_->p2);
+      apply_schur(S_->p, S_->q, 0, nullptr, nullptr, &lz);
       const double pq = fetch(1)[0];
       if (pq <= 0.0 || std::isinf(pq) || std::isnan(pq)) {
         R.status = 1;  // "Matrix is indefinite": NO_CONVERGENCE, x kept
@@ -477,8 +504,9 @@ class Solver {
     int i = 1;
     for (int batch = 4;; batch = 8) {
       for (int k = 0; k < batch && i <= std::max(o_.max_linear_solver_iterations, 1); k++, i++) {
-        HCHK(mvba_launch_cg_p(n, S_->ctl, 0, 0.0, S_->z, S_->p, s_));
-        apply_schur(S_->p, S_->q, 0, gate, S_->ctl);
+        const mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, S_->ctl, 0, 0.0};
+        std::swap(S_->p, S_->p2);
+        apply_schur(S_->p, S_->q, 0, gate, S_->ctl, &lz);
         if (i % 10 == 0) {  // residual reset: r = b - A x
           upd(1, S_->q, i, false);
           apply_schur(xv, S_->tmp, 1, gate, nullptr);
@@ -500,11 +528,11 @@ class Solver {
   // delta_p = -(V+D)^-1 (g_p + W' delta_c); returns model cost change -(g'delta + |J delta|^2 / 2)
   double back_substitute() {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
-                               nullptr, s_));
+                               nullptr, nullptr, s_));
     // |J delta|^2 over the local reprojection and depth blocks -> scal[0]
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
-                            S_->dmp + S_->ng, S_->zbuf, nullptr, S_->delta + S_->ng, S_->partial, S_->cnt + 5,
+                            S_->dmp + S_->ng, S_->zbuf, S_->delta + S_->ng, 3, S_->partial, S_->cnt + 5,
                             S_->scal + 0, flags_, cauchy_c_, h_->point_extra(), S_->delta, S_->du, nullptr, S_->prec, s_));
     HCHK(mvba_launch_axpby(3 * S_->np, -1.0, S_->delta + S_->ng, 0.0, nullptr, S_->delta + S_->ng, s_));
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)

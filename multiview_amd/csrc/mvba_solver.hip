@@ -67,36 +67,72 @@ struct RowShape {
 
 // ------------------------------------------------------------ per-frame direction
 // dir_f = [ w_f x_pose (6) | x_focal | x_center (2) | x_dist (live) ]
+// With lz.z set, x is the CG direction p_new = z (+ beta p_old) (LazyDir): the
+// frame threads evaluate it where they read it and the trailing blocks
+// (beyond the frame blocks) store it for the kernels that follow.
+__device__ __forceinline__ double lazy_p(const LazyDir& lz, int32_t first, double beta, int64_t e) {
+  return first ? lz.z[e] : __fma_rn(beta, lz.p_old[e], lz.z[e]);
+}
+
+// One wave per frame: lane k < 22 takes pose column k (w_k x_k, butterfly-summed
+// over the wave), lanes 22.. copy the intrinsic entries.
 __global__ void __launch_bounds__(64) k_frame_dir(const FrameLin* __restrict__ fl, int32_t nframes,
                                                   const FrameDesc* __restrict__ fd,
                                                   const double* __restrict__ frec,
                                                   const double* __restrict__ x, double* __restrict__ dir,
-                                                  const int32_t* __restrict__ gate) {
+                                                  const int32_t* __restrict__ gate, LazyDir lz) {
   if (gate && *gate) return;
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= nframes) return;
-  const FrameLin L = fl[f];
-  const double* w = frec + (int64_t)f * kFrameRecDoubles + 12;
+  int32_t first = lz.first;
+  double beta = lz.beta;
+  if (lz.ctl) {
+    first = lz.ctl->first;
+    beta = lz.ctl->beta;
+  }
+  const int lane = threadIdx.x;
+  if ((int32_t)blockIdx.x >= nframes) {
+    const int64_t e = (int64_t)(blockIdx.x - nframes) * blockDim.x + lane;
+    if (e < lz.n) lz.p_new[e] = lazy_p(lz, first, beta, e);
+    return;
+  }
+  const int f = blockIdx.x;
+  auto X = [&](int64_t e) { return lz.z ? lazy_p(lz, first, beta, e) : x[e]; };
+  const FrameLin& L = fl[f];
   double u[6] = {0, 0, 0, 0, 0, 0};
-  for (int blk = 0; blk < 4; blk++) {
+  if (lane < kPoseCols) {
+    const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
-    if (L.goff[b] < 0) continue;
-    const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
-    for (int c = 0; c < ncol; c++) {
-      const double xv = x[L.goff[b] + c];
-      const double* wk = w + 6 * (k0 + c);
-      for (int a = 0; a < 6; a++) u[a] += wk[a] * xv;
+    if (L.goff[b] >= 0) {
+      const double xv = X(L.goff[b] + (lane - 7 * blk));
+      const double* wk = frec + (int64_t)f * kFrameRecDoubles + 12 + 6 * lane;
+#pragma unroll
+      for (int a = 0; a < 6; a++) u[a] = wk[a] * xv;
     }
   }
+#pragma unroll
+  for (int a = 0; a < 6; a++)
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) u[a] += __shfl_xor(u[a], off, 64);  // lanes 0..31 hold all columns
   double* d = dir + (int64_t)f * kDirStride;
-  for (int a = 0; a < 6; a++) d[a] = u[a];
+  if (lane < 6) {
+    double v = u[0];
+#pragma unroll
+    for (int a = 1; a < 6; a++)
+      if (lane == a) v = u[a];
+    d[lane] = v;
+  }
+  const int m = lane - kPoseCols;  // 0 focal, 1..2 centre, 3.. distortion
   const int nd = L.width - 10;
-  const int K = fd[f].K;
-  d[6] = L.goff[MVBA_BLK_FOCAL] >= 0 ? x[L.goff[MVBA_BLK_FOCAL]] : 0.0;
-  d[7] = L.goff[MVBA_BLK_CENTER] >= 0 ? x[L.goff[MVBA_BLK_CENTER]] : 0.0;
-  d[8] = L.goff[MVBA_BLK_CENTER] >= 0 ? x[L.goff[MVBA_BLK_CENTER] + 1] : 0.0;
-  for (int q = 0; q < nd; q++)
-    d[9 + q] = (L.goff[MVBA_BLK_DIST] >= 0 && q < K) ? x[L.goff[MVBA_BLK_DIST] + q] : 0.0;
+  if (m >= 0 && m < 3 + nd) {
+    double v = 0.0;
+    if (m == 0) {
+      if (L.goff[MVBA_BLK_FOCAL] >= 0) v = X(L.goff[MVBA_BLK_FOCAL]);
+    } else if (m < 3) {
+      if (L.goff[MVBA_BLK_CENTER] >= 0) v = X(L.goff[MVBA_BLK_CENTER] + (m - 1));
+    } else if (L.goff[MVBA_BLK_DIST] >= 0 && m - 3 < fd[f].K) {
+      v = X(L.goff[MVBA_BLK_DIST] + (m - 3));
+    }
+    d[6 + m] = v;
+  }
 }
 
 // ------------------------------------------------------------ pass A (point order)
@@ -213,14 +249,18 @@ __global__ void __launch_bounds__(256) k_frame_proj(int32_t nframes, const Frame
 
 // DEPTH: the problem has BracketedDepthError blocks (their code path is heavy;
 // compiled out of the reprojection-only variant to keep its registers down).
-template <int MODEL, int DEG, bool DEPTH>
+// ROWS: a second sweep over the reprojection observations after w_p is known
+// (|u_o|^2 for the back-substitution's model cost). Without it pass A only
+// accumulates t_p and writes w_p (stride wstride); pass B recomputes u_o from
+// the frame direction and w_p, so no per-observation row cache is kept.
+template <int MODEL, int DEG, bool DEPTH, bool ROWS>
 __global__ void __launch_bounds__(256) k_pass_a(
     const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const double* __restrict__ dir,
     const double* __restrict__ tinit, const double* __restrict__ V,
-    const double* __restrict__ dp, double* __restrict__ zbuf, double* __restrict__ ubuf, double* __restrict__ wout,
+    const double* __restrict__ dp, double* __restrict__ zbuf, double* __restrict__ wout, int32_t wstride,
     double* __restrict__ sq_partial, unsigned* __restrict__ counter, double* __restrict__ sq_out,
     int32_t flags, double cauchy_c, PointExtra dc, const double* __restrict__ xcam, double* __restrict__ du,
     const int32_t* __restrict__ gate, const double* __restrict__ prec) {
@@ -232,7 +272,7 @@ __global__ void __launch_bounds__(256) k_pass_a(
   double tv[3] = {0.0, 0.0, 0.0};
   double4 X = make_double4(0, 0, 0, 0);
   int64_t jb = 0, je = 0;
-  double zc[kCacheA][8];
+  double zc[kCacheA][8];  // ROWS only (dead otherwise)
   if (valid) {
     X = pts[p];
     jb = pt_begin[p];
@@ -245,6 +285,7 @@ __global__ void __launch_bounds__(256) k_pass_a(
                                   X, po_meas[j], flags, cauchy_c, z, P0, P1);
 #pragma unroll
       for (int q = 0; q < 3; q++) tv[q] += P0[q] * z[0] + P1[q] * z[1];
+      if constexpr (!ROWS) continue;
       const double row[8] = {z[0], z[1], P0[0], P0[1], P0[2], P1[0], P1[1], P1[2]};
       bool cached = false;
 #pragma unroll
@@ -296,9 +337,9 @@ __global__ void __launch_bounds__(256) k_pass_a(
       for (int q = 0; q < 3; q++) tv[q] += tinit[3 * p + q];
     solve3(V + 6 * p, dp + 3 * p, tv, w);
   }
-  if (valid) {
-    if (wout && sub == 0)
-      for (int q = 0; q < 3; q++) wout[3 * p + q] = w[q];
+  if (valid && wout && sub == 0)
+    for (int q = 0; q < 3; q++) wout[wstride * p + q] = w[q];
+  if (ROWS && valid) {
     int k = 0;
     for (int64_t j = jb + sub; j < je; j += kLanesA, k++) {
       double row[8];
@@ -317,7 +358,6 @@ __global__ void __launch_bounds__(256) k_pass_a(
       }
       const double u0 = row[0] - (row[2] * w[0] + row[3] * w[1] + row[4] * w[2]);
       const double u1 = row[1] - (row[5] * w[0] + row[6] * w[1] + row[7] * w[2]);
-      if (ubuf) *reinterpret_cast<double2*>(ubuf + 2 * j) = make_double2(u0, u1);
       sq += u0 * u0 + u1 * u1;
     }
   }
@@ -353,9 +393,83 @@ __global__ void __launch_bounds__(256) k_pass_a(
   if (sq_partial) grid_sum_finalize(sq, sq_partial, counter, sq_out);
 }
 
+// ------------------------------------------------------------ pass A, frame order
+// The products of k_pass_a<..., DEPTH = false, ROWS = false> split in two:
+// k_pass_a_frame sweeps the observations in frame order like pass B (one wave
+// per frame chunk, so the frame's projection record and direction are scalar
+// loads instead of per-lane gathers) and stores c_o = J_pt^T z_o per slot;
+// k_point_w sums each point's c_o in point order, adds tinit and solves
+// (V + D) w = t. Slot-order stores are coalesced; the point kernel gathers.
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(64) k_pass_a_frame(
+    const int4* __restrict__ chunks, int32_t nchunks, const Segment* __restrict__ segs,
+    const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
+    const int32_t* __restrict__ slot_po, const double* __restrict__ dir, double4* __restrict__ cbuf, int32_t flags,
+    double cauchy_c,
+    const int32_t* __restrict__ gate, const double* __restrict__ prec) {
+  const int lane = threadIdx.x;
+  const int ch = blockIdx.x;
+  if (ch >= nchunks || (gate && *gate)) return;
+  const int4 c = chunks[ch];
+  const int frame = __builtin_amdgcn_readfirstlane(c.z);
+  const double* __restrict__ rec = prec + (int64_t)frame * kProjDoubles;
+  const double* __restrict__ d = dir + (int64_t)frame * kDirStride;
+  for (int sidx = 0; sidx < c.y; sidx++) {
+    const Segment sg = segs[c.x + sidx];
+    const int count = __builtin_amdgcn_readfirstlane(sg.count);
+    if (lane < count) {
+      const int64_t i = (int64_t)sg.begin + lane;
+      double z[2], P0[3], P1[3];
+      pass_a_obs<MODEL, DEG>(rec, d, pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
+      cbuf[slot_po[i]] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1], P0[2] * z[0] + P1[2] * z[1],
+                             0.0);
+    }
+  }
+}
+
+// w_p = (V + D)^-1 (tinit + sum_o c_o), kLanesW lanes per point gathering its
+// c_o (lane-strided, then a butterfly sum); cbuf null: x = 0
+constexpr int kLanesW = 8;
+__global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __restrict__ pt_begin,
+                                                 const int32_t* __restrict__ po_slot, const double4* __restrict__ cbuf,
+                                                 const double* __restrict__ tinit, const double* __restrict__ V,
+                                                 const double* __restrict__ dp, const double4* __restrict__ pts,
+                                                 double* __restrict__ wout, int32_t wstride,
+                                                 const int32_t* __restrict__ gate) {
+  if (gate && *gate) return;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = t0 / kLanesW;
+  const int sub = (int)(t0 % kLanesW);
+  const bool valid = p < npts;
+  double t[3] = {0.0, 0.0, 0.0};
+  if (valid && cbuf)
+    for (int64_t j = pt_begin[p] + sub; j < pt_begin[p + 1]; j += kLanesW) {
+      const double4 cv = cbuf[j];
+      t[0] += cv.x;
+      t[1] += cv.y;
+      t[2] += cv.z;
+    }
+#pragma unroll
+  for (int off = 1; off < kLanesW; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < 3; q++) t[q] += __shfl_xor(t[q], off, 64);
+  if (!valid || sub != 0) return;
+  double w[3] = {0.0, 0.0, 0.0};
+  if (pts[p].w != 0.0) {
+    if (tinit)
+#pragma unroll
+      for (int q = 0; q < 3; q++) t[q] += tinit[3 * p + q];
+    solve3(V + 6 * p, dp + 3 * p, t, w);
+  }
+#pragma unroll
+  for (int q = 0; q < 3; q++) wout[wstride * p + q] = w[q];
+}
+
 // ------------------------------------------------------------ pass B (frame order)
-// One wave per frame chunk: sum over its observations of Z^T u_o and J_I^T u_o,
-// wave-reduced; the lanes then map the 6 frame-local sums through the generators
+// One wave per frame chunk: per observation u_o = z_o - J_pt w_p, with
+// z_o = J_cam,o x from the frame direction (dir; null: x = 0) and w_p from pass A
+// (wbuf, double4 per point); then the sums of Z^T u_o and J_I^T u_o,
+// wave-reduced; the lanes map the 6 frame-local sums through the generators
 // w_k to the pose columns (y_k = w_k . (Z^T u)) and add pose + intrinsic columns
 // into replica (chunk mod kVecReplicas) of the camera-side vector.
 template <int MODEL, int DEG>
@@ -364,8 +478,8 @@ __global__ void __launch_bounds__(64) k_pass_b(
     const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
-    const double2* __restrict__ obs_meas, const int32_t* __restrict__ slot_po,
-    const double* __restrict__ ubuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c,
+    const double2* __restrict__ obs_meas, const double* __restrict__ dir,
+    const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c,
     const int32_t* __restrict__ gate) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
@@ -376,6 +490,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
   const int frame = __builtin_amdgcn_readfirstlane(c.z);
   const FrameDesc& F = fd[frame];
   const double* __restrict__ rec = frec + (int64_t)frame * kFrameRecDoubles;
+  const double* __restrict__ d = dir ? dir + (int64_t)frame * kDirStride : nullptr;
   double acc[NA];
 #pragma unroll
   for (int q = 0; q < NA; q++) acc[q] = 0.0;
@@ -384,14 +499,30 @@ __global__ void __launch_bounds__(64) k_pass_b(
     const int count = __builtin_amdgcn_readfirstlane(sg.count);
     if (lane < count) {
       const int64_t i = (int64_t)sg.begin + lane;
-      const double4 X = pts[obs_pid[i]];
+      const int32_t pid = obs_pid[i];
+      const double4 X = pts[pid];
       double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], P0[3], P1[3], r[2], hr;
 #pragma unroll
       for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;
       obs_rows<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, obs_meas[i], flags, cauchy_c, Z0, Z1, I0, I1, P0,
                            P1, r, &hr);
-      const int64_t j = slot_po[i];  // point-order index of this observation
-      const double2 u = *reinterpret_cast<const double2*>(ubuf + 2 * j);
+      double z0 = 0.0, z1 = 0.0;
+      if (d) {
+#pragma unroll
+        for (int a = 0; a < 6; a++) {
+          z0 += Z0[a] * d[a];
+          z1 += Z1[a] * d[a];
+        }
+#pragma unroll
+        for (int q = 0; q < RS::kIntr; q++) {
+          z0 += I0[q] * d[6 + q];
+          z1 += I1[q] * d[6 + q];
+        }
+      }
+      const double4 w = wbuf[pid];
+      double2 u;
+      u.x = z0 - (P0[0] * w.x + P0[1] * w.y + P0[2] * w.z);
+      u.y = z1 - (P1[0] * w.x + P1[1] * w.y + P1[2] * w.z);
 #pragma unroll
       for (int a = 0; a < 6; a++) acc[a] += Z0[a] * u.x + Z1[a] * u.y;
 #pragma unroll
@@ -472,21 +603,6 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
       }
     }
   }
-}
-
-// p = z (first iteration) or z + beta p; with ctl, gated by the CG control and
-// first/beta taken from it (both CG drivers use this kernel, so their
-// arithmetic is identical).
-__global__ void __launch_bounds__(256) k_cg_p(int64_t n, const CgCtl* __restrict__ ctl, int32_t first, double beta,
-                                              const double* __restrict__ z, double* __restrict__ p) {
-  if (ctl) {
-    if (ctl->done) return;
-    first = ctl->first;
-    beta = ctl->beta;
-  }
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  p[e] = first ? z[e] : z[e] + beta * p[e];
 }
 
 // y += diag .* x; dot_out = x.y (after a cross-rank sum of y)
@@ -869,11 +985,16 @@ extern "C" {
 int mvba_solver_dir_stride(void) { return mvba::kDirStride; }
 int mvba_solver_vec_replicas(void) { return mvba::kVecReplicas; }
 
+// lz (nullable): x is the lazily formed CG direction, also stored to lz->p_new
 hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
-                                 const double* x, double* dir, const int32_t* gate, hipStream_t s) {
-  if (nframes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_frame_dir, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s,
-                     (const mvba::FrameLin*)fl, nframes, fd, frec, x, dir, gate);
+                                 const double* x, double* dir, const int32_t* gate, const mvba::LazyDir* lz,
+                                 hipStream_t s) {
+  mvba::LazyDir l{};
+  if (lz) l = *lz;
+  const int64_t fblocks = std::max(nframes, 0), pblocks = lz ? (l.n + 63) / 64 : 0;
+  if (fblocks + pblocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_frame_dir, dim3((unsigned)(fblocks + pblocks)), dim3(64), 0, s,
+                     (const mvba::FrameLin*)fl, nframes, fd, frec, x, dir, gate, l);
   return hipGetLastError();
 }
 
@@ -882,35 +1003,57 @@ hipError_t mvba_launch_frame_dir(const void* fl, int32_t nframes, const mvba::Fr
 hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64_t npts, const int32_t* po_frame,
                               const double2* po_meas, const mvba::FrameDesc* fd, const double* frec,
                               const double* params, const double4* pts, const double* dir, const double* tinit,
-                              const double* V, const double* dp, double* zbuf, double* ubuf, double* wout,
+                              const double* V, const double* dp, double* zbuf, double* wout, int32_t wstride,
                               double* sq_partial, unsigned* counter, double* sq_out, int32_t flags, double cauchy_c,
                               mvba::PointExtra dc, const double* xcam, double* du, const int32_t* gate,
                               const double* prec, hipStream_t s) {
   const unsigned blocks = (unsigned)((npts * mvba::kLanesA + 255) / 256);
   if (npts <= 0) return hipSuccess;
-  const bool depth = dc.begin != nullptr;
+  const bool depth = dc.begin != nullptr, rows = sq_partial != nullptr;
+#define MVBA_PA4(M, D, DP, RW)                                                                                 \
+  hipLaunchKernelGGL((mvba::k_pass_a<M, D, DP, RW>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,   \
+                     po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, wout, wstride, sq_partial, counter, \
+                     sq_out, flags, cauchy_c, dc, xcam, du, gate, prec)
+#define MVBA_PA(M, D)                    \
+  if (depth) {                           \
+    if (rows) MVBA_PA4(M, D, true, true);   \
+    else MVBA_PA4(M, D, true, false);       \
+  } else {                               \
+    if (rows) MVBA_PA4(M, D, false, true);  \
+    else MVBA_PA4(M, D, false, false);      \
+  }
   if (model < 0) {
-    if (depth)
-      hipLaunchKernelGGL((mvba::k_pass_a<-1, 0, true>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,
-                         po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter,
-                         sq_out, flags, cauchy_c, dc, xcam, du, gate, prec);
-    else
-      hipLaunchKernelGGL((mvba::k_pass_a<-1, 0, false>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,
-                         po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter,
-                         sq_out, flags, cauchy_c, dc, xcam, du, gate, prec);
+    MVBA_PA(-1, 0)
     return hipGetLastError();
   }
-#define MVBA_PA(M, D)                                                                                          \
-  if (depth)                                                                                                 \
-    hipLaunchKernelGGL((mvba::k_pass_a<M, D, true>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,   \
-                       po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, \
-                       sq_out, flags, cauchy_c, dc, xcam, du, gate, prec);                                             \
-  else                                                                                                       \
-    hipLaunchKernelGGL((mvba::k_pass_a<M, D, false>), dim3(blocks), dim3(256), 0, s, pt_begin, npts, po_frame,  \
-                       po_meas, fd, frec, params, pts, dir, tinit, V, dp, zbuf, ubuf, wout, sq_partial, counter, \
-                       sq_out, flags, cauchy_c, dc, xcam, du, gate, prec)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PA)
 #undef MVBA_PA
+#undef MVBA_PA4
+  return hipGetLastError();
+}
+
+// Frame-order pass A (no depth blocks, no |u|^2 sweep) for one model group
+hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int32_t nchunks,
+                                    const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
+                                    const double2* obs_meas, const int32_t* slot_po, const double* dir,
+                                    double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
+                                    const double* prec, hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+#define MVBA_PAF(M, D)                                                                                      \
+  hipLaunchKernelGGL((mvba::k_pass_a_frame<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks, \
+                     segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec)
+  MVBA_SOLVER_SWITCH(model, deg, MVBA_PAF)
+#undef MVBA_PAF
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
+                               const double* tinit, const double* V, const double* dp, const double4* pts,
+                               double* wout, int32_t wstride, const int32_t* gate, hipStream_t s) {
+  if (npts <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_point_w, dim3((unsigned)((npts * mvba::kLanesW + 255) / 256)), dim3(256), 0, s, npts,
+                     pt_begin, po_slot,
+                     cbuf, tinit, V, dp, pts, wout, wstride, gate);
   return hipGetLastError();
 }
 
@@ -928,13 +1071,13 @@ int64_t mvba_pass_a_blocks(int64_t npts) { return (npts * mvba::kLanesA + 255) /
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
                               const mvba::Segment* segs, const mvba::FrameDesc* fd, const void* fl,
                               const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
-                              const double2* obs_meas, const int32_t* slot_po, const double* ubuf, double* yrep,
+                              const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PB(M, D)                                                                                       \
   hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks,        \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
-                     slot_po, ubuf, yrep, ng, flags, cauchy_c, gate)
+                     dir, wbuf, yrep, ng, flags, cauchy_c, gate)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)
 #undef MVBA_PB
   return hipGetLastError();
@@ -969,13 +1112,6 @@ hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* 
   if (blocks > 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks), dim3(256), 0, s, n, emap, goff, hoff, bsize, minv, mode, alpha,
                      p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter);
-  return hipGetLastError();
-}
-
-hipError_t mvba_launch_cg_p(int64_t n, const mvba::CgCtl* ctl, int32_t first, double beta, const double* z, double* p,
-                            hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_cg_p, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, ctl, first, beta, z, p);
   return hipGetLastError();
 }
 

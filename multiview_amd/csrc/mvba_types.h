@@ -115,6 +115,18 @@ struct CgCtl {
   int32_t max_iter;
 };
 
+// The CG search direction formed where it is first read (k_frame_dir):
+// p_new = z (first) or z + beta p_old, with first/beta from ctl when set.
+struct LazyDir {
+  const double* z;
+  const double* p_old;
+  double* p_new;
+  int64_t n;
+  const CgCtl* ctl;
+  int32_t first;
+  double beta;
+};
+
 }  // namespace mvba
 
 #endif  // MVBA_TYPES_H_
