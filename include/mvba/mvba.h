@@ -286,7 +286,8 @@ mvba_status mvba_linearize_device(struct mvba_handle* h, int32_t flags, double c
  * insertion order, Cauchy corrector applied with MVBA_EVAL_APPLY_LOSS, cost =
  * sum of 0.5*rho over depth blocks. Device: column planes res[3][ld],
  * J[MVBA_DJAC_ROWS][ld] in device order (mvba_depth_order), ld >=
- * mvba_num_depth_slots(), multiple of 16. mvba_evaluate / mvba_linearize_device
+ * mvba_num_depth_slots(), multiple of 16 (of 32 for fp32 outputs to keep every
+ * plane on 128-B lines). mvba_evaluate / mvba_linearize_device
  * / mvba_solve include the depth blocks' cost and normal equations. */
 int64_t mvba_num_depth_residuals(const struct mvba_handle* h);
 int64_t mvba_num_depth_slots(const struct mvba_handle* h);
@@ -372,8 +373,11 @@ mvba_status mvba_residual_stats(struct mvba_handle* h, double* out, int64_t* cou
 
 /* Counts for reporting. */
 int64_t mvba_num_residuals(const struct mvba_handle* h);
-/* Device slots = residuals + padding that line-aligns every frame's range; device
- * output planes need ld >= mvba_num_slots(), ld a multiple of 16. */
+/* Device slots = residuals + padding that line-aligns every frame's range (32
+ * slots); device output planes need ld >= mvba_num_slots(), ld a multiple of 16
+ * (of 32 for fp32 outputs to keep every plane on 128-B lines). Padding slots
+ * that share a 128-B line with a frame's last residual receive a copy of it
+ * (whole-line stores); no entry point reads them back. */
 int64_t mvba_num_slots(const struct mvba_handle* h);
 int64_t mvba_num_frames(const struct mvba_handle* h);
 int64_t mvba_num_points(const struct mvba_handle* h);

@@ -36,13 +36,18 @@ __global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ se
   if (seg >= nseg) return;
   const Segment sg = segs[seg];
   const int lane = threadIdx.x;
-  if (lane >= sg.count) return;
+  // padding lanes up to the next 128-B line of OT recompute the last block
+  // into their padding slots (whole-line stores, as in k_obs)
+  constexpr int kLine = 128 / (int)sizeof(OT);
+  const int count = sg.count;
+  if (lane >= ((count + kLine - 1) & ~(kLine - 1))) return;
   const int64_t i = (int64_t)sg.begin + lane;
-  const DepthDesc d = dd[i];
+  const int64_t isrc = (int64_t)sg.begin + min(lane, count - 1);
+  const DepthDesc d = dd[isrc];
   const double* rec = frec + (int64_t)d.frame * kFrameRecDoubles;
   const double4 X = pts[d.pid];
   DepthRows o;
-  depth_rows(d, rec, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
+  depth_rows(d, rec, params, dmeas[isrc], X.x, X.y, X.z, flags, cauchy_c, o);
   const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
   if (res) {
 #pragma unroll

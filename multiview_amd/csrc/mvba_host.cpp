@@ -314,10 +314,11 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     return res_frame[a] < res_frame[b];
   });
 
-  // Device slots: every frame's residuals start on a 128-byte line (16 doubles),
-  // so each wavefront's 64-element store chunk per Jacobian plane is line-aligned
-  // (misaligned chunks write at ~60% of the aligned rate: tools/store_bench.hip).
-  constexpr int64_t kAlign = 16;
+  // Device slots: every frame's residuals start on a 128-byte line (16 doubles,
+  // 32 floats), so each wavefront's 64-element store chunk per Jacobian plane is
+  // line-aligned (misaligned chunks write at ~60% of the aligned rate:
+  // tools/store_bench.hip), and K1 fills the frame's last line with padding.
+  constexpr int64_t kAlign = 32;  // one 128-B line of fp32 outputs (two of fp64)
   int64_t nslots = 0;
   {
     int32_t prev_fr = -1;
@@ -510,7 +511,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     std::vector<int64_t> didx(ND);
     for (int64_t j = 0; j < ND; j++) didx[j] = j;
     std::stable_sort(didx.begin(), didx.end(), [&](int64_t a, int64_t b) { return dep_frame[a] < dep_frame[b]; });
-    constexpr int64_t kAlign = 16;
+    constexpr int64_t kAlign = 32;  // one 128-B line of fp32 outputs (two of fp64)
     int64_t slot = 0;
     int32_t prev = -1;
     std::vector<int64_t> slot_of(ND);

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Solver iteration: GPU solver tests, then rocprof kernel stats of the c2 bench
-# (all phases) -> gpurun_out/prof_solver/ and a short summary.
+# (all phases) -> gpurun_out/prof_solver/ and a short summary; CONFIGS="c2 c3"
+# profiles more workloads.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -11,16 +12,19 @@ timeout -k 10 600 python -m pytest tests/test_solver_gpu.py tests/test_xyz_prior
 rc=$?
 tail -2 $OUT/solver_tests.log
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_solver -o run --output-format csv -- \
-  python3 bench.py --steps 10 --no-cpu-baseline > $OUT/prof_solver.log 2>&1
-rc=$?
-tail -1 $OUT/prof_solver.log | cut -c1-300
-python3 - <<'PY'
-import csv, glob
-f = glob.glob("gpurun_out/prof_solver/**/*kernel_stats.csv", recursive=True)
+for cfg in ${CONFIGS:-c2}; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_solver_$cfg -o run --output-format csv -- \
+    python3 bench.py --config $cfg --steps 10 --no-cpu-baseline > $OUT/prof_solver_$cfg.log 2>&1
+  rc=$?
+  [ $rc -ne 0 ] && { tail -5 $OUT/prof_solver_$cfg.log; exit $rc; }
+  grep -o '"ba": {[^}]*}' $OUT/prof_solver_$cfg.log | cut -c1-400
+  CFG=$cfg python3 - <<'PY'
+import csv, glob, os
+f = glob.glob(f"gpurun_out/prof_solver_{os.environ['CFG']}/**/*kernel_stats.csv", recursive=True)
 if f:
     r = list(csv.DictReader(open(f[0])))
-    for x in r[:14]:
+    for x in r[:12]:
         print(x["Name"][:48].ljust(48), x["Calls"].rjust(6), "%9.1f us" % (float(x["AverageNs"]) / 1e3))
 PY
-exit $rc
+done
+exit 0
