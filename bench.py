@@ -13,6 +13,8 @@ Multi-GPU (one process per GPU, torchrun): observations are sharded by
 landmark range; each rank owns a c2-sized shard of a global
 problem with N x 100k landmarks over the same cameras. Evaluation has no
 data-path collective ("scaling": "weak"); value = all ranks' evals / max time.
+--config c4 is the exception: its 5M landmarks / 50M observations are the whole
+job, split into N landmark ranges ("scaling": "strong").
 
 Also reported: "roofline" of the dominant kernel (K1, radtan) from HIP events on
 its launch stream, and "cpu_baseline" = the oracle's Ceres-1.14-style central
@@ -34,6 +36,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+STRONG_CONFIGS = ("c4",)  # landmark count is the whole job's (strong scaling); others are per GPU
+FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (= fp64 matrix) peak, AMD product specification
 CPU_THREADS = 16       # reference default --num_opt_threads (rig_calibrator.cc:256)
 
 
@@ -123,6 +127,24 @@ def _pmc_traffic(config):
         return None
 
 
+def _pmc_flops(config):
+    """fp64 flops per launch of each kernel from the committed PMC summary of
+    this config (tools/pmc_flops.py over one rocprofv3 --pmc pass of this same
+    command; profiles/), or {}."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    path = os.path.join(here, "profiles", "r01", f"pmc_flops_{config}.json")
+    try:
+        with open(path) as f:
+            return json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return {}
+
+
+def _flops_of(table, prefixes):
+    tot = [v["fp64_flops"] for k, v in table.items() if any(k.startswith(p) for p in prefixes)]
+    return sum(tot) if tot else None
+
+
 def main():
     args = parse()
     import torch
@@ -150,7 +172,15 @@ def main():
 
     cfg = dict(rig.CONFIGS[args.config])
     npts = cfg["num_points"]
-    cfg["point_range"] = (rank * npts, (rank + 1) * npts)
+    strong = args.config in STRONG_CONFIGS
+    if strong:
+        # the config's landmark count is the whole problem, split into contiguous
+        # landmark ranges (c4: 5M landmarks / 50M observations over the node)
+        lo, hi = rank * npts // world, (rank + 1) * npts // world
+        cfg["point_range"] = (lo, hi)
+    else:
+        # each rank owns a config-sized shard of an N x larger problem
+        cfg["point_range"] = (rank * npts, (rank + 1) * npts)
     t0 = time.perf_counter()
     R = rig.make_rig(**cfg)
     P = rig.build_problem(R, rig.FloatFlags(**rig.CONFIG_FLAGS.get(args.config, {})))
@@ -214,13 +244,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * dt_max / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (deterministic rig generator, multiview_amd/rig.py)",
         "config": {
             "workload": f"{args.config}: {cfg['num_sensors']}-sensor rig, "
-                        f"{npts} landmarks x {world} shard(s), {n} obs/GPU, "
+                        + (f"{npts} landmarks split over {world} shard(s), " if strong
+                           else f"{npts} landmarks x {world} shard(s), ")
+                        + f"{n} obs/GPU, "
                         f"{cfg['models'][0]} distortion, all blocks floating, fp64",
             "num_residuals_per_gpu": n,
             "num_frames": ev.num_frames,
@@ -247,6 +279,18 @@ def main():
     line["roofline"]["stream_copy_gbs"] = stream_gbs
     line["roofline"]["frac_of_stream"] = achieved / stream_gbs if stream_gbs else None
     line["roofline"]["stream_note"] = "1 GiB device-to-device tensor copy (read + write bytes), same stream"
+    # fp64 arithmetic of the same launch (PMC instruction counts): the second
+    # roofline, to name the binding resource
+    flops_tab = _pmc_flops(args.config)
+    k1_flops = next((v["fp64_flops"] for k, v in flops_tab.items()
+                     if k.startswith("mvba::k_obs<") and k.endswith("double>")), None)
+    if k1_flops is not None:
+        tf = k1_flops / (obs_ms * 1e-3) / 1e12
+        line["roofline"]["fp64_flops_per_launch"] = k1_flops
+        line["roofline"]["fp64_tflops"] = tf
+        line["roofline"]["fp64_peak_tflops"] = FP64_PEAK_TFLOPS
+        line["roofline"]["fp64_frac"] = tf / FP64_PEAK_TFLOPS
+        line["roofline"]["binding"] = "hbm" if achieved / HBM_PEAK_GBS >= tf / FP64_PEAK_TFLOPS else "fp64"
     # ---- depth blocks (c5): K1-depth evaluation, materialised
     if ev.num_depth > 0:
         dld = (ev.num_depth_slots + 63) // 64 * 64
@@ -380,6 +424,22 @@ def main():
             "allreduce_bytes": buf.payload_bytes if world > 1 else 0,
             "cam_params": L["cam_grad_size"],
         }
+        # fused mode: 48 B per evaluation (observation record +
+        # landmark) against the fp64 work of the linearization kernels
+        lin_flops = _flops_of(flops_tab, ["mvba::k_prep", "mvba::k_gram<", "mvba::k_points_lin<",
+                                          "mvba::k_expand", "mvba::k_rep_reduce"]) if flops_tab else None
+        lin_bytes = 48.0 * n
+        lin["hbm_bytes"] = lin_bytes
+        lin["hbm_frac"] = lin_bytes / (lin_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+        if lin_flops is not None:
+            tf = lin_flops / (lin_ms * 1e-3) / 1e12
+            lin["fp64_flops"] = lin_flops
+            lin["fp64_mfma_flops"] = sum(v["fp64_mfma_flops"] for k, v in flops_tab.items()
+                                         if k.startswith("mvba::k_gram<"))
+            lin["fp64_tflops"] = tf
+            lin["fp64_frac"] = tf / FP64_PEAK_TFLOPS
+            lin["bound_us"] = 1e6 * max(lin_bytes / (HBM_PEAK_GBS * 1e9), lin_flops / (FP64_PEAK_TFLOPS * 1e12))
+            lin["binding"] = "fp64" if lin_flops / FP64_PEAK_TFLOPS / 1e12 > lin_bytes / HBM_PEAK_GBS / 1e9 else "hbm"
     line["linearize"] = lin
 
     # ---- phase C: Levenberg-Marquardt (mvba_solve: ITERATIVE_SCHUR replacement)
