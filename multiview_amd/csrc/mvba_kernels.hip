@@ -317,7 +317,10 @@ __global__ void __launch_bounds__(256) k_obs(
 // as [column][row] (row stride kGramLd doubles, conflict-free reads).
 // One wave = one chunk (<= kChunkSegs segments of one frame, mvba_types.h); accumulators stay
 // in registers across the chunk; the chunk's Gram goes to a slab (no atomics).
-constexpr int kGramLd = 130;  // 128 rows + 2 pad doubles: bank-conflict-free reads
+// The segment's 128 rows are staged in two halves of 64 (the observations of
+// lanes 0-31, then 32-63): 8.4 KB of LDS per wave for radtan instead of 16.6,
+// twice the waves per CU.
+constexpr int kGramLd = 66;  // 64 rows + 2 pad doubles: bank-conflict-free reads
 
 
 template <int MODEL, int DEG>
@@ -361,8 +364,9 @@ __global__ void __launch_bounds__(64) k_gram(
   double cost = 0.0;
 
   // zero the padding columns once (they stay zero)
-  for (int col = S::kWidth; col < T * 16; col++)
-    *(dbl2v*)&lds[col * kGramLd + 2 * lane] = dbl2v{0.0, 0.0};
+  if (lane < 32)
+    for (int col = S::kWidth; col < T * 16; col++)
+      *(dbl2v*)&lds[col * kGramLd + 2 * lane] = dbl2v{0.0, 0.0};
 
   for (int sidx = 0; sidx < c.y; sidx++) {
     const Segment sg = segs[c.x + sidx];
@@ -403,27 +407,33 @@ __global__ void __launch_bounds__(64) k_gram(
       row0[S::kColR] = r0 * sr;
       row1[S::kColR] = r1 * sr;
     }
-    // stage B (this segment's 128 rows) in LDS as [column][row]
-#pragma unroll
-    for (int q = 0; q < S::kWidth; q++) *(dbl2v*)&lds[q * kGramLd + 2 * lane] = dbl2v{row0[q], row1[q]};
-    __syncthreads();
+    // stage B (this segment's 128 rows) in LDS as [column][row], 64 rows at a
+    // time; the halves past the segment's last observation are all zero rows
     const int col = lane & 15, rsub = lane >> 4;
+    for (int half = 0; half < 2 && 32 * half < count; half++) {
+      if ((lane >> 5) == half) {
+#pragma unroll
+        for (int q = 0; q < S::kWidth; q++)
+          *(dbl2v*)&lds[q * kGramLd + 2 * (lane & 31)] = dbl2v{row0[q], row1[q]};
+      }
+      __syncthreads();
 #pragma unroll 4
-    for (int st = 0; st < 32; st++) {
-      const int row = 4 * st + rsub;
-      double v[T];
+      for (int st = 0; st < 16; st++) {
+        const int row = 4 * st + rsub;
+        double v[T];
 #pragma unroll
-      for (int t = 0; t < T; t++) v[t] = lds[(t * 16 + col) * kGramLd + row];
-      int p = 0;
+        for (int t = 0; t < T; t++) v[t] = lds[(t * 16 + col) * kGramLd + row];
+        int p = 0;
 #pragma unroll
-      for (int ti = 0; ti < T; ti++)
+        for (int ti = 0; ti < T; ti++)
 #pragma unroll
-        for (int tj = ti; tj < T; tj++) {
-          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ti], v[tj], acc[p], 0, 0, 0);
-          p++;
-        }
+          for (int tj = ti; tj < T; tj++) {
+            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ti], v[tj], acc[p], 0, 0, 0);
+            p++;
+          }
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   // chunk Gram -> slab: lane holds G[(lane>>4) + 4r][lane & 15] of each tile pair
   double* out = slab + (int64_t)c.w * SLAB;
