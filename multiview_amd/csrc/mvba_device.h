@@ -323,18 +323,36 @@ struct FrameLin {
 
 // Last-block finalisation of a grid reduction: every block stores its partial,
 // the last block to arrive sums them into out[0] and re-arms the counter.
+// Sum of K values over the block (blockDim.x a multiple of 64, <= 1024):
+// butterflies inside each wave, then the wave sums added in wave order, so the
+// result is deterministic and every thread of the block gets it.
+template <int K>
+__device__ __forceinline__ void block_sum(double* v) {
+  __shared__ double wsum[K][16];
+#pragma unroll
+  for (int k = 0; k < K; k++)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();  // wsum may still be read by a previous call
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < K; k++) wsum[k][w] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    double s = 0.0;
+    for (int j = 0; j < nw; j++) s += wsum[k][j];
+    v[k] = s;
+  }
+}
+
 __device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__ partial,
                                                   unsigned* __restrict__ counter, double* __restrict__ out) {
-  __shared__ double red[256];
   __shared__ bool last;
-  red[threadIdx.x] = v;
-  __syncthreads();
-  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
-    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
-    __syncthreads();
-  }
+  block_sum<1>(&v);
   if (threadIdx.x == 0) {
-    partial[blockIdx.x] = red[0];
+    partial[blockIdx.x] = v;
     __threadfence();
     last = (atomicAdd(counter, 1u) == gridDim.x - 1);
   }
@@ -343,14 +361,9 @@ __device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__
   __threadfence();
   double acc = 0.0;
   for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x) acc += __builtin_nontemporal_load(&partial[e]);
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
-    if ((int)threadIdx.x < s2) red[threadIdx.x] += red[threadIdx.x + s2];
-    __syncthreads();
-  }
+  block_sum<1>(&acc);
   if (threadIdx.x == 0) {
-    out[0] = red[0];
+    out[0] = acc;
     *counter = 0u;
   }
   return true;
@@ -361,19 +374,11 @@ __device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__
 __device__ __forceinline__ bool grid_sum3_finalize(double a, double b, double c, double* __restrict__ partial,
                                                    unsigned* __restrict__ counter, double* __restrict__ out,
                                                    double* res) {
-  __shared__ double red[3][256];
   __shared__ bool last;
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = b;
-  red[2][threadIdx.x] = c;
-  __syncthreads();
-  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
-    if ((int)threadIdx.x < s2)
-      for (int k = 0; k < 3; k++) red[k][threadIdx.x] += red[k][threadIdx.x + s2];
-    __syncthreads();
-  }
+  double v[3] = {a, b, c};
+  block_sum<3>(v);
   if (threadIdx.x == 0) {
-    for (int k = 0; k < 3; k++) partial[3 * blockIdx.x + k] = red[k][0];
+    for (int k = 0; k < 3; k++) partial[3 * blockIdx.x + k] = v[k];
     __threadfence();
     last = (atomicAdd(counter, 1u) == gridDim.x - 1);
   }
@@ -383,16 +388,10 @@ __device__ __forceinline__ bool grid_sum3_finalize(double a, double b, double c,
   double acc[3] = {0.0, 0.0, 0.0};
   for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x)
     for (int k = 0; k < 3; k++) acc[k] += __builtin_nontemporal_load(&partial[3 * e + k]);
-  for (int k = 0; k < 3; k++) red[k][threadIdx.x] = acc[k];
-  __syncthreads();
-  for (int s2 = blockDim.x >> 1; s2 > 0; s2 >>= 1) {
-    if ((int)threadIdx.x < s2)
-      for (int k = 0; k < 3; k++) red[k][threadIdx.x] += red[k][threadIdx.x + s2];
-    __syncthreads();
-  }
-  for (int k = 0; k < 3; k++) res[k] = red[k][0];
+  block_sum<3>(acc);
+  for (int k = 0; k < 3; k++) res[k] = acc[k];
   if (threadIdx.x == 0) {
-    for (int k = 0; k < 3; k++) out[k] = red[k][0];
+    for (int k = 0; k < 3; k++) out[k] = acc[k];
     *counter = 0u;
   }
   return true;

@@ -62,8 +62,8 @@ hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* di
                                       mvba::CgCtl* ctl, hipStream_t s);
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
                                 unsigned* counter, double* dot_out, hipStream_t s);
-hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* goff, const int64_t* hoff,
-                                 const int32_t* bsize, const double* minv, int32_t mode, double alpha, const double* p,
+hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const double* minv, int32_t mode, double alpha,
+                                 const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
                                  int32_t iter, hipStream_t s);
@@ -129,7 +129,7 @@ struct SolverState {
   mvba::CgCtl* hctl = nullptr; // pinned host mirror
   int64_t npartial = 0;
   int32_t* bsize = nullptr;
-  int32_t* emap = nullptr;    // camera entry -> camera block
+  mvba::CgEntry* ent = nullptr;  // per camera entry: block start, size, inverse row
   int32_t max_bsize = 0;
   int64_t *goff = nullptr, *hoff = nullptr, *cam_poff = nullptr;
 };
@@ -138,7 +138,7 @@ void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
                   S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->du,
-                  S->cnt, S->partial, S->scal, S->bsize, S->emap, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
+                  S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (S->hscal) (void)hipHostFree(S->hscal);
@@ -212,12 +212,13 @@ SolverState* alloc_state(mvba_handle* h) {
       bs[k] = (int32_t)(next - h->cam_goff[k]);
     }
     HCHK(upload(&S->bsize, bs));
-    std::vector<int32_t> em((size_t)S->ng);
+    std::vector<mvba::CgEntry> em((size_t)S->ng);
     for (int32_t k = 0; k < S->nblocks; k++) {
       S->max_bsize = std::max(S->max_bsize, bs[k]);
-      for (int32_t e = 0; e < bs[k]; e++) em[(size_t)(h->cam_goff[k] + e)] = k;
+      for (int32_t e = 0; e < bs[k]; e++)
+        em[(size_t)(h->cam_goff[k] + e)] = {(int32_t)h->cam_goff[k], bs[k], h->cam_hoff[k] + (int64_t)e * bs[k]};
     }
-    HCHK(upload(&S->emap, em));
+    HCHK(upload(&S->ent, em));
     HCHK(upload(&S->goff, h->cam_goff));
     HCHK(upload(&S->hoff, h->cam_hoff));
     HCHK(upload(&S->cam_poff, h->cam_poff));
@@ -415,7 +416,7 @@ class Solver {
     if (norm_b == 0.0) return R;
     // r is double-buffered: each update reads S_->r and writes S_->r2, then they swap
     auto upd = [&](int32_t mode, double alpha, const double* q) {
-      HCHK(mvba_launch_cg_update(n, S_->emap, S_->goff, S_->hoff, S_->bsize, S_->fac, mode, alpha, S_->p, q, S_->b, xv,
+      HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, alpha, S_->p, q, S_->b, xv,
                                  S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, nullptr, 0, s_));
       std::swap(S_->r, S_->r2);
     };
@@ -495,7 +496,7 @@ class Solver {
     HCHK(hipMemcpyAsync(S_->ctl, S_->hctl, sizeof(mvba::CgCtl), hipMemcpyHostToDevice, s_));
     const int32_t* gate = &S_->ctl->done;
     auto upd = [&](int32_t mode, const double* q, int32_t iter, bool end_logic) {
-      HCHK(mvba_launch_cg_update(n, S_->emap, S_->goff, S_->hoff, S_->bsize, S_->fac, mode, 0.0, S_->p, q, S_->b, xv,
+      HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, 0.0, S_->p, q, S_->b, xv,
                                  S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl,
                                  end_logic ? iter : -1, s_));
       std::swap(S_->r, S_->r2);

@@ -421,8 +421,10 @@ __global__ void __launch_bounds__(64) k_pass_a_frame(
       const int64_t i = (int64_t)sg.begin + lane;
       double z[2], P0[3], P1[3];
       pass_a_obs<MODEL, DEG>(rec, d, pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
-      cbuf[slot_po[i]] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1], P0[2] * z[0] + P1[2] * z[1],
-                             0.0);
+      // plain store: a nontemporal store of these scattered 32-B records
+      // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM)
+      cbuf[slot_po[i]] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
+                                      P0[2] * z[0] + P1[2] * z[1], 0.0);
     }
   }
 }
@@ -473,7 +475,7 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
 // w_k to the pose columns (y_k = w_k . (Z^T u)) and add pose + intrinsic columns
 // into replica (chunk mod kVecReplicas) of the camera-side vector.
 template <int MODEL, int DEG>
-__global__ void __launch_bounds__(64) k_pass_b(
+__global__ void __launch_bounds__(64, (MODEL == kModelRadtan) ? 5 : 1) k_pass_b(
     const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
     const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
     const double* __restrict__ frec, const double* __restrict__ params,
@@ -576,12 +578,16 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double d = 0.0;
   if (e < n) {
+    // all replica loads in flight before the first add / zeroing store (the
+    // stores go through the same pointer, so a fused loop serialises them)
+    double v[kVecReplicas];
+#pragma unroll
+    for (int r = 0; r < kVecReplicas; r++) v[r] = yrep[r * n + e];
     double acc = 0.0;
-#pragma unroll 8
-    for (int r = 0; r < kVecReplicas; r++) {
-      acc += yrep[r * n + e];
-      yrep[r * n + e] = 0.0;
-    }
+#pragma unroll
+    for (int r = 0; r < kVecReplicas; r++) acc += v[r];
+#pragma unroll
+    for (int r = 0; r < kVecReplicas; r++) yrep[r * n + e] = 0.0;
     if (diag) acc += diag[e] * x[e];
     y[e] = acc;
     d = x ? x[e] * acc : 0.0;
@@ -624,9 +630,8 @@ __global__ void __launch_bounds__(256) k_add_diag(int64_t n, const double* __res
 // (conjugate_gradients_solver.cc [ext]); r is double-buffered (r_in -> r_out):
 //   mode & 1: x += alpha p;  & 2: r = r_in - alpha q;  & 4: r = b - q (q null: r = b);
 //   mode & 8: z = M^-1 r (explicit block inverses) and out = [x.b, x.r, r.z].
-__global__ void __launch_bounds__(256) k_cg_update(int64_t n, const int32_t* __restrict__ emap,
-                                                   const int64_t* __restrict__ goff, const int64_t* __restrict__ hoff,
-                                                   const int32_t* __restrict__ bsize, const double* __restrict__ minv,
+__global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __restrict__ ent,
+                                                   const double* __restrict__ minv,
                                                    int32_t mode, double alpha, const double* __restrict__ p,
                                                    const double* __restrict__ q, const double* __restrict__ b,
                                                    double* __restrict__ x, const double* __restrict__ r_in,
@@ -640,10 +645,9 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const int32_t* __r
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double xb = 0.0, xr = 0.0, rz = 0.0;
   if (i < n) {
-    const int blk = emap[i];
-    const int64_t o = goff[blk];
-    const int nb = bsize[blk];
-    const int row = (int)(i - o);
+    const CgEntry E = ent[i];
+    const int64_t o = E.o;
+    const int nb = E.nb;
     auto rnew = [&](int64_t k) -> double {
       if (mode & 2) return r_in[k] - alpha * q[k];
       if (mode & 4) return q ? b[k] - q[k] : b[k];
@@ -657,7 +661,7 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const int32_t* __r
     const double ri = rnew(i);
     r_out[i] = ri;
     if (mode & 8) {
-      const double* M = minv + hoff[blk] + (int64_t)row * nb;
+      const double* M = minv + E.moff;
       double zi = 0.0;
       for (int k = 0; k < nb; k++) zi += M[k] * rnew(o + k);
       z[i] = zi;
@@ -1102,15 +1106,15 @@ hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, 
 }
 
 // partial needs 3 x 1024 doubles, counters 3 (zero-initialised, re-armed by the kernel)
-hipError_t mvba_launch_cg_update(int64_t n, const int32_t* emap, const int64_t* goff, const int64_t* hoff,
-                                 const int32_t* bsize, const double* minv, int32_t mode, double alpha, const double* p,
+hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const double* minv, int32_t mode, double alpha,
+                                 const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
                                  int32_t iter, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   if (blocks > 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks), dim3(256), 0, s, n, emap, goff, hoff, bsize, minv, mode, alpha,
+  hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks), dim3(256), 0, s, n, ent, minv, mode, alpha,
                      p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter);
   return hipGetLastError();
 }

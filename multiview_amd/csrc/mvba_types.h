@@ -115,6 +115,15 @@ struct CgCtl {
   int32_t max_iter;
 };
 
+// Camera-side entry of the reduced system as the CG update reads it: its
+// block's first entry, the block size and the offset of the entry's row of
+// the block-Jacobi inverse (one load per entry instead of a block-id chain).
+struct CgEntry {
+  int32_t o;
+  int32_t nb;
+  int64_t moff;
+};
+
 // The CG search direction formed where it is first read (k_frame_dir):
 // p_new = z (first) or z + beta p_old, with first/beta from ctl when set.
 struct LazyDir {
