@@ -248,6 +248,7 @@ class Solver {
   double cauchy_c_;
   bool single_model_;
   bool bounded_ = false;
+  int last_cg_iters_ = 0;  // CG iterations of the previous linear solve (batch sizing only)
 
   int pa_model() const { return single_model_ ? h_->groups[0].model : -1; }
   int pa_deg() const { return single_model_ ? h_->groups[0].deg : 0; }
@@ -503,7 +504,12 @@ class Solver {
     };
     upd(4 | 8, nullptr, 0, true);  // r = b, z = M^-1 r, rho
     int i = 1;
-    for (int batch = 4;; batch = 8) {
+    // Batch sizes only decide where the host looks at the control block (gated
+    // iterations past the stop are no-ops): the first batch runs to just short
+    // of the previous solve's iteration count, later ones are short, so most
+    // solves need one or two host reads and few gated iterations.
+    const int first = std::max(4, last_cg_iters_ - 2);
+    for (int batch = first;; batch = 4) {
       for (int k = 0; k < batch && i <= std::max(o_.max_linear_solver_iterations, 1); k++, i++) {
         const mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, S_->ctl, 0, 0.0};
         std::swap(S_->p, S_->p2);
@@ -523,6 +529,7 @@ class Solver {
     }
     R.iters = S_->hctl->iters;
     R.status = S_->hctl->status;
+    last_cg_iters_ = R.iters;
     return R;
   }
 
