@@ -44,9 +44,11 @@ __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ par
       rec[9] = t0[0]; rec[10] = t0[1]; rec[11] = t0[2];
     }
     for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
-      double om[3] = {0.0, 0.0, 0.0}, dt[3] = {0.0, 0.0, 0.0};
+      double om[3] = {0.0, 0.0, 0.0};
+      // unit translation column by value (a dynamic index into dt would put the
+      // array in scratch memory)
+      double dt[3] = {k == 0 ? 1.0 : 0.0, k == 1 ? 1.0 : 0.0, k == 2 ? 1.0 : 0.0};
       if (k < 3) {
-        dt[k] = 1.0;
       } else if (k < 7) {
         quat_generator(qh0, 2.0 * in0, k - 3, om);
       }
@@ -87,13 +89,14 @@ __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ par
     const double S = sin(th), C = cos(th);
     const double s0 = sin((1.0 - alpha) * th), c0 = cos((1.0 - alpha) * th);
     const double s1 = sin(alpha * th), c1 = cos(alpha * th);
-    w0 = s0 / S;
+    w0 = s0 / S;  // Eigen's slerp weights, divided as Eigen does
     w1 = s1 / S;
-    dw0_dth = ((1.0 - alpha) * c0 * S - s0 * C) / (S * S);
-    dw1_dth = (alpha * c1 * S - s1 * C) / (S * S);
-    dw0_da = -th * c0 / S;
-    dw1_da = th * c1 / S;
-    dth_dD = -1.0 / S;
+    const double iS = 1.0 / S;  // derivative terms: one reciprocal
+    dw0_dth = ((1.0 - alpha) * c0 * S - s0 * C) * (iS * iS);
+    dw1_dth = (alpha * c1 * S - s1 * C) * (iS * iS);
+    dw0_da = -th * c0 * iS;
+    dw1_da = th * c1 * iS;
+    dth_dD = -iS;
   }
   const double sgn = (d < 0.0) ? -1.0 : 1.0;
   if (d < 0.0) {
@@ -121,25 +124,39 @@ __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ par
   }
 
   for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
+    // Every per-column choice below is made by value (selects), never by a
+    // dynamic index into a register array or a pointer to one of two arrays:
+    // either would move the arrays to scratch memory (80 B per lane before).
     double om[3] = {0.0, 0.0, 0.0}, dt[3] = {0.0, 0.0, 0.0};
     if (k < 3 || (k >= 7 && k < 10) || (k >= 14 && k < 17)) {
       // translation columns of beg / end / ref_to_cam
       const int j = (k < 3) ? k : (k < 10) ? k - 7 : k - 14;
       const double scale = (k < 3) ? (1.0 - alpha) : (k < 10) ? alpha : 0.0;
       if (k >= 14) {
-        dt[j] = 1.0;
+        dt[0] = j == 0 ? 1.0 : 0.0;
+        dt[1] = j == 1 ? 1.0 : 0.0;
+        dt[2] = j == 2 ? 1.0 : 0.0;
       } else {
-        dt[0] = scale * R2[j]; dt[1] = scale * R2[3 + j]; dt[2] = scale * R2[6 + j];
+        const double c0 = j == 0 ? R2[0] : j == 1 ? R2[1] : R2[2];
+        const double c1 = j == 0 ? R2[3] : j == 1 ? R2[4] : R2[5];
+        const double c2 = j == 0 ? R2[6] : j == 1 ? R2[7] : R2[8];
+        dt[0] = scale * c0; dt[1] = scale * c1; dt[2] = scale * c2;
       }
     } else if (k < 14) {
       // quaternion columns of beg (3..6) and end (10..13) through slerp
       const bool side = (k >= 10);
       const int kk = side ? k - 10 : k - 3;
-      const double* qh = side ? qh1 : qh0;
       const double sc = side ? sig1 * in1 : sig0 * in0;
-      const double* qo = side ? q0 : q1;
+      double qh[4], qo[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        qh[m] = side ? qh1[m] : qh0[m];
+        qo[m] = side ? q0[m] : q1[m];
+      }
+      const double qk = kk == 0 ? qh[0] : kk == 1 ? qh[1] : kk == 2 ? qh[2] : qh[3];
       double dq[4];
-      for (int m = 0; m < 4; m++) dq[m] = sc * ((m == kk ? 1.0 : 0.0) - qh[m] * qh[kk]);
+#pragma unroll
+      for (int m = 0; m < 4; m++) dq[m] = sc * ((m == kk ? 1.0 : 0.0) - qh[m] * qk);
       const double dD = sgn * (qo[0] * dq[0] + qo[1] * dq[1] + qo[2] * dq[2] + qo[3] * dq[3]);
       const double dth = dth_dD * dD;
       const double ws = side ? w1 : w0;
