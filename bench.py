@@ -472,6 +472,9 @@ def main():
             "lm_iterations": s["num_iterations"],
             "successful_steps": s["num_successful_steps"],
             "cg_iterations": s["num_linear_iterations"],
+            # pass B / K2 accumulate shared camera entries with fp64 atomics, so
+            # the CG count (and LM it/s) varies run to run; this one does not
+            "ms_per_cg_iteration": 1e3 * s["linear_solver_time_s"] / max(s["num_linear_iterations"], 1),
             "linearize_s": s["linearize_time_s"],
             "linear_solver_s": s["linear_solver_time_s"],
             "eval_s": s["eval_time_s"],

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmvba.so")
+# MVBA_LIB: another build of the same ABI (A/B measurements on one box)
+LIB_PATH = os.environ.get("MVBA_LIB") or os.path.join(_HERE, "libmvba.so")
 
 # Status codes (mvba_status).
 MVBA_OK = 0

@@ -475,7 +475,7 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
 // w_k to the pose columns (y_k = w_k . (Z^T u)) and add pose + intrinsic columns
 // into replica (chunk mod kVecReplicas) of the camera-side vector.
 template <int MODEL, int DEG>
-__global__ void __launch_bounds__(64, (MODEL == kModelRadtan) ? 5 : 1) k_pass_b(
+__global__ void __launch_bounds__(64) k_pass_b(
     const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
     const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
     const double* __restrict__ frec, const double* __restrict__ params,

@@ -21,5 +21,7 @@ for path in sys.argv[1:]:
         if "linearize" in d:
             out.append(f"lin {d['linearize']['kernel_ms'] * 1e3:.1f} us")
         if "ba" in d:
-            out.append(f"LM {d['ba']['iters_per_s']:.1f} it/s ({d['ba']['cg_iterations']} CG)")
+            cg = d['ba'].get('ms_per_cg_iteration')
+            out.append(f"LM {d['ba']['iters_per_s']:.1f} it/s ({d['ba']['cg_iterations']} CG"
+                       + (f", {1e3 * cg:.0f} us/CG)" if cg else ")"))
         print(" | ".join(out))
