@@ -347,20 +347,35 @@ __device__ __forceinline__ void block_sum(double* v) {
   }
 }
 
+// Cross-block hand-off of the reduction partials without __threadfence():
+// on gfx950 an agent-scope fence is an L2 write-back plus an L2 invalidate
+// (buffer_wbl2 sc1 / buffer_inv sc1) of the whole XCD, paid by every block.
+// The partials are the only data handed over, so they are written and read as
+// agent-scope relaxed atomics (sc1: at the coherence point), and the arrival
+// on the counter waits for the partial store to complete (s_waitcnt) instead.
+__device__ __forceinline__ void partial_put(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double partial_get(double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool arrive_last(unsigned* counter) {
+  __builtin_amdgcn_s_waitcnt(0);  // the partial stores above have completed
+  return __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+}
+
 __device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__ partial,
                                                   unsigned* __restrict__ counter, double* __restrict__ out) {
   __shared__ bool last;
   block_sum<1>(&v);
   if (threadIdx.x == 0) {
-    partial[blockIdx.x] = v;
-    __threadfence();
-    last = (atomicAdd(counter, 1u) == gridDim.x - 1);
+    partial_put(&partial[blockIdx.x], v);
+    last = arrive_last(counter);
   }
   __syncthreads();
   if (!last) return false;
-  __threadfence();
   double acc = 0.0;
-  for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x) acc += __builtin_nontemporal_load(&partial[e]);
+  for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x) acc += partial_get(&partial[e]);
   block_sum<1>(&acc);
   if (threadIdx.x == 0) {
     out[0] = acc;
@@ -378,16 +393,14 @@ __device__ __forceinline__ bool grid_sum3_finalize(double a, double b, double c,
   double v[3] = {a, b, c};
   block_sum<3>(v);
   if (threadIdx.x == 0) {
-    for (int k = 0; k < 3; k++) partial[3 * blockIdx.x + k] = v[k];
-    __threadfence();
-    last = (atomicAdd(counter, 1u) == gridDim.x - 1);
+    for (int k = 0; k < 3; k++) partial_put(&partial[3 * blockIdx.x + k], v[k]);
+    last = arrive_last(counter);
   }
   __syncthreads();
   if (!last) return false;
-  __threadfence();
   double acc[3] = {0.0, 0.0, 0.0};
   for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x)
-    for (int k = 0; k < 3; k++) acc[k] += __builtin_nontemporal_load(&partial[3 * e + k]);
+    for (int k = 0; k < 3; k++) acc[k] += partial_get(&partial[3 * e + k]);
   block_sum<3>(acc);
   for (int k = 0; k < 3; k++) res[k] = acc[k];
   if (threadIdx.x == 0) {
