@@ -69,7 +69,7 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
                                  int32_t iter, hipStream_t s);
 hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
                              hipStream_t s);
-hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, double* out,
+hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, unsigned* counter, double* out,
                            hipStream_t s);
 hipError_t mvba_launch_sum(int64_t n, const double* partial, double* out, hipStream_t s);
 hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int64_t* goff, const int64_t* hoff,
@@ -268,7 +268,7 @@ class Solver {
   }
 
   void dot(int64_t n, const double* a, const double* b, int slot) {
-    HCHK(mvba_launch_dot(n, a, b, S_->partial, S_->scal + slot, s_));
+    HCHK(mvba_launch_dot(n, a, b, S_->partial, S_->cnt + 6, S_->scal + slot, s_));
   }
 
   void prep() {

@@ -729,20 +729,14 @@ __global__ void k_axpby(int64_t n, double a, const double* __restrict__ x, doubl
   if (e < n) out[e] = a * x[e] + (y ? b * y[e] : 0.0);
 }
 
-// partial[block] = sum x.y (256-thread blocks)
-__global__ void __launch_bounds__(256) k_dot(int64_t n, const double* __restrict__ x,
-                                             const double* __restrict__ y, double* __restrict__ partial) {
-  __shared__ double red[256];
+// out[0] = x.y (y null: x.x) in one launch: grid-stride partial sums, last-block finalisation
+__global__ void __launch_bounds__(256) k_dot_fin(int64_t n, const double* __restrict__ x,
+                                                 const double* __restrict__ y, double* __restrict__ partial,
+                                                 unsigned* __restrict__ counter, double* __restrict__ out) {
   double acc = 0.0;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x)
     acc += x[e] * (y ? y[e] : x[e]);
-  red[threadIdx.x] = acc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+  grid_sum_finalize(acc, partial, counter, out);
 }
 
 // out[0] = sum partial[0..n)
@@ -1126,12 +1120,11 @@ hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, con
   return hipGetLastError();
 }
 
-// dot(x, y) -> out (device scalar) via partials[256]
-hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, double* out,
-                           hipStream_t s) {
+// dot(x, y) -> out (device scalar) via partials[256] and a counter (zero, re-armed)
+hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, unsigned* counter,
+                           double* out, hipStream_t s) {
   const int blocks = 256;
-  hipLaunchKernelGGL(mvba::k_dot, dim3(blocks), dim3(256), 0, s, n, x, y, partial);
-  hipLaunchKernelGGL(mvba::k_sum, dim3(1), dim3(256), 0, s, (int64_t)blocks, partial, out);
+  hipLaunchKernelGGL(mvba::k_dot_fin, dim3(blocks), dim3(256), 0, s, n, x, y, partial, counter, out);
   return hipGetLastError();
 }
 
