@@ -353,6 +353,17 @@ __device__ __forceinline__ void block_sum(double* v) {
 // The partials are the only data handed over, so they are written and read as
 // agent-scope relaxed atomics (sc1: at the coherence point), and the arrival
 // on the counter waits for the partial store to complete (s_waitcnt) instead.
+//
+// ISA assumption (gfx950 only; this library is built for gfx950 alone): this is
+// the first row of MI355X_MICROARCH.md's "hand-offs measured with sc1 loads in
+// place of the acquire" table: ONE lane per workgroup stores its partials sc1,
+// waits vmcnt(0) (stores are counted in vmcnt), then adds to ONE unsharded
+// agent-scope counter; the workgroup whose add returned gridDim.x - 1 loads
+// every partial with sc1 loads after a workgroup barrier. The C++ memory model
+// gives no happens-before for relaxed atomics, so the waitcnt is an inline-asm
+// statement with a memory clobber: a compiler barrier that keeps the partial
+// store above it and the counter add below it (the builtin waitcnt is IntrNoMem
+// and would not stop the compiler from reordering the two relaxed atomics).
 __device__ __forceinline__ void partial_put(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -360,8 +371,10 @@ __device__ __forceinline__ double partial_get(double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool arrive_last(unsigned* counter) {
-  __builtin_amdgcn_s_waitcnt(0);  // the partial stores above have completed
-  return __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial stores above have completed
+  const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // partial loads of the last block stay below the add
+  return prev == gridDim.x - 1;
 }
 
 __device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__ partial,

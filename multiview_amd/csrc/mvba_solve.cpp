@@ -197,8 +197,9 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(hipMemset(S->cnt, 0, 8 * sizeof(unsigned)));
     int64_t ncost = 0;
     for (const Group& G : h->groups) ncost = std::max<int64_t>(ncost, (G.seg_count + 3) / 4);
-    S->npartial = std::max<int64_t>({3072, mvba_pass_a_blocks(S->np), ncost, (int64_t)h->ndep_segs,
-                                    (h->ndep_slots + 255) / 256});
+    // k_cg_update: 3 partials per 256-entry block; k_vec_rep_reduce / k_add_diag one
+    S->npartial = std::max<int64_t>({3072, 3 * ((S->ng + 255) / 256), mvba_pass_a_blocks(S->np), ncost,
+                                    (int64_t)h->ndep_segs, (h->ndep_slots + 255) / 256});
     HCHK(dalloc(&S->partial, (size_t)S->npartial));
     HCHK(dalloc(&S->scal, 32));
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hscal), 32 * sizeof(double)));

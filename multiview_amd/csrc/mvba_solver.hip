@@ -1099,7 +1099,7 @@ hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, 
   return hipGetLastError();
 }
 
-// partial needs 3 x 1024 doubles, counters 3 (zero-initialised, re-armed by the kernel)
+// partial needs 3 x ceil(n / 256) doubles, counters 3 (zero-initialised, re-armed by the kernel)
 hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const double* minv, int32_t mode, double alpha,
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
@@ -1107,7 +1107,6 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
                                  int32_t iter, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 255) / 256);
-  if (blocks > 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks), dim3(256), 0, s, n, ent, minv, mode, alpha,
                      p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter);
   return hipGetLastError();

@@ -122,6 +122,23 @@ class Evaluator:
         _lib.check(self.lib.mvba_residual_order(self.h, out.ctypes.data), self.h)
         return out
 
+    def depth_order(self) -> np.ndarray:
+        """device depth slot -> depth insertion index (-1 = padding slot)."""
+        out = np.empty(self.num_depth_slots, dtype=np.int64)
+        _lib.check(self.lib.mvba_depth_order(self.h, out.ctypes.data), self.h)
+        return out
+
+    def evaluate_depth_device(self, jacobian: bool = True, residuals=None, jac=None, ld: int = 0,
+                              stream=None, phase: int = 0):
+        """Asynchronous device evaluation of the depth blocks into caller-owned
+        torch planes [3, ld] / [DJAC_ROWS, ld] (float64 or float32)."""
+        flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0) | phase
+        f32 = str(residuals.dtype) == "torch.float32"
+        fn = self.lib.mvba_evaluate_depth_device_f32 if f32 else self.lib.mvba_evaluate_depth_device
+        st = fn(self.h, flags, 0.0, C.c_void_p(residuals.data_ptr()),
+                C.c_void_p(jac.data_ptr()) if jac is not None else None, int(ld), C.c_void_p(stream or 0))
+        _lib.check(st, self.h)
+
     def eval_bytes(self, jacobian: bool = True) -> float:
         flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0)
         return float(self.lib.mvba_eval_bytes(self.h, flags))
@@ -190,6 +207,13 @@ class Evaluator:
         (mvba_solve; ceres::Solve replacement). Keyword arguments override
         fields of mvba_solver_default_options. Returns the summary as a dict;
         the solution stays in the handle (get_params)."""
+        if options is None:
+            n = self.problem.params.size
+            for k in ("lower_bounds", "upper_bounds"):
+                v = kw.get(k)
+                if v is not None and np.asarray(v).size != n:
+                    # the library reads num_param_doubles values from each bound array
+                    raise ValueError(f"{k} has {np.asarray(v).size} values, the packed parameter vector {n}")
         o = options or default_solver_options(**kw)
         s = _lib.SolverSummary()
         st = self.lib.mvba_solve(self.h, C.byref(o), C.byref(s), C.c_void_p(stream or 0))

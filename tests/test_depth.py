@@ -15,7 +15,7 @@ import pytest
 
 from multiview_amd import _lib, rig
 from multiview_amd.evaluator import Evaluator
-from multiview_amd.problem import normal_equations_reference
+from oracle.normal_equations import normal_equations_reference
 
 
 def _rig(affine=False, seed=3, **kw):

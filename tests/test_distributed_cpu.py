@@ -48,7 +48,7 @@ CFG = dict(num_sensors=3, num_ref=12, num_points=400, obs_per_point=5, models=["
 
 
 def _linearize(P):
-    from multiview_amd.problem import normal_equations_reference
+    from oracle.normal_equations import normal_equations_reference
     from oracle import oracle_py
 
     L = _Layout.of(P)

@@ -8,7 +8,7 @@ import pytest
 
 from multiview_amd import rig
 from multiview_amd.evaluator import Evaluator
-from multiview_amd.problem import normal_equations_reference
+from oracle.normal_equations import normal_equations_reference
 
 pytestmark = pytest.mark.gpu
 

@@ -62,6 +62,57 @@ def test_one_exact_step_matches_dense_lm(use_loss):
     assert np.array_equal(x[~m], P.params[~m])
 
 
+def test_one_exact_step_multiblock_camera_side():
+    """Camera side wide enough that the CG vector kernels (k_vec_rep_reduce,
+    k_cg_update, 256 entries per block) and the reductions they finalise run on
+    many blocks: --no_rig with the non-reference sensors' image poses floating
+    (about 2,100 camera-side unknowns = 9 blocks). One exact-CG LM step equals
+    the dense step (relative 1e-8), with and without the Cauchy loss."""
+    from oracle import lm_reference
+
+    R = rig.make_rig(num_sensors=3, num_ref=150, num_points=1000, obs_per_point=8, models=["radtan", "fov", "none"],
+                     seed=91)
+    P = rig.build_problem(R, rig.FloatFlags(no_rig=True, camera_poses_to_float=("cam1", "cam2"),
+                                            float_timestamp_offsets=False))
+    with Evaluator(P) as ev:
+        ng = ev.lin_layout()["cam_grad_size"]
+    assert ng > 8 * 256, ng
+    for use_loss in (False, True):
+        x_ref, s_ref = lm_reference.solve(P, max_num_iterations=1, use_loss=use_loss, **TOL)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=4000, use_loss=int(use_loss),
+                         robust_threshold=3.0, **TOL)
+            x = ev.get_params()
+        assert np.isclose(s["initial_cost"], s_ref["initial_cost"], rtol=1e-11)
+        assert s["num_iterations"] == 1
+        m = _free_mask(P)
+        assert _close(x[m], x_ref[m], 1e-8), (use_loss, np.abs(x[m] - x_ref[m]).max())
+
+
+def test_camera_side_past_1024_blocks():
+    """More than 1024 blocks' worth of camera-side unknowns (--no_rig, every
+    image pose floating: about 283k unknowns): the CG kernels' grid reductions
+    run with >1024 partials (their partial buffer is sized from the camera
+    side). One LM iteration: no failure, and the step removes most of the
+    perturbation's cost (the initial values are the truth perturbed by 1 cm /
+    0.1 deg poses and 2 cm points)."""
+    R = rig.make_rig(num_sensors=3, num_ref=13500, num_points=120000, obs_per_point=10,
+                     models=["radtan"] * 3, seed=93, window=12)
+    P = rig.build_problem(R, rig.FloatFlags(no_rig=True, camera_poses_to_float=("ref_cam", "cam1", "cam2"),
+                                            float_timestamp_offsets=False))
+    with Evaluator(P) as ev:
+        ng = ev.lin_layout()["cam_grad_size"]
+        assert ng > 1024 * 256, ng
+        ev.set_params()
+        s = ev.solve(max_num_iterations=2, use_loss=1, robust_threshold=3.0, **TOL)
+        x = ev.get_params()
+    assert s["termination_type"] != 2, s["message"]
+    assert s["num_linear_iterations"] > 0 and s["num_successful_steps"] >= 2
+    assert s["final_cost"] < 0.2 * s["initial_cost"], (s["initial_cost"], s["final_cost"])
+    assert np.all(np.isfinite(x))
+
+
 def _poses(P, x):
     """Free 7-parameter blocks as (t, q/|q| with qw >= 0): the cost only sees the
     normalized quaternion (array_to_rigid_transform, dense_map_utils.cc:171-178),

@@ -10,7 +10,7 @@ import pytest
 
 from multiview_amd import _lib, rig
 from multiview_amd.evaluator import Evaluator
-from multiview_amd.problem import normal_equations_reference
+from oracle.normal_equations import normal_equations_reference
 
 TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
 
