@@ -10,11 +10,13 @@ analytic Jacobian kernel (K1), outputs written to HBM (materialised Ceres
 columns).
 
 Multi-GPU (one process per GPU, torchrun): observations are sharded by
-landmark range; each rank owns a c2-sized shard of a global
-problem with N x 100k landmarks over the same cameras. Evaluation has no
-data-path collective ("scaling": "weak"); value = all ranks' evals / max time.
---config c4 is the exception: its 5M landmarks / 50M observations are the whole
-job, split into N landmark ranges ("scaling": "strong").
+landmark range. The headline is STRONG scaling: the config's
+landmarks (c2: 100k landmarks / 1M observations) are the whole job, split into
+N contiguous landmark ranges; evaluation has no data-path collective; value =
+all ranks' evals / max time. With N > 1 a "weak" object adds the weak-scaling
+line (each rank owns a config-sized shard of an N x larger problem). The LM
+phase exchanges through the library's RCCL communicator (mvba_comm, stream-
+ordered ncclAllReduce on the solver's stream).
 
 Also reported: "roofline" of the dominant kernel (K1, radtan) from HIP events on
 its launch stream, and "cpu_baseline" = the oracle's Ceres-1.14-style central
@@ -36,7 +38,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-STRONG_CONFIGS = ("c4",)  # landmark count is the whole job's (strong scaling); others are per GPU
 FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (= fp64 matrix) peak, AMD product specification
 CPU_THREADS = 16       # reference default --num_opt_threads (rig_calibrator.cc:256)
 
@@ -52,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=0, help="residuals in the CPU sample (0 = auto)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (rehearsal of the multi-rank path on one GPU)")
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
+                    help="strong (default): the config is the whole job, split over the ranks; "
+                         "weak: every rank owns a config-sized shard")
     return ap.parse_args()
 
 
@@ -70,6 +74,16 @@ def _time_numdiff(oracle_py, problem, n, threads, min_seconds):
             return done / dt, passes, dt
 
 
+def _cgroup_cpu_quota():
+    """CPUs granted by the cgroup v2 quota (cpu.max 'quota period'), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else max(1, int(-(-int(q) // int(p))))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(problem, sample: int, min_seconds: float = 10.0):
     """Oracle (port of the reference evaluator: per-residual functor + Ceres
     central differences) on the first `sample` residual blocks, timed at the
@@ -82,12 +96,15 @@ def cpu_baseline(problem, sample: int, min_seconds: float = 10.0):
     oracle_py.load()
     nproc = os.cpu_count() or 1
     usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    quota = _cgroup_cpu_quota()
+    if quota:
+        usable = min(usable, quota)
     runs = {}
-    for threads in sorted({CPU_THREADS, usable}):
+    for threads in sorted({CPU_THREADS, usable, nproc}):
         runs[threads] = _time_numdiff(oracle_py, problem, n, threads, min_seconds)
     best = max(runs, key=lambda t: runs[t][0])
     v16 = runs[CPU_THREADS]
-    vall = runs[usable]
+    vall = runs[nproc]
     # the oracle's analytic evaluator on the same sample ("also
     # report the build's analytic CPU evaluator on the same cores"), ~3 s
     t1 = time.perf_counter()
@@ -99,14 +116,14 @@ def cpu_baseline(problem, sample: int, min_seconds: float = 10.0):
         if adt >= 3.0 or adone >= 64 * n:
             break
     return {"value": runs[best][0], "unit": "evals/s", "cores": best, "kind": "port",
-            "nproc": nproc, "usable_cores": usable,
-            "value_16_threads": v16[0], "value_all_cores": vall[0],
+            "nproc": nproc, "usable_cores": usable, "cgroup_cpu_quota": quota,
+            "value_16_threads": v16[0], "value_nproc_threads": vall[0],
             "sample": f"{runs[best][1]} pass(es) over {n} of {problem.num_residuals} residual blocks of the "
                       f"same workload: oracle NUMDIFF = per-block functor + Ceres 1.14 central "
                       f"differences (1 + 2*n_free calls per block), {best} OpenMP threads, "
                       f"{runs[best][2]:.1f} s; also timed at "
                       + ", ".join(f"{t} threads: {runs[t][0]:.3e} evals/s" for t in sorted(runs))
-                      + f" (nproc {nproc}, {usable} cores usable by this process)",
+                      + f" (nproc {nproc}; affinity/cgroup quota leave {usable} cores to this process)",
             "analytic_value": adone / adt,
             "analytic_sample": f"oracle ANALYTIC (exact derivative, dual numbers) over the same {n} blocks, "
                                f"{best} threads, {adt:.1f} s"}
@@ -188,66 +205,76 @@ def main():
 
     cfg = dict(rig.CONFIGS[args.config])
     npts = cfg["num_points"]
-    strong = args.config in STRONG_CONFIGS
-    if strong:
-        # the config's landmark count is the whole problem, split into contiguous
-        # landmark ranges (c4: 5M landmarks / 50M observations over the node)
-        lo, hi = rank * npts // world, (rank + 1) * npts // world
-        cfg["point_range"] = (lo, hi)
-    else:
-        # each rank owns a config-sized shard of an N x larger problem
-        cfg["point_range"] = (rank * npts, (rank + 1) * npts)
+    flags = rig.FloatFlags(**rig.CONFIG_FLAGS.get(args.config, {}))
+    strong = args.scaling == "strong"
+
+    def shard_cfg(strong_split):
+        c = dict(cfg)
+        if strong_split:
+            # the config's landmark count is the whole problem, split into
+            # contiguous landmark ranges
+            c["point_range"] = (rank * npts // world, (rank + 1) * npts // world)
+        else:
+            # each rank owns a config-sized shard of an N x larger problem
+            c["point_range"] = (rank * npts, (rank + 1) * npts)
+        return c
+
     t0 = time.perf_counter()
-    R = rig.make_rig(**cfg)
-    P = rig.build_problem(R, rig.FloatFlags(**rig.CONFIG_FLAGS.get(args.config, {})))
+    R = rig.make_rig(**shard_cfg(strong))
+    P = rig.build_problem(R, flags)
     t_gen = time.perf_counter() - t0
+
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def time_eval(ev):
+        """W warm-up + K timed evaluation steps (barrier + synchronize on both
+        sides, max over ranks). Returns (max seconds, all ranks' evals, prep ms,
+        K1 ms, planes)."""
+        n = ev.num_residuals
+        ld = ev.ld
+        res = torch.empty((2, ld), dtype=torch.float64, device="cuda")
+        jac = torch.empty((ev.stride, ld), dtype=torch.float64, device="cuda")
+
+        def step(events=None):
+            if events is None:
+                ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh)
+            else:
+                events[0].record(stream)
+                ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh, phase=_lib.EVAL_PREP_ONLY)
+                events[1].record(stream)
+                ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh, phase=_lib.EVAL_SKIP_PREP)
+                events[2].record(stream)
+
+        for _ in range(args.warmup):
+            step()
+        ev.sync(sh)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        ev.sync(sh)  # raises on device-side errors (alpha out of range)
+        prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        obs_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tot = torch.tensor([float(n)], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        del res, jac
+        return float(t.item()), float(tot.item()) * args.steps, prep_ms, obs_ms
 
     ev = Evaluator(P, device=dev)
     ev.set_params()
     n = ev.num_residuals
-    ld = ev.ld
-    res = torch.empty((2, ld), dtype=torch.float64, device="cuda")
-    jac = torch.empty((ev.stride, ld), dtype=torch.float64, device="cuda")
-    stream = torch.cuda.current_stream()
-    sh = stream.cuda_stream
-
-    def step(events=None):
-        if events is None:
-            ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh)
-        else:
-            events[0].record(stream)
-            ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh, phase=_lib.EVAL_PREP_ONLY)
-            events[1].record(stream)
-            ev.evaluate_device(True, residuals=res, jac=jac, ld=ld, stream=sh, phase=_lib.EVAL_SKIP_PREP)
-            events[2].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    ev.sync(sh)
-
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    ev.sync(sh)  # raises on device-side errors (alpha out of range)
-
-    prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    obs_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
-
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    tot = torch.tensor([float(n)], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    dt_max = float(t.item())
-    total_evals = float(tot.item()) * args.steps
+    dt_max, total_evals, prep_ms, obs_ms = time_eval(ev)
 
     bytes_eval = ev.eval_bytes(True)                 # algorithmic bytes of K1 per launch set
     achieved = bytes_eval / (obs_ms * 1e-3) / 1e9    # GB/s
@@ -266,7 +293,7 @@ def main():
         "data": "synthetic (deterministic rig generator, multiview_amd/rig.py)",
         "config": {
             "workload": f"{args.config}: {cfg['num_sensors']}-sensor rig, "
-                        + (f"{npts} landmarks split over {world} shard(s), " if strong
+                        + (f"{npts} landmarks split over {world} landmark-range shard(s), " if strong
                            else f"{npts} landmarks x {world} shard(s), ")
                         + f"{n} obs/GPU, "
                         f"{cfg['models'][0]} distortion, all blocks floating, fp64",
@@ -341,6 +368,7 @@ def main():
 
     # ---- fp32 evaluation (config c5 is quoted "fp32 eval / fp64 solve"): the same
     # fp64 arithmetic, outputs rounded to float at the store (half the output bytes)
+    ld = ev.ld
     res32 = torch.empty((2, ld), dtype=torch.float32, device="cuda")
     jac32 = torch.empty((ev.stride, ld), dtype=torch.float32, device="cuda")
     for _ in range(args.warmup):
@@ -460,11 +488,16 @@ def main():
 
     # ---- phase C: Levenberg-Marquardt (mvba_solve: ITERATIVE_SCHUR replacement)
     if L["supported"] and args.ba_iters > 0:
-        from multiview_amd.dist import SolverExchange
+        from multiview_amd.dist import Comm, SolverExchange
 
-        ex = SolverExchange(device=dev) if world > 1 else None
+        comm = ex = None
+        if world > 1:
+            if args.dist_backend == "nccl":
+                comm = Comm.rccl(dev)       # library-native RCCL, stream-ordered exchange
+            else:
+                ex = SolverExchange(device=dev)  # gloo rehearsal: host-staged exchange
         solve_kw = dict(max_num_iterations=args.ba_iters, function_tolerance=0.0, gradient_tolerance=0.0,
-                        parameter_tolerance=0.0, use_loss=1, robust_threshold=3.0, allreduce=ex)
+                        parameter_tolerance=0.0, use_loss=1, robust_threshold=3.0, allreduce=ex, comm=comm)
         ev.set_params()
         ev.solve(**dict(solve_kw, max_num_iterations=1), stream=sh)  # allocation + warm-up
         ev.set_params()
@@ -496,7 +529,27 @@ def main():
             "eval_s": s["eval_time_s"],
             "initial_cost": s["initial_cost"],
             "final_cost": s["final_cost"],
-            "exchange_calls": ex.calls if ex else 0,
+            "exchange": ("rccl (mvba_comm_allreduce, stream-ordered)" if comm else
+                         "gloo (host-staged callback)" if ex else "none (single rank)"),
+            "exchange_calls": ex.calls if ex else None,
+        }
+        if comm is not None:
+            comm.close()
+
+    # ---- N > 1: the weak-scaling line as well (config-sized shard per rank)
+    if world > 1 and strong:
+        ev.close()
+        Rw = rig.make_rig(**shard_cfg(False))
+        Pw = rig.build_problem(Rw, flags)
+        ev = Evaluator(Pw, device=dev)
+        ev.set_params()
+        wdt, wtot, _, w_obs_ms = time_eval(ev)
+        line["weak"] = {
+            "what": f"weak scaling: every rank owns a {args.config}-sized shard of a {world} x larger problem",
+            "value": wtot / wdt,
+            "ms_per_step": 1e3 * wdt / args.steps,
+            "num_residuals_per_gpu": ev.num_residuals,
+            "kernel_ms": w_obs_ms,
         }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

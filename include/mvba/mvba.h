@@ -399,14 +399,45 @@ double mvba_eval_bytes(const struct mvba_handle* h, int32_t flags);
  * Sharded solves: each rank's handle holds all camera-side
  * blocks and the observations of its landmark range; `allreduce` (non-null)
  * is called with an in-place device buffer to sum (op MVBA_REDUCE_SUM) or max
- * (MVBA_REDUCE_MAX) across ranks. The library synchronises its stream before
- * the call; the callback must return with the result in the buffer (e.g.
- * ncclAllReduce + stream sync, or torch.distributed.all_reduce). It is called
- * once per linearization (camera gradient + block Hessians + cost), once per
- * CG iteration (the reduced-system product) and for a few scalars per step. */
+ * (MVBA_REDUCE_MAX) across ranks. The call is STREAM-ORDERED: the library
+ * does not synchronise before it, and the reduction must be enqueued on
+ * hip_stream so that work enqueued after the call sees the result (e.g.
+ * ncclAllReduce on that stream: mvba_comm_allreduce below). A callback that
+ * works on the host must synchronise hip_stream itself before reading the
+ * buffer and leave the result there before returning. Every rank must obtain
+ * bit-identical results (the camera-side CG state is replicated and its
+ * device-side stopping decisions must agree, or the collectives fall out of
+ * step). It is called once per linearization (camera gradient + block
+ * Hessians + cost), once per CG iteration (the reduced-system product, also
+ * for iterations the device has gated off past the CG stop) and for a few
+ * scalars per LM step. */
 enum { MVBA_REDUCE_SUM = 0, MVBA_REDUCE_MAX = 1 };
 typedef int32_t (*mvba_allreduce_fn)(double* device_buf, int64_t count, int32_t op, void* hip_stream,
                                      void* user);
+
+/* Communicators for sharded solves (mvba_comm.hip). Pass
+ * `allreduce = mvba_comm_allreduce, allreduce_user = comm` in the solver
+ * options.
+ *   RCCL, one process per GPU: rank 0 calls mvba_comm_unique_id and the caller
+ *   broadcasts the MVBA_COMM_ID_BYTES bytes (e.g. torch.distributed); every
+ *   rank then calls mvba_comm_init_rccl (collective: blocks until all joined).
+ *   Local, several shards in one process (one host thread and one HIP stream
+ *   per shard; shards may share a device): mvba_comm_init_local fills
+ *   comms[nranks]; the all-reduce meets the other shards' threads at enqueue
+ *   time only and sums the shards' buffers on the device in rank order.
+ * mvba_comm_abort releases every rank of a failed solve (RCCL: ncclCommAbort;
+ * local: the waiting threads return failure). */
+#define MVBA_COMM_ID_BYTES 128
+typedef struct mvba_comm mvba_comm;
+mvba_status mvba_comm_unique_id(uint8_t* id /* [MVBA_COMM_ID_BYTES] */);
+mvba_status mvba_comm_init_rccl(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, mvba_comm** out);
+mvba_status mvba_comm_init_local(int32_t nranks, const int32_t* devices, mvba_comm** comms /* [nranks] */);
+mvba_status mvba_comm_abort(mvba_comm* comm);
+void mvba_comm_destroy(mvba_comm* comm);
+int32_t mvba_comm_rank(const mvba_comm* comm);
+int32_t mvba_comm_size(const mvba_comm* comm);
+const char* mvba_comm_error(void);
+int32_t mvba_comm_allreduce(double* device_buf, int64_t count, int32_t op, void* hip_stream, void* comm);
 
 enum { MVBA_CONVERGENCE = 0, MVBA_NO_CONVERGENCE = 1, MVBA_FAILURE = 2 };
 

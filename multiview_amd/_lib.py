@@ -262,7 +262,18 @@ SIGNATURES = {
     "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
     "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),
     "mvba_get_params": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mvba_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "mvba_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "mvba_comm_init_local": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
+    "mvba_comm_abort": (C.c_int, [C.c_void_p]),
+    "mvba_comm_destroy": (None, [C.c_void_p]),
+    "mvba_comm_rank": (C.c_int32, [C.c_void_p]),
+    "mvba_comm_size": (C.c_int32, [C.c_void_p]),
+    "mvba_comm_error": (C.c_char_p, []),
+    "mvba_comm_allreduce": (C.c_int32, [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_void_p]),
 }
+
+COMM_ID_BYTES = 128
 
 _lib = None
 

@@ -12,7 +12,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmvba.so")
 SOURCES = ["mvba_kernels.hip", "mvba_solver.hip", "mvba_depth.hip", "mvba_stats.hip", "mvba_tracks.hip", "mvba_rpc.hip",
-           "mvba_host.cpp", "mvba_solve.cpp"]
+           "mvba_comm.hip", "mvba_host.cpp", "mvba_solve.cpp"]
+# RCCL for the sharded solve's stream-ordered all-reduce (mvba_comm.hip). In a
+# torch process the already loaded librccl.so.1 (same SONAME) is the one used.
+LIBS = ["-L/opt/rocm/lib", "-lrccl"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wall",
          "-Wno-unused-function"]
@@ -32,7 +35,7 @@ def build(verbose: bool = False) -> str:
             subprocess.run(cmd, check=True)
         objs.append(obj)
     if not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fopenmp", "-o", OUT] + objs
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fopenmp", "-o", OUT] + objs + LIBS
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -619,66 +619,6 @@ static void check(mvba_handle* h, mvba_status st) {
   if (st != MVBA_OK) fatal(handle_error(h, st));
 }
 
-// Host all-reduce across the shards' solver threads (one GPU each): device ->
-// host staging, a barrier, the same rank-ordered sum on every rank, a barrier,
-// host -> device. Used only with --num_gpus > 1 in one process.
-struct HostAllreduce {
-  int n;
-  std::mutex m;
-  std::condition_variable cv;
-  int arrived = 0;
-  long gen = 0;
-  bool aborted = false;
-  std::vector<std::vector<double>> stage;
-  explicit HostAllreduce(int n_) : n(n_), stage((size_t)n_) {}
-  bool barrier() {
-    std::unique_lock<std::mutex> lk(m);
-    if (aborted) return false;
-    const long g = gen;
-    if (++arrived == n) {
-      arrived = 0;
-      gen++;
-      cv.notify_all();
-      return true;
-    }
-    cv.wait(lk, [&] { return gen != g || aborted; });
-    return !aborted;
-  }
-  void abort() {
-    std::lock_guard<std::mutex> lk(m);
-    aborted = true;
-    cv.notify_all();
-  }
-};
-struct RankCtx {
-  HostAllreduce* ar;
-  int rank;
-};
-
-static int32_t host_allreduce(double* dbuf, int64_t count, int32_t op, void* /*stream*/, void* user) {
-  auto* c = (RankCtx*)user;
-  HostAllreduce& ar = *c->ar;
-  auto& mine = ar.stage[(size_t)c->rank];
-  mine.resize((size_t)count);
-  if (hipMemcpy(mine.data(), dbuf, (size_t)count * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
-    ar.abort();
-    return 1;
-  }
-  if (!ar.barrier()) return 1;
-  std::vector<double> out(ar.stage[0]);
-  for (int r = 1; r < ar.n; r++) {
-    const auto& o = ar.stage[(size_t)r];
-    for (int64_t k = 0; k < count; k++)
-      out[(size_t)k] = op == MVBA_REDUCE_MAX ? std::max(out[(size_t)k], o[(size_t)k]) : out[(size_t)k] + o[(size_t)k];
-  }
-  if (!ar.barrier()) return 1;
-  if (hipMemcpy(dbuf, out.data(), (size_t)count * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
-    ar.abort();
-    return 1;
-  }
-  return 0;
-}
-
 using Clock = std::chrono::steady_clock;
 static double secs(Clock::time_point a) { return std::chrono::duration<double>(Clock::now() - a).count(); }
 
@@ -1194,8 +1134,22 @@ static int run(int argc, char** argv) {
 
     // Solve (:1910-1919)
     t0 = Clock::now();
-    HostAllreduce ar(ngpu);
-    std::vector<RankCtx> ctx((size_t)ngpu);
+    // --num_gpus > 1: one solver thread and HIP stream per shard; the exchange
+    // steps are stream-ordered device all-reduces over a local communicator
+    // (mvba_comm_init_local: shards may share a device)
+    std::vector<mvba_comm*> comms((size_t)ngpu, nullptr);
+    std::vector<hipStream_t> streams((size_t)ngpu, nullptr);
+    if (ngpu > 1) {
+      std::vector<int32_t> devs((size_t)ngpu);
+      for (int s = 0; s < ngpu; s++) devs[(size_t)s] = shards[(size_t)s].device;
+      if (mvba_comm_init_local(ngpu, devs.data(), comms.data()) != MVBA_OK)
+        fatal(std::string("mvba_comm_init_local: ") + mvba_comm_error());
+      for (int s = 0; s < ngpu; s++) {
+        if (hipSetDevice(devs[(size_t)s]) != hipSuccess ||
+            hipStreamCreateWithFlags(&streams[(size_t)s], hipStreamNonBlocking) != hipSuccess)
+          fatal("hipStreamCreate failed");
+      }
+    }
     auto solve_one = [&](int s) {
       Shard& S = shards[(size_t)s];
       mvba_solver_options o;
@@ -1210,14 +1164,13 @@ static int run(int argc, char** argv) {
       o.upper_bounds = S.blocks.hi.data();
       o.progress_to_stdout = s == 0 ? 1 : 0;
       if (ngpu > 1) {
-        ctx[(size_t)s] = {&ar, s};
-        o.allreduce = host_allreduce;
-        o.allreduce_user = &ctx[(size_t)s];
+        o.allreduce = mvba_comm_allreduce;
+        o.allreduce_user = comms[(size_t)s];
       }
-      S.status = mvba_solve(S.h, &o, &S.summary, nullptr);
+      S.status = mvba_solve(S.h, &o, &S.summary, streams[(size_t)s]);
       if (S.status != MVBA_OK) {
         S.error = handle_error(S.h, S.status);
-        ar.abort();
+        if (comms[(size_t)s]) mvba_comm_abort(comms[(size_t)s]);  // release the other shards
       }
     };
     if (ngpu == 1) {
@@ -1226,6 +1179,11 @@ static int run(int argc, char** argv) {
       std::vector<std::thread> th;
       for (int s = 0; s < ngpu; s++) th.emplace_back(solve_one, s);
       for (auto& x : th) x.join();
+    }
+    for (int s = 0; s < ngpu && ngpu > 1; s++) {
+      (void)hipStreamSynchronize(streams[(size_t)s]);
+      (void)hipStreamDestroy(streams[(size_t)s]);
+      mvba_comm_destroy(comms[(size_t)s]);
     }
     for (auto& S : shards)
       if (S.status != MVBA_OK) fatal(S.error);

@@ -61,7 +61,8 @@ hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* di
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
                                       mvba::CgCtl* ctl, hipStream_t s);
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
-                                unsigned* counter, double* dot_out, hipStream_t s);
+                                unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
+                                hipStream_t s);
 hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const double* minv, int32_t mode, double alpha,
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
@@ -254,9 +255,10 @@ class Solver {
   int pa_model() const { return single_model_ ? h_->groups[0].model : -1; }
   int pa_deg() const { return single_model_ ? h_->groups[0].deg : 0; }
 
+  // Cross-rank sum / max of a device buffer, stream-ordered (mvba_allreduce_fn:
+  // enqueued on s_, no host wait here).
   void exchange(double* buf, int64_t n, int32_t op) {
     if (!o_.allreduce || n <= 0) return;
-    HCHK(hipStreamSynchronize(s_));
     if (o_.allreduce(buf, n, op, (void*)s_, o_.allreduce_user) != 0)
       throw StatusErr{MVBA_E_INVALID, "allreduce callback failed"};
   }
@@ -337,9 +339,9 @@ class Solver {
 
   // pass B over every model group into the replicas, then y = sum of replicas.
   // Single rank: damping and the x.y dot are fused into the replica reduction
-  // (dot -> scal[dot_slot]); sharded: cross-rank sum of y first.
-  // gate: device CG stop flag (nullptr: always run); ctl: CG step-length logic
-  // in the finalising block of the x.y reduction (single rank only)
+  // (dot -> scal[dot_slot]); sharded: cross-rank sum of y first (stream-ordered),
+  // then damping + dot. gate: device CG stop flag (nullptr: always run); ctl:
+  // CG step-length logic in the finalising block of the x.y reduction
   // dir: the frame directions of xv (null: pass B with x = 0, u_o = -J_pt w_p)
   void reduce_frames(double* y, const double* xv, int dot_slot, const double* dir, const int32_t* gate = nullptr,
                      mvba::CgCtl* ctl = nullptr) {
@@ -358,7 +360,8 @@ class Solver {
                                     s_));
     exchange(y, S_->ng, MVBA_REDUCE_SUM);
     if (xv && !fuse)
-      HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, s_));
+      HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, gate, ctl,
+                                s_));
   }
 
   // w_p = (V + D)^-1 (tinit + sum J_pt^T J_cam x) into wbuf (dir: frame
@@ -405,82 +408,11 @@ class Solver {
     int status = 0;  // 0 success, 1 no convergence (usable), 2 failure
   };
 
-  // PCG on S delta_c = b (conjugate_gradients_solver.cc [ext]). Device-side
-  // scalars: per iteration two host reads (p'q; then x'b, x'r, r'z together).
-  CgResult cg() {
-    CgResult R;
-    const int64_t n = S_->ng;
-    double* xv = S_->delta;
-    HCHK(hipMemsetAsync(xv, 0, (size_t)std::max<int64_t>(n, 1) * sizeof(double), s_));
-    if (n == 0) return R;
-    dot(n, S_->b, S_->b, 0);
-    const double norm_b = std::sqrt(fetch(1)[0]);
-    if (norm_b == 0.0) return R;
-    // r is double-buffered: each update reads S_->r and writes S_->r2, then they swap
-    auto upd = [&](int32_t mode, double alpha, const double* q) {
-      HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, alpha, S_->p, q, S_->b, xv,
-                                 S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, nullptr, 0, s_));
-      std::swap(S_->r, S_->r2);
-    };
-    // r = b (x = 0); z = M^-1 r; rho = r'z. Q0 = -x'(b + r) = 0
-    upd(4 | 8, 0.0, nullptr);
-    double rho_next = fetch(11)[10];
-    double Q0 = 0.0, rho = 1.0;
-    auto bad = [](double v) { return v == 0.0 || std::isinf(v) || std::isnan(v); };
-    for (int i = 1;; i++) {
-      R.iters = i;
-      const double last_rho = rho;
-      rho = rho_next;
-      if (bad(rho)) {
-        R.status = 2;
-        break;
-      }
-      // p = z (i = 1) or z + beta p, formed by the frame-direction kernel
-      mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, nullptr, i == 1 ? 1 : 0, 0.0};
-      if (i > 1) {
-        lz.beta = rho / last_rho;
-        if (bad(lz.beta)) {
-          R.status = 2;
-          break;
-        }
-      }
-      std::swap(S_->p, S_->p2);
-      apply_schur(S_->p, S_->q, 0, nullptr, nullptr, &lz);
-      const double pq = fetch(1)[0];
-      if (pq <= 0.0 || std::isinf(pq) || std::isnan(pq)) {
-        R.status = 1;  // "Matrix is indefinite": NO_CONVERGENCE, x kept
-        break;
-      }
-      const double alpha = rho / pq;
-      if (std::isinf(alpha)) {
-        R.status = 2;
-        break;
-      }
-      if (i % 10 == 0) {  // residual reset: r = b - A x
-        upd(1, alpha, S_->q);
-        apply_schur(xv, S_->tmp, 1);
-        upd(4 | 8, 0.0, S_->tmp);
-      } else {
-        upd(1 | 2 | 8, alpha, S_->q);
-      }
-      const double* hs = fetch(11);
-      const double Q1 = -(hs[8] + hs[9]);
-      rho_next = hs[10];
-      const double zeta = i * (Q1 - Q0) / Q1;
-      if (zeta < o_.eta && i >= o_.min_linear_solver_iterations) break;
-      Q0 = Q1;
-      if (i >= o_.max_linear_solver_iterations) {
-        R.status = 1;
-        break;
-      }
-    }
-    return R;
-  }
-
-  // The same PCG with every scalar step on the device (CgCtl): iterations are
-  // enqueued in batches and gated by ctl->done, one host read per batch
-  // instead of two per iteration. Single rank only (the all-reduce callback
-  // needs the host between kernels).
+  // PCG on S delta_c = b (conjugate_gradients_solver.cc [ext]) with every
+  // scalar step on the device (CgCtl): iterations are enqueued in batches and
+  // gated by ctl->done, one host read per batch. Sharded solves run the same
+  // loop: the per-iteration exchange of the product is stream-ordered and the
+  // replicated camera-side state gives every rank the same stopping decisions.
   CgResult cg_device() {
     CgResult R;
     const int64_t n = S_->ng;
@@ -884,7 +816,7 @@ void Solver::run(mvba_solver_summary* sum) {
     HCHK(mvba_launch_block_prec(S_->nblocks, S_->max_bsize, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->dmp,
                                 S_->fac, s_));
     schur_rhs();
-    const CgResult cgr = o_.allreduce ? cg() : cg_device();
+    const CgResult cgr = cg_device();
     sum->num_linear_iterations += cgr.iters;
     bool valid = cgr.status != 2;
     double mcc = 0.0;

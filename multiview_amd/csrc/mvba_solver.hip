@@ -568,6 +568,23 @@ __global__ void __launch_bounds__(64) k_pass_b(
 
 // y = sum_r yrep[r] (replicas re-zeroed); with diag: y += diag .* x; with dot_out
 // the grid also reduces x.y into dot_out (p'q when no cross-rank exchange follows).
+// CG step length (conjugate_gradients_solver.cc [ext]): pq <= 0 -> "Matrix is
+// indefinite" (NO_CONVERGENCE, x kept); alpha = rho / pq, inf -> failure
+__device__ __forceinline__ void cg_step_length(CgCtl* ctl, double pq) {
+  ctl->first = 0;
+  if (pq <= 0.0 || isinf(pq) || isnan(pq)) {
+    ctl->status = 1;
+    ctl->done = 1;
+  } else {
+    const double alpha = ctl->rho / pq;
+    ctl->alpha = alpha;
+    if (isinf(alpha)) {
+      ctl->status = 2;
+      ctl->done = 1;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yrep, int64_t n,
                                                         const double* __restrict__ diag,
                                                         const double* __restrict__ x, double* __restrict__ y,
@@ -592,30 +609,19 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
     y[e] = acc;
     d = x ? x[e] * acc : 0.0;
   }
-  if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0) {
-    // CG step length (conjugate_gradients_solver.cc [ext]): pq <= 0 -> "Matrix
-    // is indefinite" (NO_CONVERGENCE, x kept); alpha = rho / pq, inf -> failure
-    const double pq = dot_out[0];
-    ctl->first = 0;
-    if (pq <= 0.0 || isinf(pq) || isnan(pq)) {
-      ctl->status = 1;
-      ctl->done = 1;
-    } else {
-      const double alpha = ctl->rho / pq;
-      ctl->alpha = alpha;
-      if (isinf(alpha)) {
-        ctl->status = 2;
-        ctl->done = 1;
-      }
-    }
-  }
+  if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
+    cg_step_length(ctl, dot_out[0]);
 }
 
-// y += diag .* x; dot_out = x.y (after a cross-rank sum of y)
+// y += diag .* x; dot_out = x.y (after a cross-rank sum of y); with ctl the
+// finalising block also takes the CG step length (sharded device CG), gated
+// like the rest of the iteration
 __global__ void __launch_bounds__(256) k_add_diag(int64_t n, const double* __restrict__ diag,
                                                   const double* __restrict__ x, double* __restrict__ y,
                                                   double* __restrict__ partial, unsigned* __restrict__ counter,
-                                                  double* __restrict__ dot_out) {
+                                                  double* __restrict__ dot_out, const int32_t* __restrict__ gate,
+                                                  CgCtl* __restrict__ ctl) {
+  if (gate && *gate) return;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double d = 0.0;
   if (e < n) {
@@ -623,7 +629,8 @@ __global__ void __launch_bounds__(256) k_add_diag(int64_t n, const double* __res
     y[e] = v;
     d = x[e] * v;
   }
-  if (dot_out) grid_sum_finalize(d, partial, counter, dot_out);
+  if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
+    cg_step_length(ctl, dot_out[0]);
 }
 
 // One CG step on the camera side, one thread per camera entry
@@ -1092,10 +1099,11 @@ hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* di
 }
 
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
-                                unsigned* counter, double* dot_out, hipStream_t s) {
+                                unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
+                                hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_add_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, diag, x, y, partial,
-                     counter, dot_out);
+                     counter, dot_out, gate, ctl);
   return hipGetLastError();
 }
 

@@ -73,7 +73,8 @@ _HIP = None
 
 
 def _hip():
-    """libamdhip64 (already loaded by torch) for raw-pointer copies in the callback."""
+    """libamdhip64 (already loaded by torch) for raw-pointer copies in the host
+    callback path."""
     global _HIP
     if _HIP is None:
         import ctypes as C
@@ -81,19 +82,30 @@ def _hip():
         lib = C.CDLL("libamdhip64.so")
         lib.hipMemcpy.restype = C.c_int
         lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        lib.hipStreamSynchronize.restype = C.c_int
+        lib.hipStreamSynchronize.argtypes = [C.c_void_p]
         _HIP = lib
     return _HIP
 
 
+class _DevicePtr:
+    """A library-owned device buffer seen by torch without a copy."""
+
+    def __init__(self, ptr: int, count: int):
+        self.__cuda_array_interface__ = {"shape": (count,), "typestr": "<f8", "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+
 class SolverExchange:
-    """The mvba_allreduce_fn of a sharded mvba_solve, over torch.distributed.
+    """The mvba_allreduce_fn of a sharded mvba_solve over torch.distributed.
 
-    The library hands a raw device pointer; it is staged through a persistent
-    buffer (device memory for RCCL — backend "nccl" — host memory for gloo),
-    all-reduced in place, and copied back. Calls are synchronous, as the ABI
-    requires."""
+    Stream-ordered (the ABI contract, include/mvba/mvba.h): with the RCCL
+    backend ("nccl") the library's device buffer is wrapped as a tensor (no
+    copy) and all-reduced in place on the solver's stream — no host wait. With
+    gloo (CPU rehearsal) the callback synchronises the stream, stages the
+    buffer through host memory and copies the result back before returning."""
 
-    H2D, D2H, D2D = 1, 2, 3
+    H2D, D2H = 1, 2
 
     def __init__(self, device=None):
         import torch
@@ -101,29 +113,114 @@ class SolverExchange:
 
         self.dist = dist
         self.on_device = dist.get_backend() == "nccl"
-        self.device = device if self.on_device else "cpu"
-        self.buf = torch.empty(0, dtype=torch.float64, device=self.device)
+        self.device = device
+        self.host = torch.empty(0, dtype=torch.float64)
+        self.views = {}
         self.calls = 0
         self.doubles = 0
 
-    def __call__(self, ptr: int, count: int, op: int):
+    def _view(self, ptr, count):
         import torch
 
-        if self.buf.numel() < count:
-            self.buf = torch.empty(max(count, 2 * self.buf.numel()), dtype=torch.float64, device=self.device)
-        view = self.buf[:count]
-        nbytes = count * 8
-        kind_in = self.D2D if self.on_device else self.D2H
-        kind_out = self.D2D if self.on_device else self.H2D
-        hip = _hip()
+        key = (ptr, count)
+        v = self.views.get(key)
+        if v is None:
+            v = torch.as_tensor(_DevicePtr(ptr, count), device=torch.device("cuda", self.device or 0))
+            self.views[key] = v
+        return v
+
+    def __call__(self, ptr: int, count: int, op: int, stream: int = 0):
+        import torch
+
+        red = self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX
         if self.on_device:
-            torch.cuda.synchronize(self.device)
-        if hip.hipMemcpy(view.data_ptr(), ptr, nbytes, kind_in) != 0:
-            raise RuntimeError("hipMemcpy into the exchange buffer failed")
-        self.dist.all_reduce(view, op=self.dist.ReduceOp.SUM if op == 0 else self.dist.ReduceOp.MAX)
-        if self.on_device:
-            torch.cuda.synchronize(self.device)
-        if hip.hipMemcpy(ptr, view.data_ptr(), nbytes, kind_out) != 0:
-            raise RuntimeError("hipMemcpy out of the exchange buffer failed")
+            st = torch.cuda.ExternalStream(stream) if stream else torch.cuda.default_stream()
+            with torch.cuda.stream(st):
+                self.dist.all_reduce(self._view(ptr, count), op=red)
+        else:
+            hip = _hip()
+            if hip.hipStreamSynchronize(stream or None) != 0:
+                raise RuntimeError("hipStreamSynchronize failed")
+            if self.host.numel() < count:
+                self.host = torch.empty(max(count, 2 * self.host.numel()), dtype=torch.float64)
+            view = self.host[:count]
+            if hip.hipMemcpy(view.data_ptr(), ptr, count * 8, self.D2H) != 0:
+                raise RuntimeError("hipMemcpy into the exchange buffer failed")
+            self.dist.all_reduce(view, op=red)
+            if hip.hipMemcpy(ptr, view.data_ptr(), count * 8, self.H2D) != 0:
+                raise RuntimeError("hipMemcpy out of the exchange buffer failed")
         self.calls += 1
         self.doubles += count
+
+
+class Comm:
+    """A library-native communicator (mvba_comm, include/mvba/mvba.h) for the
+    solver option ``comm=``: the exchange is ``mvba_comm_allreduce``, enqueued
+    on the solver's stream in C++ (no Python in the CG loop).
+
+    Comm.rccl(device): one process per GPU over torch.distributed — rank 0's
+    RCCL unique id is broadcast with torch.distributed, then every rank joins.
+    Comm.local(devices): several shards in one process (one thread and stream
+    per shard), returns one Comm per shard."""
+
+    def __init__(self, handle):
+        from . import _lib
+
+        self.lib = _lib.load()
+        self.h = handle
+
+    @classmethod
+    def rccl(cls, device: int):
+        import ctypes as C
+
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+
+        lib = _lib.load()
+        ident = np.zeros(_lib.COMM_ID_BYTES, dtype=np.uint8)
+        if dist.get_rank() == 0:
+            _lib.check(lib.mvba_comm_unique_id(ident.ctypes.data))
+        t = torch.from_numpy(ident)
+        if dist.get_backend() == "nccl":
+            t = t.cuda(device)
+        dist.broadcast(t, 0)
+        ident = np.ascontiguousarray(t.cpu().numpy())
+        h = C.c_void_p()
+        st = lib.mvba_comm_init_rccl(ident.ctypes.data, dist.get_world_size(), dist.get_rank(), device, C.byref(h))
+        if st != 0:
+            raise _lib.MvbaError(st, lib.mvba_comm_error().decode())
+        return cls(h)
+
+    @classmethod
+    def local(cls, devices):
+        import ctypes as C
+
+        import numpy as np
+
+        from . import _lib
+
+        lib = _lib.load()
+        dev = np.ascontiguousarray(devices, dtype=np.int32)
+        out = (C.c_void_p * len(dev))()
+        st = lib.mvba_comm_init_local(len(dev), dev.ctypes.data, out)
+        if st != 0:
+            raise _lib.MvbaError(st, lib.mvba_comm_error().decode())
+        return [cls(C.c_void_p(out[i])) for i in range(len(dev))]
+
+    def abort(self):
+        if self.h is not None and self.h.value:
+            self.lib.mvba_comm_abort(self.h)
+
+    def close(self):
+        if self.h is not None and self.h.value:
+            self.lib.mvba_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

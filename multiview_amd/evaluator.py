@@ -241,7 +241,8 @@ class Evaluator:
 def default_solver_options(**kw) -> _lib.SolverOptions:
     """mvba_solver_default_options, then overrides (lower_bounds/upper_bounds as
     numpy arrays over the packed parameter vector; allreduce as a Python callable
-    ``f(device_ptr, count, op) -> None``)."""
+    ``f(device_ptr, count, op[, hip_stream]) -> None`` honouring the
+    stream-ordered contract of mvba_allreduce_fn; comm as a dist.Comm)."""
     lib = _lib.load()
     o = _lib.SolverOptions()
     lib.mvba_solver_default_options(C.byref(o))
@@ -253,13 +254,27 @@ def default_solver_options(**kw) -> _lib.SolverOptions:
             arr = np.ascontiguousarray(v, dtype=np.float64)
             keep.append(arr)
             setattr(o, k, arr.ctypes.data)
+        elif k == "comm":
+            # library-native communicator (dist.Comm): the C all-reduce itself
+            if v is None:
+                continue
+            addr = C.cast(lib.mvba_comm_allreduce, C.c_void_p).value
+            o.allreduce = _lib.AllreduceFn(addr)
+            o.allreduce_user = v.h
+            keep.append(v)
         elif k == "allreduce":
             if v is None:
                 continue
+            import inspect
 
-            def _cb(ptr, count, op, stream, user, _f=v):
+            nargs = len(inspect.signature(v).parameters)
+
+            def _cb(ptr, count, op, stream, user, _f=v, _n=nargs):
                 try:
-                    _f(ptr, count, op)
+                    if _n >= 4:
+                        _f(ptr, count, op, stream or 0)
+                    else:
+                        _f(ptr, count, op)
                     return 0
                 except Exception as e:  # noqa: BLE001 - reported as a failed status
                     print(f"allreduce callback failed: {e!r}")

@@ -41,9 +41,11 @@ def _check_sample(P, oracle, r_g, J_g, idx):
     return r_o, J_o
 
 
-def _full_size_properties(P, oracle, sample, seed, ld=None, fill_nan=False):
+def _full_size_properties(P, oracle, sample, seed, ld=None):
     """Determinism, residual-only agreement, permutation and a random oracle
-    sample on one problem. Returns (ev-free summary dict) for further checks."""
+    sample on one problem. The Jacobian planes start NaN-filled (entries of
+    constant blocks are never written, as Ceres passes NULL for them). Returns
+    a summary dict (sizes, last valid slot and its column) for further checks."""
     import torch
 
     out = {}
@@ -51,9 +53,7 @@ def _full_size_properties(P, oracle, sample, seed, ld=None, fill_nan=False):
         ev.set_params()
         n, S = ev.num_residuals, ev.num_slots
         ld = ld or ev.ld
-        j1 = torch.empty((ev.stride, ld), dtype=torch.float64, device="cuda")
-        if fill_nan:
-            j1.fill_(float("nan"))
+        j1 = torch.full((ev.stride, ld), float("nan"), dtype=torch.float64, device="cuda")
         r1 = torch.empty((2, ld), dtype=torch.float64, device="cuda")
         ev.evaluate_device(True, residuals=r1, jac=j1, ld=ld)
         ev.sync()
@@ -77,7 +77,7 @@ def _full_size_properties(P, oracle, sample, seed, ld=None, fill_nan=False):
         _check_sample(P, oracle, r_g, J_g, order[pos])
         # determinism: a second residual+Jacobian evaluation, bit-identical
         # (compared plane by plane so only one extra plane set is resident)
-        j2 = torch.empty_like(j1)
+        j2 = torch.full_like(j1, float("nan"))
         r2 = torch.empty_like(r1)
         ev.evaluate_device(True, residuals=r2, jac=j2, ld=ld)
         ev.sync()
@@ -116,7 +116,7 @@ def test_full_size_c3_rpc3_planes_past_int32(oracle):
     stride = 56 + 2 * K
     ld = ((INT32_LIMIT // (stride - 1) + 4096 + 63) // 64) * 64
     assert (stride - 1) * ld > INT32_LIMIT  # the whole last plane lies past 2^31 elements
-    info = _full_size_properties(P, oracle, sample=3000, seed=37, ld=ld, fill_nan=True)
+    info = _full_size_properties(P, oracle, sample=3000, seed=37, ld=ld)
     assert info["stride"] == stride and info["ld"] == ld
     col, res = info["last_col"], info["last_res"]
     assert col[stride - 1] == 0.0  # undistortion half, last coefficient, row y

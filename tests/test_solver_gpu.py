@@ -316,19 +316,11 @@ def _shard_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_sharded_solve_matches_unsharded(tmp_path):
-    import torch.multiprocessing as mp
-
+def _union_problem(world):
+    """The unsharded problem = union of the shards' landmarks (point order: first
+    use in residual order = shard 0's points, then shard 1's, ...)."""
     from multiview_amd.dist import shard_range
 
-    world = 2
-    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    cams = [np.load(tmp_path / f"cam{r}.npy") for r in range(world)]
-    pts = np.concatenate([np.load(tmp_path / f"pts{r}.npy") for r in range(world)])
-    costs = [np.load(tmp_path / f"cost{r}.npy") for r in range(world)]
-    assert np.array_equal(cams[0], cams[1])
-    assert costs[0][1] == 0 and costs[0][0] == costs[1][0]
-    # unsharded problem = union of the shards' landmarks
     parts = [rig.make_rig(**dict(CFG, point_range=shard_range(CFG["num_points"], world, r))) for r in range(world)]
     R0 = parts[0]
     off = 0
@@ -343,7 +335,22 @@ def test_sharded_solve_matches_unsharded(tmp_path):
     R0.xyz = np.concatenate(xyz)
     R0.init["xyz"] = np.concatenate(init_xyz)
     R0.obs_pid, R0.obs_cid, R0.obs_pix = np.concatenate(pid), np.concatenate(cid), np.concatenate(pix)
-    P = rig.build_problem(R0, FLAGS)
+    return rig.build_problem(R0, FLAGS)
+
+
+def test_sharded_solve_matches_unsharded(tmp_path):
+    import torch.multiprocessing as mp
+
+    from multiview_amd.dist import shard_range
+
+    world = 2
+    mp.spawn(_shard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    cams = [np.load(tmp_path / f"cam{r}.npy") for r in range(world)]
+    pts = np.concatenate([np.load(tmp_path / f"pts{r}.npy") for r in range(world)])
+    costs = [np.load(tmp_path / f"cost{r}.npy") for r in range(world)]
+    assert np.array_equal(cams[0], cams[1])
+    assert costs[0][1] == 0 and costs[0][0] == costs[1][0]
+    P = _union_problem(world)
     with Evaluator(P) as ev:
         ev.set_params()
         s = ev.solve(max_num_iterations=100, **TOL)
@@ -355,3 +362,69 @@ def test_sharded_solve_matches_unsharded(tmp_path):
     assert _close(cams[0], cam, 1e-6)
     # point order: first use in residual order = shard 0's points then shard 1's
     assert _close(pts, pts_ref, 1e-6)
+
+
+def test_local_comm_sharded_solve_device_resident():
+    """Two landmark shards in ONE process, one thread and one HIP stream each,
+    both on cuda:0, exchanging through the library's local communicator
+    (mvba_comm_init_local + mvba_comm_allreduce: stream-ordered device
+    all-reduce, no host staging). The device CG runs in sharded mode; both
+    shards end with bit-identical camera blocks, and the result equals the
+    unsharded solve."""
+    import threading
+
+    import torch
+
+    from multiview_amd.dist import Comm, shard_range
+
+    world = 2
+    comms = Comm.local([0] * world)
+    evs, probs = [], []
+    for r in range(world):
+        R = rig.make_rig(**dict(CFG, point_range=shard_range(CFG["num_points"], world, r)))
+        P = rig.build_problem(R, FLAGS)
+        ev = Evaluator(P, device=0)
+        ev.set_params()
+        evs.append(ev)
+        probs.append(P)
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    out = [None] * world
+    errs = []
+
+    def run(r):
+        try:
+            out[r] = evs[r].solve(max_num_iterations=100, comm=comms[r], stream=streams[r].cuda_stream, **TOL)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            comms[r].abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    cams, pts = [], []
+    for r in range(world):
+        probs[r].params = evs[r].get_params()
+        cams.append(_cam_values(evs[r], probs[r]))
+        pts.append(np.concatenate([probs[r].block_values(int(b)) for b in evs[r].lin_layout()["point_block_ids"]]))
+    assert out[0]["termination_type"] == 0, out[0]["message"]
+    assert out[0]["final_cost"] == out[1]["final_cost"]
+    assert out[0]["num_linear_iterations"] == out[1]["num_linear_iterations"]
+    assert np.array_equal(cams[0], cams[1])
+    for ev in evs:
+        ev.close()
+    for c in comms:
+        c.close()
+    P = _union_problem(world)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=100, **TOL)
+        P.params = ev.get_params()
+        cam = _cam_values(ev, P)
+        pts_ref = np.concatenate([P.block_values(int(b)) for b in ev.lin_layout()["point_block_ids"]])
+    assert np.isclose(out[0]["final_cost"], s["final_cost"], rtol=1e-9)
+    assert _close(cams[0], cam, 1e-6)
+    assert _close(np.concatenate(pts), pts_ref, 1e-6)
