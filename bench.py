@@ -147,12 +147,23 @@ def _stream_copy_gbs(torch, stream, nbytes=1 << 30, reps=10):
     return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
+PROFILE_ROUNDS = ("r02", "r01")  # newest first: committed PMC summaries are read from here
+
+
+def _profile_path(name):
+    here = os.path.dirname(os.path.abspath(__file__))
+    for r in PROFILE_ROUNDS:
+        path = os.path.join(here, "profiles", r, name)
+        if os.path.exists(path):
+            return path
+    return os.path.join(here, "profiles", PROFILE_ROUNDS[-1], name)
+
+
 def _pmc_traffic(config):
     """HBM bytes per K1 launch from the committed PMC summary of this config
     (tools/pmc_summary.py over separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
     passes of this same command; profiles/), or None."""
-    here = os.path.dirname(os.path.abspath(__file__))
-    path = os.path.join(here, "profiles", "r01", f"pmc_k1_{config}.json")
+    path = _profile_path(f"pmc_k1_{config}.json")
     try:
         with open(path) as f:
             return float(json.load(f)["traffic_bytes_per_launch"])
@@ -164,8 +175,7 @@ def _pmc_flops(config):
     """fp64 flops per launch of each kernel from the committed PMC summary of
     this config (tools/pmc_flops.py over one rocprofv3 --pmc pass of this same
     command; profiles/), or {}."""
-    here = os.path.dirname(os.path.abspath(__file__))
-    path = os.path.join(here, "profiles", "r01", f"pmc_flops_{config}.json")
+    path = _profile_path(f"pmc_flops_{config}.json")
     try:
         with open(path) as f:
             return json.load(f)["kernels"]
@@ -460,7 +470,8 @@ def main():
         ar_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in levs]))
         lin = {
             "what": "K2 linearization (Cauchy-corrected J^T r, block-diagonal J^T J: camera side "
-                    "via fp64 MFMA Gram, point side) + RCCL all-reduce of the camera blocks",
+                    "via fp64 MFMA Gram + in-block expansion, point side on a second stream) + RCCL "
+                    "all-reduce of the camera blocks",
             "evals_per_s": total_evals / float(ldt.item()),
             "ms_per_step": 1e3 * float(ldt.item()) / args.steps,
             "kernel_ms": lin_ms,
@@ -468,10 +479,42 @@ def main():
             "allreduce_bytes": buf.payload_bytes if world > 1 else 0,
             "cam_params": L["cam_grad_size"],
         }
+
+        # the two sides timed alone (same stream, HIP events, parameters and K0
+        # records unchanged): camera side = k_frame_lin + replica reduce,
+        # point side = k_points_lin on the library's second stream
+        def side_ms(side):
+            kw = dict(apply_loss=True, robust_threshold=3.0, stream=sh, skip_prep=True, side=side)
+            for _ in range(args.warmup):
+                ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(args.steps):
+                ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, **kw)
+            e1.record(stream)
+            e1.synchronize()
+            return e0.elapsed_time(e1) / args.steps
+
+        cam_ms, pts_ms = side_ms("camera"), side_ms("points")
+        mfma = float(ev.lib.mvba_lin_mfma_flops(ev.h))
+        lin["camera_side_ms"] = cam_ms
+        lin["point_side_ms"] = pts_ms
+        # X1 evidence (north_star: MFMA for the dense normal-equation blocks):
+        # fp64 MFMA work issued by the camera-side Gram kernel against the
+        # MI355X fp64 matrix peak, over the camera side's time
+        lin["mfma"] = {
+            "kernel": "k_frame_lin (v_mfma_f64_16x16x4f64)",
+            "flops_per_launch": mfma,
+            "achieved_tflops": mfma / (cam_ms * 1e-3) / 1e12,
+            "peak_tflops": FP64_PEAK_TFLOPS,
+            "util": mfma / (cam_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+            "note": "issued MFMA flops (zero-padded tile columns included) / camera-side time "
+                    "(Gram + expansion + replica reduce)",
+        }
         # fused mode: 48 B per evaluation (observation record +
         # landmark) against the fp64 work of the linearization kernels
-        lin_flops = _flops_of(flops_tab, ["mvba::k_prep", "mvba::k_gram<", "mvba::k_points_lin<",
-                                          "mvba::k_expand", "mvba::k_rep_reduce"]) if flops_tab else None
+        lin_flops = _flops_of(flops_tab, ["mvba::k_prep", "mvba::k_frame_lin<", "mvba::k_points_lin<",
+                                          "mvba::k_rep_reduce"]) if flops_tab else None
         lin_bytes = 48.0 * n
         lin["hbm_bytes"] = lin_bytes
         lin["hbm_frac"] = lin_bytes / (lin_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
@@ -479,7 +522,7 @@ def main():
             tf = lin_flops / (lin_ms * 1e-3) / 1e12
             lin["fp64_flops"] = lin_flops
             lin["fp64_mfma_flops"] = sum(v["fp64_mfma_flops"] for k, v in flops_tab.items()
-                                         if k.startswith("mvba::k_gram<"))
+                                         if k.startswith("mvba::k_frame_lin<"))
             lin["fp64_tflops"] = tf
             lin["fp64_frac"] = tf / FP64_PEAK_TFLOPS
             lin["bound_us"] = 1e6 * max(lin_bytes / (HBM_PEAK_GBS * 1e9), lin_flops / (FP64_PEAK_TFLOPS * 1e12))

@@ -276,10 +276,20 @@ mvba_status mvba_cam_block_map(const struct mvba_handle* h, int32_t* block_ids, 
                                int64_t* hoff);
 /* [num_points]: parameter block id of point index p */
 mvba_status mvba_point_block_map(const struct mvba_handle* h, int32_t* block_ids);
-/* flags: MVBA_EVAL_APPLY_LOSS, MVBA_EVAL_SKIP_PREP. Asynchronous on hip_stream. */
+/* flags: MVBA_EVAL_APPLY_LOSS, MVBA_EVAL_SKIP_PREP, and for timing the two
+ * sides separately MVBA_LIN_CAMERA_ONLY (camera-side gradient, block Hessians
+ * and cost only; point outputs untouched, nullable) or MVBA_LIN_POINTS_ONLY.
+ * The point side runs on a library stream beside the camera side and is
+ * joined to hip_stream before the call's work on hip_stream completes.
+ * Asynchronous on hip_stream. */
+#define MVBA_LIN_CAMERA_ONLY 0x20
+#define MVBA_LIN_POINTS_ONLY 0x40
 mvba_status mvba_linearize_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                                   double* d_cam_grad, double* d_cam_hess, double* d_pt_grad,
                                   double* d_pt_hess, double* d_cost, void* hip_stream);
+/* fp64 MFMA flops the camera-side Gram kernel issues per linearization
+ * (v_mfma_f64_16x16x4: 2048 flops each, zero-padded tile columns included). */
+double mvba_lin_mfma_flops(const struct mvba_handle* h);
 
 /* ---- Depth residuals (BracketedDepthError) -------------------------------
  * Host: residuals [3n] and Jacobian [n * MVBA_DJAC_ROWS] (nullable) in depth

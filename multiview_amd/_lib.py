@@ -111,6 +111,7 @@ DJAC_BASE = (0, 21, 42, 63, 99, 102, 111)
 DJAC_ROWS = 114
 
 REDUCE_SUM, REDUCE_MAX = 0, 1
+LIN_CAMERA_ONLY, LIN_POINTS_ONLY = 0x20, 0x40
 CONVERGENCE, NO_CONVERGENCE, FAILURE = 0, 1, 2
 
 # int32_t (*)(double* device_buf, int64_t count, int32_t op, void* stream, void* user)
@@ -262,6 +263,7 @@ SIGNATURES = {
     "mvba_solver_default_options": (None, [C.POINTER(SolverOptions)]),
     "mvba_solve": (C.c_int, [C.c_void_p, C.POINTER(SolverOptions), C.POINTER(SolverSummary), C.c_void_p]),
     "mvba_get_params": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "mvba_lin_mfma_flops": (C.c_double, [C.c_void_p]),
     "mvba_comm_unique_id": (C.c_int, [C.c_void_p]),
     "mvba_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "mvba_comm_init_local": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),

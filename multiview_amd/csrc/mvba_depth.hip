@@ -110,7 +110,7 @@ constexpr int kDRows = 192;      // 3 rows x 64 lanes
 // either way): 17 KB of LDS per wave instead of 50, 2.7x the waves per CU
 constexpr int kDStage = 64;
 constexpr int kDLd = kDStage + 2; // LDS leading dimension (doubles)
-constexpr int kDReplicas = 32;
+constexpr int kDReplicas = kDepthReplicas;
 
 __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ segs, int32_t nseg,
                                                    const DepthDesc* __restrict__ dd,

@@ -313,8 +313,8 @@ __device__ __forceinline__ double loss_scale(double r0, double r1, int32_t flags
 
 // Per-frame record of the linearization (K2 expand), see mvba_kernels.hip.
 struct FrameLin {
-  int64_t slab_off;                  // offset (doubles) of this frame's first chunk slab
-  int32_t chunk_count;               // consecutive chunk slabs of w16*w16+1 doubles
+  int64_t slab_off;                  // reserved (0)
+  int32_t chunk_count;               // solver chunks of this frame
   int32_t width, w16;                // Gram width and padded width
   int32_t first_chunk;               // global index of the frame's first chunk
   int64_t goff[8];                   // camera-side gradient offsets per block (-1: constant/none)

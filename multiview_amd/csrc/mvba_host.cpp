@@ -34,13 +34,18 @@ static void free_all(mvba_handle* h) {
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
-                  h->d_slab, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
+                  h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
                   h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xpid,
                   h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt};
   solver_state_free(h->solver);
   h->solver = nullptr;
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->aux_stream) (void)hipStreamDestroy(h->aux_stream);
+  h->ev_fork = h->ev_join = nullptr;
+  h->aux_stream = nullptr;
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -395,7 +400,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   h->bytes_jac = bytes_jac;
 
   // ---- linearization structures (K2)
-  std::vector<int4> chunks;
+  std::vector<int4> chunks, parts;
   std::vector<mvba::FrameLinHost> flin(frames.size());
   std::vector<int64_t> pt_begin;
   std::vector<int32_t> po_frame, po_slot;
@@ -426,15 +431,11 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       h->cam_hess_size += sz * sz;
       for (int64_t q = 0; q < sz; q++) h->cam_poff.push_back(d->block_offset[b] + q);
     }
-    int64_t slab_base = 0;
     for (Group& G : h->groups) {
       G.chunk_begin = (int32_t)chunks.size();
+      G.part_begin = (int32_t)parts.size();
       G.gram_width = h->lin_ok ? mvba_gram_width(G.model, G.deg) : 0;
       G.w16 = (G.gram_width + 15) / 16 * 16;
-      h->max_w16 = std::max(h->max_w16, G.w16);
-      const int64_t SL = (int64_t)G.w16 * G.w16 + 1;
-      G.slab_base = slab_base;
-      int32_t local = 0;
       for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++) {
         const Segment& sg = segs[sidx];
         if (chunks.size() == (size_t)G.chunk_begin || chunks.back().z != sg.frame ||
@@ -443,23 +444,32 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
           c.x = sidx;
           c.y = 0;
           c.z = sg.frame;
-          c.w = local++;
+          c.w = (int32_t)chunks.size() - G.chunk_begin;
           chunks.push_back(c);
           mvba::FrameLinHost& L = flin[sg.frame];
-          if (L.chunk_count == 0) {
-            L.slab_off = slab_base + (int64_t)c.w * SL;
-            L.first_chunk = (int32_t)chunks.size() - 1;
-          }
+          if (L.chunk_count == 0) L.first_chunk = (int32_t)chunks.size() - 1;
           L.chunk_count++;
           L.width = G.gram_width;
           L.w16 = G.w16;
         }
         chunks.back().y++;
+        if (parts.size() == (size_t)G.part_begin || parts.back().z != sg.frame ||
+            parts.back().y == mvba::kPartSegs)
+          parts.push_back(make_int4(sidx, 0, sg.frame, 0));
+        parts.back().y++;
       }
       G.chunk_count = (int32_t)chunks.size() - G.chunk_begin;
-      slab_base += (int64_t)G.chunk_count * SL;
+      G.part_count = (int32_t)parts.size() - G.part_begin;
+      // k_frame_lin: per 32-observation half of a segment, 16 K=4 steps over
+      // the T(T+1)/2 tile pairs, 2048 flops per v_mfma_f64_16x16x4
+      if (G.gram_width > 0) {
+        const int64_t T = (G.gram_width + 15) / 16;
+        int64_t halves = 0;
+        for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++)
+          halves += (segs[sidx].count + 31) / 32;
+        h->lin_mfma_flops += (double)halves * 16.0 * (double)(T * (T + 1) / 2) * 2048.0;
+      }
     }
-    h->slab_size = slab_base;
     for (size_t f = 0; f < frames.size(); f++) {
       for (int b = 0; b < 8; b++) {
         const int32_t bid = frame_blocks[f][b];
@@ -636,9 +646,11 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     if (e == hipSuccess && !flin.empty())
       chk(hipMemcpy(p, flin.data(), flin.size() * sizeof(mvba::FrameLinHost), hipMemcpyHostToDevice));
   }
-  chk(dalloc(&h->d_slab, (size_t)std::max<int64_t>(h->slab_size, 1)));
+  chk(upload(&h->d_parts, parts));
   {
-    const size_t nrep = (size_t)mvba_num_replicas() * (size_t)(h->cam_grad_size + h->cam_hess_size + 1);
+    // the depth Gram adds into kDepthReplicas replicas, the camera side into mvba_num_replicas()
+    h->nrep = h->ndep > 0 ? std::max(mvba::kDepthReplicas, mvba_num_replicas()) : mvba_num_replicas();
+    const size_t nrep = (size_t)h->nrep * (size_t)(h->cam_grad_size + h->cam_hess_size + 1);
     chk(dalloc(&h->d_rep, nrep));
     if (e == hipSuccess) chk(hipMemset(h->d_rep, 0, nrep * sizeof(double)));
   }
@@ -842,7 +854,10 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
   if (!h) return MVBA_E_INVALID;
   if (!h->lin_ok) return h->fail(MVBA_E_INVALID, h->lin_err);
   if (!h->params_set) return h->fail(MVBA_E_INVALID, "parameters were not set (mvba_set_params)");
-  if ((h->cam_grad_size && (!d_cam_grad || !d_cam_hess)) || (h->npts && (!d_pt_grad || !d_pt_hess)))
+  const bool cam_side = !(flags & MVBA_LIN_POINTS_ONLY), pt_side = !(flags & MVBA_LIN_CAMERA_ONLY);
+  if (!cam_side && !pt_side) return h->fail(MVBA_E_INVALID, "MVBA_LIN_CAMERA_ONLY with MVBA_LIN_POINTS_ONLY");
+  if ((cam_side && h->cam_grad_size && (!d_cam_grad || !d_cam_hess)) ||
+      (pt_side && h->npts && (!d_pt_grad || !d_pt_hess)))
     return h->fail(MVBA_E_INVALID, "null output buffer");
   if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
   if (mvba_frame_lin_size() != sizeof(mvba::FrameLinHost) || mvba_depth_desc_size() != sizeof(mvba::DepthDesc))
@@ -863,25 +878,39 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
     return h->fail(MVBA_E_INVALID, "MVBA_EVAL_SKIP_PREP before any full evaluation");
   }
   const int32_t lflags = flags & MVBA_EVAL_APPLY_LOSS;
-  for (size_t g = 0; g < h->groups.size() && e == hipSuccess; g++) {
-    const Group& G = h->groups[g];
-    e = mvba_launch_gram(G.model, G.deg, h->d_chunks + G.chunk_begin, G.chunk_count, h->d_segs, h->d_fd,
-                         h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
-                         h->d_slab + G.slab_base, lflags, cauchy_c, s);
+  // point side (K2b) on the auxiliary stream, beside the camera side (K2a):
+  // both read the K0 records and points of the prep above and write disjoint
+  // outputs; the caller's stream joins the point side before returning
+  if (e == hipSuccess && !h->aux_stream) {
+    e = hipStreamCreateWithFlags(&h->aux_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
   }
-  if (e == hipSuccess && h->ndep_segs > 0)
+  if (pt_side) {
+    if (e == hipSuccess) e = hipEventRecord(h->ev_fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->aux_stream, h->ev_fork, 0);
+    if (e == hipSuccess)
+      e = mvba_launch_points_lin(h->groups.size() == 1 ? h->groups[0].model : -1,
+                                 h->groups.size() == 1 ? h->groups[0].deg : 0, h->d_pt_begin, h->npts,
+                                 h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
+                                 d_pt_grad, d_pt_hess, lflags, cauchy_c, h->point_extra(), h->aux_stream);
+    if (e == hipSuccess) e = hipEventRecord(h->ev_join, h->aux_stream);
+  }
+  for (size_t g = 0; cam_side && g < h->groups.size() && e == hipSuccess; g++) {
+    const Group& G = h->groups[g];
+    e = mvba_launch_frame_lin(G.model, G.deg, h->d_parts + G.part_begin, G.part_count, h->d_segs, h->d_fd,
+                              h->d_frame_lin, h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
+                              h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags, cauchy_c, s);
+  }
+  if (cam_side && e == hipSuccess && h->ndep_segs > 0)
     e = mvba_launch_depth_gram(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_frec, h->d_params,
                                h->d_pts, h->d_frame_lin, h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags,
                                cauchy_c, s);
-  if (e == hipSuccess)
-    e = mvba_launch_expand(h->d_frame_lin, (int32_t)h->nframes, h->max_w16, h->d_fd, h->d_frec, h->d_slab,
-                           h->d_rep, h->cam_grad_size, h->cam_hess_size, d_cam_grad, d_cam_hess, d_cost, s);
-  if (e == hipSuccess)
-    e = mvba_launch_points_lin(h->groups.size() == 1 ? h->groups[0].model : -1,
-                               h->groups.size() == 1 ? h->groups[0].deg : 0, h->d_pt_begin, h->npts,
-                               h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
-                               d_pt_grad, d_pt_hess, lflags, cauchy_c, h->point_extra(), s);
-  if (e == hipSuccess && h->nxyz > 0 && d_cost) {
+  if (cam_side && e == hipSuccess)
+    e = mvba_launch_rep_reduce(h->d_rep, h->nrep, h->cam_grad_size, h->cam_hess_size, d_cam_grad, d_cam_hess, d_cost,
+                               s);
+  if (pt_side && e == hipSuccess) e = hipStreamWaitEvent(s, h->ev_join, 0);
+  if (cam_side && e == hipSuccess && h->nxyz > 0 && d_cost) {
     e = mvba_launch_xyz_cost(h->nxyz, h->d_xpid, h->d_xref, h->d_xcc, h->d_pts, lflags, h->d_xscal + 1, h->d_xcnt,
                              h->d_xscal, s);
     if (e == hipSuccess) e = mvba_launch_axpby(1, 1.0, d_cost, 1.0, h->d_xscal, d_cost, s);
@@ -889,6 +918,8 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
   if (e != hipSuccess) return h->hip_fail(e, "mvba_linearize_device launch");
   return MVBA_OK;
 }
+
+double mvba_lin_mfma_flops(const mvba_handle* h) { return h ? h->lin_mfma_flops : 0.0; }
 
 mvba_status mvba_evaluate(mvba_handle* h, int32_t flags, double cauchy_threshold, double* cost,
                           double* residuals, double* jacobian) {

@@ -28,13 +28,12 @@ hipError_t mvba_launch_prep(const FrameDesc* fd, int64_t nframes, const double* 
                             double4* pts, int gen, int* err, hipStream_t s);
 int mvba_gram_width(int model, int deg);
 size_t mvba_frame_lin_size(void);
-hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchunks, const Segment* segs,
-                            const FrameDesc* fd, const double* frec, const double* params,
-                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
-                            double* slab, int32_t flags, double cauchy_c, hipStream_t s);
-hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16, const FrameDesc* fd,
-                              const double* frec, const double* slab, double* rep, int64_t ng, int64_t nh,
-                              double* grad, double* hess, double* cost, hipStream_t s);
+hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t nparts, const Segment* segs,
+                                 const FrameDesc* fd, const void* fl, const double* frec, const double* params,
+                                 const double4* pts, const int32_t* obs_pid, const double2* obs_meas, double* rep,
+                                 int64_t ng, int64_t nh, int32_t flags, double cauchy_c, hipStream_t s);
+hipError_t mvba_launch_rep_reduce(double* rep, int32_t nrep, int64_t ng, int64_t nh, double* grad, double* hess,
+                                  double* cost, hipStream_t s);
 int mvba_num_replicas(void);
 hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, int64_t npts,
                                   const int32_t* po_frame, const double2* po_meas, const FrameDesc* fd,
@@ -122,9 +121,10 @@ struct Group {
   int model = 0, deg = 0;
   int32_t seg_begin = 0, seg_count = 0;
   int64_t res_begin = 0, res_count = 0;
-  // linearization (K2): chunks of <= 4 segments of one frame, slab per chunk
+  // solver passes: chunks of <= 4 segments of one frame (one wave each)
   int32_t chunk_begin = 0, chunk_count = 0;
-  int64_t slab_base = 0;
+  // linearization (K2): parts of <= kPartSegs segments of one frame (one block each)
+  int32_t part_begin = 0, part_count = 0;
   int32_t gram_width = 0, w16 = 0;
 };
 
@@ -185,15 +185,18 @@ struct mvba_handle {
   // linearization (K2): camera-side compact layout, chunks, point CSR
   bool lin_ok = false;
   std::string lin_err;
-  int64_t cam_grad_size = 0, cam_hess_size = 0, slab_size = 0;
-  int32_t max_w16 = 0;
+  int64_t cam_grad_size = 0, cam_hess_size = 0;
+  int32_t nrep = 0;                     // replicas of [cam_grad | cam_hess | cost] in d_rep
+  double lin_mfma_flops = 0.0;          // MFMA flops of one camera-side Gram launch set
   std::vector<int32_t> cam_block_ids;   // camera-side blocks in block-id order
   std::vector<int64_t> cam_goff, cam_hoff;
   std::vector<int32_t> pt_block_ids;    // point index -> block id
   int4* d_chunks = nullptr;
   void* d_frame_lin = nullptr;
-  double* d_slab = nullptr;
-  double* d_rep = nullptr;  // kReplicas copies of [cam_grad | cam_hess | cost], kept zero between calls
+  int4* d_parts = nullptr;              // K2 frame parts (seg_begin, seg_count, frame, -)
+  double* d_rep = nullptr;  // nrep copies of [cam_grad | cam_hess | cost], kept zero between calls
+  hipStream_t aux_stream = nullptr;     // K2 point side runs beside the camera side
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t* d_pt_begin = nullptr;
   int32_t* d_po_frame = nullptr;
   double2* d_po_meas = nullptr;

@@ -323,22 +323,28 @@ __global__ void __launch_bounds__(256) k_obs(
   }
 }
 
-// ------------------------------------------------------------ K2a: camera-side Gram
+// ------------------------------------------------------------ K2a: camera side, one launch
 // Normal equations, camera side. For a frame f, every pose column is
 // J_k = Z w_k with Z_i = [Xc x G_i | G_i] (per observation, 6 numbers per row)
 // and w_k = [omega_k; v_k] (per frame), so the frame's whole camera-camera block
 // follows from the Gram matrix of B = [Z | J_focal | J_center | J_dist | r]
 // (2 rows per observation): B^T B holds Z^T Z, Z^T J_intr, J_intr^T J_intr and
-// the gradients Z^T r, J_intr^T r (k_expand applies w). The Gram product is a
-// K = 128-deep GEMM per wave: fp64 MFMA v_mfma_f64_16x16x4 with B staged in LDS
-// as [column][row] (row stride kGramLd doubles, conflict-free reads).
-// One wave = one chunk (<= kChunkSegs segments of one frame, mvba_types.h); accumulators stay
-// in registers across the chunk; the chunk's Gram goes to a slab (no atomics).
-// The segment's 128 rows are staged in two halves of 64 (the observations of
-// lanes 0-31, then 32-63): 8.4 KB of LDS per wave for radtan instead of 16.6,
-// twice the waves per CU.
+// the gradients Z^T r, J_intr^T r; the expansion applies w.
+//
+// k_frame_lin: one block per frame part (<= kPartSegs segments of ONE frame),
+// WAVES waves per block. Each wave builds the Gram of its segments' rows (a
+// K = 128-deep GEMM per segment on fp64 MFMA v_mfma_f64_16x16x4, B staged in
+// the wave's own LDS area as [column][row], row stride kGramLd doubles: no
+// block barrier inside the loop, waves run their segments independently). The
+// waves' accumulators are summed through LDS in wave order, and the block maps
+// the frame's Gram through w and adds pose / intrinsic blocks into replica
+// (frame mod kLinReplicas) of [grad | hess | cost]: a sensor's extrinsic and
+// intrinsic blocks are shared by all its frames, so the replicas keep the
+// atomic adds per address low; k_rep_reduce sums them (and re-zeroes).
+// The Gram entries stay in the accumulator layout: pair p = (ti, tj), ti <= tj,
+// lane l and register r hold G[16 ti + (l >> 4) + 4 r][16 tj + (l & 15)].
 constexpr int kGramLd = 66;  // 64 rows + 2 pad doubles: bank-conflict-free reads
-
+constexpr int kLinReplicas = 8;
 
 template <int MODEL, int DEG>
 struct GramShape {
@@ -348,25 +354,49 @@ struct GramShape {
   static constexpr int kTiles = (kWidth + 15) / 16;
   static constexpr int kPairs = kTiles * (kTiles + 1) / 2;
   static constexpr int kColR = kWidth - 1;              // residual column
+  // waves per block: LDS staging is kTiles*16*kGramLd doubles per wave
+  static constexpr int kWaves = kTiles <= 2 ? 4 : kTiles <= 4 ? 2 : 1;
+  static constexpr int kStage = kTiles * 16 * kGramLd;
+  static constexpr size_t kLdsBytes = sizeof(double) * ((size_t)kWaves * kStage + 2 * 6 * kPoseCols + kWaves);
 };
 
+// Entry (a, b) of a Gram held in the accumulator layout (T tiles per side).
+template <int T>
+__device__ __forceinline__ double gram_at(const double* __restrict__ G, int a, int b) {
+  if (a / 16 > b / 16) {
+    const int t = a;
+    a = b;
+    b = t;
+  }
+  const int ti = a >> 4, tj = b >> 4, i = a & 15, j = b & 15;
+  const int p = ti * T - ti * (ti - 1) / 2 + (tj - ti);
+  return G[(p * 4 + (i >> 2)) * 64 + (i & 3) * 16 + j];
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  // LDS hand-off between the lanes of ONE wave: wait for the wave's LDS ops
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int MODEL, int DEG>
-__global__ void __launch_bounds__(64) k_gram(
-    const int4* __restrict__ chunks, int32_t nchunks, const Segment* __restrict__ segs,
-    const FrameDesc* __restrict__ fd, const double* __restrict__ frec,
+__global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_lin(
+    const int4* __restrict__ parts, int32_t nparts, const Segment* __restrict__ segs,
+    const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl, const double* __restrict__ frec,
     const double* __restrict__ params, const double4* __restrict__ pts,
     const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
-    double* __restrict__ slab, int32_t flags, double cauchy_c) {
+    double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c) {
   using S = GramShape<MODEL, DEG>;
   constexpr int T = S::kTiles;
   constexpr int NP = S::kPairs;
-  constexpr int SLAB = T * 16 * T * 16 + 1;  // Gram (full square, upper tiles) + cost
-  extern __shared__ double lds[];            // [T*16][kGramLd]
-  const int lane = threadIdx.x;
-  const int ch = blockIdx.x;
-  if (ch >= nchunks) return;
-  const int4 c = chunks[ch];  // seg_begin, seg_count, frame, slab index
-  const int frame = __builtin_amdgcn_readfirstlane(c.z);
+  constexpr int WAVES = S::kWaves;
+  constexpr int W16 = T * 16;
+  extern __shared__ double lds[];  // [WAVES][kStage] | w [6 x 22] | Tm [6 x 22] | cost [WAVES]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if ((int)blockIdx.x >= nparts) return;
+  const int4 part = parts[blockIdx.x];  // seg_begin, seg_count, frame, -
+  const int frame = __builtin_amdgcn_readfirstlane(part.z);
   const FrameDesc& F = fd[frame];
   const double* __restrict__ rec = frec + (int64_t)frame * kFrameRecDoubles;
   const double f = params[F.off[MVBA_BLK_FOCAL]];
@@ -374,19 +404,19 @@ __global__ void __launch_bounds__(64) k_gram(
   const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
   const double* __restrict__ kd = params + F.off[MVBA_BLK_DIST];
   const int K = F.K;
+  double* st = lds + wave * S::kStage;
 
   dbl4 acc[NP];
 #pragma unroll
   for (int p = 0; p < NP; p++) acc[p] = dbl4{0.0, 0.0, 0.0, 0.0};
   double cost = 0.0;
 
-  // zero the padding columns once (they stay zero)
+  // zero the padding columns of this wave's staging area once (they stay zero)
   if (lane < 32)
-    for (int col = S::kWidth; col < T * 16; col++)
-      *(dbl2v*)&lds[col * kGramLd + 2 * lane] = dbl2v{0.0, 0.0};
+    for (int col = S::kWidth; col < W16; col++) *(dbl2v*)&st[col * kGramLd + 2 * lane] = dbl2v{0.0, 0.0};
 
-  for (int sidx = 0; sidx < c.y; sidx++) {
-    const Segment sg = segs[c.x + sidx];
+  for (int sidx = wave; sidx < part.y; sidx += WAVES) {
+    const Segment sg = segs[part.x + sidx];
     const int count = __builtin_amdgcn_readfirstlane(sg.count);
     const int64_t i = (int64_t)sg.begin + lane;
     double row0[S::kWidth], row1[S::kWidth];
@@ -424,22 +454,22 @@ __global__ void __launch_bounds__(64) k_gram(
       row0[S::kColR] = r0 * sr;
       row1[S::kColR] = r1 * sr;
     }
-    // stage B (this segment's 128 rows) in LDS as [column][row], 64 rows at a
-    // time; the halves past the segment's last observation are all zero rows
+    // stage this segment's 128 rows as [column][row], 64 rows at a time; the
+    // halves past the segment's last observation are all zero rows
     const int col = lane & 15, rsub = lane >> 4;
     for (int half = 0; half < 2 && 32 * half < count; half++) {
       if ((lane >> 5) == half) {
 #pragma unroll
         for (int q = 0; q < S::kWidth; q++)
-          *(dbl2v*)&lds[q * kGramLd + 2 * (lane & 31)] = dbl2v{row0[q], row1[q]};
+          *(dbl2v*)&st[q * kGramLd + 2 * (lane & 31)] = dbl2v{row0[q], row1[q]};
       }
-      __syncthreads();
+      wave_lds_sync();
 #pragma unroll 4
-      for (int st = 0; st < 16; st++) {
-        const int row = 4 * st + rsub;
+      for (int stp = 0; stp < 16; stp++) {
+        const int row = 4 * stp + rsub;
         double v[T];
 #pragma unroll
-        for (int t = 0; t < T; t++) v[t] = lds[(t * 16 + col) * kGramLd + row];
+        for (int t = 0; t < T; t++) v[t] = st[(t * 16 + col) * kGramLd + row];
         int p = 0;
 #pragma unroll
         for (int ti = 0; ti < T; ti++)
@@ -449,130 +479,114 @@ __global__ void __launch_bounds__(64) k_gram(
             p++;
           }
       }
-      __syncthreads();
+      wave_lds_sync();
     }
   }
-  // chunk Gram -> slab: lane holds G[(lane>>4) + 4r][lane & 15] of each tile pair
-  double* out = slab + (int64_t)c.w * SLAB;
-  const int W16 = T * 16;
-  int p = 0;
-#pragma unroll
-  for (int ti = 0; ti < T; ti++)
-#pragma unroll
-    for (int tj = ti; tj < T; tj++) {
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        out[(ti * 16 + (lane >> 4) + 4 * r) * W16 + tj * 16 + (lane & 15)] = acc[p][r];
-      p++;
-    }
-  // chunk cost: wave reduction
+  // ---- the block's Gram: waves' accumulators summed in wave order (in place
+  // in wave 0's staging area, accumulator layout)
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) cost += __shfl_xor(cost, off, 64);
-  if (lane == 0) out[W16 * W16] = cost;
-}
-
-// ------------------------------------------------------------ K2 expand (per frame)
-// Sums the frame's chunk Grams and scatters gradient and block-diagonal Hessian
-// of every free camera-side block: pose blocks via w (J_pose = Z w), intrinsics
-// directly. Layout per block: gradient at goff, row-major size x size Hessian at
-// hoff. Camera blocks shared by many frames (a sensor's
-// extrinsics/intrinsics: ~1000 frames at c2) would serialise on atomics, so
-// frame f adds into replica (f mod kReplicas) of the output and k_rep_reduce
-// sums the replicas (and re-zeroes them for the next call).
-constexpr int kReplicas = 32;
-
-__global__ void __launch_bounds__(64) k_expand(const FrameLin* __restrict__ fl, int32_t nframes,
-                                               const FrameDesc* __restrict__ fd,
-                                               const double* __restrict__ frec,
-                                               const double* __restrict__ slab,
-                                               double* __restrict__ rep, int64_t ng, int64_t nh) {
-  extern __shared__ double sh[];  // Gram [w16*w16+1] then w [6*22] then T [6*22]
-  const int f = blockIdx.x;
-  if (f >= nframes) return;
-  const FrameLin L = fl[f];
-  const int W16 = L.w16, Wd = L.width;
-  const int n = W16 * W16 + 1;
-  const int SL = n;
-  double* G = sh;
-  double* w = sh + n;
-  double* Tm = w + 6 * kPoseCols;
-  for (int e = threadIdx.x; e < n; e += 64) {
-    double acc = 0.0;
-    for (int c = 0; c < L.chunk_count; c++) acc += slab[L.slab_off + (int64_t)c * SL + e];
-    G[e] = acc;
-  }
-  const double* rec = frec + (int64_t)f * kFrameRecDoubles;
-  for (int e = threadIdx.x; e < 6 * kPoseCols; e += 64) {
+  double* wbuf = lds + WAVES * S::kStage;  // w [a * 22 + k]
+  double* Tm = wbuf + 6 * kPoseCols;        // T = G_ZZ w [a * 22 + k]
+  double* wcost = Tm + 6 * kPoseCols;
+  __syncthreads();  // every wave is done with its staging area
+#pragma unroll
+  for (int p = 0; p < NP; p++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) st[(p * 4 + r) * 64 + lane] = acc[p][r];
+  if (lane == 0) wcost[wave] = cost;
+  for (int e = tid; e < 6 * kPoseCols; e += 64 * WAVES) {
     const int k = e / 6, a = e % 6;
-    w[a * kPoseCols + k] = rec[12 + 6 * k + a];
+    wbuf[a * kPoseCols + k] = rec[12 + 6 * k + a];
   }
   __syncthreads();
-  // Gram is stored in upper tiles only: read (a,b) with a <= b from the upper part
-  auto g = [&](int a, int b) -> double { return (a / 16 <= b / 16) ? G[a * W16 + b] : G[b * W16 + a]; };
-  // T = G_ZZ w (6 x 22)
-  for (int e = threadIdx.x; e < 6 * kPoseCols; e += 64) {
+  if (WAVES > 1)
+    for (int e = tid; e < NP * 256; e += 64 * WAVES) {
+      double v = lds[e];
+#pragma unroll
+      for (int w = 1; w < WAVES; w++) v += lds[w * S::kStage + e];
+      lds[e] = v;
+    }
+  __syncthreads();
+  const double* G = lds;
+  auto g = [&](int a, int b) -> double { return gram_at<T>(G, a, b); };
+  for (int e = tid; e < 6 * kPoseCols; e += 64 * WAVES) {
     const int a = e / kPoseCols, k = e % kPoseCols;
     double t = 0.0;
-    for (int b = 0; b < 6; b++) t += g(a, b) * w[b * kPoseCols + k];
+#pragma unroll
+    for (int b = 0; b < 6; b++) t += g(a, b) * wbuf[b * kPoseCols + k];
     Tm[e] = t;
   }
   __syncthreads();
-  const int R = Wd - 1;  // residual column
-  const FrameDesc& F = fd[f];
-  double* grad = rep + (int64_t)(f & (kReplicas - 1)) * (ng + nh + 1);
+  const FrameLin& L = fl[frame];
+  const int R = S::kColR;
+  double* grad = rep + (int64_t)(frame & (kLinReplicas - 1)) * (ng + nh + 1);
   double* hess = grad + ng;
-  double* cost = hess + nh;
   // pose blocks: beg(0) cols 0..6, end(1) 7..13, ref_to_cam(2) 14..20, offset(4) 21
+#pragma unroll
   for (int blk = 0; blk < 4; blk++) {
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
-    if (L.goff[b] < 0) continue;
+    const int64_t go = L.goff[b];
+    if (go < 0) continue;
     const int ncol = (blk == 3) ? 1 : 7, k0 = blk * 7;
-    for (int e = threadIdx.x; e < ncol; e += 64) {
-      double gv = 0.0;
-      for (int a = 0; a < 6; a++) gv += w[a * kPoseCols + k0 + e] * g(a, R);
-      atomicAdd(&grad[L.goff[b] + e], gv);
-    }
-    for (int e = threadIdx.x; e < ncol * ncol; e += 64) {
-      const int kk = e / ncol, kc = e % ncol;
-      double hv = 0.0;
-      for (int a = 0; a < 6; a++) hv += w[a * kPoseCols + k0 + kk] * Tm[a * kPoseCols + k0 + kc];
-      atomicAdd(&hess[L.hoff[b] + e], hv);
+    const int64_t ho = L.hoff[b];
+    for (int e = tid; e < ncol + ncol * ncol; e += 64 * WAVES) {
+      double v = 0.0;
+      if (e < ncol) {
+#pragma unroll
+        for (int a = 0; a < 6; a++) v += wbuf[a * kPoseCols + k0 + e] * g(a, R);
+        atomicAdd(&grad[go + e], v);
+      } else {
+        const int h = e - ncol, kk = h / ncol, kc = h % ncol;
+#pragma unroll
+        for (int a = 0; a < 6; a++) v += wbuf[a * kPoseCols + k0 + kk] * Tm[a * kPoseCols + k0 + kc];
+        atomicAdd(&hess[ho + h], v);
+      }
     }
   }
-  // intrinsics: focal col 6, center cols 7..8, dist cols 9.. (live columns)
-  const int nd = Wd - 10;  // live distortion columns in the Gram
-  const int blocks[3] = {MVBA_BLK_FOCAL, MVBA_BLK_CENTER, MVBA_BLK_DIST};
-  const int c0s[3] = {6, 7, 9};
-  const int ncs[3] = {1, 2, nd < F.K ? nd : F.K};  // radtan K=4: 4 of the 5 Gram columns
+  // intrinsics: focal col 6, center cols 7..8, dist cols 9..
+  constexpr int kDistLive = S::kWidth - 10;
+#pragma unroll
   for (int q = 0; q < 3; q++) {
-    const int b = blocks[q];
-    if (L.goff[b] < 0) continue;
-    const int nc = ncs[q], cs = c0s[q];
-    const int bs = (b == MVBA_BLK_DIST) ? F.K : nc;  // Hessian row length (RPC: K incl. zero half)
-    for (int e = threadIdx.x; e < nc; e += 64) atomicAdd(&grad[L.goff[b] + e], g(cs + e, R));
-    for (int e = threadIdx.x; e < nc * nc; e += 64) {
-      const int r = e / nc, cc = e % nc;
-      atomicAdd(&hess[L.hoff[b] + r * bs + cc], g(cs + r, cs + cc));
+    const int b = q == 0 ? MVBA_BLK_FOCAL : q == 1 ? MVBA_BLK_CENTER : MVBA_BLK_DIST;
+    const int64_t go = L.goff[b];
+    if (go < 0) continue;
+    const int cs = q == 0 ? 6 : q == 1 ? 7 : 9;
+    const int nc = q == 0 ? 1 : q == 1 ? 2 : (kDistLive < K ? kDistLive : K);  // radtan K=4: 4 of 5 columns
+    const int bs = q == 2 ? K : nc;  // Hessian row length (RPC: K incl. the zero half)
+    const int64_t ho = L.hoff[b];
+    for (int e = tid; e < nc + nc * nc; e += 64 * WAVES) {
+      if (e < nc) {
+        atomicAdd(&grad[go + e], g(cs + e, R));
+      } else {
+        const int h = e - nc, r = h / nc, cc = h % nc;
+        atomicAdd(&hess[ho + r * bs + cc], g(cs + r, cs + cc));
+      }
     }
   }
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     double cv = 0.0;
-    for (int c = 0; c < L.chunk_count; c++) cv += slab[L.slab_off + (int64_t)c * SL + W16 * W16];
-    atomicAdd(cost, cv);
+    for (int w = 0; w < WAVES; w++) cv += wcost[w];
+    atomicAdd(hess + nh, cv);
   }
 }
 
-__global__ void __launch_bounds__(256) k_rep_reduce(double* __restrict__ rep, int64_t ng, int64_t nh,
+__global__ void __launch_bounds__(256) k_rep_reduce(double* __restrict__ rep, int32_t nrep, int64_t ng, int64_t nh,
                                                     double* __restrict__ grad, double* __restrict__ hess,
                                                     double* __restrict__ cost) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = ng + nh + 1;
   if (e >= stride) return;
+  double v[8];
   double acc = 0.0;
-#pragma unroll 8
-  for (int r = 0; r < kReplicas; r++) {
-    acc += rep[r * stride + e];
-    rep[r * stride + e] = 0.0;
+  // loads of 8 replicas in flight before the adds and the zeroing stores
+  for (int r0 = 0; r0 < nrep; r0 += 8) {
+#pragma unroll
+    for (int r = 0; r < 8; r++) v[r] = rep[(int64_t)(r0 + r) * stride + e];
+#pragma unroll
+    for (int r = 0; r < 8; r++) acc += v[r];
+#pragma unroll
+    for (int r = 0; r < 8; r++) rep[(int64_t)(r0 + r) * stride + e] = 0.0;
   }
   if (e < ng) grad[e] = acc;
   else if (e < ng + nh) hess[e - ng] = acc;
@@ -756,7 +770,7 @@ hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_
   return hipGetLastError();
 }
 
-// Gram shape of a model (host side, for slab sizing and the expand step).
+// Gram width of a model (host side; -1: no fused linearization for it).
 int mvba_gram_width(int model, int deg) {
   switch (model) {
     case mvba::kModelNone: return mvba::GramShape<mvba::kModelNone, 0>::kWidth;
@@ -773,52 +787,47 @@ int mvba_gram_width(int model, int deg) {
   }
 }
 
-hipError_t mvba_launch_gram(int model, int deg, const int4* chunks, int32_t nchunks,
-                            const mvba::Segment* segs, const mvba::FrameDesc* fd, const double* frec,
-                            const double* params, const double4* pts, const int32_t* obs_pid,
-                            const double2* obs_meas, double* slab, int32_t flags, double cauchy_c,
-                            hipStream_t s) {
-  if (nchunks <= 0) return hipSuccess;
-#define MVBA_GRAM(M, D)                                                                              \
-  {                                                                                                  \
-    const size_t lds = sizeof(double) * mvba::GramShape<M, D>::kTiles * 16 * mvba::kGramLd;          \
-    hipLaunchKernelGGL((mvba::k_gram<M, D>), dim3((unsigned)nchunks), dim3(64), lds, s, chunks, nchunks, \
-                       segs, fd, frec, params, pts, obs_pid, obs_meas, slab, flags, cauchy_c);        \
+// Camera side of the linearization into the replicas (one launch per model group).
+hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t nparts, const mvba::Segment* segs,
+                                 const mvba::FrameDesc* fd, const void* fl, const double* frec, const double* params,
+                                 const double4* pts, const int32_t* obs_pid, const double2* obs_meas, double* rep,
+                                 int64_t ng, int64_t nh, int32_t flags, double cauchy_c, hipStream_t s) {
+  if (nparts <= 0) return hipSuccess;
+#define MVBA_FLIN(M, D)                                                                                    \
+  {                                                                                                        \
+    using GS = mvba::GramShape<M, D>;                                                                      \
+    hipLaunchKernelGGL((mvba::k_frame_lin<M, D>), dim3((unsigned)nparts), dim3(64 * GS::kWaves),           \
+                       GS::kLdsBytes, s, parts, nparts, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, \
+                       obs_pid, obs_meas, rep, ng, nh, flags, cauchy_c);                                   \
   }
   switch (model) {
-    case mvba::kModelNone: MVBA_GRAM(mvba::kModelNone, 0); break;
-    case mvba::kModelFov: MVBA_GRAM(mvba::kModelFov, 0); break;
-    case mvba::kModelRadtan: MVBA_GRAM(mvba::kModelRadtan, 0); break;
+    case mvba::kModelNone: MVBA_FLIN(mvba::kModelNone, 0); break;
+    case mvba::kModelFov: MVBA_FLIN(mvba::kModelFov, 0); break;
+    case mvba::kModelRadtan: MVBA_FLIN(mvba::kModelRadtan, 0); break;
     case mvba::kModelRpc:
       switch (deg) {
-        case 1: MVBA_GRAM(mvba::kModelRpc, 1); break;
-        case 2: MVBA_GRAM(mvba::kModelRpc, 2); break;
-        case 3: MVBA_GRAM(mvba::kModelRpc, 3); break;
+        case 1: MVBA_FLIN(mvba::kModelRpc, 1); break;
+        case 2: MVBA_FLIN(mvba::kModelRpc, 2); break;
+        case 3: MVBA_FLIN(mvba::kModelRpc, 3); break;
         default: return hipErrorInvalidValue;
       }
       break;
     default: return hipErrorInvalidValue;
   }
-#undef MVBA_GRAM
+#undef MVBA_FLIN
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_expand(const void* fl, int32_t nframes, int32_t max_w16,
-                              const mvba::FrameDesc* fd, const double* frec, const double* slab,
-                              double* rep, int64_t ng, int64_t nh, double* grad, double* hess,
-                              double* cost, hipStream_t s) {
-  if (nframes > 0) {
-    const size_t lds = sizeof(double) * ((size_t)max_w16 * max_w16 + 1 + 2 * 6 * mvba::kPoseCols);
-    hipLaunchKernelGGL(mvba::k_expand, dim3((unsigned)nframes), dim3(64), lds, s,
-                       (const mvba::FrameLin*)fl, nframes, fd, frec, slab, rep, ng, nh);
-  }
+hipError_t mvba_launch_rep_reduce(double* rep, int32_t nrep, int64_t ng, int64_t nh, double* grad, double* hess,
+                                  double* cost, hipStream_t s) {
   const int64_t n = ng + nh + 1;
-  hipLaunchKernelGGL(mvba::k_rep_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rep, ng, nh,
+  if (nrep % 8 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mvba::k_rep_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rep, nrep, ng, nh,
                      grad, hess, cost);
   return hipGetLastError();
 }
 
-int mvba_num_replicas(void) { return mvba::kReplicas; }
+int mvba_num_replicas(void) { return mvba::kLinReplicas; }
 
 // model < 0: mixed models (runtime dispatch).
 hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, int64_t npts,

@@ -56,7 +56,9 @@ enum ModelKind : int32_t {
 
 constexpr int kMaxRpcDegree = 6;
 constexpr int kMaxLinRpcDegree = 3;
-constexpr int kChunkSegs = 4;       // segments per K2a chunk (one wave)  // the MFMA Gram linearization covers RPC degree <= 3
+constexpr int kChunkSegs = 4;       // segments per solver chunk (one wave)
+constexpr int kPartSegs = 16;       // segments per K2 frame part (one block)
+constexpr int kDepthReplicas = 32;  // replicas the depth Gram adds into (frame-segment mod 32)  // the MFMA Gram linearization covers RPC degree <= 3
 
 // Per-frame record of the linearization (K2 expand); mirrors mvba::FrameLin in
 // mvba_kernels.hip (checked with mvba_frame_lin_size()).

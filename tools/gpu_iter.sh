@@ -17,7 +17,7 @@ run() {
   tail -3 "$OUT/$name.log" | cut -c1-300
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-run pytest_gpu_$TAG 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
+run pytest_gpu_$TAG 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 400 --timeout-method thread
 run prof_${CFG}_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_${CFG}_$TAG -o run --output-format csv -- python3 bench.py --config $CFG --steps 10 --no-cpu-baseline
 python3 tools/bench_summary.py $OUT/prof_${CFG}_$TAG.log
 exit 0
