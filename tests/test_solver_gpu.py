@@ -230,7 +230,10 @@ def test_depth_converged_params_match_cpu_lm():
 
 def test_bounded_offsets_and_callback_path():
     """Floated timestamp offsets carry the reference's bracket bounds; a no-op
-    allreduce callback (single rank) must not change the result."""
+    allreduce callback (single rank: the sharded code path, exchange, then
+    damping and dot as separate kernels) reaches the same solution. The camera
+    side adds shared blocks with fp64 atomics, so two solves agree to rounding,
+    not bit for bit (bit-identity: the deterministic mode, below)."""
     R, P = _problem(["radtan", "radtan", "fov"], seed=55)
     lo, hi = rig.offset_bounds(R, P, FLAGS)
     assert np.isfinite(lo).sum() == 2
@@ -245,7 +248,8 @@ def test_bounded_offsets_and_callback_path():
         x1 = ev.get_params()
     assert calls and all(op in (0, 1) for _, op in calls)
     assert s0["termination_type"] == 0 and s1["termination_type"] == 0
-    assert np.array_equal(x0, x1)
+    assert np.isclose(s0["final_cost"], s1["final_cost"], rtol=1e-10)
+    assert _close(x0, x1, 1e-7)
     assert np.all(x0 >= lo) and np.all(x0 <= hi)
 
 
