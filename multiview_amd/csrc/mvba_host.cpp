@@ -41,11 +41,6 @@ static void free_all(mvba_handle* h) {
                   h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt};
   solver_state_free(h->solver);
   h->solver = nullptr;
-  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
-  if (h->aux_stream) (void)hipStreamDestroy(h->aux_stream);
-  h->ev_fork = h->ev_join = nullptr;
-  h->aux_stream = nullptr;
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
 }
@@ -878,30 +873,26 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
     return h->fail(MVBA_E_INVALID, "MVBA_EVAL_SKIP_PREP before any full evaluation");
   }
   const int32_t lflags = flags & MVBA_EVAL_APPLY_LOSS;
-  // point side (K2b) on the auxiliary stream, beside the camera side (K2a):
-  // both read the K0 records and points of the prep above and write disjoint
-  // outputs; the caller's stream joins the point side before returning
-  if (e == hipSuccess && !h->aux_stream) {
-    e = hipStreamCreateWithFlags(&h->aux_stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming);
+  // Camera side (K2a) per model group; a single-model problem runs the point
+  // side (K2b) as extra blocks of the same launch, so the two overlap on the
+  // device without a second stream. Mixed models: a separate point launch.
+  const bool single = h->groups.size() == 1;
+  const mvba::PointExtra dc = h->point_extra();
+  if (cam_side) {
+    for (size_t g = 0; g < h->groups.size() && e == hipSuccess; g++) {
+      const Group& G = h->groups[g];
+      const bool pts_here = single && pt_side;
+      e = mvba_launch_frame_lin(G.model, G.deg, h->d_parts + G.part_begin, G.part_count, h->d_segs, h->d_fd,
+                                h->d_frame_lin, h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
+                                h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags, cauchy_c,
+                                pts_here ? h->d_pt_begin : nullptr, h->npts, h->d_po_frame, h->d_po_meas, d_pt_grad,
+                                d_pt_hess, dc, s);
+    }
   }
-  if (pt_side) {
-    if (e == hipSuccess) e = hipEventRecord(h->ev_fork, s);
-    if (e == hipSuccess) e = hipStreamWaitEvent(h->aux_stream, h->ev_fork, 0);
-    if (e == hipSuccess)
-      e = mvba_launch_points_lin(h->groups.size() == 1 ? h->groups[0].model : -1,
-                                 h->groups.size() == 1 ? h->groups[0].deg : 0, h->d_pt_begin, h->npts,
-                                 h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
-                                 d_pt_grad, d_pt_hess, lflags, cauchy_c, h->point_extra(), h->aux_stream);
-    if (e == hipSuccess) e = hipEventRecord(h->ev_join, h->aux_stream);
-  }
-  for (size_t g = 0; cam_side && g < h->groups.size() && e == hipSuccess; g++) {
-    const Group& G = h->groups[g];
-    e = mvba_launch_frame_lin(G.model, G.deg, h->d_parts + G.part_begin, G.part_count, h->d_segs, h->d_fd,
-                              h->d_frame_lin, h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
-                              h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags, cauchy_c, s);
-  }
+  if (pt_side && (!single || !cam_side) && e == hipSuccess)
+    e = mvba_launch_points_lin(single ? h->groups[0].model : -1, single ? h->groups[0].deg : 0, h->d_pt_begin,
+                               h->npts, h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
+                               d_pt_grad, d_pt_hess, lflags, cauchy_c, dc, s);
   if (cam_side && e == hipSuccess && h->ndep_segs > 0)
     e = mvba_launch_depth_gram(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_frec, h->d_params,
                                h->d_pts, h->d_frame_lin, h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags,
@@ -909,7 +900,6 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
   if (cam_side && e == hipSuccess)
     e = mvba_launch_rep_reduce(h->d_rep, h->nrep, h->cam_grad_size, h->cam_hess_size, d_cam_grad, d_cam_hess, d_cost,
                                s);
-  if (pt_side && e == hipSuccess) e = hipStreamWaitEvent(s, h->ev_join, 0);
   if (cam_side && e == hipSuccess && h->nxyz > 0 && d_cost) {
     e = mvba_launch_xyz_cost(h->nxyz, h->d_xpid, h->d_xref, h->d_xcc, h->d_pts, lflags, h->d_xscal + 1, h->d_xcnt,
                              h->d_xscal, s);

@@ -31,7 +31,9 @@ size_t mvba_frame_lin_size(void);
 hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t nparts, const Segment* segs,
                                  const FrameDesc* fd, const void* fl, const double* frec, const double* params,
                                  const double4* pts, const int32_t* obs_pid, const double2* obs_meas, double* rep,
-                                 int64_t ng, int64_t nh, int32_t flags, double cauchy_c, hipStream_t s);
+                                 int64_t ng, int64_t nh, int32_t flags, double cauchy_c, const int64_t* pt_begin,
+                                 int64_t npts, const int32_t* po_frame, const double2* po_meas, double* pgrad,
+                                 double* phess, mvba::PointExtra dc, hipStream_t s);
 hipError_t mvba_launch_rep_reduce(double* rep, int32_t nrep, int64_t ng, int64_t nh, double* grad, double* hess,
                                   double* cost, hipStream_t s);
 int mvba_num_replicas(void);
@@ -195,8 +197,6 @@ struct mvba_handle {
   void* d_frame_lin = nullptr;
   int4* d_parts = nullptr;              // K2 frame parts (seg_begin, seg_count, frame, -)
   double* d_rep = nullptr;  // nrep copies of [cam_grad | cam_hess | cost], kept zero between calls
-  hipStream_t aux_stream = nullptr;     // K2 point side runs beside the camera side
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t* d_pt_begin = nullptr;
   int32_t* d_po_frame = nullptr;
   double2* d_po_meas = nullptr;

@@ -381,12 +381,32 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 template <int MODEL, int DEG>
+__device__ __forceinline__ void points_lin_body(
+    int64_t t, const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
+    const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, double* __restrict__ pgrad, double* __restrict__ phess,
+    int32_t flags, double cauchy_c, const PointExtra& dc);
+
+// The point side (K2b) as extra blocks of the same launch (single-model problems):
+// blocks past the frame parts take kLanesPerPoint threads per point.
+struct PointLinArgs {
+  const int64_t* pt_begin;
+  int64_t npts;
+  const int32_t* po_frame;
+  const double2* po_meas;
+  double* pgrad;
+  double* phess;
+  PointExtra dc;
+};
+
+template <int MODEL, int DEG, bool POINTS>
 __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_lin(
     const int4* __restrict__ parts, int32_t nparts, const Segment* __restrict__ segs,
     const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl, const double* __restrict__ frec,
     const double* __restrict__ params, const double4* __restrict__ pts,
     const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
-    double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c) {
+    double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c, PointLinArgs pa) {
   using S = GramShape<MODEL, DEG>;
   constexpr int T = S::kTiles;
   constexpr int NP = S::kPairs;
@@ -394,7 +414,13 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
   constexpr int W16 = T * 16;
   extern __shared__ double lds[];  // [WAVES][kStage] | w [6 x 22] | Tm [6 x 22] | cost [WAVES]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  if ((int)blockIdx.x >= nparts) return;
+  if ((int)blockIdx.x >= nparts) {
+    if constexpr (POINTS)
+      points_lin_body<MODEL, DEG>((int64_t)(blockIdx.x - nparts) * blockDim.x + tid, pa.pt_begin, pa.npts,
+                                  pa.po_frame, pa.po_meas, fd, frec, params, pts, pa.pgrad, pa.phess, flags,
+                                  cauchy_c, pa.dc);
+    return;
+  }
   const int4 part = parts[blockIdx.x];  // seg_begin, seg_count, frame, -
   const int frame = __builtin_amdgcn_readfirstlane(part.z);
   const FrameDesc& F = fd[frame];
@@ -633,14 +659,14 @@ __device__ __forceinline__ void point_obs(const FrameDesc& F, const double* __re
 // dispatch per observation); otherwise the single model of the problem.
 constexpr int kLanesPerPoint = 4;
 
+// t: thread index of the point role (kLanesPerPoint consecutive threads per point)
 template <int MODEL, int DEG>
-__global__ void __launch_bounds__(256) k_points_lin(
-    const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
+__device__ __forceinline__ void points_lin_body(
+    int64_t t, const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
     const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, double* __restrict__ pgrad, double* __restrict__ phess,
-    int32_t flags, double cauchy_c, PointExtra dc) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int32_t flags, double cauchy_c, const PointExtra& dc) {
   const int64_t p = t / kLanesPerPoint;
   const int sub = (int)(t % kLanesPerPoint);
   const bool valid = p < npts;
@@ -715,6 +741,17 @@ __global__ void __launch_bounds__(256) k_points_lin(
   }
 }
 
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(256) k_points_lin(
+    const int64_t* __restrict__ pt_begin, int64_t npts, const int32_t* __restrict__ po_frame,
+    const double2* __restrict__ po_meas, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, double* __restrict__ pgrad, double* __restrict__ phess,
+    int32_t flags, double cauchy_c, PointExtra dc) {
+  points_lin_body<MODEL, DEG>((int64_t)blockIdx.x * blockDim.x + threadIdx.x, pt_begin, npts, po_frame, po_meas, fd,
+                              frec, params, pts, pgrad, phess, flags, cauchy_c, dc);
+}
+
 }  // namespace mvba
 
 // ------------------------------------------------------------ launchers
@@ -787,18 +824,32 @@ int mvba_gram_width(int model, int deg) {
   }
 }
 
-// Camera side of the linearization into the replicas (one launch per model group).
+// Camera side of the linearization into the replicas (one launch per model
+// group); with pt_begin non-null the same launch also runs the point side
+// (single-model problems: the point blocks follow the frame-part blocks).
 hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t nparts, const mvba::Segment* segs,
                                  const mvba::FrameDesc* fd, const void* fl, const double* frec, const double* params,
                                  const double4* pts, const int32_t* obs_pid, const double2* obs_meas, double* rep,
-                                 int64_t ng, int64_t nh, int32_t flags, double cauchy_c, hipStream_t s) {
-  if (nparts <= 0) return hipSuccess;
+                                 int64_t ng, int64_t nh, int32_t flags, double cauchy_c, const int64_t* pt_begin,
+                                 int64_t npts, const int32_t* po_frame, const double2* po_meas, double* pgrad,
+                                 double* phess, mvba::PointExtra dc, hipStream_t s) {
+  const bool with_pts = pt_begin != nullptr && npts > 0;
+  if (nparts <= 0 && !with_pts) return hipSuccess;
+  const mvba::PointLinArgs pa{pt_begin, npts, po_frame, po_meas, pgrad, phess, dc};
 #define MVBA_FLIN(M, D)                                                                                    \
   {                                                                                                        \
     using GS = mvba::GramShape<M, D>;                                                                      \
-    hipLaunchKernelGGL((mvba::k_frame_lin<M, D>), dim3((unsigned)nparts), dim3(64 * GS::kWaves),           \
-                       GS::kLdsBytes, s, parts, nparts, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, \
-                       obs_pid, obs_meas, rep, ng, nh, flags, cauchy_c);                                   \
+    const int64_t threads = 64 * GS::kWaves;                                                               \
+    const int64_t pblocks = with_pts ? (npts * mvba::kLanesPerPoint + threads - 1) / threads : 0;          \
+    if (with_pts)                                                                                          \
+      hipLaunchKernelGGL((mvba::k_frame_lin<M, D, true>), dim3((unsigned)(nparts + pblocks)),             \
+                         dim3((unsigned)threads), GS::kLdsBytes, s, parts, nparts, segs, fd,               \
+                         (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas, rep, ng, nh, flags, \
+                         cauchy_c, pa);                                                                    \
+    else                                                                                                   \
+      hipLaunchKernelGGL((mvba::k_frame_lin<M, D, false>), dim3((unsigned)nparts), dim3((unsigned)threads), \
+                         GS::kLdsBytes, s, parts, nparts, segs, fd, (const mvba::FrameLin*)fl, frec, params, \
+                         pts, obs_pid, obs_meas, rep, ng, nh, flags, cauchy_c, pa);                        \
   }
   switch (model) {
     case mvba::kModelNone: MVBA_FLIN(mvba::kModelNone, 0); break;
