@@ -448,10 +448,18 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
           L.w16 = G.w16;
         }
         chunks.back().y++;
-        if (parts.size() == (size_t)G.part_begin || parts.back().z != sg.frame ||
-            parts.back().y == mvba::kPartSegs)
-          parts.push_back(make_int4(sidx, 0, sg.frame, 0));
-        parts.back().y++;
+      }
+      // K2 parts: a frame's run of segments split evenly into ceil(n / kPartSegs) parts
+      for (int32_t r0 = G.seg_begin; r0 < G.seg_begin + G.seg_count;) {
+        int32_t r1 = r0;
+        while (r1 < G.seg_begin + G.seg_count && segs[r1].frame == segs[r0].frame) r1++;
+        const int32_t n = r1 - r0, np = (n + mvba::kPartSegs - 1) / mvba::kPartSegs;
+        for (int32_t q = 0, at = r0; q < np; q++) {
+          const int32_t len = n / np + (q < n % np ? 1 : 0);
+          parts.push_back(make_int4(at, len, segs[r0].frame, 0));
+          at += len;
+        }
+        r0 = r1;
       }
       G.chunk_count = (int32_t)chunks.size() - G.chunk_begin;
       G.part_count = (int32_t)parts.size() - G.part_begin;

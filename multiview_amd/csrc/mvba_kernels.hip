@@ -345,6 +345,10 @@ __global__ void __launch_bounds__(256) k_obs(
 // lane l and register r hold G[16 ti + (l >> 4) + 4 r][16 tj + (l & 15)].
 constexpr int kGramLd = 66;  // 64 rows + 2 pad doubles: bank-conflict-free reads
 constexpr int kLinReplicas = 8;
+#ifndef MVBA_FLIN_WAVES
+#define MVBA_FLIN_WAVES 2
+#endif
+#define MVBA_FLIN_WAVES_SMALL_T_OVERRIDE (kTiles <= 2 ? MVBA_FLIN_WAVES : kTiles <= 4 ? 2 : 1)
 
 template <int MODEL, int DEG>
 struct GramShape {
@@ -355,7 +359,7 @@ struct GramShape {
   static constexpr int kPairs = kTiles * (kTiles + 1) / 2;
   static constexpr int kColR = kWidth - 1;              // residual column
   // waves per block: LDS staging is kTiles*16*kGramLd doubles per wave
-  static constexpr int kWaves = kTiles <= 2 ? 4 : kTiles <= 4 ? 2 : 1;
+  static constexpr int kWaves = MVBA_FLIN_WAVES_SMALL_T_OVERRIDE;
   static constexpr int kStage = kTiles * 16 * kGramLd;
   static constexpr size_t kLdsBytes = sizeof(double) * ((size_t)kWaves * kStage + 2 * 6 * kPoseCols + kWaves);
 };
