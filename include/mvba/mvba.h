@@ -267,7 +267,7 @@ typedef struct mvba_lin_layout {
   int64_t cam_hess_size;   /* doubles */
   int64_t num_points;
   int32_t num_cam_blocks;
-  int32_t supported;       /* 0 if a camera model is outside the Gram path (RPC degree > 3) */
+  int32_t supported;       /* 0 if a camera model is outside the linearization (RPC degree > 6) */
 } mvba_lin_layout;
 
 mvba_status mvba_lin_layout_info(const struct mvba_handle* h, mvba_lin_layout* out);

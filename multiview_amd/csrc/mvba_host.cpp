@@ -407,7 +407,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     for (const Group& G : h->groups)
       if (G.model == mvba::kModelRpc && G.deg > mvba::kMaxLinRpcDegree) {
         h->lin_ok = false;
-        h->lin_err = "linearization supports RPC degree <= 3";
+        h->lin_err = "linearization supports RPC degree <= " + std::to_string(mvba::kMaxLinRpcDegree);
       }
     // camera-side blocks: not constant, not a point block, in block-id order
     std::vector<uint8_t> is_point(d->num_blocks, 0);

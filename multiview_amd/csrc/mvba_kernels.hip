@@ -361,6 +361,8 @@ struct GramShape {
   // waves per block: LDS staging is kTiles*16*kGramLd doubles per wave
   static constexpr int kWaves = MVBA_FLIN_WAVES_SMALL_T_OVERRIDE;
   static constexpr int kStage = kTiles * 16 * kGramLd;
+  // rows straight into LDS (no register row arrays) from 3 tiles up
+  static constexpr bool kDirect = kTiles >= 3;
   static constexpr size_t kLdsBytes = sizeof(double) * ((size_t)kWaves * kStage + 2 * 6 * kPoseCols + kWaves);
 };
 
@@ -445,71 +447,96 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
   if (lane < 32)
     for (int col = S::kWidth; col < W16; col++) *(dbl2v*)&st[col * kGramLd + 2 * lane] = dbl2v{0.0, 0.0};
 
+  // One observation's row pair [Z | focal | centre | dist | r] (Cauchy-corrected),
+  // emitted column by column as put(q, v_row0, v_row1).
+  auto rows = [&](int64_t i, auto&& put) {
+    const double4 P = pts[obs_pid[i]];
+    const double2 meas = obs_meas[i];
+    Proj o;
+    project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, kd, K, F.h0, F.h1, o);
+    const double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
+    double half_rho;
+    const double sr = loss_scale(r0, r1, flags, cauchy_c, &half_rho);
+    cost += half_rho;
+    const double fz = f / o.Xc[2] * sr;
+    const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+    const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
+    double a0[3], a1[3];
+    cross(o.Xc, G0, a0);
+    cross(o.Xc, G1, a1);
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      put(q, a0[q], a1[q]);
+      put(3 + q, G0[q], G1[q]);
+    }
+    put(6, o.df0 * sr, o.df1 * sr);
+    const double cc = (MODEL == kModelRpc) ? 0.0 : sr;
+    put(7, cc, 0.0);
+    put(8, 0.0, cc);
+    dist_columns<MODEL, DEG>(o, f, K, sr, [&](int q, double v0, double v1) { put(9 + q, v0, v1); });
+    put(S::kColR, r0 * sr, r1 * sr);
+  };
+  // MFMA over the 64 staged rows: acc[(ti, tj)] += B_ti^T B_tj
+  auto gram64 = [&]() {
+    const int col = lane & 15, rsub = lane >> 4;
+#pragma unroll 4
+    for (int stp = 0; stp < 16; stp++) {
+      const int row = 4 * stp + rsub;
+      double v[T];
+#pragma unroll
+      for (int t = 0; t < T; t++) v[t] = st[(t * 16 + col) * kGramLd + row];
+      int p = 0;
+#pragma unroll
+      for (int ti = 0; ti < T; ti++)
+#pragma unroll
+        for (int tj = ti; tj < T; tj++) {
+          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ti], v[tj], acc[p], 0, 0, 0);
+          p++;
+        }
+    }
+  };
+
   for (int sidx = wave; sidx < part.y; sidx += WAVES) {
     const Segment sg = segs[part.x + sidx];
     const int count = __builtin_amdgcn_readfirstlane(sg.count);
     const int64_t i = (int64_t)sg.begin + lane;
-    double row0[S::kWidth], row1[S::kWidth];
+    if constexpr (!S::kDirect) {
+      // rows in registers, then staged as [column][row] 64 rows at a time; the
+      // halves past the segment's last observation are all zero rows
+      double row0[S::kWidth], row1[S::kWidth];
 #pragma unroll
-    for (int q = 0; q < S::kWidth; q++) row0[q] = row1[q] = 0.0;
-    if (lane < count) {
-      const double4 P = pts[obs_pid[i]];
-      const double2 meas = obs_meas[i];
-      Proj o;
-      project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, kd, K, F.h0, F.h1, o);
-      double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
-      double half_rho;
-      const double sr = loss_scale(r0, r1, flags, cauchy_c, &half_rho);
-      cost += half_rho;
-      const double fz = f / o.Xc[2] * sr;
-      const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
-      const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
-      double a0[3], a1[3];
-      cross(o.Xc, G0, a0);
-      cross(o.Xc, G1, a1);
+      for (int q = 0; q < S::kWidth; q++) row0[q] = row1[q] = 0.0;
+      if (lane < count)
+        rows(i, [&](int q, double v0, double v1) {
+          row0[q] = v0;
+          row1[q] = v1;
+        });
+      for (int half = 0; half < 2 && 32 * half < count; half++) {
+        if ((lane >> 5) == half) {
 #pragma unroll
-      for (int q = 0; q < 3; q++) {
-        row0[q] = a0[q]; row0[3 + q] = G0[q];
-        row1[q] = a1[q]; row1[3 + q] = G1[q];
+          for (int q = 0; q < S::kWidth; q++)
+            *(dbl2v*)&st[q * kGramLd + 2 * (lane & 31)] = dbl2v{row0[q], row1[q]};
+        }
+        wave_lds_sync();
+        gram64();
+        wave_lds_sync();
       }
-      row0[6] = o.df0 * sr;
-      row1[6] = o.df1 * sr;
-      const double cc = (MODEL == kModelRpc) ? 0.0 : sr;
-      row0[7] = cc; row0[8] = 0.0;
-      row1[7] = 0.0; row1[8] = cc;
-      dist_columns<MODEL, DEG>(o, f, K, sr, [&](int q, double v0, double v1) {
-        row0[9 + q] = v0;
-        row1[9 + q] = v1;
-      });
-      row0[S::kColR] = r0 * sr;
-      row1[S::kColR] = r1 * sr;
-    }
-    // stage this segment's 128 rows as [column][row], 64 rows at a time; the
-    // halves past the segment's last observation are all zero rows
-    const int col = lane & 15, rsub = lane >> 4;
-    for (int half = 0; half < 2 && 32 * half < count; half++) {
-      if ((lane >> 5) == half) {
-#pragma unroll
-        for (int q = 0; q < S::kWidth; q++)
-          *(dbl2v*)&st[q * kGramLd + 2 * (lane & 31)] = dbl2v{row0[q], row1[q]};
+    } else {
+      // wide Grams (RPC degree >= 2): the lanes of the active half write their
+      // columns straight into the staging area as they are produced (no row
+      // arrays in registers; the other half idles through the projection)
+      for (int half = 0; half < 2 && 32 * half < count; half++) {
+        if ((lane >> 5) == half) {
+          const int slot = 2 * (lane & 31);
+          if (lane < count)
+            rows(i, [&](int q, double v0, double v1) { *(dbl2v*)&st[q * kGramLd + slot] = dbl2v{v0, v1}; });
+          else
+            for (int q = 0; q < S::kWidth; q++) *(dbl2v*)&st[q * kGramLd + slot] = dbl2v{0.0, 0.0};
+        }
+        wave_lds_sync();
+        gram64();
+        wave_lds_sync();
       }
-      wave_lds_sync();
-#pragma unroll 4
-      for (int stp = 0; stp < 16; stp++) {
-        const int row = 4 * stp + rsub;
-        double v[T];
-#pragma unroll
-        for (int t = 0; t < T; t++) v[t] = st[(t * 16 + col) * kGramLd + row];
-        int p = 0;
-#pragma unroll
-        for (int ti = 0; ti < T; ti++)
-#pragma unroll
-          for (int tj = ti; tj < T; tj++) {
-            acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ti], v[tj], acc[p], 0, 0, 0);
-            p++;
-          }
-      }
-      wave_lds_sync();
     }
   }
   // ---- the block's Gram: waves' accumulators summed in wave order (in place
@@ -693,6 +720,9 @@ __device__ __forceinline__ void points_lin_body(
         else if (K == 20) point_obs<kModelRpc, 1>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
         else if (K == 44) point_obs<kModelRpc, 2>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
         else if (K == 76) point_obs<kModelRpc, 3>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 116) point_obs<kModelRpc, 4>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 164) point_obs<kModelRpc, 5>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
+        else if (K == 220) point_obs<kModelRpc, 6>(F, rec, params, X.x, X.y, X.z, m, flags, cauchy_c, V, g);
       }
     }
   }
@@ -822,7 +852,10 @@ int mvba_gram_width(int model, int deg) {
         case 1: return mvba::GramShape<mvba::kModelRpc, 1>::kWidth;
         case 2: return mvba::GramShape<mvba::kModelRpc, 2>::kWidth;
         case 3: return mvba::GramShape<mvba::kModelRpc, 3>::kWidth;
-        default: return -1;  // the MFMA Gram path covers RPC degree <= 3
+        case 4: return mvba::GramShape<mvba::kModelRpc, 4>::kWidth;
+        case 5: return mvba::GramShape<mvba::kModelRpc, 5>::kWidth;
+        case 6: return mvba::GramShape<mvba::kModelRpc, 6>::kWidth;
+        default: return -1;  // the evaluator covers RPC degree <= kMaxRpcDegree
       }
     default: return -1;
   }
@@ -864,6 +897,9 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
         case 1: MVBA_FLIN(mvba::kModelRpc, 1); break;
         case 2: MVBA_FLIN(mvba::kModelRpc, 2); break;
         case 3: MVBA_FLIN(mvba::kModelRpc, 3); break;
+        case 4: MVBA_FLIN(mvba::kModelRpc, 4); break;
+        case 5: MVBA_FLIN(mvba::kModelRpc, 5); break;
+        case 6: MVBA_FLIN(mvba::kModelRpc, 6); break;
         default: return hipErrorInvalidValue;
       }
       break;
@@ -907,6 +943,9 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
           case 1: MVBA_PTS(mvba::kModelRpc, 1); break;
           case 2: MVBA_PTS(mvba::kModelRpc, 2); break;
           case 3: MVBA_PTS(mvba::kModelRpc, 3); break;
+          case 4: MVBA_PTS(mvba::kModelRpc, 4); break;
+          case 5: MVBA_PTS(mvba::kModelRpc, 5); break;
+          case 6: MVBA_PTS(mvba::kModelRpc, 6); break;
           default: return hipErrorInvalidValue;
         }
         break;

@@ -14,7 +14,7 @@
 
 namespace mvba {
 
-constexpr int kDirStride = 64;     // per-frame direction record: u (6) | x_intr (<= 58)
+constexpr int kDirStride = 128;    // per-frame direction record: u (6) | x_intr (<= 122: RPC degree 6 has 113)
 constexpr int kVecReplicas = 32;
 
 // Camera-side columns of one observation at a frame, as a row pair:
@@ -120,9 +120,9 @@ __global__ void __launch_bounds__(64) k_frame_dir(const FrameLin* __restrict__ f
       if (lane == a) v = u[a];
     d[lane] = v;
   }
-  const int m = lane - kPoseCols;  // 0 focal, 1..2 centre, 3.. distortion
+  // lanes 22.. copy the intrinsic entries: 0 focal, 1..2 centre, 3.. distortion
   const int nd = L.width - 10;
-  if (m >= 0 && m < 3 + nd) {
+  for (int m = lane - kPoseCols; m >= 0 && m < 3 + nd; m += 64 - kPoseCols) {
     double v = 0.0;
     if (m == 0) {
       if (L.goff[MVBA_BLK_FOCAL] >= 0) v = X(L.goff[MVBA_BLK_FOCAL]);
@@ -221,7 +221,10 @@ __device__ __forceinline__ void pass_a_dispatch(const double* __restrict__ rec, 
     else if (K == 4 || K == 5) pass_a_obs<kModelRadtan, 0>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
     else if (K == 20) pass_a_obs<kModelRpc, 1>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
     else if (K == 44) pass_a_obs<kModelRpc, 2>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
-    else pass_a_obs<kModelRpc, 3>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 76) pass_a_obs<kModelRpc, 3>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 116) pass_a_obs<kModelRpc, 4>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else if (K == 164) pass_a_obs<kModelRpc, 5>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
+    else pass_a_obs<kModelRpc, 6>(rec, dirf, X, m, flags, cauchy_c, z, P0, P1);
   }
 }
 
@@ -467,6 +470,134 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
   for (int q = 0; q < 3; q++) wout[wstride * p + q] = w[q];
 }
 
+// ------------------------------------------------------------ pass B, wide rows
+// Wide intrinsic blocks (RPC degree >= 4: up to 113 intrinsic columns) do not
+// fit per-lane accumulators: the lanes of one half-segment write their row pair
+// [Z | I] and u_o straight into LDS ([column][row], as the Gram staging of K2),
+// then every lane reduces its columns (lane, lane + 64) over the 64 rows.
+constexpr int kPassBRegCols = 48;  // register accumulators up to this many columns
+constexpr int kWideLd = 66;
+
+template <int MODEL, int DEG>
+constexpr size_t pass_b_lds() {
+  constexpr int NA = 6 + RowShape<MODEL, DEG>::kIntr;
+  return NA > kPassBRegCols ? sizeof(double) * (size_t)(NA + 1) * kWideLd : 0;
+}
+
+template <int MODEL, int DEG>
+__device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segment* __restrict__ segs,
+                                            const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
+                                            const double* __restrict__ frec, const double* __restrict__ params,
+                                            const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
+                                            const double2* __restrict__ obs_meas, const double* __restrict__ dir,
+                                            const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng,
+                                            int32_t flags, double cauchy_c) {
+  using RS = RowShape<MODEL, DEG>;
+  constexpr int NA = 6 + RS::kIntr;
+  extern __shared__ double st[];  // [NA + 1][kWideLd]: columns, then u
+  const int lane = threadIdx.x;
+  const int frame = __builtin_amdgcn_readfirstlane(c.z);
+  const FrameDesc& F = fd[frame];
+  const double* __restrict__ rec = frec + (int64_t)frame * kFrameRecDoubles;
+  const double* __restrict__ d = dir ? dir + (int64_t)frame * kDirStride : nullptr;
+  const double f = params[F.off[MVBA_BLK_FOCAL]];
+  const double c0 = params[F.off[MVBA_BLK_CENTER]];
+  const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
+  double acc0 = 0.0, acc1 = 0.0;  // columns lane, lane + 64
+  for (int sidx = 0; sidx < c.y; sidx++) {
+    const Segment sg = segs[c.x + sidx];
+    const int count = __builtin_amdgcn_readfirstlane(sg.count);
+    for (int half = 0; half < 2 && 32 * half < count; half++) {
+      if ((lane >> 5) == half) {
+        const int slot = 2 * (lane & 31);
+        if (lane < count) {
+          const int64_t i = (int64_t)sg.begin + lane;
+          const int32_t pid = obs_pid[i];
+          const double4 X = pts[pid];
+          const double2 m = obs_meas[i];
+          Proj o;
+          project<MODEL, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+          double hr;
+          const double sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
+          const double fz = f / o.Xc[2] * sr;
+          const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+          const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
+          double a0[3], a1[3];
+          cross(o.Xc, G0, a0);
+          cross(o.Xc, G1, a1);
+          double z0 = 0.0, z1 = 0.0;
+          auto put = [&](int q, double v0, double v1) {
+            *(dbl2v*)&st[q * kWideLd + slot] = dbl2v{v0, v1};
+            if (d) {
+              z0 += v0 * d[q];
+              z1 += v1 * d[q];
+            }
+          };
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            put(q, a0[q], a1[q]);
+            put(3 + q, G0[q], G1[q]);
+          }
+          put(6, o.df0 * sr, o.df1 * sr);
+          const double cc = (MODEL == kModelRpc) ? 0.0 : sr;
+          put(7, cc, 0.0);
+          put(8, 0.0, cc);
+          dist_columns<MODEL, DEG>(o, f, F.K, sr, [&](int q, double v0, double v1) { put(9 + q, v0, v1); });
+          double P0[3], P1[3];
+#pragma unroll
+          for (int q = 0; q < 3; q++) {
+            P0[q] = G0[0] * rec[q] + G0[1] * rec[3 + q] + G0[2] * rec[6 + q];
+            P1[q] = G1[0] * rec[q] + G1[1] * rec[3 + q] + G1[2] * rec[6 + q];
+          }
+          const double4 w = wbuf[pid];
+          const double ux = z0 - (P0[0] * w.x + P0[1] * w.y + P0[2] * w.z);
+          const double uy = z1 - (P1[0] * w.x + P1[1] * w.y + P1[2] * w.z);
+          *(dbl2v*)&st[NA * kWideLd + slot] = dbl2v{ux, uy};
+        } else {
+          for (int q = 0; q <= NA; q++) *(dbl2v*)&st[q * kWideLd + slot] = dbl2v{0.0, 0.0};
+        }
+      }
+      __syncthreads();  // one wave per block: a wave barrier with the LDS drained
+#pragma unroll 4
+      for (int r = 0; r < 64; r++) {
+        const double u = st[NA * kWideLd + r];
+        if (lane < NA) acc0 += st[lane * kWideLd + r] * u;
+        if (lane + 64 < NA) acc1 += st[(lane + 64) * kWideLd + r] * u;
+      }
+      __syncthreads();
+    }
+  }
+  // Z^T u (columns 0..5, lanes 0..5) to every lane; pose columns through w_k
+  double zs[6];
+#pragma unroll
+  for (int a = 0; a < 6; a++) zs[a] = __shfl(acc0, a, 64);
+  const FrameLin& L = fl[frame];
+  double* y = yrep + (int64_t)(chunk_id & (kVecReplicas - 1)) * ng;
+  if (lane < kPoseCols) {
+    const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
+    const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+    if (L.goff[b] >= 0) {
+      const double* wk = rec + 12 + 6 * lane;
+      double v = 0.0;
+#pragma unroll
+      for (int a = 0; a < 6; a++) v += wk[a] * zs[a];
+      atomicAdd(&y[L.goff[b] + (lane - 7 * blk)], v);
+    }
+  }
+  // intrinsic entries: column 6 + q held by lane (6 + q) mod 64
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int col = lane + 64 * h;
+    const int q = col - 6;  // 0 focal, 1..2 center, 3.. distortion
+    if (q < 0 || col >= NA) continue;
+    int64_t dst = -1;
+    if (q == 0) dst = L.goff[MVBA_BLK_FOCAL];
+    else if (q < 3) dst = L.goff[MVBA_BLK_CENTER] >= 0 ? L.goff[MVBA_BLK_CENTER] + (q - 1) : -1;
+    else if (q - 3 < F.K) dst = L.goff[MVBA_BLK_DIST] >= 0 ? L.goff[MVBA_BLK_DIST] + (q - 3) : -1;
+    if (dst >= 0) atomicAdd(&y[dst], h == 0 ? acc0 : acc1);
+  }
+}
+
 // ------------------------------------------------------------ pass B (frame order)
 // One wave per frame chunk: per observation u_o = z_o - J_pt w_p, with
 // z_o = J_cam,o x from the frame direction (dir; null: x = 0) and w_p from pass A
@@ -488,6 +619,11 @@ __global__ void __launch_bounds__(64) k_pass_b(
   const int lane = threadIdx.x;
   const int ch = blockIdx.x;
   if (ch >= nchunks || (gate && *gate)) return;
+  if constexpr (NA > kPassBRegCols) {
+    pass_b_wide<MODEL, DEG>(chunks[ch], chunk_base + ch, segs, fd, fl, frec, params, pts, obs_pid, obs_meas, dir,
+                            wbuf, yrep, ng, flags, cauchy_c);
+    return;
+  } else {
   const int4 c = chunks[ch];
   const int frame = __builtin_amdgcn_readfirstlane(c.z);
   const FrameDesc& F = fd[frame];
@@ -564,6 +700,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     }
   }
   if (dst >= 0) atomicAdd(&y[dst], v);
+  }
 }
 
 // y = sum_r yrep[r] (replicas re-zeroed); with diag: y += diag .* x; with dot_out
@@ -979,6 +1116,9 @@ __global__ void __launch_bounds__(256) k_cost(const Segment* __restrict__ segs, 
         case 1: CALL(mvba::kModelRpc, 1); break;                   \
         case 2: CALL(mvba::kModelRpc, 2); break;                   \
         case 3: CALL(mvba::kModelRpc, 3); break;                   \
+        case 4: CALL(mvba::kModelRpc, 4); break;                   \
+        case 5: CALL(mvba::kModelRpc, 5); break;                   \
+        case 6: CALL(mvba::kModelRpc, 6); break;                   \
         default: return hipErrorInvalidValue;                      \
       }                                                            \
       break;                                                       \
@@ -1080,7 +1220,8 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PB(M, D)                                                                                       \
-  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks,        \
+  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), (mvba::pass_b_lds<M, D>()), s,\
+                     chunks, nchunks,                                                                         \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
                      dir, wbuf, yrep, ng, flags, cauchy_c, gate)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)

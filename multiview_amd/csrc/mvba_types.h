@@ -33,7 +33,7 @@ constexpr int kFrameRecDoubles = 144;
 // the frame descriptor -> parameter vector chain:
 //   [0..11] R_wc, t_wc | 12 f | 13, 14 optical centre | 15, 16 half size |
 //   17 K (as double) | 18.. live distortion coefficients (<= kProjDist)
-constexpr int kProjDoubles = 64;
+constexpr int kProjDoubles = 128;
 constexpr int kProjDist = kProjDoubles - 18;
 constexpr int kPoseCols = 22;
 
@@ -55,10 +55,10 @@ enum ModelKind : int32_t {
 };
 
 constexpr int kMaxRpcDegree = 6;
-constexpr int kMaxLinRpcDegree = 3;
+constexpr int kMaxLinRpcDegree = 6;
 constexpr int kChunkSegs = 4;       // segments per solver chunk (one wave)
 constexpr int kPartSegs = 16;       // segments per K2 frame part (one block)
-constexpr int kDepthReplicas = 32;  // replicas the depth Gram adds into (frame-segment mod 32)  // the MFMA Gram linearization covers RPC degree <= 3
+constexpr int kDepthReplicas = 32;  // replicas the depth Gram adds into (frame-segment mod 32)
 
 // Per-frame record of the linearization (K2 expand); mirrors mvba::FrameLin in
 // mvba_kernels.hip (checked with mvba_frame_lin_size()).

@@ -145,14 +145,15 @@ def test_high_rpc_degree_evaluation(oracle, deg):
     assert (np.abs(J_g - J_o) / colmax).max() <= 1e-9
 
 
-@pytest.mark.gpu
-def test_solver_rejects_rpc_beyond_gram_range():
-    """The normal-equation (MFMA Gram) path covers RPC degree <= 3; the solver
-    says so instead of running."""
-    R = rig.make_rig(num_sensors=2, num_ref=6, num_points=60, obs_per_point=3, models=["rpc4", "radtan"], seed=40)
+def test_rpc_degree_beyond_compiled_maximum_rejected():
+    """RPC degree 7 (K = 2 (2 * 8 * 9 - 2) = 284) is a valid rpc_distortion size but
+    above this build's compiled maximum (kMaxRpcDegree = 6): mvba_create says so
+    (before touching the device)."""
+    R = rig.make_rig(num_sensors=2, num_ref=6, num_points=60, obs_per_point=3, models=["rpc2", "radtan"], seed=40)
     P = rig.build_problem(R)
-    with Evaluator(P) as ev:
-        ev.set_params()
-        with pytest.raises(_lib.MvbaError) as e:
-            ev.solve()
-    assert e.value.status == _lib.MVBA_E_INVALID
+    P.camera_dist_size = P.camera_dist_size.copy()
+    P.camera_dist_size[0] = 284
+    with pytest.raises(_lib.MvbaError) as e:
+        Evaluator(P)
+    assert e.value.status == _lib.MVBA_E_BAD_DISTORTION
+    assert "compiled maximum" in e.value.message

@@ -20,7 +20,11 @@ MODEL_SETS = {
     "rpc1": ["rpc1"] * 3,
     "rpc2": ["rpc2"] * 3,
     "rpc3": ["rpc3"] * 3,
+    "rpc4": ["rpc4", "radtan"],
+    "rpc5": ["rpc5", "fov"],
+    "rpc6": ["rpc6", "none"],
     "mixed": ["radtan", "rpc2", "fov", "none"],
+    "mixed_high": ["rpc4", "rpc6", "radtan"],
 }
 
 
@@ -75,6 +79,17 @@ def test_linearize_constant_blocks_and_no_rig(oracle):
     P2 = rig.build_problem(R, rig.FloatFlags(no_rig=True, camera_poses_to_float=("ref_cam", "cam1"),
                                              float_timestamp_offsets=False))
     _run(P2, oracle, False)
+
+
+def test_linearize_long_frames_rpc_wide(oracle):
+    # a frame split into several parts (> kPartSegs segments) with the wide-Gram
+    # (rows straight into LDS) path of RPC degree 2
+    R = rig.make_rig(num_sensors=2, num_ref=4, num_points=5000, obs_per_point=3, models=["rpc2", "radtan"], seed=94,
+                     window=2)
+    P = rig.build_problem(R)
+    counts = np.bincount(R.obs_cid)
+    assert counts.max() > 16 * 64
+    _run(P, oracle, True)
 
 
 def test_linearize_long_frames(oracle):

@@ -62,6 +62,28 @@ def test_one_exact_step_matches_dense_lm(use_loss):
     assert np.array_equal(x[~m], P.params[~m])
 
 
+@pytest.mark.parametrize("models", [["rpc4", "radtan"], ["rpc6", "fov"]])
+def test_one_exact_step_high_rpc_degree(models):
+    """RPC degree 4 and 6 (K = 116 / 220: the wide-row pass B and Gram paths,
+    distortion blocks of 116 / 220 entries): one exact-CG LM step equals the
+    dense step (relative 1e-8), focal + distortion floating."""
+    from oracle import lm_reference
+
+    R = rig.make_rig(num_sensors=len(models), num_ref=10, num_points=250, obs_per_point=5, models=models, seed=97)
+    P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=(), intrinsics_to_float=("focal_length",
+                                                                                           "distortion")))
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=1, use_loss=True, **TOL)
+    with Evaluator(P) as ev:
+        assert ev.lin_layout()["supported"]
+        ev.set_params()
+        s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=4000, use_loss=1,
+                     robust_threshold=3.0, **TOL)
+        x = ev.get_params()
+    assert np.isclose(s["initial_cost"], s_ref["initial_cost"], rtol=1e-11)
+    m = _free_mask(P)
+    assert _close(x[m], x_ref[m], 1e-8), np.abs(x[m] - x_ref[m]).max()
+
+
 def test_one_exact_step_multiblock_camera_side():
     """Camera side wide enough that the CG vector kernels (k_vec_rep_reduce,
     k_cg_update, 256 entries per block) and the reductions they finalise run on
