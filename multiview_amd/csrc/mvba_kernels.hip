@@ -360,7 +360,8 @@ struct GramShape {
   static constexpr int kColR = kWidth - 1;              // residual column
   // waves per block: LDS staging is kTiles*16*kGramLd doubles per wave
   static constexpr int kWaves = MVBA_FLIN_WAVES_SMALL_T_OVERRIDE;
-  static constexpr int kStage = kTiles * 16 * kGramLd;
+  // the staging area also holds the wave's accumulators (kPairs * 256 doubles)
+  static constexpr int kStage = kTiles * 16 * kGramLd > kPairs * 256 ? kTiles * 16 * kGramLd : kPairs * 256;
   // rows straight into LDS (no register row arrays) from 3 tiles up
   static constexpr bool kDirect = kTiles >= 3;
   static constexpr size_t kLdsBytes = sizeof(double) * ((size_t)kWaves * kStage + 2 * 6 * kPoseCols + kWaves);

@@ -902,18 +902,62 @@ __global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict
 // blocks of F'F + D^2): one workgroup (one wave) per camera block factors
 // H_bb + diag(d) in LDS (column-parallel Cholesky) and writes the explicit
 // inverse (lane j solves for column j), so applying it is a block mat-vec.
+// Blocks wider than kPrecLds (RPC distortion of degree >= 4: 116..220 entries)
+// are inverted in place in the output by Gauss-Jordan elimination (symmetric
+// positive definite: no pivoting; a vanishing pivot = a direction the block
+// does not see, inverted as identity like the Cholesky path).
+constexpr int kPrecLds = 96;
+
+__device__ void block_inverse_gj(int n, const double* __restrict__ H, const double* __restrict__ db,
+                                 double* __restrict__ A, double* colk, double* rowk) {
+  const int lane = threadIdx.x;
+  for (int e = lane; e < n * n; e += 64) {
+    const int i = e / n, j = e % n;
+    const double h = (j <= i) ? H[e] : H[j * n + i];  // full symmetric matrix from the lower triangle
+    A[e] = h + (i == j ? db[i] : 0.0);
+  }
+  __syncthreads();
+  for (int k = 0; k < n; k++) {
+    for (int i = lane; i < n; i += 64) {
+      colk[i] = A[i * n + k];
+      rowk[i] = A[k * n + i];
+    }
+    __syncthreads();
+    const double piv = colk[k];
+    const bool ok = piv > 1e-300;
+    const double ip = ok ? 1.0 / piv : 0.0;
+    for (int e = lane; e < n * n; e += 64) {
+      const int i = e / n, j = e % n;
+      double v;
+      if (!ok) {
+        v = (i == k || j == k) ? (i == j ? 1.0 : 0.0) : A[e];
+      } else if (i == k) {
+        v = (j == k) ? ip : rowk[j] * ip;
+      } else {
+        v = (j == k) ? -colk[i] * ip : A[e] - colk[i] * rowk[j] * ip;
+      }
+      A[e] = v;
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void __launch_bounds__(64) k_block_prec(int32_t nblocks, const int64_t* __restrict__ goff,
                                                    const int64_t* __restrict__ hoff,
                                                    const int32_t* __restrict__ bsize,
                                                    const double* __restrict__ hess, const double* __restrict__ d,
                                                    double* __restrict__ minv) {
-  extern __shared__ double Ls[];  // [n * n]
+  extern __shared__ double Ls[];  // [n * n], or the pivot column and row of the wide path
   const int b = blockIdx.x;
   if (b >= nblocks) return;
   const int n = bsize[b];
   const int lane = threadIdx.x;
   const double* H = hess + hoff[b];
   const double* db = d + goff[b];
+  if (n > kPrecLds) {
+    block_inverse_gj(n, H, db, minv + hoff[b], Ls, Ls + n);
+    return;
+  }
   for (int e = lane; e < n * n; e += 64) {
     const int i = e / n, j = e % n;
     Ls[e] = (j <= i) ? H[e] + (i == j ? db[i] : 0.0) : 0.0;
@@ -939,7 +983,7 @@ __global__ void __launch_bounds__(64) k_block_prec(int32_t nblocks, const int64_
     __syncthreads();
   }
   double* M = minv + hoff[b];
-  double y[96];
+  double y[kPrecLds];
   for (int j = lane; j < n; j += 64) {
     // L y = e_j
     for (int i = 0; i < n; i++) {
@@ -1286,8 +1330,10 @@ hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int6
                                   hipStream_t s) {
   if (nblocks <= 0) return hipSuccess;
   if (max_bsize > 96) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(64),
-                     (size_t)max_bsize * max_bsize * sizeof(double), s, nblocks, goff, hoff, bsize, hess, d, minv);
+  const int m = max_bsize < mvba::kPrecLds ? max_bsize : mvba::kPrecLds;
+  const size_t lds = sizeof(double) * (size_t)(m * m > 2 * max_bsize ? m * m : 2 * max_bsize);
+  hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(64), lds, s, nblocks, goff, hoff, bsize, hess,
+                     d, minv);
   return hipGetLastError();
 }
 
