@@ -906,7 +906,7 @@ __global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict
 // are inverted in place in the output by Gauss-Jordan elimination (symmetric
 // positive definite: no pivoting; a vanishing pivot = a direction the block
 // does not see, inverted as identity like the Cholesky path).
-constexpr int kPrecLds = 96;
+constexpr int kPrecLds = 88;  // 88^2 doubles = 62 KB: within the 64 KB of dynamic LDS a plain launch gets
 
 __device__ void block_inverse_gj(int n, const double* __restrict__ H, const double* __restrict__ db,
                                  double* __restrict__ A, double* colk, double* rowk) {
