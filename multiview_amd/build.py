@@ -22,18 +22,27 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-fopenmp", "-Wa
 
 
 def build(verbose: bool = False) -> str:
-    objs = []
+    from concurrent.futures import ThreadPoolExecutor
+
+    headers = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
+        [os.path.join(HERE, "..", "include", "mvba", "mvba.h")]
+    objs, cmds = [], []
     for src in SOURCES:
         obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
         srcp = os.path.join(CSRC, src)
-        deps = [srcp] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
-            [os.path.join(HERE, "..", "include", "mvba", "mvba.h")]
+        deps = [srcp] + headers
         if not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps):
-            cmd = [HIPCC] + FLAGS + ["-x", "hip" if src.endswith(".hip") else "hip", "-c", srcp, "-o", obj]
-            if verbose:
-                print(" ".join(cmd))
-            subprocess.run(cmd, check=True)
+            cmds.append([HIPCC] + FLAGS + ["-x", "hip", "-c", srcp, "-o", obj])
         objs.append(obj)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "8"))))
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    with ThreadPoolExecutor(jobs) as pool:
+        list(pool.map(run, cmds))
     if not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
         cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fopenmp", "-o", OUT] + objs + LIBS
         if verbose:

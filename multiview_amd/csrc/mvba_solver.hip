@@ -1329,7 +1329,6 @@ hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int6
                                   const int32_t* bsize, const double* hess, const double* d, double* minv,
                                   hipStream_t s) {
   if (nblocks <= 0) return hipSuccess;
-  if (max_bsize > 96) return hipErrorInvalidValue;
   const int m = max_bsize < mvba::kPrecLds ? max_bsize : mvba::kPrecLds;
   const size_t lds = sizeof(double) * (size_t)(m * m > 2 * max_bsize ? m * m : 2 * max_bsize);
   hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(64), lds, s, nblocks, goff, hoff, bsize, hess,
