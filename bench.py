@@ -188,6 +188,76 @@ def _flops_of(table, prefixes):
     return sum(tot) if tot else None
 
 
+def ceres_surface(ev, P, torch, args):
+    """What BracketedCamBatch::Refresh does per PrepareForEvaluation: upload the
+    host parameter arrays (mvba_set_params), evaluate, rewrite the planes as
+    insertion-order rows on the device (k_rows, Cauchy corrector applied) and
+    copy them to pinned host memory (mvba_evaluate_packed, default transfer set
+    = every non-constant block). Timed end to end on the host clock; the PCIe
+    ceiling is a plain device-to-pinned copy of the same bytes."""
+    from multiview_amd.evaluator import PinnedBuffer
+
+    n = ev.num_residuals
+    off = ev.set_transfer_blocks(None)
+    packed = int(off[-1])
+    reps = max(3, min(args.steps, 10))
+    out = {}
+    with PinnedBuffer(packed) as buf, PinnedBuffer(2 * n) as rbuf:
+        def run(jac):
+            # as the adapter: residuals and rows into pinned memory, no cost
+            # (Ceres sums the cost from the residuals itself)
+            ev.set_params()
+            ev.evaluate_packed(jacobian=jac, apply_loss=True, out=buf.array if jac else None,
+                               res_out=rbuf.array, want_cost=False)
+
+        for jac in (True, False):
+            run(jac)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                run(jac)
+            dt = (time.perf_counter() - t0) / reps
+            nbytes = 8.0 * (packed * jac + 2 * n)  # rows + residuals
+            out["jacobian" if jac else "residuals_only"] = {
+                "evals_per_s": n / dt, "ms": 1e3 * dt, "bytes_to_host": nbytes,
+                "achieved_GBps": nbytes / dt / 1e9}
+    # achievable device -> pinned host rate for the same byte count
+    nb = int(8 * packed)
+    d = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    h = torch.empty(nb, dtype=torch.uint8, pin_memory=True)
+    h.copy_(d)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        h.copy_(d)
+    torch.cuda.synchronize()
+    copy_gbs = nb / ((time.perf_counter() - t0) / reps) / 1e9
+    del d, h
+    # the same evaluation into pageable numpy memory (staged through pinned buffers)
+    ev.evaluate(jacobian=True, apply_loss=True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ev.set_params()
+        ev.evaluate(jacobian=True, apply_loss=True)
+    full_dt = (time.perf_counter() - t0) / reps
+    j = out["jacobian"]
+    return {
+        "what": "Ceres-surface hand-over per evaluation point: mvba_set_params (host arrays) + "
+                "evaluate + device transposition into AddResidualBlock-order rows (Cauchy "
+                "corrector) + one device-to-pinned copy (mvba_evaluate_packed)",
+        "evals_per_s": j["evals_per_s"],
+        "ms": j["ms"],
+        "packed_doubles": packed,
+        "pcie_GBps": j["achieved_GBps"],
+        "pcie_copy_GBps": copy_gbs,
+        "frac_of_copy": j["achieved_GBps"] / copy_gbs,
+        "pcie_spec_GBps": 64.0,
+        "residuals_only": out["residuals_only"],
+        "pageable_full_layout": {"evals_per_s": n / full_dt, "ms": 1e3 * full_dt,
+                                 "note": "mvba_evaluate into pageable numpy arrays (Ceres jac_stride "
+                                         "layout, zero-filled), staged through two pinned 32 MB buffers"},
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -424,6 +494,11 @@ def main():
         line["eval_f32"]["depth_kernel_ms"] = fd_ms
         line["eval_f32"]["depth_achieved_GBps"] = (dreads + (dbytes - dreads) / 2.0) / (fd_ms * 1e-3) / 1e9
         del dres32, dJ32
+
+    # ---- the Ceres-surface hand-over (include/mvba/ceres_surface.h): host
+    # parameters in, AddResidualBlock-order rows out through one PCIe copy
+    if world == 1:
+        line["ceres_surface"] = ceres_surface(ev, P, torch, args)
 
     # ---- phase B: normal equations (K2) + the per-iteration exchange (§8e)
     from multiview_amd.dist import NormalEquationBuffer, check_layouts_agree

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MVBA_ABI_VERSION 3
+#define MVBA_ABI_VERSION 4
 
 /* Status codes. Non-zero codes mirror the reference's fatal checks. */
 typedef enum mvba_status {
@@ -228,6 +228,28 @@ mvba_status mvba_set_params_device(struct mvba_handle* h, const double* d_packed
 mvba_status mvba_evaluate(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                           double* cost, double* residuals, double* jacobian);
 int32_t mvba_jacobian_stride(const struct mvba_handle* h);
+
+/* ---- Host hand-over (the ceres::CostFunction surface) --------------------
+ * mvba_evaluate / mvba_evaluate_packed / mvba_evaluate_depth rewrite the
+ * device's column planes into AddResidualBlock-order rows ON THE DEVICE and
+ * move them with one device-to-host copy (rig_calibrator.cc:1695-1699 is the
+ * layout Ceres consumes). Outputs in pinned memory (mvba_host_alloc, or a
+ * caller's hipHostRegister) are DMA targets; pageable outputs go through the
+ * library's pinned double buffer. */
+void* mvba_host_alloc(size_t bytes);  /* pinned host memory, NULL on failure */
+void mvba_host_free(void* p);
+/* Packed Jacobian: only the columns of the parameter blocks with transfer[b]
+ * != 0 (num_blocks bytes; NULL = every non-constant block). Residual block i's
+ * entries start at offsets[i] (num_residuals + 1 int64, nullable) and hold,
+ * in block-position order (MVBA_BLK_*), the row-major 2 x size_b Jacobian of
+ * each transferred block it references (zero if that block is constant).
+ * Replaces CostFunction::Evaluate's per-block jacobians[b] (NULL for the blocks
+ * Ceres holds constant), so blocks nobody asks for never cross PCIe. */
+mvba_status mvba_set_transfer_blocks(struct mvba_handle* h, const uint8_t* transfer, int64_t* offsets);
+int64_t mvba_packed_size(const struct mvba_handle* h); /* doubles; -1 before mvba_set_transfer_blocks */
+/* Like mvba_evaluate with the packed Jacobian layout (mvba_packed_size doubles). */
+mvba_status mvba_evaluate_packed(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
+                                 double* cost, double* residuals, double* packed_jacobian);
 
 /* Device-resident evaluation (no host transfer). Outputs go to the library's
  * buffers (see mvba_device_buffers) or, if d_residuals/d_jacobian are non-null,

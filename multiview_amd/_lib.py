@@ -224,6 +224,11 @@ SIGNATURES = {
     "mvba_set_params_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_evaluate": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_jacobian_stride": (C.c_int32, [C.c_void_p]),
+    "mvba_host_alloc": (C.c_void_p, [C.c_size_t]),
+    "mvba_host_free": (None, [C.c_void_p]),
+    "mvba_set_transfer_blocks": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_packed_size": (C.c_int64, [C.c_void_p]),
+    "mvba_evaluate_packed": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_evaluate_device": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,
                                        C.c_int64, C.c_void_p]),
     "mvba_evaluate_device_f32": (C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_void_p, C.c_void_p,

@@ -38,11 +38,17 @@ static void free_all(mvba_handle* h) {
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
                   h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xpid,
-                  h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt};
+                  h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt, h->d_varsize, h->d_tres, h->d_tcost,
+                  h->d_trows, h->d_xmask, h->d_xoff, h->d_dwritten, h->d_dvarsize, h->d_tdres,
+                  h->d_tdcost, h->d_tdrows};
   solver_state_free(h->solver);
   h->solver = nullptr;
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (int k = 0; k < 2; k++) {
+    if (h->h_stage[k]) (void)hipHostFree(h->h_stage[k]);
+    if (h->stage_ev[k]) (void)hipEventDestroy(h->stage_ev[k]);
+  }
 }
 
 extern "C" {
@@ -292,6 +298,15 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   }
   h->nframes = (int64_t)frames.size();
   h->res_frame = res_frame;
+  h->frame_blocks = frame_blocks;
+  h->res_pt = res_pt;
+  h->pt_free_h = pt_free;
+  h->frame_mask.resize(frames.size());
+  h->frame_kdist.resize(frames.size());
+  for (size_t f = 0; f < frames.size(); f++) {
+    h->frame_mask[f] = frames[f].free_mask;
+    h->frame_kdist[f] = frames[f].K;
+  }
 
   // ---- groups by (model, degree), then device order
   std::vector<int> gkey_of_cam(d->num_cameras);
@@ -639,6 +654,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_segs, segs));
   chk(upload(&h->d_order, h->order));
   chk(upload(&h->d_row_written, h->row_written));
+  chk(upload(&h->d_varsize, h->pos_K));
   chk(dalloc(&h->d_err, 1));
   if (e == hipSuccess) chk(hipMemset(h->d_err, 0, sizeof(int)));
   chk(upload(&h->d_chunks, chunks));
@@ -919,79 +935,6 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
 
 double mvba_lin_mfma_flops(const mvba_handle* h) { return h ? h->lin_mfma_flops : 0.0; }
 
-mvba_status mvba_evaluate(mvba_handle* h, int32_t flags, double cauchy_threshold, double* cost,
-                          double* residuals, double* jacobian) {
-  if (!h) return MVBA_E_INVALID;
-  const bool want_jac = jacobian != nullptr && (flags & MVBA_EVAL_JACOBIAN);
-  const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
-  if (loss && !(cauchy_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
-  // Raw residuals/Jacobian on the device; the Ceres corrector is applied here
-  // so the cost can use the uncorrected squared norm.
-  const int32_t dflags = MVBA_EVAL_RESIDUALS | (want_jac ? MVBA_EVAL_JACOBIAN : 0);
-  mvba_status st = mvba_evaluate_device(h, dflags, 0.0, nullptr, nullptr, 0, nullptr);
-  if (st != MVBA_OK) return st;
-  st = mvba_sync_status(h, nullptr);
-  if (st != MVBA_OK) return st;
-  const int64_t N = h->nres, S = h->nslots, ld = h->ld;
-  h->h_res.resize((size_t)(2 * ld));
-  hipError_t e = hipMemcpy(h->h_res.data(), h->d_res, (size_t)(2 * ld) * sizeof(double), hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate residual copy");
-  if (want_jac) {
-    h->h_J.resize((size_t)h->jac_rows * (size_t)ld);
-    e = hipMemcpy(h->h_J.data(), h->d_J, h->h_J.size() * sizeof(double), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate Jacobian copy");
-  }
-  const double b = cauchy_threshold * cauchy_threshold;
-  const double c = loss ? 1.0 / b : 0.0;
-  const int stride = h->jac_rows;
-  std::vector<double> cost_ins(cost ? (size_t)N : 0);
-#pragma omp parallel for schedule(static)
-  for (int64_t p = 0; p < S; p++) {
-    const int64_t i = h->order[p];
-    if (i < 0) continue;  // padding slot
-    const double r0 = h->h_res[p], r1 = h->h_res[ld + p];
-    const double s2 = r0 * r0 + r1 * r1;
-    double sr = 1.0, ci;
-    if (!loss) {
-      ci = 0.5 * s2;
-    } else {
-      // Ceres 1.14 CauchyLoss + Corrector [ext]
-      const double sum = 1.0 + s2 * c;
-      const double inv = 1.0 / sum;
-      ci = 0.5 * (b * std::log(sum));
-      sr = std::sqrt(std::max(std::numeric_limits<double>::min(), inv));
-    }
-    if (cost) cost_ins[i] = ci;
-    if (residuals) {
-      residuals[2 * i] = r0 * sr;
-      residuals[2 * i + 1] = r1 * sr;
-    }
-    if (want_jac) {
-      double* Jo = jacobian + i * stride;
-      const int mask = h->row_written[p];
-      for (int row = 0; row < stride; row++) Jo[row] = 0.0;
-      static const int base[8] = {MVBA_JAC_BASE_BEG, MVBA_JAC_BASE_END, MVBA_JAC_BASE_REF_TO_CAM,
-                                  MVBA_JAC_BASE_XYZ, MVBA_JAC_BASE_OFFSET, MVBA_JAC_BASE_FOCAL,
-                                  MVBA_JAC_BASE_CENTER, MVBA_JAC_BASE_DIST};
-      for (int bb = 0; bb < 8; bb++) {
-        if (!(mask & (1 << bb))) continue;
-        const int rows = (bb == 7) ? 2 * h->pos_K[p] : 2 * kFixedSize[bb];
-        for (int q = 0; q < rows; q++) {
-          const int row = base[bb] + q;
-          Jo[row] = h->h_J[(size_t)row * ld + p] * sr;
-        }
-      }
-    }
-  }
-  if (cost) {
-    // Summed in AddResidualBlock order (Problem::Evaluate with num_threads = 1).
-    double total = 0.0;
-    for (int64_t i = 0; i < N; i++) total += cost_ins[i];
-    *cost = total;
-  }
-  return MVBA_OK;
-}
-
 int64_t mvba_num_depth_residuals(const mvba_handle* h) { return h ? h->ndep : 0; }
 int64_t mvba_num_depth_slots(const mvba_handle* h) { return h ? h->ndep_slots : 0; }
 
@@ -1045,88 +988,6 @@ static mvba_status evaluate_depth_device_impl(mvba_handle* h, int32_t flags, dou
                               h->d_params, h->d_pts, d_res, d_J, ld, flags & (MVBA_EVAL_APPLY_LOSS), cauchy_c,
                               out_f32, s);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth_device launch");
-  return MVBA_OK;
-}
-
-mvba_status mvba_evaluate_depth(mvba_handle* h, int32_t flags, double cauchy_threshold, double* cost,
-                                double* residuals, double* jacobian) {
-  if (!h) return MVBA_E_INVALID;
-  const bool want_jac = jacobian != nullptr && (flags & MVBA_EVAL_JACOBIAN);
-  const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
-  if (loss && !(cauchy_threshold > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
-  const int64_t ND = h->ndep, S = h->ndep_slots;
-  if (ND == 0) {
-    if (cost) *cost = 0.0;
-    return MVBA_OK;
-  }
-  if (!h->d_dres) {
-    h->dld = (S + 63) / 64 * 64;
-    hipError_t e = dalloc(&h->d_dres, (size_t)(3 * h->dld));
-    if (e == hipSuccess) e = dalloc(&h->d_dJ, (size_t)MVBA_DJAC_ROWS * (size_t)h->dld);
-    if (e != hipSuccess) return h->hip_fail(e, "allocating depth outputs");
-  }
-  const int64_t ld = h->dld;
-  // raw residuals / Jacobian on the device; Ceres' corrector applied here
-  mvba_status st = mvba_evaluate_depth_device(h, MVBA_EVAL_RESIDUALS | (want_jac ? MVBA_EVAL_JACOBIAN : 0), 0.0,
-                                              h->d_dres, want_jac ? h->d_dJ : nullptr, ld, nullptr);
-  if (st != MVBA_OK) return st;
-  st = mvba_sync_status(h, nullptr);
-  if (st != MVBA_OK) return st;
-  h->h_dres.resize((size_t)(3 * ld));
-  hipError_t e = hipMemcpy(h->h_dres.data(), h->d_dres, (size_t)(3 * ld) * sizeof(double), hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth residual copy");
-  std::vector<mvba::DepthDesc> desc;
-  if (want_jac) {
-    h->h_dJ.resize((size_t)MVBA_DJAC_ROWS * (size_t)ld);
-    e = hipMemcpy(h->h_dJ.data(), h->d_dJ, h->h_dJ.size() * sizeof(double), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth Jacobian copy");
-    desc.resize((size_t)S);
-    e = hipMemcpy(desc.data(), h->d_dep_desc, (size_t)S * sizeof(mvba::DepthDesc), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth record copy");
-  }
-  const double b = cauchy_threshold * cauchy_threshold;
-  const double c = loss ? 1.0 / b : 0.0;
-  std::vector<double> cost_ins(cost ? (size_t)ND : 0);
-  static const int kBase[7] = {MVBA_DJAC_BASE_BEG, MVBA_DJAC_BASE_END, MVBA_DJAC_BASE_REF_TO_CAM,
-                               MVBA_DJAC_BASE_DEPTH_TO_IMAGE, MVBA_DJAC_BASE_SCALE, MVBA_DJAC_BASE_XYZ,
-                               MVBA_DJAC_BASE_OFFSET};
-#pragma omp parallel for schedule(static)
-  for (int64_t p = 0; p < S; p++) {
-    const int64_t j = h->dep_order[p];
-    if (j < 0) continue;
-    const double r0 = h->h_dres[p], r1 = h->h_dres[ld + p], r2 = h->h_dres[2 * ld + p];
-    const double s2 = r0 * r0 + r1 * r1 + r2 * r2;
-    double sr = 1.0, cj;
-    if (!loss) {
-      cj = 0.5 * s2;
-    } else {
-      const double sum = 1.0 + s2 * c;
-      cj = 0.5 * (b * std::log(sum));
-      sr = std::sqrt(std::max(std::numeric_limits<double>::min(), 1.0 / sum));
-    }
-    if (cost) cost_ins[(size_t)j] = cj;
-    if (residuals) {
-      residuals[3 * j] = r0 * sr;
-      residuals[3 * j + 1] = r1 * sr;
-      residuals[3 * j + 2] = r2 * sr;
-    }
-    if (want_jac) {
-      double* Jo = jacobian + j * MVBA_DJAC_ROWS;
-      for (int row = 0; row < MVBA_DJAC_ROWS; row++) Jo[row] = 0.0;
-      const int mask = desc[(size_t)p].free_mask;
-      for (int bb = 0; bb < 7; bb++) {
-        if (!(mask & (1 << bb))) continue;
-        const int size = (bb == MVBA_DBLK_DEPTH_TO_IMAGE) ? desc[(size_t)p].dti_n
-                         : (bb == MVBA_DBLK_SCALE || bb == MVBA_DBLK_OFFSET) ? 1 : (bb == MVBA_DBLK_XYZ ? 3 : 7);
-        for (int q = 0; q < 3 * size; q++) Jo[kBase[bb] + q] = h->h_dJ[(size_t)(kBase[bb] + q) * ld + p] * sr;
-      }
-    }
-  }
-  if (cost) {
-    double total = 0.0;
-    for (int64_t j = 0; j < ND; j++) total += cost_ins[(size_t)j];
-    *cost = total;
-  }
   return MVBA_OK;
 }
 

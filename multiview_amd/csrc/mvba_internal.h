@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <cstdint>
@@ -71,6 +72,19 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
                                   int32_t flags, double cauchy_c, double* partial, hipStream_t s,
                                   int64_t* nblocks_out);
 }
+
+// Row layout of a host hand-over (mvba_transfer.hip): residual rows per block,
+// parameter blocks, the block with a per-slot width, first plane row and width
+// of every block.
+struct mvba_rows_layout {
+  int32_t jac_rows, nres, nblocks, var_block;
+  int32_t base[8], size[8];
+};
+extern "C" hipError_t mvba_launch_rows(const double* res, const double* J, int64_t ld, int64_t nslots,
+                                       const mvba_rows_layout* L, double cauchy_c, const int64_t* order,
+                                       const uint8_t* written, const int16_t* varsize, const uint8_t* xmask,
+                                       const int64_t* xoff, double* out_res, double* out_cost, double* out_rows,
+                                       hipStream_t s);
 
 namespace mvba_internal {
 
@@ -182,7 +196,28 @@ struct mvba_handle {
   bool prep_done = false;
   int gen = 0;  // generation of the last prep launch (error word protocol)
 
-  std::vector<double> h_res, h_J;  // host staging for mvba_evaluate
+  // host hand-over (mvba_evaluate / mvba_evaluate_packed / mvba_evaluate_depth)
+  std::vector<std::array<int32_t, 8>> frame_blocks;  // frame -> block ids (MVBA_BLK_* order)
+  std::vector<int32_t> res_pt;     // AddResidualBlock index -> point index
+  std::vector<int32_t> frame_mask, frame_kdist;  // frame -> written blocks, distortion length
+  std::vector<uint8_t> pt_free_h;  // point index -> not constant
+  int16_t* d_varsize = nullptr;    // slot -> K
+  double* d_tres = nullptr;        // [2N] corrected residuals, insertion order
+  double* d_tcost = nullptr;       // [N] per-block cost, insertion order
+  double* d_trows = nullptr;       // rows (full or packed)
+  size_t trows_cap = 0;            // doubles
+  uint8_t* d_xmask = nullptr;      // packed layout: slot -> transferred blocks
+  int64_t* d_xoff = nullptr;       // packed layout: slot -> row offset
+  std::vector<int64_t> xoffsets;   // packed layout: insertion index -> row offset (N + 1)
+  bool packed_set = false;
+  uint8_t* d_dwritten = nullptr;   // depth slot -> free blocks
+  int16_t* d_dvarsize = nullptr;   // depth slot -> depth_to_image width
+  double* d_tdres = nullptr;       // depth: [3 ND] residuals, [ND] cost, rows
+  double* d_tdcost = nullptr;
+  double* d_tdrows = nullptr;
+  void* h_stage[2] = {nullptr, nullptr};  // pinned staging for pageable destinations
+  size_t stage_bytes = 0;
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
 
   // linearization (K2): camera-side compact layout, chunks, point CSR
   bool lin_ok = false;
@@ -241,7 +276,6 @@ struct mvba_handle {
   double* d_dres = nullptr;               // library-owned depth outputs (lazy)
   double* d_dJ = nullptr;
   int64_t dld = 0;
-  std::vector<double> h_dres, h_dJ;
 
   SolverState* solver = nullptr;         // LM state, allocated by the first mvba_solve
 

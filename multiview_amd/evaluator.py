@@ -14,6 +14,31 @@ from . import _lib
 from .problem import CamProblem
 
 
+class PinnedBuffer:
+    """Pinned host doubles from mvba_host_alloc (a DMA target for the host
+    evaluations); ``array`` is a numpy view, valid until ``free()``."""
+
+    def __init__(self, n: int):
+        self.lib = _lib.load()
+        self.n = int(n)
+        self.ptr = self.lib.mvba_host_alloc(max(self.n, 1) * 8)
+        if not self.ptr:
+            raise MemoryError("mvba_host_alloc failed")
+        self.array = np.ctypeslib.as_array((C.c_double * max(self.n, 1)).from_address(self.ptr))[:self.n]
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            self.lib.mvba_host_free(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.free()
+
+
 class Evaluator:
     """GPU evaluator for a CamProblem (BracketedCamError residual blocks)."""
 
@@ -65,6 +90,46 @@ class Evaluator:
                                     r.ctypes.data, J.ctypes.data if J is not None else None)
         _lib.check(st, self.h)
         return cost.value, r, J
+
+    def set_transfer_blocks(self, transfer=None) -> np.ndarray:
+        """Select the parameter blocks whose Jacobian columns evaluate_packed
+        transfers (bool per block; None = every non-constant block). Returns the
+        per-residual row offsets [N + 1]."""
+        off = np.empty(self.num_residuals + 1, dtype=np.int64)
+        tp = None
+        if transfer is not None:
+            t = np.ascontiguousarray(transfer, dtype=np.uint8)
+            if t.size != len(self.problem.block_size):
+                raise ValueError("transfer needs one entry per parameter block")
+            tp = t.ctypes.data
+        _lib.check(self.lib.mvba_set_transfer_blocks(self.h, tp, off.ctypes.data), self.h)
+        return off
+
+    def evaluate_packed(self, jacobian: bool = True, apply_loss: bool = False, robust_threshold: float = 3.0,
+                        out=None, res_out=None, want_cost: bool = True):
+        """Host evaluation with the packed Jacobian layout (set_transfer_blocks).
+        out / res_out: optional float64 arrays of mvba_packed_size() / 2N entries
+        (e.g. views of pinned memory from PinnedBuffer). Returns (cost or None,
+        residuals [N, 2], packed)."""
+        n = self.num_residuals
+        size = int(self.lib.mvba_packed_size(self.h))
+        if size < 0:
+            self.set_transfer_blocks(None)
+            size = int(self.lib.mvba_packed_size(self.h))
+        r = np.empty((n, 2), dtype=np.float64) if res_out is None else res_out.reshape(n, 2)
+        J = None
+        if jacobian:
+            J = np.empty(size, dtype=np.float64) if out is None else out
+            if J.size < size or J.dtype != np.float64 or not J.flags.c_contiguous:
+                raise ValueError("out must be a contiguous float64 array of mvba_packed_size() entries")
+        cost = C.c_double(0.0)
+        flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0) | \
+            (_lib.EVAL_APPLY_LOSS if apply_loss else 0)
+        st = self.lib.mvba_evaluate_packed(self.h, flags, float(robust_threshold),
+                                           C.byref(cost) if want_cost else None, r.ctypes.data,
+                                           J.ctypes.data if J is not None else None)
+        _lib.check(st, self.h)
+        return (cost.value if want_cost else None), r, J
 
     def evaluate_depth(self, jacobian: bool = True, apply_loss: bool = False, robust_threshold: float = 3.0):
         """BracketedDepthError blocks, host, depth insertion order: (cost,

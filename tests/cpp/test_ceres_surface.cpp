@@ -4,7 +4,10 @@
 // Cases: (0) lazy refresh (Problem::Evaluate path, no callback),
 // (1) some jacobians NULL, (2) parameters changed in user memory -> refresh,
 // (3) evaluation point not in user memory -> Evaluate() returns false,
-// (4) callback path, (5) 8 threads evaluating concurrently.
+// (4) callback path, (5) 8 threads evaluating concurrently,
+// (6) packed transfer: blocks Ceres never asks for stop crossing PCIe after the
+//     first Jacobian pass, and asking for one later extends the set,
+// (7) BracketedDepthError + XYZError blocks served from the same batch.
 #include <array>
 #include <atomic>
 #include <cstdio>
@@ -44,6 +47,14 @@ int main(int argc, char** argv) {
   auto rmeas = read_vec<double>(in);
   auto rstamps = read_vec<double>(in);
   auto params2 = read_vec<double>(in);  // a second evaluation point
+  auto dblocks = read_vec<int32_t>(in);  // depth blocks [7 nd]
+  auto dsizes = read_vec<int32_t>(in);   // depth_to_image width per depth block
+  auto dmeas = read_vec<double>(in);
+  auto dweight = read_vec<double>(in);
+  auto dstamps = read_vec<double>(in);
+  auto xblock = read_vec<int32_t>(in);   // xyz priors
+  auto xref = read_vec<double>(in);
+  auto xweight = read_vec<double>(in);
   const int64_t n = (int64_t)rcam.size();
 
   std::vector<double> user = params;  // the integrator's parameter arrays
@@ -124,6 +135,95 @@ int main(int argc, char** argv) {
   for (auto& t : th) t.join();
   flags.push_back(bad.load());
   write_vec(out, R5); write_vec(out, J5);
+
+  // (6) a batch whose Ceres never asks for end (1) and distortion (7) Jacobians
+  user = params;
+  {
+    mvba::BracketedCamBatch b6(0);
+    std::vector<std::unique_ptr<ceres::CostFunction>> c6;
+    for (int64_t i = 0; i < n; i++) {
+      std::array<double*, 8> ptr;
+      for (int b = 0; b < 8; b++) ptr[b] = &user[(size_t)block_offset[rblocks[8 * i + b]]];
+      const int c = rcam[i];
+      c6.emplace_back(b6.Create(&rmeas[2 * i], rstamps[3 * i], rstamps[3 * i + 1], rstamps[3 * i + 2], bs, cam_K[c],
+                                &cam_half[2 * c], ptr));
+    }
+    auto eval6 = [&](int null_mask, std::vector<double>& R6, std::vector<double>& J6) {
+      R6.assign(2 * n, 0.0);
+      J6.assign(n * stride, 0.0);
+      bool ok = true;
+      for (int64_t i = 0; i < n; i++) {
+        const double* p[8];
+        double* jp[8];
+        for (int b = 0; b < 8; b++) {
+          p[b] = &user[(size_t)block_offset[rblocks[8 * i + b]]];
+          jp[b] = (null_mask & (1 << b)) ? nullptr : &J6[i * stride + base[b]];
+        }
+        ok &= c6[i]->Evaluate(p, &R6[2 * i], jp);
+      }
+      return ok;
+    };
+    std::vector<double> R6, J6;
+    const int nulls = (1 << 1) | (1 << 7);
+    b6.callback()->PrepareForEvaluation(true, true);
+    flags.push_back(eval6(nulls, R6, J6));
+    const int64_t full = b6.transferred_jacobian_doubles();
+    b6.callback()->PrepareForEvaluation(true, true);
+    flags.push_back(eval6(nulls, R6, J6));
+    const int64_t packed = b6.transferred_jacobian_doubles();
+    write_vec(out, R6); write_vec(out, J6);
+    // now a block that was not transferred: one more GPU pass, then served
+    before = b6.gpu_evaluations();
+    flags.push_back(eval6(0, R6, J6));
+    flags.push_back((int32_t)(b6.gpu_evaluations() - before));
+    write_vec(out, J6);
+    std::vector<int64_t> sizes6 = {full, packed, b6.transferred_jacobian_doubles()};
+    write_vec(out, sizes6);
+  }
+
+  // (7) depth + xyz blocks next to the reprojection blocks of the same images
+  const int64_t nd = (int64_t)dweight.size(), nx = (int64_t)xweight.size();
+  {
+    mvba::BracketedCamBatch b7(0);
+    std::vector<std::unique_ptr<ceres::CostFunction>> c7, d7, x7;
+    for (int64_t i = 0; i < n; i++) {
+      std::array<double*, 8> ptr;
+      for (int b = 0; b < 8; b++) ptr[b] = &user[(size_t)block_offset[rblocks[8 * i + b]]];
+      const int c = rcam[i];
+      c7.emplace_back(b7.Create(&rmeas[2 * i], rstamps[3 * i], rstamps[3 * i + 1], rstamps[3 * i + 2], bs, cam_K[c],
+                                &cam_half[2 * c], ptr));
+    }
+    for (int64_t j = 0; j < nd; j++) {
+      std::array<double*, 7> ptr;
+      for (int b = 0; b < 7; b++) ptr[b] = &user[(size_t)block_offset[dblocks[7 * j + b]]];
+      const std::vector<int> dbs = {7, 7, 7, dsizes[j], 1, 3, 1};
+      d7.emplace_back(b7.CreateDepth(dweight[j], &dmeas[3 * j], dstamps[3 * j], dstamps[3 * j + 1],
+                                     dstamps[3 * j + 2], dbs, ptr));
+    }
+    for (int64_t j = 0; j < nx; j++)
+      x7.emplace_back(b7.CreateXyz(&xref[3 * j], {3}, xweight[j], &user[(size_t)block_offset[xblock[j]]]));
+    static const int dbase[7] = {0, 21, 42, 63, 99, 102, 111};
+    std::vector<double> RD(3 * nd), JD(114 * nd, 0.0), RX(3 * nx), JX(9 * nx);
+    b7.callback()->PrepareForEvaluation(true, true);
+    bool ok = true;
+    for (int64_t j = 0; j < nd; j++) {
+      const double* p[7];
+      double* jp[7];
+      for (int b = 0; b < 7; b++) {
+        p[b] = &user[(size_t)block_offset[dblocks[7 * j + b]]];
+        jp[b] = &JD[114 * j + dbase[b]];
+      }
+      ok &= d7[j]->Evaluate(p, &RD[3 * j], jp);
+    }
+    for (int64_t j = 0; j < nx; j++) {
+      const double* p[1] = {&user[(size_t)block_offset[xblock[j]]]};
+      double* jp[1] = {&JX[9 * j]};
+      ok &= x7[j]->Evaluate(p, &RX[3 * j], jp);
+    }
+    flags.push_back(ok);
+    flags.push_back((int32_t)b7.gpu_evaluations());
+    write_vec(out, RD); write_vec(out, JD); write_vec(out, RX); write_vec(out, JX);
+  }
   write_vec(out, flags);
   return 0;
 }

@@ -29,8 +29,11 @@ def test_ceres_adapter(tmp_path, oracle):
     if not os.path.exists(BIN):
         subprocess.run(["make", "-s", "-C", os.path.dirname(BIN)], check=True)
     R = rig.make_rig(num_sensors=3, num_ref=12, num_points=150, obs_per_point=5,
-                     models=["radtan", "rpc1", "fov"], seed=31)
-    P = rig.build_problem(R)
+                     models=["radtan", "rpc1", "fov"], seed=31, depth_sensors=(2,), affine_depth=False)
+    F = rig.FloatFlags(depth_tri_weight=10.0, depth_to_image_transforms_to_float=("cam2",), float_scale=True,
+                       tri_weight=0.5, tri_robust_threshold=0.1)
+    P = rig.build_problem(R, F)
+    assert P.num_depth_residuals > 0 and P.num_xyz_residuals > 0
     params2 = P.params.copy()
     params2 += np.random.default_rng(1).normal(0, 1e-4, params2.shape) * (P.params != 0)
     src = tmp_path / "prob.bin"
@@ -45,6 +48,14 @@ def test_ceres_adapter(tmp_path, oracle):
         _write(fh, P.residual_meas, np.float64)
         _write(fh, P.residual_stamps, np.float64)
         _write(fh, params2, np.float64)
+        _write(fh, P.depth_blocks, np.int32)
+        _write(fh, P.block_size[P.depth_blocks[:, 3]], np.int32)
+        _write(fh, P.depth_meas, np.float64)
+        _write(fh, P.depth_weight, np.float64)
+        _write(fh, P.depth_stamps, np.float64)
+        _write(fh, P.xyz_block, np.int32)
+        _write(fh, P.xyz_ref, np.float64)
+        _write(fh, P.xyz_weight, np.float64)
     out = tmp_path / "out.bin"
     subprocess.run([BIN, str(src), str(out)], check=True, timeout=120)
     n = P.num_residuals
@@ -55,12 +66,16 @@ def test_ceres_adapter(tmp_path, oracle):
         R2, J2 = _read(fh, np.float64), _read(fh, np.float64)
         R4, J4 = _read(fh, np.float64), _read(fh, np.float64)
         R5, J5 = _read(fh, np.float64), _read(fh, np.float64)
+        R6, J6 = _read(fh, np.float64), _read(fh, np.float64)
+        J6b = _read(fh, np.float64)
+        sizes6 = _read(fh, np.int64)
+        RD, JD, RX, JX = (_read(fh, np.float64) for _ in range(4))
         flags = _read(fh, np.int32)
     # full Jacobians: the adapter evaluates every block (all free)
-    Pf = rig.build_problem(R)
+    Pf = rig.build_problem(R, F)
     Pf.block_constant[:] = 0
     _, r_o, J_o = oracle.evaluate(Pf, oracle.ANALYTIC)
-    P2 = rig.build_problem(R)
+    P2 = rig.build_problem(R, F)
     P2.block_constant[:] = 0
     P2.params = params2
     _, r_o2, J_o2 = oracle.evaluate(P2, oracle.ANALYTIC)
@@ -79,3 +94,34 @@ def test_ceres_adapter(tmp_path, oracle):
     assert flags[4] == 0  # point not in user memory -> Evaluate() false
     assert flags[5] == 1 and flags[6] == 1 and close(R4, J4, r_o, J_o)
     assert flags[7] == 0 and close(R5, J5, r_o2, J_o2)
+    # (6) packed transfer: end and distortion never asked -> not transferred
+    assert flags[8] == 1 and flags[9] == 1
+    K = P.camera_dist_size[P.residual_camera]
+    width = np.array([7, 7, 7, 3, 1, 1, 2, 0])[None, :].repeat(n, 0)
+    width[:, 7] = K
+    assert sizes6[0] == 2 * int(width.sum())                    # first pass: every block
+    # afterwards only blocks Ceres asked for at some position (a world_to_ref block
+    # is the end of one bracket and the beginning of the next)
+    asked = np.zeros(len(P.block_size), bool)
+    for b in (0, 2, 3, 4, 5, 6):
+        asked[P.residual_blocks[:, b]] = True
+    assert sizes6[1] == 2 * int((width * asked[P.residual_blocks]).sum()) < sizes6[0]
+    J6 = J6.reshape(n, stride)
+    mask = np.ones(stride, bool)
+    mask[14:28] = False
+    mask[56:] = False
+    assert np.all(J6[:, ~mask] == 0) and close(R6, np.where(mask, J6, J_o), r_o, J_o)
+    assert flags[10] == 1 and flags[11] == 1 and close(R6, J6b, r_o, J_o)  # one extension pass
+    assert sizes6[2] == sizes6[0]
+    # (7) depth + xyz blocks from the same batch, one GPU pass
+    assert flags[12] == 1 and flags[13] == 1
+    _, rd_o, Jd_o = oracle.evaluate_depth(Pf, oracle.ANALYTIC)
+    nd = P.num_depth_residuals
+    dscale = max(np.abs(rd_o).max(), 1.0)
+    assert np.abs(RD.reshape(nd, 3) - rd_o).max() <= 1e-9 * dscale
+    JD = JD.reshape(nd, -1)
+    assert (np.abs(JD - Jd_o) / np.maximum(np.abs(Jd_o).max(axis=0), 1e-12)).max() <= 1e-9
+    X = np.stack([Pf.block_values(int(b)) for b in P.xyz_block])
+    w = P.xyz_weight[:, None]
+    assert np.allclose(RX.reshape(-1, 3), w * (X - P.xyz_ref), rtol=0, atol=1e-12)
+    assert np.allclose(JX.reshape(-1, 3, 3), P.xyz_weight[:, None, None] * np.eye(3), rtol=0, atol=0)
