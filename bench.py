@@ -651,6 +651,25 @@ def main():
                          "gloo (host-staged callback)" if ex else "none (single rank)"),
             "exchange_calls": ex.calls if ex else None,
         }
+        if world == 1:
+            # deterministic mode (fixed-order slab gathers instead of fp64 atomics):
+            # same LM iterations, reproducible CG count; its cost per CG iteration
+            ev.set_params()
+            ev.solve(**dict(solve_kw, max_num_iterations=1, deterministic=1), stream=sh)
+            ev.set_params()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sd = ev.solve(**dict(solve_kw, deterministic=1), stream=sh)
+            torch.cuda.synchronize()
+            ddt = time.perf_counter() - t0
+            line["ba_deterministic"] = {
+                "what": "the same LM run with mvba_solver_options.deterministic = 1",
+                "iters_per_s": max(sd["num_iterations"], 1) / ddt,
+                "cg_iterations": sd["num_linear_iterations"],
+                "ms_per_cg_iteration": 1e3 * sd["linear_solver_time_s"] / max(sd["num_linear_iterations"], 1),
+                "linearize_s": sd["linearize_time_s"],
+                "final_cost": sd["final_cost"],
+            }
         if comm is not None:
             comm.close()
 

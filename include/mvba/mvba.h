@@ -306,6 +306,8 @@ mvba_status mvba_point_block_map(const struct mvba_handle* h, int32_t* block_ids
  * Asynchronous on hip_stream. */
 #define MVBA_LIN_CAMERA_ONLY 0x20
 #define MVBA_LIN_POINTS_ONLY 0x40
+/* Camera side summed in a fixed order (no fp64 atomics): bit-reproducible. */
+#define MVBA_LIN_DETERMINISTIC 0x80
 mvba_status mvba_linearize_device(struct mvba_handle* h, int32_t flags, double cauchy_threshold,
                                   double* d_cam_grad, double* d_cam_hess, double* d_pt_grad,
                                   double* d_pt_hess, double* d_cost, void* hip_stream);
@@ -496,6 +498,10 @@ typedef struct mvba_solver_options {
   int32_t progress_to_stdout;          /* minimizer_progress_to_stdout (:1914) */
   mvba_allreduce_fn allreduce;         /* NULL: single rank */
   void* allreduce_user;
+  int32_t deterministic;               /* 1: no fp64 atomics in the normal equations and the
+                                          Schur products (fixed-order slab gathers): two runs
+                                          give bit-identical CG counts and parameters, at some
+                                          cost per CG iteration. Default 0. */
 } mvba_solver_options;
 
 typedef struct mvba_solver_summary {

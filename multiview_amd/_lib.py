@@ -111,7 +111,7 @@ DJAC_BASE = (0, 21, 42, 63, 99, 102, 111)
 DJAC_ROWS = 114
 
 REDUCE_SUM, REDUCE_MAX = 0, 1
-LIN_CAMERA_ONLY, LIN_POINTS_ONLY = 0x20, 0x40
+LIN_CAMERA_ONLY, LIN_POINTS_ONLY, LIN_DETERMINISTIC = 0x20, 0x40, 0x80
 CONVERGENCE, NO_CONVERGENCE, FAILURE = 0, 1, 2
 
 # int32_t (*)(double* device_buf, int64_t count, int32_t op, void* stream, void* user)
@@ -142,6 +142,7 @@ class SolverOptions(C.Structure):
         ("progress_to_stdout", C.c_int32),
         ("allreduce", AllreduceFn),
         ("allreduce_user", C.c_void_p),
+        ("deterministic", C.c_int32),
     ]
 
 

@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ s
                                                    const double* __restrict__ params,
                                                    const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
                                                    double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags,
-                                                   double cauchy_c) {
+                                                   double cauchy_c, Slab sl) {
   __shared__ double lds[kDT * 16 * kDLd];
   __shared__ double G[kDW * kDW];
   const int seg = blockIdx.x;
@@ -194,7 +194,6 @@ __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ s
   // expand (frame-uniform blocks)
   const FrameLin& L = fl[frame];
   double* grad = rep + (int64_t)(seg & (kDReplicas - 1)) * (ng + nh + 1);
-  double* hess = grad + ng;
   const double* wv = rec + 12;
   for (int blk = 0; blk < 4; blk++) {
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
@@ -204,7 +203,7 @@ __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ s
       const double* wk = wv + 6 * (k0 + e);
       double g = 0.0;
       for (int a = 0; a < 6; a++) g += wk[a] * G[a * kDW + 19];
-      atomicAdd(&grad[L.goff[b] + e], g);
+      accumulate(grad, L.goff[b] + e, g, sl, seg, 56 * blk + e);
     }
     for (int e = lane; e < ncol * ncol; e += 64) {
       const int kk = e / ncol, kc = e % ncol;
@@ -216,24 +215,24 @@ __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ s
         for (int c = 0; c < 6; c++) t += G[a * kDW + c] * wb[c];
         h += wa[a] * t;
       }
-      atomicAdd(&hess[L.hoff[b] + e], h);
+      accumulate(grad, ng + L.hoff[b] + e, h, sl, seg, 56 * blk + ncol + e);
     }
   }
   // depth_to_image and scale: sensor blocks, the same for the whole segment
   // (one image = one sensor), so take them from the first block's record.
   if (d0.goff_dti >= 0) {
     const int n = d0.dti_n;
-    for (int e = lane; e < n; e += 64) atomicAdd(&grad[d0.goff_dti + e], G[(6 + e) * kDW + 19]);
+    for (int e = lane; e < n; e += 64) accumulate(grad, d0.goff_dti + e, G[(6 + e) * kDW + 19], sl, seg, kSlabDti + e);
     for (int e = lane; e < n * n; e += 64) {
       const int a = e / n, c = e % n;
-      atomicAdd(&hess[d0.hoff_dti + e], G[(6 + a) * kDW + 6 + c]);
+      accumulate(grad, ng + d0.hoff_dti + e, G[(6 + a) * kDW + 6 + c], sl, seg, kSlabDtiHess + e);
     }
   }
   if (d0.goff_scale >= 0 && lane == 0) {
-    atomicAdd(&grad[d0.goff_scale], G[18 * kDW + 19]);
-    atomicAdd(&hess[d0.hoff_scale], G[18 * kDW + 18]);
+    accumulate(grad, d0.goff_scale, G[18 * kDW + 19], sl, seg, kSlabScale);
+    accumulate(grad, ng + d0.hoff_scale, G[18 * kDW + 18], sl, seg, kSlabScale + 1);
   }
-  if (lane == 0) atomicAdd(&grad[ng + nh], cost);
+  if (lane == 0) accumulate(grad, ng + nh, cost, sl, seg, (int)(sl.width - 1));
 }
 
 // Cost partials (sum 0.5 rho) per 256-thread block over the depth slots.
@@ -274,7 +273,8 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
                                                  const double* __restrict__ frec, const double* __restrict__ params,
                                                  const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
                                                  const double* __restrict__ du, double* __restrict__ yrep, int64_t ng,
-                                                 int32_t flags, double cauchy_c, const int32_t* __restrict__ gate) {
+                                                 int32_t flags, double cauchy_c, const int32_t* __restrict__ gate,
+                                                 Slab sl) {
   if (gate && *gate) return;
   constexpr int NA = 6 + 12 + 1;
   const int seg = blockIdx.x;
@@ -329,7 +329,7 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
       v = acc[18];
       dst = d0.goff_scale;
     }
-    if (dst >= 0) atomicAdd(&y[dst], v);
+    if (dst >= 0) accumulate(y, dst, v, sl, seg, lane);
   }
 }
 
@@ -390,10 +390,10 @@ hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const 
 hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
-                                  hipStream_t s) {
+                                  mvba::Slab sl, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_depth_gram, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params,
-                     pts, (const mvba::FrameLin*)fl, rep, ng, nh, flags, cauchy_c);
+                     pts, (const mvba::FrameLin*)fl, rep, ng, nh, flags, cauchy_c, sl);
   return hipGetLastError();
 }
 
@@ -412,10 +412,10 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
-                                double cauchy_c, const int32_t* gate, hipStream_t s) {
+                                double cauchy_c, const int32_t* gate, mvba::Slab sl, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params, pts,
-                     (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c, gate);
+                     (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c, gate, sl);
   return hipGetLastError();
 }
 

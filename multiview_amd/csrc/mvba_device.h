@@ -321,6 +321,46 @@ struct FrameLin {
   int64_t hoff[8];                   // camera-side Hessian offsets per block
 };
 
+// Add v into camera-side entry dst: an fp64 atomic into the replica `rep`, or,
+// in deterministic mode, a plain store into the producer's slab row (and, in
+// the record pass, the destination of that slab position).
+__device__ __forceinline__ void accumulate(double* rep, int64_t dst, double v, const Slab& s, int64_t unit,
+                                           int local) {
+  if (s.val) {
+    const int64_t pos = (s.unit_base + unit) * s.width + local;
+    s.val[pos] = v;
+    if (s.dst) s.dst[pos] = (int32_t)dst;
+  } else {
+    atomicAdd(rep + dst, v);
+  }
+}
+
+// Sum of val[pos[j]] for j in [b, e) over one wave, in a fixed order: lane l
+// adds items l, l + 64, l + 128, ... in sequence, then a fixed butterfly. The
+// loads of 8 consecutive items per lane are issued before their adds (a heavy
+// entry, e.g. a sensor's intrinsics, has thousands of producers). Returns the
+// total in every lane.
+__device__ __forceinline__ double slab_entry_sum(int64_t b, int64_t e, const int64_t* __restrict__ pos,
+                                                 const double* __restrict__ val) {
+  const int lane = threadIdx.x & 63;
+  double acc = 0.0;
+  int64_t j = b + lane;
+  for (; j + 7 * 64 < e; j += 8 * 64) {
+    int64_t q[8];
+    double v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) q[k] = pos[j + 64 * k];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = val[q[k]];
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc += v[k];
+  }
+  for (; j < e; j += 64) acc += val[pos[j]];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  return acc;
+}
+
 // Last-block finalisation of a grid reduction: every block stores its partial,
 // the last block to arrive sums them into out[0] and re-arms the counter.
 // Sum of K values over the block (blockDim.x a multiple of 64, <= 1024):

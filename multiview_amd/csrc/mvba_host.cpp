@@ -43,6 +43,7 @@ static void free_all(mvba_handle* h) {
                   h->d_tdcost, h->d_tdrows};
   solver_state_free(h->solver);
   h->solver = nullptr;
+  h->lin_det.release();
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (int k = 0; k < 2; k++) {
@@ -518,6 +519,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     for (int64_t p = 0; p < nslots; p++)
       if (slot_po[p] >= 0) po_slot[slot_po[p]] = (int32_t)p;
     h->nchunks = (int32_t)chunks.size();
+    h->nparts = (int32_t)parts.size();
   }
 
   // ---- depth blocks: device order by frame, line-aligned frame ranges, segments
@@ -902,6 +904,13 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
   // device without a second stream. Mixed models: a separate point launch.
   const bool single = h->groups.size() == 1;
   const mvba::PointExtra dc = h->point_extra();
+  // deterministic camera side: slab rows per frame part / depth segment, then a
+  // fixed-order gather; the first call records the slab destinations
+  const bool det = cam_side && (flags & MVBA_LIN_DETERMINISTIC);
+  DetPlan& D = h->lin_det;
+  if (det && !D.ready)
+    e = det_plan_begin(D, (int64_t)h->nparts + h->ndep_segs, mvba::lin_slab_width(h->kmax),
+                       h->cam_grad_size + h->cam_hess_size + 1, s);
   if (cam_side) {
     for (size_t g = 0; g < h->groups.size() && e == hipSuccess; g++) {
       const Group& G = h->groups[g];
@@ -910,7 +919,7 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
                                 h->d_frame_lin, h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
                                 h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags, cauchy_c,
                                 pts_here ? h->d_pt_begin : nullptr, h->npts, h->d_po_frame, h->d_po_meas, d_pt_grad,
-                                d_pt_hess, dc, s);
+                                d_pt_hess, dc, det ? D.slab(0) : no_slab(), G.part_begin, s);
     }
   }
   if (pt_side && (!single || !cam_side) && e == hipSuccess)
@@ -920,8 +929,12 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
   if (cam_side && e == hipSuccess && h->ndep_segs > 0)
     e = mvba_launch_depth_gram(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_frec, h->d_params,
                                h->d_pts, h->d_frame_lin, h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags,
-                               cauchy_c, s);
-  if (cam_side && e == hipSuccess)
+                               cauchy_c, det ? D.slab(h->nparts) : no_slab(), s);
+  if (det && e == hipSuccess && !D.ready) e = det_plan_finish(D, s);
+  if (det && e == hipSuccess)
+    e = mvba_launch_slab_lin(D.nout, D.begin, D.pos, D.val, h->cam_grad_size, h->cam_hess_size, d_cam_grad,
+                             d_cam_hess, d_cost, s);
+  else if (cam_side && e == hipSuccess)
     e = mvba_launch_rep_reduce(h->d_rep, h->nrep, h->cam_grad_size, h->cam_hess_size, d_cam_grad, d_cam_hess, d_cost,
                                s);
   if (cam_side && e == hipSuccess && h->nxyz > 0 && d_cost) {

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <cstdint>
@@ -34,7 +35,10 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
                                  const double4* pts, const int32_t* obs_pid, const double2* obs_meas, double* rep,
                                  int64_t ng, int64_t nh, int32_t flags, double cauchy_c, const int64_t* pt_begin,
                                  int64_t npts, const int32_t* po_frame, const double2* po_meas, double* pgrad,
-                                 double* phess, mvba::PointExtra dc, hipStream_t s);
+                                 double* phess, mvba::PointExtra dc, mvba::Slab sl, int32_t part_base,
+                                 hipStream_t s);
+hipError_t mvba_launch_slab_lin(int64_t n, const int64_t* begin, const int64_t* pos, const double* val, int64_t ng,
+                                int64_t nh, double* grad, double* hess, double* cost, hipStream_t s);
 hipError_t mvba_launch_rep_reduce(double* rep, int32_t nrep, int64_t ng, int64_t nh, double* grad, double* hess,
                                   double* cost, hipStream_t s);
 int mvba_num_replicas(void);
@@ -59,7 +63,7 @@ hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const 
 hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
-                                  hipStream_t s);
+                                  mvba::Slab sl, hipStream_t s);
 hipError_t mvba_launch_xyz_cost(int64_t n, const int32_t* xpid, const double4* xref, const double* xcc,
                                 const double4* pts, int32_t flags, double* partial, unsigned* counter,
                                 double* out, hipStream_t s);
@@ -115,6 +119,8 @@ struct PoseKeyHash {
 
 constexpr int kFixedSize[7] = {7, 7, 7, 3, 1, 1, 2};
 
+
+
 inline int rpc_degree(int n) { return static_cast<int>(std::round(std::sqrt(2.0 * n + 5.0) / 2.0 - 1.5)); }
 inline int rpc_num_dist_params(int d) { return 2 * (d + 1) * (d + 2) - 2; }
 
@@ -157,6 +163,64 @@ hipError_t upload(T** p, const std::vector<T>& v) {
   if (e != hipSuccess) return e;
   if (v.empty()) return hipSuccess;
   return hipMemcpy(*p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+// Deterministic accumulation plan (mvba::Slab): slab rows of `units` producers,
+// `width` doubles each, and the CSR entry -> slab positions (in slab order)
+// built once from a record pass.
+struct DetPlan {
+  int64_t units = 0, width = 0, nout = 0;
+  double* val = nullptr;
+  int64_t* begin = nullptr;  // [nout + 1]
+  int64_t* pos = nullptr;
+  int32_t* dst = nullptr;    // record pass only
+  bool ready = false;
+  mvba::Slab slab(int64_t unit_base) const { return mvba::Slab{val, ready ? nullptr : dst, width, unit_base}; }
+  void release() {
+    for (void* p : {(void*)val, (void*)begin, (void*)pos, (void*)dst})
+      if (p) (void)hipFree(p);
+    val = nullptr;
+    begin = pos = nullptr;
+    dst = nullptr;
+    ready = false;
+  }
+};
+inline mvba::Slab no_slab() { return mvba::Slab{nullptr, nullptr, 0, 0}; }
+
+// Allocate the slab and the record-pass destination array (set to -1).
+inline hipError_t det_plan_begin(DetPlan& P, int64_t units, int64_t width, int64_t nout, hipStream_t s) {
+  P.units = units;
+  P.width = width;
+  P.nout = nout;
+  const size_t n = (size_t)std::max<int64_t>(units * width, 1);
+  hipError_t e = hipSuccess;
+  if (!P.val) e = hipMalloc(reinterpret_cast<void**>(&P.val), n * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&P.dst), n * sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(P.dst, 0xFF, n * sizeof(int32_t), s);
+  return e;
+}
+
+// After the record pass: CSR of destination entry -> slab positions, positions
+// in increasing order (the fixed summation order), uploaded; dst released.
+inline hipError_t det_plan_finish(DetPlan& P, hipStream_t s) {
+  const size_t n = (size_t)std::max<int64_t>(P.units * P.width, 1);
+  std::vector<int32_t> dst(n);
+  hipError_t e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipMemcpy(dst.data(), P.dst, n * sizeof(int32_t), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  std::vector<int64_t> begin((size_t)P.nout + 1, 0);
+  for (size_t k = 0; k < n; k++)
+    if (dst[k] >= 0 && dst[k] < P.nout) begin[(size_t)dst[k] + 1]++;
+  for (int64_t k = 0; k < P.nout; k++) begin[(size_t)k + 1] += begin[(size_t)k];
+  std::vector<int64_t> fill(begin.begin(), begin.end() - 1), pos((size_t)std::max<int64_t>(begin.back(), 1));
+  for (size_t k = 0; k < n; k++)
+    if (dst[k] >= 0 && dst[k] < P.nout) pos[(size_t)fill[(size_t)dst[k]]++] = (int64_t)k;
+  e = upload(&P.begin, begin);
+  if (e == hipSuccess) e = upload(&P.pos, pos);
+  if (e == hipSuccess) e = hipFree(P.dst);
+  P.dst = nullptr;
+  P.ready = e == hipSuccess;
+  return e;
 }
 
 }  // namespace mvba_internal
@@ -239,6 +303,8 @@ struct mvba_handle {
   int32_t* d_po_slot = nullptr;          // point-order index -> device slot
   std::vector<int64_t> cam_poff;         // camera-side entry -> packed parameter offset
   int32_t nchunks = 0;
+  int32_t nparts = 0;                    // K2 frame parts over all model groups
+  DetPlan lin_det;                       // deterministic K2 camera side (MVBA_LIN_DETERMINISTIC)
 
   // BracketedDepthError blocks (device order by frame)
   int64_t ndep = 0, ndep_slots = 0;

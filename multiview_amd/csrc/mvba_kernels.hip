@@ -413,7 +413,8 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
     const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl, const double* __restrict__ frec,
     const double* __restrict__ params, const double4* __restrict__ pts,
     const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
-    double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c, PointLinArgs pa) {
+    double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c, PointLinArgs pa, Slab sl,
+    int32_t part_base) {
   using S = GramShape<MODEL, DEG>;
   constexpr int T = S::kTiles;
   constexpr int NP = S::kPairs;
@@ -578,8 +579,9 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
   __syncthreads();
   const FrameLin& L = fl[frame];
   const int R = S::kColR;
+  // replica (frame mod kLinReplicas) of [grad | hess | cost], or this part's slab row
   double* grad = rep + (int64_t)(frame & (kLinReplicas - 1)) * (ng + nh + 1);
-  double* hess = grad + ng;
+  const int64_t unit = part_base + (int64_t)blockIdx.x;
   // pose blocks: beg(0) cols 0..6, end(1) 7..13, ref_to_cam(2) 14..20, offset(4) 21
 #pragma unroll
   for (int blk = 0; blk < 4; blk++) {
@@ -593,12 +595,12 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
       if (e < ncol) {
 #pragma unroll
         for (int a = 0; a < 6; a++) v += wbuf[a * kPoseCols + k0 + e] * g(a, R);
-        atomicAdd(&grad[go + e], v);
+        accumulate(grad, go + e, v, sl, unit, 56 * blk + e);
       } else {
         const int h = e - ncol, kk = h / ncol, kc = h % ncol;
 #pragma unroll
         for (int a = 0; a < 6; a++) v += wbuf[a * kPoseCols + k0 + kk] * Tm[a * kPoseCols + k0 + kc];
-        atomicAdd(&hess[ho + h], v);
+        accumulate(grad, ng + ho + h, v, sl, unit, 56 * blk + e);
       }
     }
   }
@@ -613,20 +615,38 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
     const int nc = q == 0 ? 1 : q == 1 ? 2 : (kDistLive < K ? kDistLive : K);  // radtan K=4: 4 of 5 columns
     const int bs = q == 2 ? K : nc;  // Hessian row length (RPC: K incl. the zero half)
     const int64_t ho = L.hoff[b];
+    const int sbase = q == 0 ? kSlabFocal : q == 1 ? kSlabCenter : kSlabDist;
     for (int e = tid; e < nc + nc * nc; e += 64 * WAVES) {
       if (e < nc) {
-        atomicAdd(&grad[go + e], g(cs + e, R));
+        accumulate(grad, go + e, g(cs + e, R), sl, unit, sbase + e);
       } else {
         const int h = e - nc, r = h / nc, cc = h % nc;
-        atomicAdd(&hess[ho + r * bs + cc], g(cs + r, cs + cc));
+        accumulate(grad, ng + ho + r * bs + cc, g(cs + r, cs + cc), sl, unit, sbase + e);
       }
     }
   }
   if (tid == 0) {
     double cv = 0.0;
     for (int w = 0; w < WAVES; w++) cv += wcost[w];
-    atomicAdd(hess + nh, cv);
+    accumulate(grad, ng + nh, cv, sl, unit, (int)(sl.width - 1));
   }
+}
+
+// Deterministic mode: out[e] = sum of entry e's slab positions in slab order
+// (CSR e -> positions), one wave per entry (lane-strided partial sums, then a
+// fixed butterfly), written to grad | hess | cost.
+__global__ void __launch_bounds__(256) k_slab_lin(int64_t n, const int64_t* __restrict__ begin,
+                                                  const int64_t* __restrict__ pos, const double* __restrict__ val,
+                                                  int64_t ng, int64_t nh, double* __restrict__ grad,
+                                                  double* __restrict__ hess, double* __restrict__ cost) {
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (e >= n) return;
+  const double acc = slab_entry_sum(begin[e], begin[e + 1], pos, val);
+  if (lane != 0) return;
+  if (e < ng) grad[e] = acc;
+  else if (e < ng + nh) hess[e - ng] = acc;
+  else if (cost) *cost = acc;
 }
 
 __global__ void __launch_bounds__(256) k_rep_reduce(double* __restrict__ rep, int32_t nrep, int64_t ng, int64_t nh,
@@ -870,7 +890,8 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
                                  const double4* pts, const int32_t* obs_pid, const double2* obs_meas, double* rep,
                                  int64_t ng, int64_t nh, int32_t flags, double cauchy_c, const int64_t* pt_begin,
                                  int64_t npts, const int32_t* po_frame, const double2* po_meas, double* pgrad,
-                                 double* phess, mvba::PointExtra dc, hipStream_t s) {
+                                 double* phess, mvba::PointExtra dc, mvba::Slab sl, int32_t part_base,
+                                 hipStream_t s) {
   const bool with_pts = pt_begin != nullptr && npts > 0;
   if (nparts <= 0 && !with_pts) return hipSuccess;
   const mvba::PointLinArgs pa{pt_begin, npts, po_frame, po_meas, pgrad, phess, dc};
@@ -883,11 +904,11 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
       hipLaunchKernelGGL((mvba::k_frame_lin<M, D, true>), dim3((unsigned)(nparts + pblocks)),             \
                          dim3((unsigned)threads), GS::kLdsBytes, s, parts, nparts, segs, fd,               \
                          (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas, rep, ng, nh, flags, \
-                         cauchy_c, pa);                                                                    \
+                         cauchy_c, pa, sl, part_base);                                                     \
     else                                                                                                   \
       hipLaunchKernelGGL((mvba::k_frame_lin<M, D, false>), dim3((unsigned)nparts), dim3((unsigned)threads), \
                          GS::kLdsBytes, s, parts, nparts, segs, fd, (const mvba::FrameLin*)fl, frec, params, \
-                         pts, obs_pid, obs_meas, rep, ng, nh, flags, cauchy_c, pa);                        \
+                         pts, obs_pid, obs_meas, rep, ng, nh, flags, cauchy_c, pa, sl, part_base);         \
   }
   switch (model) {
     case mvba::kModelNone: MVBA_FLIN(mvba::kModelNone, 0); break;
@@ -907,6 +928,14 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
     default: return hipErrorInvalidValue;
   }
 #undef MVBA_FLIN
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_slab_lin(int64_t n, const int64_t* begin, const int64_t* pos, const double* val, int64_t ng,
+                                int64_t nh, double* grad, double* hess, double* cost, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_slab_lin, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, n, begin, pos, val, ng, nh, grad,
+                     hess, cost);
   return hipGetLastError();
 }
 

@@ -51,12 +51,17 @@ hipError_t mvba_launch_frame_proj(int32_t nframes, const mvba::FrameDesc* fd, co
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
-                                double cauchy_c, const int32_t* gate, hipStream_t s);
+                                double cauchy_c, const int32_t* gate, mvba::Slab sl, hipStream_t s);
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
                               const Segment* segs, const FrameDesc* fd, const void* fl, const double* frec,
                               const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
-                              int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, hipStream_t s);
+                              int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
+                              hipStream_t s);
+hipError_t mvba_launch_slab_reduce_vec(int64_t ng, const int64_t* begin, const int64_t* pos, const double* val,
+                                       const double* diag, const double* x, double* y, double* partial,
+                                       unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
+                                       hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
                                       mvba::CgCtl* ctl, hipStream_t s);
@@ -133,6 +138,7 @@ struct SolverState {
   mvba::CgEntry* ent = nullptr;  // per camera entry: block start, size, inverse row
   int32_t max_bsize = 0;
   int64_t *goff = nullptr, *hoff = nullptr, *cam_poff = nullptr;
+  DetPlan b_det;              // deterministic pass B (slab rows per chunk / depth segment)
 };
 
 void solver_state_free(SolverState* S) {
@@ -144,6 +150,7 @@ void solver_state_free(SolverState* S) {
     if (p) (void)hipFree(p);
   if (S->hscal) (void)hipHostFree(S->hscal);
   if (S->hctl) (void)hipHostFree(S->hctl);
+  S->b_det.release();
   delete S;
 }
 
@@ -199,7 +206,7 @@ SolverState* alloc_state(mvba_handle* h) {
     int64_t ncost = 0;
     for (const Group& G : h->groups) ncost = std::max<int64_t>(ncost, (G.seg_count + 3) / 4);
     // k_cg_update: 3 partials per 256-entry block; k_vec_rep_reduce / k_add_diag one
-    S->npartial = std::max<int64_t>({3072, 3 * ((S->ng + 255) / 256), mvba_pass_a_blocks(S->np), ncost,
+    S->npartial = std::max<int64_t>({3072, 3 * ((S->ng + 255) / 256), (S->ng + 3) / 4, mvba_pass_a_blocks(S->np), ncost,
                                     (int64_t)h->ndep_segs, (h->ndep_slots + 255) / 256});
     HCHK(dalloc(&S->partial, (size_t)S->npartial));
     HCHK(dalloc(&S->scal, 32));
@@ -290,7 +297,8 @@ class Solver {
 
   // Jacobian at the handle's parameters -> lin (all-reduced), G, phess, cdiag. Returns cost.
   double linearize() {
-    mvba_status st = mvba_linearize_device(h_, flags_, o_.robust_threshold, S_->lin, S_->lin + S_->ng,
+    const int32_t lf = flags_ | (o_.deterministic ? MVBA_LIN_DETERMINISTIC : 0);
+    mvba_status st = mvba_linearize_device(h_, lf, o_.robust_threshold, S_->lin, S_->lin + S_->ng,
                                            S_->G + S_->ng, S_->phess, S_->lin + S_->ng + S_->nh, (void*)s_);
     if (st != MVBA_OK) throw StatusErr{st, h_->err};
     check_alpha();
@@ -345,19 +353,31 @@ class Solver {
   // dir: the frame directions of xv (null: pass B with x = 0, u_o = -J_pt w_p)
   void reduce_frames(double* y, const double* xv, int dot_slot, const double* dir, const int32_t* gate = nullptr,
                      mvba::CgCtl* ctl = nullptr) {
+    // deterministic mode: slab rows per chunk / depth segment and a fixed-order
+    // gather instead of replica atomics (the first product records the plan)
+    DetPlan& D = S_->b_det;
+    const bool det = o_.deterministic != 0;
+    if (det && !D.ready)
+      HCHK(det_plan_begin(D, (int64_t)h_->nchunks + h_->ndep_segs, mvba::vec_slab_width(h_->kmax), S_->ng, s_));
     for (const Group& G : h_->groups)
       HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
                               h_->d_segs, h_->d_fd, h_->d_frame_lin, h_->d_frec, h_->d_params, h_->d_pts,
                               h_->d_obs_pid, h_->d_obs_meas, dir, (const double4*)S_->wbuf, S_->yrep, S_->ng, flags_,
-                              cauchy_c_, gate, s_));
+                              cauchy_c_, gate, det ? D.slab(0) : no_slab(), s_));
     if (h_->ndep > 0)
       HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
                                 h_->d_params, h_->d_pts, h_->d_frame_lin, S_->du, S_->yrep, S_->ng, flags_, cauchy_c_,
-                                gate, s_));
+                                gate, det ? D.slab(h_->nchunks) : no_slab(), s_));
+    if (det && !D.ready) HCHK(det_plan_finish(D, s_));
     const bool fuse = xv && !o_.allreduce;
-    HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr, y, S_->partial,
-                                    S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate, fuse ? ctl : nullptr,
-                                    s_));
+    if (det)
+      HCHK(mvba_launch_slab_reduce_vec(S_->ng, D.begin, D.pos, D.val, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr,
+                                       y, S_->partial, S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate,
+                                       fuse ? ctl : nullptr, s_));
+    else
+      HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr, y,
+                                      S_->partial, S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate,
+                                      fuse ? ctl : nullptr, s_));
     exchange(y, S_->ng, MVBA_REDUCE_SUM);
     if (xv && !fuse)
       HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, gate, ctl,

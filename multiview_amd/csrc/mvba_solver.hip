@@ -491,7 +491,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
                                             const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
                                             const double2* __restrict__ obs_meas, const double* __restrict__ dir,
                                             const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng,
-                                            int32_t flags, double cauchy_c) {
+                                            int32_t flags, double cauchy_c, const Slab& sl) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   extern __shared__ double st[];  // [NA + 1][kWideLd]: columns, then u
@@ -581,7 +581,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
       double v = 0.0;
 #pragma unroll
       for (int a = 0; a < 6; a++) v += wk[a] * zs[a];
-      atomicAdd(&y[L.goff[b] + (lane - 7 * blk)], v);
+      accumulate(y, L.goff[b] + (lane - 7 * blk), v, sl, chunk_id, lane);
     }
   }
   // intrinsic entries: column 6 + q held by lane (6 + q) mod 64
@@ -594,7 +594,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
     if (q == 0) dst = L.goff[MVBA_BLK_FOCAL];
     else if (q < 3) dst = L.goff[MVBA_BLK_CENTER] >= 0 ? L.goff[MVBA_BLK_CENTER] + (q - 1) : -1;
     else if (q - 3 < F.K) dst = L.goff[MVBA_BLK_DIST] >= 0 ? L.goff[MVBA_BLK_DIST] + (q - 3) : -1;
-    if (dst >= 0) atomicAdd(&y[dst], h == 0 ? acc0 : acc1);
+    if (dst >= 0) accumulate(y, dst, h == 0 ? acc0 : acc1, sl, chunk_id, kPoseCols + q);
   }
 }
 
@@ -613,7 +613,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
     const double2* __restrict__ obs_meas, const double* __restrict__ dir,
     const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c,
-    const int32_t* __restrict__ gate) {
+    const int32_t* __restrict__ gate, Slab sl) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   const int lane = threadIdx.x;
@@ -621,7 +621,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
   if (ch >= nchunks || (gate && *gate)) return;
   if constexpr (NA > kPassBRegCols) {
     pass_b_wide<MODEL, DEG>(chunks[ch], chunk_base + ch, segs, fd, fl, frec, params, pts, obs_pid, obs_meas, dir,
-                            wbuf, yrep, ng, flags, cauchy_c);
+                            wbuf, yrep, ng, flags, cauchy_c, sl);
     return;
   } else {
   const int4 c = chunks[ch];
@@ -699,7 +699,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
       else if (q - 3 < F.K) dst = L.goff[MVBA_BLK_DIST] >= 0 ? L.goff[MVBA_BLK_DIST] + (q - 3) : -1;
     }
   }
-  if (dst >= 0) atomicAdd(&y[dst], v);
+  if (dst >= 0) accumulate(y, dst, v, sl, chunk_base + ch, lane);
   }
 }
 
@@ -742,6 +742,32 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
     for (int r = 0; r < kVecReplicas; r++) acc += v[r];
 #pragma unroll
     for (int r = 0; r < kVecReplicas; r++) yrep[r * n + e] = 0.0;
+    if (diag) acc += diag[e] * x[e];
+    y[e] = acc;
+    d = x ? x[e] * acc : 0.0;
+  }
+  if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
+    cg_step_length(ctl, dot_out[0]);
+}
+
+// Deterministic mode: y[e] = sum of entry e's slab positions in slab order (CSR
+// e -> positions; one wave per entry, lane-strided sums and a fixed butterfly),
+// then the same damping, x.y reduction and CG step length as k_vec_rep_reduce.
+__global__ void __launch_bounds__(256) k_vec_slab_reduce(int64_t n, const int64_t* __restrict__ begin,
+                                                         const int64_t* __restrict__ pos,
+                                                         const double* __restrict__ val,
+                                                         const double* __restrict__ diag,
+                                                         const double* __restrict__ x, double* __restrict__ y,
+                                                         double* __restrict__ partial, unsigned* __restrict__ counter,
+                                                         double* __restrict__ dot_out,
+                                                         const int32_t* __restrict__ gate, CgCtl* __restrict__ ctl) {
+  if (gate && *gate) return;
+  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  double acc = 0.0;
+  if (e < n) acc = slab_entry_sum(begin[e], begin[e + 1], pos, val);
+  double d = 0.0;
+  if (e < n && lane == 0) {
     if (diag) acc += diag[e] * x[e];
     y[e] = acc;
     d = x ? x[e] * acc : 0.0;
@@ -1261,19 +1287,30 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const mvba::Segment* segs, const mvba::FrameDesc* fd, const void* fl,
                               const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
-                              int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, hipStream_t s) {
+                              int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
+                              hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PB(M, D)                                                                                       \
   hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), (mvba::pass_b_lds<M, D>()), s,\
                      chunks, nchunks,                                                                         \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
-                     dir, wbuf, yrep, ng, flags, cauchy_c, gate)
+                     dir, wbuf, yrep, ng, flags, cauchy_c, gate, sl)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)
 #undef MVBA_PB
   return hipGetLastError();
 }
 
 // y = sum of replicas (+ diag .* x, and x.y -> dot_out when dot_out != null)
+hipError_t mvba_launch_slab_reduce_vec(int64_t ng, const int64_t* begin, const int64_t* pos, const double* val,
+                                       const double* diag, const double* x, double* y, double* partial,
+                                       unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
+                                       hipStream_t s) {
+  if (ng <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_vec_slab_reduce, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, ng, begin, pos, val,
+                     diag, x, y, partial, counter, dot_out, gate, ctl);
+  return hipGetLastError();
+}
+
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
                                       mvba::CgCtl* ctl, hipStream_t s) {

@@ -60,6 +60,34 @@ constexpr int kChunkSegs = 4;       // segments per solver chunk (one wave)
 constexpr int kPartSegs = 16;       // segments per K2 frame part (one block)
 constexpr int kDepthReplicas = 32;  // replicas the depth Gram adds into (frame-segment mod 32)
 
+// Deterministic accumulation (mvba_solver_options.deterministic,
+// MVBA_LIN_DETERMINISTIC): a producer (K2 frame part, solver chunk, depth
+// segment) stores each of its contributions to a shared camera-side entry in
+// its own slab row instead of adding it into a replica with an fp64 atomic;
+// a gather kernel then sums every entry over its producers in a fixed order,
+// so the result no longer depends on the order atomics arrive in.
+struct Slab {
+  double* val;        // [units x width]; null: replica atomics (default mode)
+  int32_t* dst;       // record pass only: destination entry of every slab position
+  int64_t width;      // doubles per unit
+  int64_t unit_base;  // slab row of this launch's first unit
+};
+// Slab row layout of one K2 producer (frame part or depth segment): pose
+// blocks beg / end / ref_to_cam at 56 b (7 gradient + 49 Hessian entries),
+// offset at 168 (2), focal at 170 (2), centre at 172 (6), distortion at 178
+// (K + K^2), cost in the last position; depth: depth_to_image gradient at 170
+// (12), Hessian at 182 (144), scale at 326 (2).
+constexpr int kSlabFocal = 170, kSlabCenter = 172, kSlabDist = 178;
+constexpr int kSlabDti = 170, kSlabDtiHess = 182, kSlabScale = 326;
+inline int64_t lin_slab_width(int kmax) {
+  const int64_t w = kSlabDist + (int64_t)kmax + (int64_t)kmax * kmax + 1;
+  return w > kSlabScale + 3 ? w : kSlabScale + 3;
+}
+// Solver pass B producers (chunk or depth segment): one position per lane of
+// the final scatter: 22 pose columns, then focal, centre (2), distortion (K);
+// depth segments: depth_to_image (12) at 22, scale at 34.
+inline int64_t vec_slab_width(int kmax) { return 25 + kmax > 35 ? 25 + kmax : 35; }
+
 // Per-frame record of the linearization (K2 expand); mirrors mvba::FrameLin in
 // mvba_kernels.hip (checked with mvba_frame_lin_size()).
 struct FrameLinHost {

@@ -226,12 +226,14 @@ class Evaluator:
 
     def linearize_device(self, cam_grad, cam_hess, pt_grad, pt_hess, cost=None,
                          apply_loss: bool = False, robust_threshold: float = 3.0, stream=None,
-                         skip_prep: bool = False, side: str = "both"):
+                         skip_prep: bool = False, side: str = "both", deterministic: bool = False):
         """Gradient and block-diagonal Hessian into caller-owned torch float64
         CUDA tensors (layouts: include/mvba/mvba.h, mvba_linearize_device).
-        side: "both", "camera" (MVBA_LIN_CAMERA_ONLY) or "points" (timing)."""
+        side: "both", "camera" (MVBA_LIN_CAMERA_ONLY) or "points" (timing);
+        deterministic: MVBA_LIN_DETERMINISTIC (fixed-order camera-side sums)."""
         flags = (_lib.EVAL_APPLY_LOSS if apply_loss else 0) | (_lib.EVAL_SKIP_PREP if skip_prep else 0) | \
-            {"both": 0, "camera": _lib.LIN_CAMERA_ONLY, "points": _lib.LIN_POINTS_ONLY}[side]
+            {"both": 0, "camera": _lib.LIN_CAMERA_ONLY, "points": _lib.LIN_POINTS_ONLY}[side] | \
+            (_lib.LIN_DETERMINISTIC if deterministic else 0)
         ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         st = self.lib.mvba_linearize_device(self.h, flags, float(robust_threshold), ptr(cam_grad),
                                             ptr(cam_hess), ptr(pt_grad), ptr(pt_hess), ptr(cost),
