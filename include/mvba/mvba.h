@@ -240,9 +240,11 @@ void* mvba_host_alloc(size_t bytes);  /* pinned host memory, NULL on failure */
 void mvba_host_free(void* p);
 /* Packed Jacobian: only the columns of the parameter blocks with transfer[b]
  * != 0 (num_blocks bytes; NULL = every non-constant block). Residual block i's
- * entries start at offsets[i] (num_residuals + 1 int64, nullable) and hold,
- * in block-position order (MVBA_BLK_*), the row-major 2 x size_b Jacobian of
- * each transferred block it references (zero if that block is constant).
+ * entries start at offsets[i] (num_residuals + 1 int64, nullable; rows are
+ * stored in the device's frame order, so offsets are not increasing in i;
+ * offsets[num_residuals] = the total) and hold, in block-position order
+ * (MVBA_BLK_*), the row-major 2 x size_b Jacobian of each transferred block it
+ * references (zero if that block is constant).
  * Replaces CostFunction::Evaluate's per-block jacobians[b] (NULL for the blocks
  * Ceres holds constant), so blocks nobody asks for never cross PCIe. */
 mvba_status mvba_set_transfer_blocks(struct mvba_handle* h, const uint8_t* transfer, int64_t* offsets);

@@ -387,6 +387,65 @@ __device__ __forceinline__ void block_sum(double* v) {
   }
 }
 
+// Deterministic gather over a DetPlan (host: mvba_internal.h), three tiers by
+// producer count so the grid stays small (its reduction counter is contended
+// per arriving block): blocks [0, nheavy) take one heavy entry each (more than
+// kSlabMedium producers: a sensor's extrinsics and intrinsics; 256 threads,
+// lane-strided, fixed block reduction); the next nmed_blocks blocks take four
+// medium entries, one wave each (slab_entry_sum); the rest take 256 light
+// entries (at most kSlabLight producers, e.g. a reference pose), one thread
+// each summing its producers in order. Returns true in the one thread holding
+// entry *e's total in *acc. Control flow is block-uniform.
+__device__ __forceinline__ bool slab_gather(const SlabTiers& t, const int64_t* __restrict__ begin,
+                                            const int64_t* __restrict__ pos, const double* __restrict__ val,
+                                            int64_t* e_out, double* acc_out) {
+  const int64_t blk = blockIdx.x;
+  if (blk < t.nheavy) {
+    const int64_t e = t.heavy[blk];
+    const int64_t b = begin[e], end = begin[e + 1];
+    double acc = 0.0;
+    int64_t j = b + threadIdx.x;
+    for (; j + 3 * 256 < end; j += 4 * 256) {
+      int64_t q[4];
+      double v[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) q[k] = pos[j + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[k] = val[q[k]];
+#pragma unroll
+      for (int k = 0; k < 4; k++) acc += v[k];
+    }
+    for (; j < end; j += 256) acc += val[pos[j]];
+    block_sum<1>(&acc);
+    *e_out = e;
+    *acc_out = acc;
+    return threadIdx.x == 0;
+  }
+  const int64_t med_blocks = (t.nmedium + 3) / 4;
+  if (blk < t.nheavy + med_blocks) {
+    const int64_t k = (blk - t.nheavy) * 4 + (threadIdx.x >> 6);
+    if (k >= t.nmedium) return false;
+    const int64_t e = t.medium[k];
+    *e_out = e;
+    *acc_out = slab_entry_sum(begin[e], begin[e + 1], pos, val);
+    return (threadIdx.x & 63) == 0;
+  }
+  const int64_t k = (blk - t.nheavy - med_blocks) * 256 + threadIdx.x;
+  if (k >= t.nlight) return false;
+  const int64_t e = t.light[k];
+  const int64_t b = begin[e], n = begin[e + 1] - b;
+  int64_t q[kSlabLight];
+#pragma unroll
+  for (int u = 0; u < kSlabLight; u++) q[u] = u < n ? pos[b + u] : -1;
+  double acc = 0.0;
+#pragma unroll
+  for (int u = 0; u < kSlabLight; u++)
+    if (u < n) acc += val[q[u]];
+  *e_out = e;
+  *acc_out = acc;
+  return true;
+}
+
 // Cross-block hand-off of the reduction partials without __threadfence():
 // on gfx950 an agent-scope fence is an L2 write-back plus an L2 invalidate
 // (buffer_wbl2 sc1 / buffer_inv sc1) of the whole XCD, paid by every block.

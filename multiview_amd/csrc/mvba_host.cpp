@@ -50,6 +50,9 @@ static void free_all(mvba_handle* h) {
     if (h->h_stage[k]) (void)hipHostFree(h->h_stage[k]);
     if (h->stage_ev[k]) (void)hipEventDestroy(h->stage_ev[k]);
   }
+  for (hipEvent_t ev : h->xfer_ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (h->xfer_stream) (void)hipStreamDestroy(h->xfer_stream);
 }
 
 extern "C" {
@@ -932,8 +935,8 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
                                cauchy_c, det ? D.slab(h->nparts) : no_slab(), s);
   if (det && e == hipSuccess && !D.ready) e = det_plan_finish(D, s);
   if (det && e == hipSuccess)
-    e = mvba_launch_slab_lin(D.nout, D.begin, D.pos, D.val, h->cam_grad_size, h->cam_hess_size, d_cam_grad,
-                             d_cam_hess, d_cost, s);
+    e = mvba_launch_slab_lin(D.tier_view(), D.grid(), D.begin, D.pos, D.val, h->cam_grad_size, h->cam_hess_size,
+                             d_cam_grad, d_cam_hess, d_cost, s);
   else if (cam_side && e == hipSuccess)
     e = mvba_launch_rep_reduce(h->d_rep, h->nrep, h->cam_grad_size, h->cam_hess_size, d_cam_grad, d_cam_hess, d_cost,
                                s);

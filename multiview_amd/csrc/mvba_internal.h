@@ -37,8 +37,9 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
                                  int64_t npts, const int32_t* po_frame, const double2* po_meas, double* pgrad,
                                  double* phess, mvba::PointExtra dc, mvba::Slab sl, int32_t part_base,
                                  hipStream_t s);
-hipError_t mvba_launch_slab_lin(int64_t n, const int64_t* begin, const int64_t* pos, const double* val, int64_t ng,
-                                int64_t nh, double* grad, double* hess, double* cost, hipStream_t s);
+hipError_t mvba_launch_slab_lin(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
+                                const double* val, int64_t ng, int64_t nh, double* grad, double* hess, double* cost,
+                                hipStream_t s);
 hipError_t mvba_launch_rep_reduce(double* rep, int32_t nrep, int64_t ng, int64_t nh, double* grad, double* hess,
                                   double* cost, hipStream_t s);
 int mvba_num_replicas(void);
@@ -84,7 +85,7 @@ struct mvba_rows_layout {
   int32_t jac_rows, nres, nblocks, var_block;
   int32_t base[8], size[8];
 };
-extern "C" hipError_t mvba_launch_rows(const double* res, const double* J, int64_t ld, int64_t nslots,
+extern "C" hipError_t mvba_launch_rows(const double* res, const double* J, int64_t ld, int64_t slot0, int64_t nslots,
                                        const mvba_rows_layout* L, double cauchy_c, const int64_t* order,
                                        const uint8_t* written, const int16_t* varsize, const uint8_t* xmask,
                                        const int64_t* xoff, double* out_res, double* out_cost, double* out_rows,
@@ -174,13 +175,19 @@ struct DetPlan {
   int64_t* begin = nullptr;  // [nout + 1]
   int64_t* pos = nullptr;
   int32_t* dst = nullptr;    // record pass only
+  int64_t* tiers = nullptr;  // entry ids: heavy | medium | light (mvba::SlabTiers)
+  int64_t nheavy = 0, nmedium = 0, nlight = 0;
   bool ready = false;
+  mvba::SlabTiers tier_view() const {
+    return mvba::SlabTiers{tiers, tiers + nheavy, tiers + nheavy + nmedium, nheavy, nmedium, nlight};
+  }
+  int64_t grid() const { return nheavy + (nmedium + 3) / 4 + (nlight + 255) / 256; }
   mvba::Slab slab(int64_t unit_base) const { return mvba::Slab{val, ready ? nullptr : dst, width, unit_base}; }
   void release() {
-    for (void* p : {(void*)val, (void*)begin, (void*)pos, (void*)dst})
+    for (void* p : {(void*)val, (void*)begin, (void*)pos, (void*)dst, (void*)tiers})
       if (p) (void)hipFree(p);
     val = nullptr;
-    begin = pos = nullptr;
+    begin = pos = tiers = nullptr;
     dst = nullptr;
     ready = false;
   }
@@ -215,8 +222,19 @@ inline hipError_t det_plan_finish(DetPlan& P, hipStream_t s) {
   std::vector<int64_t> fill(begin.begin(), begin.end() - 1), pos((size_t)std::max<int64_t>(begin.back(), 1));
   for (size_t k = 0; k < n; k++)
     if (dst[k] >= 0 && dst[k] < P.nout) pos[(size_t)fill[(size_t)dst[k]]++] = (int64_t)k;
+  std::vector<int64_t> heavy, medium, light;
+  for (int64_t k = 0; k < P.nout; k++) {
+    const int64_t c = begin[(size_t)k + 1] - begin[(size_t)k];
+    (c > mvba::kSlabMedium ? heavy : c > mvba::kSlabLight ? medium : light).push_back(k);
+  }
+  P.nheavy = (int64_t)heavy.size();
+  P.nmedium = (int64_t)medium.size();
+  P.nlight = (int64_t)light.size();
+  heavy.insert(heavy.end(), medium.begin(), medium.end());
+  heavy.insert(heavy.end(), light.begin(), light.end());
   e = upload(&P.begin, begin);
   if (e == hipSuccess) e = upload(&P.pos, pos);
+  if (e == hipSuccess) e = upload(&P.tiers, heavy);
   if (e == hipSuccess) e = hipFree(P.dst);
   P.dst = nullptr;
   P.ready = e == hipSuccess;
@@ -273,6 +291,9 @@ struct mvba_handle {
   uint8_t* d_xmask = nullptr;      // packed layout: slot -> transferred blocks
   int64_t* d_xoff = nullptr;       // packed layout: slot -> row offset
   std::vector<int64_t> xoffsets;   // packed layout: insertion index -> row offset (N + 1)
+  std::vector<int64_t> slot_rows;  // packed layout: slot -> first row offset at or after it (S + 1)
+  hipStream_t xfer_stream = nullptr;  // device-to-host copies overlapping k_rows chunks
+  hipEvent_t xfer_ev[8] = {};
   bool packed_set = false;
   uint8_t* d_dwritten = nullptr;   // depth slot -> free blocks
   int16_t* d_dvarsize = nullptr;   // depth slot -> depth_to_image width

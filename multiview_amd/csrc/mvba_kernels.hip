@@ -633,17 +633,15 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
 }
 
 // Deterministic mode: out[e] = sum of entry e's slab positions in slab order
-// (CSR e -> positions), one wave per entry (lane-strided partial sums, then a
-// fixed butterfly), written to grad | hess | cost.
-__global__ void __launch_bounds__(256) k_slab_lin(int64_t n, const int64_t* __restrict__ begin,
+// (CSR e -> positions, slab_gather: a block per heavy entry, a wave per light
+// one), written to grad | hess | cost.
+__global__ void __launch_bounds__(256) k_slab_lin(SlabTiers tiers, const int64_t* __restrict__ begin,
                                                   const int64_t* __restrict__ pos, const double* __restrict__ val,
                                                   int64_t ng, int64_t nh, double* __restrict__ grad,
                                                   double* __restrict__ hess, double* __restrict__ cost) {
-  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (e >= n) return;
-  const double acc = slab_entry_sum(begin[e], begin[e + 1], pos, val);
-  if (lane != 0) return;
+  int64_t e;
+  double acc;
+  if (!slab_gather(tiers, begin, pos, val, &e, &acc)) return;
   if (e < ng) grad[e] = acc;
   else if (e < ng + nh) hess[e - ng] = acc;
   else if (cost) *cost = acc;
@@ -931,11 +929,12 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_slab_lin(int64_t n, const int64_t* begin, const int64_t* pos, const double* val, int64_t ng,
-                                int64_t nh, double* grad, double* hess, double* cost, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_slab_lin, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, n, begin, pos, val, ng, nh, grad,
-                     hess, cost);
+hipError_t mvba_launch_slab_lin(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
+                                const double* val, int64_t ng, int64_t nh, double* grad, double* hess, double* cost,
+                                hipStream_t s) {
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_slab_lin, dim3((unsigned)grid), dim3(256), 0, s, t, begin, pos, val, ng, nh, grad, hess,
+                     cost);
   return hipGetLastError();
 }
 

@@ -58,10 +58,10 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
                               hipStream_t s);
-hipError_t mvba_launch_slab_reduce_vec(int64_t ng, const int64_t* begin, const int64_t* pos, const double* val,
-                                       const double* diag, const double* x, double* y, double* partial,
-                                       unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
-                                       hipStream_t s);
+hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
+                                       const double* val, const double* diag, const double* x, double* y,
+                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
+                                       mvba::CgCtl* ctl, hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
                                       mvba::CgCtl* ctl, hipStream_t s);
@@ -206,7 +206,7 @@ SolverState* alloc_state(mvba_handle* h) {
     int64_t ncost = 0;
     for (const Group& G : h->groups) ncost = std::max<int64_t>(ncost, (G.seg_count + 3) / 4);
     // k_cg_update: 3 partials per 256-entry block; k_vec_rep_reduce / k_add_diag one
-    S->npartial = std::max<int64_t>({3072, 3 * ((S->ng + 255) / 256), (S->ng + 3) / 4, mvba_pass_a_blocks(S->np), ncost,
+    S->npartial = std::max<int64_t>({3072, 3 * ((S->ng + 255) / 256), S->ng + 1, mvba_pass_a_blocks(S->np), ncost,
                                     (int64_t)h->ndep_segs, (h->ndep_slots + 255) / 256});
     HCHK(dalloc(&S->partial, (size_t)S->npartial));
     HCHK(dalloc(&S->scal, 32));
@@ -371,7 +371,8 @@ class Solver {
     if (det && !D.ready) HCHK(det_plan_finish(D, s_));
     const bool fuse = xv && !o_.allreduce;
     if (det)
-      HCHK(mvba_launch_slab_reduce_vec(S_->ng, D.begin, D.pos, D.val, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr,
+      HCHK(mvba_launch_slab_reduce_vec(D.tier_view(), D.grid(), D.begin, D.pos, D.val,
+                                       fuse ? S_->dmp : nullptr, fuse ? xv : nullptr,
                                        y, S_->partial, S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate,
                                        fuse ? ctl : nullptr, s_));
     else

@@ -753,7 +753,7 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
 // Deterministic mode: y[e] = sum of entry e's slab positions in slab order (CSR
 // e -> positions; one wave per entry, lane-strided sums and a fixed butterfly),
 // then the same damping, x.y reduction and CG step length as k_vec_rep_reduce.
-__global__ void __launch_bounds__(256) k_vec_slab_reduce(int64_t n, const int64_t* __restrict__ begin,
+__global__ void __launch_bounds__(256) k_vec_slab_reduce(SlabTiers tiers, const int64_t* __restrict__ begin,
                                                          const int64_t* __restrict__ pos,
                                                          const double* __restrict__ val,
                                                          const double* __restrict__ diag,
@@ -762,12 +762,10 @@ __global__ void __launch_bounds__(256) k_vec_slab_reduce(int64_t n, const int64_
                                                          double* __restrict__ dot_out,
                                                          const int32_t* __restrict__ gate, CgCtl* __restrict__ ctl) {
   if (gate && *gate) return;
-  const int64_t e = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  double acc = 0.0;
-  if (e < n) acc = slab_entry_sum(begin[e], begin[e + 1], pos, val);
+  int64_t e;
+  double acc;
   double d = 0.0;
-  if (e < n && lane == 0) {
+  if (slab_gather(tiers, begin, pos, val, &e, &acc)) {
     if (diag) acc += diag[e] * x[e];
     y[e] = acc;
     d = x ? x[e] * acc : 0.0;
@@ -1301,13 +1299,13 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
 }
 
 // y = sum of replicas (+ diag .* x, and x.y -> dot_out when dot_out != null)
-hipError_t mvba_launch_slab_reduce_vec(int64_t ng, const int64_t* begin, const int64_t* pos, const double* val,
-                                       const double* diag, const double* x, double* y, double* partial,
-                                       unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
-                                       hipStream_t s) {
-  if (ng <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_vec_slab_reduce, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, ng, begin, pos, val,
-                     diag, x, y, partial, counter, dot_out, gate, ctl);
+hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
+                                       const double* val, const double* diag, const double* x, double* y,
+                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
+                                       mvba::CgCtl* ctl, hipStream_t s) {
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_vec_slab_reduce, dim3((unsigned)grid), dim3(256), 0, s, t, begin, pos, val, diag, x, y,
+                     partial, counter, dot_out, gate, ctl);
   return hipGetLastError();
 }
 

@@ -118,7 +118,11 @@ static double cauchy_c_of(int32_t flags, double thr) { return (flags & MVBA_EVAL
 
 // Evaluate on the device and rewrite the planes as rows (full layout when
 // packed == false). Leaves d_tres / d_tcost / d_trows filled, stream synced.
-static mvba_status eval_rows(mvba_handle* h, int32_t flags, double thr, bool want_jac, bool packed, bool want_cost) {
+// pinned_dst (packed layout only): the rows are produced in slot-range chunks
+// and each chunk's rows (contiguous: device order) are copied to pinned_dst on
+// a second stream while the next chunk is transposed; then the copy is done too.
+static mvba_status eval_rows(mvba_handle* h, int32_t flags, double thr, bool want_jac, bool packed, bool want_cost,
+                             double* pinned_dst = nullptr) {
   const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
   if (loss && !(thr > 0.0)) return h->fail(MVBA_E_INVALID, "The robust threshold must be positive.");
   const int32_t dflags = MVBA_EVAL_RESIDUALS | (want_jac ? MVBA_EVAL_JACOBIAN : 0);
@@ -138,12 +142,40 @@ static mvba_status eval_rows(mvba_handle* h, int32_t flags, double thr, bool wan
     }
   }
   const mvba_rows_layout L = cam_layout(h);
-  hipError_t e = mvba_launch_rows(h->d_res, want_jac ? h->d_J : nullptr, h->ld, h->nslots, &L, cauchy_c_of(flags, thr),
-                                  h->d_order, h->d_row_written, h->d_varsize, packed ? h->d_xmask : nullptr,
-                                  packed ? h->d_xoff : nullptr, h->d_tres, want_cost ? h->d_tcost : nullptr,
-                                  want_jac ? h->d_trows : nullptr, nullptr);
+  const bool pipe = pinned_dst && packed && want_jac;
+  constexpr int kChunks = 8;
+  hipError_t e = hipSuccess;
+  if (pipe && !h->xfer_stream) {
+    e = hipStreamCreateWithFlags(&h->xfer_stream, hipStreamNonBlocking);
+    for (int c = 0; c < kChunks && e == hipSuccess; c++)
+      e = hipEventCreateWithFlags(&h->xfer_ev[c], hipEventDisableTiming);
+    if (e != hipSuccess) return h->hip_fail(e, "creating the copy stream");
+  }
+  const int nch = pipe ? kChunks : 1;
+  // chunk boundaries on 64-slot tiles (every k_rows tile size divides 64)
+  const int64_t step = (h->nslots + 64 * nch - 1) / (64 * nch) * 64;
+  for (int c = 0; c < nch && e == hipSuccess; c++) {
+    const int64_t a0 = std::min<int64_t>(h->nslots, c * step), a1 = (c == nch - 1) ? h->nslots
+                                                                                   : std::min<int64_t>(h->nslots, (c + 1) * step);
+    e = mvba_launch_rows(h->d_res, want_jac ? h->d_J : nullptr, h->ld, a0, a1, &L, cauchy_c_of(flags, thr), h->d_order,
+                         h->d_row_written, h->d_varsize, packed ? h->d_xmask : nullptr, packed ? h->d_xoff : nullptr,
+                         h->d_tres, want_cost ? h->d_tcost : nullptr, want_jac ? h->d_trows : nullptr, nullptr);
+    if (pipe && e == hipSuccess) {
+      const int64_t r0 = h->slot_rows[(size_t)a0], r1 = h->slot_rows[(size_t)a1];
+      e = hipEventRecord(h->xfer_ev[c], nullptr);
+      if (e == hipSuccess) e = hipStreamWaitEvent(h->xfer_stream, h->xfer_ev[c], 0);
+      if (e == hipSuccess && r1 > r0)
+        e = hipMemcpyAsync(pinned_dst + r0, h->d_trows + r0, (size_t)(r1 - r0) * sizeof(double),
+                           hipMemcpyDeviceToHost, h->xfer_stream);
+    }
+  }
   if (e != hipSuccess) return h->hip_fail(e, "mvba_launch_rows");
-  return mvba_sync_status(h, nullptr);
+  st = mvba_sync_status(h, nullptr);
+  if (pipe) {
+    e = hipStreamSynchronize(h->xfer_stream);
+    if (e != hipSuccess) return h->hip_fail(e, "packed Jacobian copy");
+  }
+  return st;
 }
 
 // cost = sum over blocks in AddResidualBlock order (Problem::Evaluate, one thread).
@@ -216,22 +248,31 @@ mvba_status mvba_set_transfer_blocks(mvba_handle* h, const uint8_t* transfer, in
     }
     rmask[(size_t)i] = (uint8_t)m;
   }
+  // Rows are laid out in the device's slot order (frame by frame), so each wave
+  // of k_rows writes one contiguous range: whole 128-B lines instead of rows
+  // scattered in insertion order (a line shared by two rows written by two
+  // waves at different times costs HBM a read-modify-write). offsets[i] still
+  // locates residual i's row; offsets[N] is the total.
   h->xoffsets.assign((size_t)N + 1, 0);
-  for (int64_t i = 0; i < N; i++) {
+  std::vector<uint8_t> xm((size_t)S, 0);
+  std::vector<int64_t> xo((size_t)S, 0);
+  int64_t at = 0;
+  h->slot_rows.assign((size_t)S + 1, 0);
+  for (int64_t p = 0; p < S; p++) {
+    h->slot_rows[(size_t)p] = at;
+    const int64_t i = h->order[(size_t)p];
+    if (i < 0) continue;
     const int K = h->frame_kdist[(size_t)h->res_frame[(size_t)i]];
     int64_t n = 0;
     for (int b = 0; b < 8; b++)
       if ((rmask[(size_t)i] >> b) & 1) n += 2 * (b < 7 ? kFixedSize[b] : K);
-    h->xoffsets[(size_t)i + 1] = h->xoffsets[(size_t)i] + n;
-  }
-  std::vector<uint8_t> xm((size_t)S, 0);
-  std::vector<int64_t> xo((size_t)S, 0);
-  for (int64_t p = 0; p < S; p++) {
-    const int64_t i = h->order[(size_t)p];
-    if (i < 0) continue;
     xm[(size_t)p] = rmask[(size_t)i];
-    xo[(size_t)p] = h->xoffsets[(size_t)i];
+    xo[(size_t)p] = at;
+    h->xoffsets[(size_t)i] = at;
+    at += n;
   }
+  h->xoffsets[(size_t)N] = at;
+  h->slot_rows[(size_t)S] = at;
   hipError_t e = hipSuccess;
   if (!h->d_xmask) e = dalloc(&h->d_xmask, (size_t)S);
   if (e == hipSuccess && !h->d_xoff) e = dalloc(&h->d_xoff, (size_t)S);
@@ -253,14 +294,16 @@ mvba_status mvba_evaluate_packed(mvba_handle* h, int32_t flags, double cauchy_th
   mvba_status st;
   if (!h->packed_set && (st = mvba_set_transfer_blocks(h, nullptr, nullptr)) != MVBA_OK) return st;
   const bool want_jac = packed != nullptr && (flags & MVBA_EVAL_JACOBIAN);
-  st = eval_rows(h, flags, cauchy_threshold, want_jac, true, cost != nullptr);
-  if (st != MVBA_OK) return st;
   const int64_t N = h->nres;
+  const size_t jbytes = (size_t)h->xoffsets[(size_t)N] * sizeof(double);
+  const bool pinned = want_jac && registered_pinned(packed, std::max<size_t>(jbytes, 1));
+  st = eval_rows(h, flags, cauchy_threshold, want_jac, true, cost != nullptr, pinned ? packed : nullptr);
+  if (st != MVBA_OK) return st;
   if (residuals &&
       (st = copy_to_host(h, residuals, h->d_tres, (size_t)(2 * N) * sizeof(double), "residual copy")) != MVBA_OK)
     return st;
-  if (want_jac && (st = copy_to_host(h, packed, h->d_trows, (size_t)h->xoffsets[(size_t)N] * sizeof(double),
-                                     "packed Jacobian copy")) != MVBA_OK)
+  if (want_jac && !pinned &&
+      (st = copy_to_host(h, packed, h->d_trows, jbytes, "packed Jacobian copy")) != MVBA_OK)
     return st;
   if (cost) return fetch_cost(h, h->d_tcost, N, cost);
   return MVBA_OK;
@@ -322,7 +365,7 @@ mvba_status mvba_evaluate_depth(mvba_handle* h, int32_t flags, double cauchy_thr
     L.base[b] = b < 7 ? base[b] : MVBA_DJAC_ROWS;
     L.size[b] = b < 7 ? size[b] : 0;
   }
-  e = mvba_launch_rows(h->d_dres, want_jac ? h->d_dJ : nullptr, h->dld, S, &L, cauchy_c_of(flags, cauchy_threshold),
+  e = mvba_launch_rows(h->d_dres, want_jac ? h->d_dJ : nullptr, h->dld, 0, S, &L, cauchy_c_of(flags, cauchy_threshold),
                        h->d_dep_order, h->d_dwritten, h->d_dvarsize, nullptr, nullptr, h->d_tdres,
                        cost ? h->d_tdcost : nullptr, want_jac ? h->d_tdrows : nullptr, nullptr);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_launch_rows (depth)");

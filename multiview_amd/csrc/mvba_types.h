@@ -86,6 +86,16 @@ inline int64_t lin_slab_width(int kmax) {
 // Solver pass B producers (chunk or depth segment): one position per lane of
 // the final scatter: 22 pose columns, then focal, centre (2), distortion (K);
 // depth segments: depth_to_image (12) at 22, scale at 34.
+// Gather tiers by producer count (slab_gather): <= kSlabLight one thread,
+// <= kSlabMedium one wave, more one block.
+constexpr int kSlabLight = 16;
+constexpr int kSlabMedium = 512;
+struct SlabTiers {
+  const int64_t* heavy;
+  const int64_t* medium;
+  const int64_t* light;
+  int64_t nheavy, nmedium, nlight;
+};
 inline int64_t vec_slab_width(int kmax) { return 25 + kmax > 35 ? 25 + kmax : 35; }
 
 // Per-frame record of the linearization (K2 expand); mirrors mvba::FrameLin in

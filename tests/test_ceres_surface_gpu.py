@@ -28,6 +28,12 @@ def _read(fh, dtype):
 def test_ceres_adapter(tmp_path, oracle):
     if not os.path.exists(BIN):
         subprocess.run(["make", "-s", "-C", os.path.dirname(BIN)], check=True)
+    run_adapter_case(BIN, tmp_path, oracle)
+
+
+def run_adapter_case(binary, tmp_path, oracle, env=None):
+    """Drive the adapter binary on a dumped problem and check every case;
+    returns the binary's stderr (the sanitizer build checks it is clean)."""
     R = rig.make_rig(num_sensors=3, num_ref=12, num_points=150, obs_per_point=5,
                      models=["radtan", "rpc1", "fov"], seed=31, depth_sensors=(2,), affine_depth=False)
     F = rig.FloatFlags(depth_tri_weight=10.0, depth_to_image_transforms_to_float=("cam2",), float_scale=True,
@@ -57,7 +63,8 @@ def test_ceres_adapter(tmp_path, oracle):
         _write(fh, P.xyz_ref, np.float64)
         _write(fh, P.xyz_weight, np.float64)
     out = tmp_path / "out.bin"
-    subprocess.run([BIN, str(src), str(out)], check=True, timeout=120)
+    p = subprocess.run([binary, str(src), str(out)], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-4000:]
     n = P.num_residuals
     stride = P.jacobian_stride()
     with open(out, "rb") as fh:
@@ -125,3 +132,4 @@ def test_ceres_adapter(tmp_path, oracle):
     w = P.xyz_weight[:, None]
     assert np.allclose(RX.reshape(-1, 3), w * (X - P.xyz_ref), rtol=0, atol=1e-12)
     assert np.allclose(JX.reshape(-1, 3, 3), P.xyz_weight[:, None, None] * np.eye(3), rtol=0, atol=0)
+    return p.stderr

@@ -54,16 +54,19 @@ def _planes_to_rows(ev, P, loss, thr=3.0):
     return R * sr[:, None], JJ * sr[:, None]
 
 
-def _pack(P, J, transfer):
-    """Packed rows from full rows, per mvba_set_transfer_blocks' layout."""
+def _pack(P, J, transfer, off):
+    """Packed rows from full rows, per mvba_set_transfer_blocks' layout: residual
+    i's transferred blocks in block order at off[i] (rows in device order)."""
     K = P.camera_dist_size[P.residual_camera]
-    out = []
+    out = np.full(int(off[-1]), np.nan)
     for i in range(P.num_residuals):
-        for b in range(8):
-            if transfer[P.residual_blocks[i, b]]:
-                w = 2 * (K[i] if b == 7 else _lib.FIXED_BLOCK_SIZES[b])
-                out.append(J[i, JAC_BASE[b]:JAC_BASE[b] + w])
-    return np.concatenate(out) if out else np.zeros(0)
+        row = [J[i, JAC_BASE[b]:JAC_BASE[b] + 2 * (K[i] if b == 7 else _lib.FIXED_BLOCK_SIZES[b])]
+               for b in range(8) if transfer[P.residual_blocks[i, b]]]
+        if row:
+            row = np.concatenate(row)
+            out[off[i]:off[i] + row.size] = row
+    assert not np.isnan(out).any()  # the rows tile the packed buffer
+    return out
 
 
 @pytest.fixture(scope="module")
@@ -103,8 +106,7 @@ def test_packed_rows(problem, pattern):
         r_ref, J_ref = _planes_to_rows(ev, P, True)
         off = ev.set_transfer_blocks(transfer)
         t = (1 - P.block_constant).astype(np.uint8) if transfer is None else transfer
-        expect = _pack(P, J_ref, t)
-        assert off[-1] == expect.size
+        expect = _pack(P, J_ref, t, off)
         with PinnedBuffer(max(expect.size, 1)) as buf:
             _, r, Jp = ev.evaluate_packed(jacobian=True, apply_loss=True, out=buf.array)
             assert np.array_equal(r, r_ref)
@@ -132,4 +134,5 @@ def test_large_copy_through_staging():
             off = ev.set_transfer_blocks(np.ones(len(P.block_size), np.uint8))
             _, r2, Jp = ev.evaluate_packed(jacobian=True, out=buf.array)
             assert off[-1] == J_ref.size  # one distortion size everywhere: packed == full rows
-            assert np.array_equal(Jp, J_ref.reshape(-1))
+            rows = Jp[off[:-1, None] + np.arange(ev.stride)[None, :]]
+            assert np.array_equal(rows, J_ref)
