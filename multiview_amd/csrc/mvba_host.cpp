@@ -33,7 +33,7 @@ static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
-                  h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_frame_lin,
+                  h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
@@ -663,6 +663,13 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(dalloc(&h->d_err, 1));
   if (e == hipSuccess) chk(hipMemset(h->d_err, 0, sizeof(int)));
   chk(upload(&h->d_chunks, chunks));
+  {
+    // one-segment chunks: the solver's frame-order pass A takes one segment per
+    // wave (it writes per-observation records, nothing per frame to reduce)
+    std::vector<int4> sc(segs.size());
+    for (size_t k = 0; k < segs.size(); k++) sc[k] = make_int4((int32_t)k, 1, segs[k].frame, 0);
+    chk(upload(&h->d_segchunks, sc));
+  }
   {
     void* p = nullptr;
     chk(hipMalloc(&p, std::max<size_t>(flin.size(), 1) * sizeof(mvba::FrameLinHost)));

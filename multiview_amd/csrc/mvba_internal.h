@@ -314,6 +314,7 @@ struct mvba_handle {
   std::vector<int64_t> cam_goff, cam_hoff;
   std::vector<int32_t> pt_block_ids;    // point index -> block id
   int4* d_chunks = nullptr;
+  int4* d_segchunks = nullptr;          // one chunk per segment (seg, 1, frame, -)
   void* d_frame_lin = nullptr;
   int4* d_parts = nullptr;              // K2 frame parts (seg_begin, seg_count, frame, -)
   double* d_rep = nullptr;  // nrep copies of [cam_grad | cam_hess | cost], kept zero between calls

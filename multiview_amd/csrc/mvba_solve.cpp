@@ -19,6 +19,7 @@
 #include <chrono>
 #include <complex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -42,7 +43,9 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                                     const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
                                     const double2* obs_meas, const int32_t* slot_po, const double* dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
-                                    const double* prec, hipStream_t s);
+                                    const double* prec, const double4* obsX, hipStream_t s);
+hipError_t mvba_launch_gather_obs_pts(int64_t nslots, const int32_t* obs_pid, const double4* pts, double4* out,
+                                      hipStream_t s);
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
                                const double* tinit, const double* V, const double* dp, const double4* pts,
                                double* wout, int32_t wstride, const int32_t* gate, hipStream_t s);
@@ -57,7 +60,7 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
-                              hipStream_t s);
+                              const double4* obsX, hipStream_t s);
 hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
                                        const double* val, const double* diag, const double* x, double* y,
                                        double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
@@ -125,6 +128,7 @@ struct SolverState {
   double* zbuf = nullptr;     // [8 N] point-order z_o | J_pt rows
   double* wbuf = nullptr;     // [4 np] w_p of the last pass A (double4 per point)
   double* cbuf = nullptr;     // [4 slots] frame-order pass A: J_pt^T z per slot
+  double* obsX = nullptr;     // [4 slots] landmark of each slot (fixed during a linear solve)
   double* du = nullptr;       // [3 depth slots] u_d of the depth blocks (pass A -> k_depth_sb)
   double* partial = nullptr;  // [npartial]
   double* scal = nullptr;     // [32] device scalars
@@ -144,7 +148,7 @@ struct SolverState {
 void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
-                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->du,
+                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du,
                   S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -200,6 +204,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
     HCHK(dalloc(&S->wbuf, (size_t)(4 * std::max<int64_t>(S->np, 1))));
     HCHK(dalloc(&S->cbuf, (size_t)(4 * std::max<int64_t>(N, 1))));
+    HCHK(dalloc(&S->obsX, (size_t)(4 * std::max<int64_t>(h->nslots, 1))));
     HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
     HCHK(dalloc(&S->cnt, 8));
     HCHK(hipMemset(S->cnt, 0, 8 * sizeof(unsigned)));
@@ -260,6 +265,12 @@ class Solver {
   int last_cg_iters_ = 0;  // CG iterations of the previous linear solve (batch sizing only)
 
   int pa_model() const { return single_model_ ? h_->groups[0].model : -1; }
+  // per-slot landmark copy for the frame-order passes (MVBA_NO_OBSX=1: gather
+  // through obs_pid as before, for A/B timing)
+  const double4* obsx() const {
+    static const bool off = std::getenv("MVBA_NO_OBSX") && std::getenv("MVBA_NO_OBSX")[0] == '1';
+    return off ? nullptr : (const double4*)S_->obsX;
+  }
   int pa_deg() const { return single_model_ ? h_->groups[0].deg : 0; }
 
   // Cross-rank sum / max of a device buffer, stream-ordered (mvba_allreduce_fn:
@@ -363,7 +374,7 @@ class Solver {
       HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
                               h_->d_segs, h_->d_fd, h_->d_frame_lin, h_->d_frec, h_->d_params, h_->d_pts,
                               h_->d_obs_pid, h_->d_obs_meas, dir, (const double4*)S_->wbuf, S_->yrep, S_->ng, flags_,
-                              cauchy_c_, gate, det ? D.slab(0) : no_slab(), s_));
+                              cauchy_c_, gate, det ? D.slab(0) : no_slab(), obsx(), s_));
     if (h_->ndep > 0)
       HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
                                 h_->d_params, h_->d_pts, h_->d_frame_lin, S_->du, S_->yrep, S_->ng, flags_, cauchy_c_,
@@ -395,11 +406,15 @@ class Solver {
                               S_->dmp + S_->ng, S_->zbuf, S_->wbuf, 4, nullptr, nullptr, nullptr, flags_, cauchy_c_,
                               h_->point_extra(), xv, S_->du, gate, S_->prec, s_));
     else {
+      // one segment per wave (MVBA_PASS_A_CHUNKS=1: the 4-segment solver chunks, for A/B timing)
+      static const bool chunked = std::getenv("MVBA_PASS_A_CHUNKS") && std::getenv("MVBA_PASS_A_CHUNKS")[0] == '1';
       if (dir)
         for (const Group& G : h_->groups)
-          HCHK(mvba_launch_pass_a_frame(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, h_->d_segs,
+          HCHK(mvba_launch_pass_a_frame(G.model, G.deg,
+                                        chunked ? h_->d_chunks + G.chunk_begin : h_->d_segchunks + G.seg_begin,
+                                        chunked ? G.chunk_count : G.seg_count, h_->d_segs,
                                         h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dir, (double4*)S_->cbuf, flags_,
-                                        cauchy_c_, gate, S_->prec, s_));
+                                        cauchy_c_, gate, S_->prec, obsx(), s_));
       HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, h_->d_po_slot, dir ? (const double4*)S_->cbuf : nullptr,
                                tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate, s_));
     }
@@ -419,6 +434,7 @@ class Solver {
   // records for pass A are built here (parameters fixed until the next step).
   void schur_rhs() {
     HCHK(mvba_launch_frame_proj((int32_t)h_->nframes, h_->d_fd, h_->d_frec, h_->d_params, S_->prec, s_));
+    HCHK(mvba_launch_gather_obs_pts(h_->nslots, h_->d_obs_pid, h_->d_pts, (double4*)S_->obsX, s_));
     pass_a_w(nullptr, S_->G + S_->ng, nullptr, nullptr);
     reduce_frames(S_->tmp, nullptr, 0, nullptr);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));

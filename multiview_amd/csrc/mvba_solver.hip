@@ -403,15 +403,19 @@ __global__ void __launch_bounds__(256) k_pass_a(
 // loads instead of per-lane gathers) and stores c_o = J_pt^T z_o per slot;
 // k_point_w sums each point's c_o in point order, adds tinit and solves
 // (V + D) w = t. Slot-order stores are coalesced; the point kernel gathers.
+// One wave per chunk, kPassAWaves waves per block (the solver passes it one
+// segment per chunk: nothing is reduced per frame here, and 4x the waves of
+// the 4-segment chunks hide the point gathers better).
+constexpr int kPassAWaves = 4;
 template <int MODEL, int DEG>
-__global__ void __launch_bounds__(64) k_pass_a_frame(
+__global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
     const int4* __restrict__ chunks, int32_t nchunks, const Segment* __restrict__ segs,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
     const int32_t* __restrict__ slot_po, const double* __restrict__ dir, double4* __restrict__ cbuf, int32_t flags,
     double cauchy_c,
-    const int32_t* __restrict__ gate, const double* __restrict__ prec) {
-  const int lane = threadIdx.x;
-  const int ch = blockIdx.x;
+    const int32_t* __restrict__ gate, const double* __restrict__ prec, const double4* __restrict__ obsX) {
+  const int lane = threadIdx.x & 63;
+  const int ch = blockIdx.x * kPassAWaves + (threadIdx.x >> 6);
   if (ch >= nchunks || (gate && *gate)) return;
   const int4 c = chunks[ch];
   const int frame = __builtin_amdgcn_readfirstlane(c.z);
@@ -423,13 +427,22 @@ __global__ void __launch_bounds__(64) k_pass_a_frame(
     if (lane < count) {
       const int64_t i = (int64_t)sg.begin + lane;
       double z[2], P0[3], P1[3];
-      pass_a_obs<MODEL, DEG>(rec, d, pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
+      pass_a_obs<MODEL, DEG>(rec, d, obsX ? obsX[i] : pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
       // plain store: a nontemporal store of these scattered 32-B records
       // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM)
       cbuf[slot_po[i]] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
                                       P0[2] * z[0] + P1[2] * z[1], 0.0);
     }
   }
+}
+
+// Landmark of every observation slot, in slot order: the points are fixed for
+// a whole linear solve, so the frame-order passes read them coalesced instead
+// of gathering pts[obs_pid[i]] behind the index load every CG iteration.
+__global__ void k_gather_obs_pts(int64_t nslots, const int32_t* __restrict__ obs_pid,
+                                 const double4* __restrict__ pts, double4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nslots) out[i] = pts[obs_pid[i]];
 }
 
 // w_p = (V + D)^-1 (tinit + sum_o c_o), kLanesW lanes per point gathering its
@@ -491,7 +504,8 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
                                             const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
                                             const double2* __restrict__ obs_meas, const double* __restrict__ dir,
                                             const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng,
-                                            int32_t flags, double cauchy_c, const Slab& sl) {
+                                            int32_t flags, double cauchy_c, const Slab& sl,
+                                            const double4* __restrict__ obsX) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   extern __shared__ double st[];  // [NA + 1][kWideLd]: columns, then u
@@ -513,7 +527,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
         if (lane < count) {
           const int64_t i = (int64_t)sg.begin + lane;
           const int32_t pid = obs_pid[i];
-          const double4 X = pts[pid];
+          const double4 X = obsX ? obsX[i] : pts[pid];
           const double2 m = obs_meas[i];
           Proj o;
           project<MODEL, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
@@ -613,7 +627,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
     const double2* __restrict__ obs_meas, const double* __restrict__ dir,
     const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c,
-    const int32_t* __restrict__ gate, Slab sl) {
+    const int32_t* __restrict__ gate, Slab sl, const double4* __restrict__ obsX) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   const int lane = threadIdx.x;
@@ -621,7 +635,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
   if (ch >= nchunks || (gate && *gate)) return;
   if constexpr (NA > kPassBRegCols) {
     pass_b_wide<MODEL, DEG>(chunks[ch], chunk_base + ch, segs, fd, fl, frec, params, pts, obs_pid, obs_meas, dir,
-                            wbuf, yrep, ng, flags, cauchy_c, sl);
+                            wbuf, yrep, ng, flags, cauchy_c, sl, obsX);
     return;
   } else {
   const int4 c = chunks[ch];
@@ -638,7 +652,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     if (lane < count) {
       const int64_t i = (int64_t)sg.begin + lane;
       const int32_t pid = obs_pid[i];
-      const double4 X = pts[pid];
+      const double4 X = obsX ? obsX[i] : pts[pid];
       double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], P0[3], P1[3], r[2], hr;
 #pragma unroll
       for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;
@@ -1250,13 +1264,22 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                                     const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
                                     const double2* obs_meas, const int32_t* slot_po, const double* dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
-                                    const double* prec, hipStream_t s) {
+                                    const double* prec, const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PAF(M, D)                                                                                      \
-  hipLaunchKernelGGL((mvba::k_pass_a_frame<M, D>), dim3((unsigned)nchunks), dim3(64), 0, s, chunks, nchunks, \
-                     segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec)
+  hipLaunchKernelGGL((mvba::k_pass_a_frame<M, D>), dim3((unsigned)((nchunks + mvba::kPassAWaves - 1) /        \
+                     mvba::kPassAWaves)), dim3(64 * mvba::kPassAWaves), 0, s, chunks, nchunks,                 \
+                     segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec, obsX)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PAF)
 #undef MVBA_PAF
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_gather_obs_pts(int64_t nslots, const int32_t* obs_pid, const double4* pts, double4* out,
+                                      hipStream_t s) {
+  if (nslots <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_gather_obs_pts, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s, nslots, obs_pid,
+                     pts, out);
   return hipGetLastError();
 }
 
@@ -1286,13 +1309,13 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
-                              hipStream_t s) {
+                              const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PB(M, D)                                                                                       \
   hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), (mvba::pass_b_lds<M, D>()), s,\
                      chunks, nchunks,                                                                         \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
-                     dir, wbuf, yrep, ng, flags, cauchy_c, gate, sl)
+                     dir, wbuf, yrep, ng, flags, cauchy_c, gate, sl, obsX)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)
 #undef MVBA_PB
   return hipGetLastError();
