@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MVBA_ABI_VERSION 4
+#define MVBA_ABI_VERSION 5
 
 /* Status codes. Non-zero codes mirror the reference's fatal checks. */
 typedef enum mvba_status {
@@ -63,7 +63,8 @@ typedef enum mvba_status {
   MVBA_E_INVALID = 5,
   /* No usable GPU (the product path has no CPU fallback). */
   MVBA_E_NO_DEVICE = 6,
-  /* "BracketedDepthError: The block sizes were not set up properly." rig_calibrator.cc:534-543 */
+  /* "BracketedDepthError: The block sizes were not set up properly." rig_calibrator.cc:534-543
+   * (or "BracketedDepthMeshError: ..." rig_calibrator.cc:630-638 for a mesh block) */
   MVBA_E_DEPTH_BLOCK_SIZES = 7,
   /* "XYZError: The block sizes were not set up properly." rig_calibrator.cc:714-715 */
   MVBA_E_XYZ_BLOCK_SIZES = 8
@@ -127,7 +128,12 @@ typedef struct mvba_problem_desc {
    * these fields when there are none. */
   int64_t num_depth_residuals;
   const int32_t* depth_blocks;   /* [7*n] beg, end, ref_to_cam, depth_to_image (7 rigid | 12 affine),
-                                    scale (1), xyz (3), offset (1): MVBA_DBLK_* order */
+                                    scale (1), xyz (3), offset (1): MVBA_DBLK_* order.
+                                    xyz = -1 marks a BracketedDepthMeshError block
+                                    (rig_calibrator.cc:615-705, added by :1796-1834 with
+                                    --mesh and --depth_mesh_weight): r = weight *
+                                    (mesh_xyz - M), mesh_xyz from depth_mesh_xyz. Both
+                                    kinds share this list in AddResidualBlock order. */
   const double* depth_meas;      /* [3*n] meas_depth_xyz (depth-cloud point) */
   const double* depth_weight;    /* [n] weight (FLAGS_depth_tri_weight) */
   const double* depth_stamps;    /* [3*n] left_ref, right_ref, cam stamp */
@@ -141,6 +147,15 @@ typedef struct mvba_problem_desc {
   const double* xyz_ref;         /* [3*n] reference xyz */
   const double* xyz_weight;      /* [n] weight */
   const double* xyz_threshold;   /* [n] Cauchy threshold used with MVBA_EVAL_APPLY_LOSS (> 0) */
+
+  /* ABI 5. [3*num_depth_residuals], nullable when no depth block has xyz = -1:
+   * the fixed mesh point of each BracketedDepthMeshError block (rows of other
+   * blocks are ignored). */
+  const double* depth_mesh_xyz;
+  /* ABI 5. [num_xyz_residuals], nullable (all 0): 0 = "tri" prior (--tri_weight,
+   * :1880-1898), 1 = "mesh_tri" prior (--mesh_tri_weight, :1857-1877). Only the
+   * residual statistics' grouping reads it. */
+  const uint8_t* xyz_kind;
 } mvba_problem_desc;
 
 /* Depth block order (BracketedDepthError) and its Jacobian layout: rows
@@ -298,7 +313,8 @@ mvba_status mvba_lin_layout_info(const struct mvba_handle* h, mvba_lin_layout* o
 /* [num_cam_blocks] each, nullable */
 mvba_status mvba_cam_block_map(const struct mvba_handle* h, int32_t* block_ids, int64_t* goff,
                                int64_t* hoff);
-/* [num_points]: parameter block id of point index p */
+/* [num_points]: parameter block id of point index p; -1 for the fixed point of
+ * a BracketedDepthMeshError block (constant: zero gradient and Hessian) */
 mvba_status mvba_point_block_map(const struct mvba_handle* h, int32_t* block_ids);
 /* flags: MVBA_EVAL_APPLY_LOSS, MVBA_EVAL_SKIP_PREP, and for timing the two
  * sides separately MVBA_LIN_CAMERA_ONLY (camera-side gradient, block Hessians
@@ -389,16 +405,58 @@ mvba_status mvba_frame_poses(struct mvba_handle* h, double* out, int32_t* frame_
 /* Message of the last failed mvba_triangulate / mvba_flag_outliers on this thread. */
 const char* mvba_tracks_error(void);
 
+/* ---- Mesh constraints (--mesh) ----------------------
+ * The reference loads a PLY mesh and builds rayint's BVH over it
+ * (loadMeshBuildTree, texture_processing.cc:264-285), then per pass intersects
+ * every inlier feature's ray with it (meshTriangulations,
+ * texture_processing.cc:1566-1625 -> ray_mesh_intersect, :1436-1479): the ray
+ * leaves the camera centre through the undistorted pixel, in float (rayint's
+ * Ray: origin, unit dir, tmin = --min_ray_dist, tmax = --max_ray_dist), and the
+ * closest hit t gives intersection = cam_ctr + t * world_ray (double). Each
+ * track's mesh point is the mean of its features' hits; features that are
+ * outliers or miss keep `bad` = (1e100, 1e100, 1e100) (:1546), as do tracks
+ * without any hit. Those feed BracketedDepthMeshError blocks and "mesh_tri"
+ * XYZError priors.
+ * Here the BVH is built on the host once per mesh (median splits, leaves of <= 4
+ * triangles, depth <= 31) and traversed on the GPU, one lane per ray. */
+typedef struct mvba_mesh_desc {
+  int64_t num_vertices;
+  const float* vertices;   /* [3*num_vertices] x y z (mve's Vec3f) */
+  int64_t num_faces;
+  const uint32_t* faces;   /* [3*num_faces] vertex indices */
+} mvba_mesh_desc;
+struct mvba_mesh;
+mvba_status mvba_mesh_create(const mvba_mesh_desc* d, int32_t device, struct mvba_mesh** out);
+void mvba_mesh_destroy(struct mvba_mesh* m);
+/* BVH size (nodes) and depth, for reporting. */
+mvba_status mvba_mesh_info(const struct mvba_mesh* m, int64_t* num_nodes, int32_t* depth);
+/* Closest hit of n rays (device buffers, float, rayint's Ray): orig/dir [3n]
+ * (dir unit length), hit parameter t_out [n] (-1 = no hit in [tmin, tmax]) and
+ * face_out [n] (-1 = none; ties in t go to the lower face index). Asynchronous
+ * on hip_stream. */
+mvba_status mvba_mesh_intersect_device(struct mvba_mesh* m, int64_t n, const float* d_orig, const float* d_dir,
+                                       float tmin, float tmax, float* d_t, int32_t* d_face, void* hip_stream);
+/* meshTriangulations over a tracks description (same rules as mvba_triangulate):
+ * inlier [num_obs] in; feature_xyz [3*num_obs] out (nullable); point_xyz
+ * [3*num_points] out. Synchronous. */
+mvba_status mvba_mesh_triangulate(const mvba_tracks_desc* d, struct mvba_mesh* m, const uint8_t* inlier,
+                                  double min_ray_dist, double max_ray_dist, double* feature_xyz,
+                                  double* point_xyz);
+/* Message of the last failed mvba_mesh_* call on this thread. */
+const char* mvba_mesh_error(void);
+
 /* ---- Residual statistics (evalResiduals + calc_residuals_stats,
  * rig_calibrator.cc:1157-1180, :753-789) ------------------------------------
  * Raw residuals (no loss) divided by their scale (1 for pixels, the depth weight
  * for depth blocks), |r| grouped by residual name, and per group the values at
  * sorted positions int(0.25 len), int(0.5 len), int(0.75 len), len-1.
- * Groups (num_cameras*2 + 6): 2c + k = camera c, pixel component k
+ * Groups (num_cameras*2 + 12): 2c + k = camera c, pixel component k
  * ("<sensor>_pix_x", "<sensor>_pix_y"); 2*num_cameras + k = depth component k
  * ("depth_tri_{x,y,z}_m"); 2*num_cameras + 3 + k = XYZ prior component k
- * ("tri_{x,y,z}_m", scale = its weight). out [4*groups] (NaN for empty groups),
- * counts [groups].
+ * ("tri_{x,y,z}_m", scale = its weight); 2*num_cameras + 6 + k = mesh depth
+ * block component k ("depth_mesh_{x,y,z}_m"); 2*num_cameras + 9 + k =
+ * mesh_tri prior component k ("mesh_tri_{x,y,z}_m"). out [4*groups] (NaN for
+ * empty groups), counts [groups].
  * Synchronous. */
 mvba_status mvba_residual_stats(struct mvba_handle* h, double* out, int64_t* counts, void* hip_stream);
 

@@ -74,6 +74,8 @@ class ProblemDesc(C.Structure):
         ("xyz_ref", C.c_void_p),
         ("xyz_weight", C.c_void_p),
         ("xyz_threshold", C.c_void_p),
+        ("depth_mesh_xyz", C.c_void_p),   # ABI 5: BracketedDepthMeshError targets (depth xyz block -1)
+        ("xyz_kind", C.c_void_p),         # ABI 5: 0 tri prior, 1 mesh_tri prior (statistics groups)
     ]
 
 
@@ -184,6 +186,15 @@ class TracksDesc(C.Structure):
     ]
 
 
+class MeshDesc(C.Structure):
+    _fields_ = [
+        ("num_vertices", C.c_int64),
+        ("vertices", C.c_void_p),
+        ("num_faces", C.c_int64),
+        ("faces", C.c_void_p),
+    ]
+
+
 RPC_FIT_DISTORTION = 0
 RPC_FIT_UNDISTORTION = 1
 
@@ -262,6 +273,14 @@ SIGNATURES = {
                                      C.c_double, C.c_void_p, C.c_void_p]),
     "mvba_frame_poses": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_tracks_error": (C.c_char_p, []),
+    "mvba_mesh_create": (C.c_int, [C.POINTER(MeshDesc), C.c_int32, C.POINTER(C.c_void_p)]),
+    "mvba_mesh_destroy": (None, [C.c_void_p]),
+    "mvba_mesh_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "mvba_mesh_intersect_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_float, C.c_float,
+                                             C.c_void_p, C.c_void_p, C.c_void_p]),
+    "mvba_mesh_triangulate": (C.c_int, [C.POINTER(TracksDesc), C.c_void_p, C.c_void_p, C.c_double, C.c_double,
+                                        C.c_void_p, C.c_void_p]),
+    "mvba_mesh_error": (C.c_char_p, []),
     "mvba_rpc_fit": (C.c_int, [C.POINTER(RpcCamera), C.c_int32, C.c_int32, C.c_void_p, C.c_int32, C.c_int32,
                                C.c_double, C.c_int32, C.c_void_p, C.POINTER(RpcFitReport)]),
     "mvba_rpc_error": (C.c_char_p, []),

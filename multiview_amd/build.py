@@ -11,8 +11,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libmvba.so")
-SOURCES = ["mvba_kernels.hip", "mvba_solver.hip", "mvba_depth.hip", "mvba_stats.hip", "mvba_tracks.hip", "mvba_rpc.hip",
-           "mvba_comm.hip", "mvba_transfer.hip", "mvba_host.cpp", "mvba_transfer_host.cpp", "mvba_solve.cpp"]
+SOURCES = ["mvba_kernels.hip", "mvba_solver.hip", "mvba_depth.hip", "mvba_stats.hip", "mvba_tracks.hip",
+           "mvba_mesh.hip", "mvba_rpc.hip", "mvba_comm.hip", "mvba_transfer.hip", "mvba_host.cpp", "mvba_transfer_host.cpp", "mvba_solve.cpp"]
 # RCCL for the sharded solve's stream-ordered all-reduce (mvba_comm.hip). In a
 # torch process the already loaded librccl.so.1 (same SONAME) is the one used.
 LIBS = ["-L/opt/rocm/lib", "-lrccl"]

@@ -37,7 +37,7 @@ static void free_all(mvba_handle* h) {
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
-                  h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xpid,
+                  h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xkind, h->d_xpid,
                   h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt, h->d_varsize, h->d_tres, h->d_tcost,
                   h->d_trows, h->d_xmask, h->d_xoff, h->d_dwritten, h->d_dvarsize, h->d_tdres,
                   h->d_tdcost, h->d_tdrows};
@@ -149,15 +149,24 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       pose_first.emplace(PoseKey::make(blk[0], blk[1], blk[2], blk[4], d->residual_stamps + 3 * i), i);
     }
   }
+  int64_t nmesh = 0;  // BracketedDepthMeshError blocks (xyz block id -1, target in depth_mesh_xyz)
   for (int64_t j = 0; j < ND; j++) {
     const int32_t* blk = d->depth_blocks + 7 * j;
+    const bool mesh = blk[MVBA_DBLK_XYZ] == -1;
+    if (mesh && !d->depth_mesh_xyz)
+      return bad(MVBA_E_INVALID, "depth block without a point block needs depth_mesh_xyz (BracketedDepthMeshError)");
+    nmesh += mesh ? 1 : 0;
     for (int b = 0; b < 7; b++)
-      if (blk[b] < 0 || blk[b] >= d->num_blocks) return bad(MVBA_E_INVALID, "parameter block index out of range");
+      if (!(mesh && b == MVBA_DBLK_XYZ) && (blk[b] < 0 || blk[b] >= d->num_blocks))
+        return bad(MVBA_E_INVALID, "parameter block index out of range");
     static const int kDepthSize[7] = {7, 7, 7, 7, 1, 3, 1};
     for (int b = 0; b < 7; b++) {
+      if (mesh && b == MVBA_DBLK_XYZ) continue;
       const int sz = d->block_size[blk[b]];
       const bool ok = (b == MVBA_DBLK_DEPTH_TO_IMAGE) ? (sz == 7 || sz == 12) : (sz == kDepthSize[b]);
-      if (!ok) return bad(MVBA_E_DEPTH_BLOCK_SIZES, "BracketedDepthError: The block sizes were not set up properly.\n");
+      if (!ok)
+        return bad(MVBA_E_DEPTH_BLOCK_SIZES, mesh ? "BracketedDepthMeshError: The block sizes were not set up properly.\n"
+                                                  : "BracketedDepthError: The block sizes were not set up properly.\n");
     }
     if (pose_first.find(PoseKey::make(blk[0], blk[1], blk[2], blk[6], d->depth_stamps + 3 * j)) == pose_first.end())
       return bad(MVBA_E_INVALID,
@@ -212,6 +221,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   std::vector<int32_t> dep_pt(ND);
   for (int64_t j = 0; j < ND; j++) {
     const int32_t b = d->depth_blocks[7 * j + MVBA_DBLK_XYZ];
+    if (b == -1) continue;  // mesh blocks: virtual points below
     auto it = pt_index.find(b);
     if (it == pt_index.end()) {
       const int32_t id = (int32_t)pt_off.size();
@@ -236,6 +246,22 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     } else {
       xyz_pt[j] = it->second;
     }
+  }
+  // BracketedDepthMeshError (rig_calibrator.cc:615-705) is BracketedDepthError
+  // with the landmark replaced by a fixed mesh point: r = w (mesh_xyz - M). Each
+  // gets a virtual CONSTANT point after the user's points, backed by a tail of
+  // the device parameter vector that mvba_set_params never overwrites, so every
+  // depth kernel and solver pass serves it unchanged (constant points contribute
+  // camera-side rows only).
+  h->npts_user = (int64_t)pt_off.size();
+  std::vector<double> mesh_tail;
+  mesh_tail.reserve((size_t)(3 * nmesh));
+  for (int64_t j = 0; j < ND; j++) {
+    if (d->depth_blocks[7 * j + MVBA_DBLK_XYZ] != -1) continue;
+    dep_pt[j] = (int32_t)pt_off.size();
+    pt_off.push_back(d->num_param_doubles + (int64_t)mesh_tail.size());
+    pt_free.push_back(0);
+    for (int q = 0; q < 3; q++) mesh_tail.push_back(d->depth_mesh_xyz[3 * j + q]);
   }
   h->npts = (int64_t)pt_off.size();
 
@@ -431,7 +457,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     // camera-side blocks: not constant, not a point block, in block-id order
     std::vector<uint8_t> is_point(d->num_blocks, 0);
     for (auto& kv : pt_index) is_point[kv.first] = 1;
-    h->pt_block_ids.resize(h->npts);
+    h->pt_block_ids.assign(h->npts, -1);  // -1: virtual point of a mesh block
     for (auto& kv : pt_index) h->pt_block_ids[kv.second] = kv.first;
     for (int b = 0; b < d->num_blocks; b++) {
       if (is_point[b] || d->block_constant[b]) continue;
@@ -621,6 +647,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   std::vector<double4> xref;
   std::vector<double> xcc;
   std::vector<int32_t> xpid;
+  std::vector<uint8_t> xkind;
   h->nxyz = NX;
   h->xfree.assign((size_t)NX, 0);
   for (int64_t j = 0; j < NX; j++) h->xfree[(size_t)j] = pt_free[xyz_pt[j]];
@@ -633,6 +660,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     xcc.resize(NX);
     xpid.resize(NX);
     xorder.resize(NX);
+    xkind.resize(NX);
     for (int64_t j = 0; j < NX; j++) {
       const int64_t q = fill[xyz_pt[j]]++;
       xref[q] = make_double4(d->xyz_ref[3 * j], d->xyz_ref[3 * j + 1], d->xyz_ref[3 * j + 2], d->xyz_weight[j]);
@@ -640,6 +668,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       xcc[q] = t > 0.0 ? 1.0 / (t * t) : 0.0;
       xpid[q] = xyz_pt[j];
       xorder[q] = j;
+      xkind[q] = d->xyz_kind ? (d->xyz_kind[j] ? 1 : 0) : 0;
     }
   }
 
@@ -648,7 +677,10 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   auto chk = [&](hipError_t x) {
     if (e == hipSuccess && x != hipSuccess) e = x;
   };
-  chk(dalloc(&h->d_params, (size_t)std::max<int64_t>(d->num_param_doubles, 1)));
+  chk(dalloc(&h->d_params, (size_t)std::max<int64_t>(d->num_param_doubles + (int64_t)mesh_tail.size(), 1)));
+  if (e == hipSuccess && !mesh_tail.empty())
+    chk(hipMemcpy(h->d_params + d->num_param_doubles, mesh_tail.data(), mesh_tail.size() * sizeof(double),
+                  hipMemcpyHostToDevice));
   chk(upload(&h->d_fd, frames));
   chk(dalloc(&h->d_frec, (size_t)h->nframes * mvba::kFrameRecDoubles));
   chk(upload(&h->d_pt_off, pt_off));
@@ -699,6 +731,7 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_xpt_begin, xpt_begin));
   chk(upload(&h->d_xref, xref));
   chk(upload(&h->d_xcc, xcc));
+  chk(upload(&h->d_xkind, xkind));
   chk(upload(&h->d_xpid, xpid));
   chk(upload(&h->d_xorder, xorder));
   chk(dalloc(&h->d_xscal, (size_t)(1 + std::max<int64_t>((NX + 255) / 256, 1))));

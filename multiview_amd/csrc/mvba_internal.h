@@ -249,6 +249,7 @@ struct mvba_handle {
   int device = 0;
   std::string err;
   int64_t nres = 0, nslots = 0, nframes = 0, npts = 0, nparams = 0;
+  int64_t npts_user = 0;  // points of the caller's xyz blocks; [npts_user, npts) = mesh blocks' fixed points
   int64_t nsegs = 0;
   int32_t ncams = 0;
   int kmax = 0, jac_rows = 0;
@@ -356,6 +357,7 @@ struct mvba_handle {
   int64_t* d_xpt_begin = nullptr;         // CSR point -> prior entries
   double4* d_xref = nullptr;              // (x, y, z, weight)
   double* d_xcc = nullptr;                // Cauchy c = 1/threshold^2
+  uint8_t* d_xkind = nullptr;             // entry -> 0 tri prior, 1 mesh_tri prior (stats groups)
   int32_t* d_xpid = nullptr;              // point of each entry
   int64_t* d_xorder = nullptr;            // entry -> insertion index
   double* d_xout = nullptr;               // [3 nxyz] raw residuals (insertion order), lazy

@@ -4,7 +4,7 @@
 // The reference evaluates all residuals (Problem::Evaluate, no loss), divides
 // each by its residual scale (1 for pixels, depth_tri_weight for depth
 // residuals), groups |r| by residual name (<sensor>_pix_x, <sensor>_pix_y,
-// depth_tri_{x,y,z}_m), sorts each group and prints vals[int(0.25 len)],
+// depth_tri_{x,y,z}_m, tri_*, depth_mesh_*, mesh_tri_*), sorts each group and prints vals[int(0.25 len)],
 // vals[int(0.5 len)], vals[int(0.75 len)], vals[len - 1].
 // Here: one key per residual component (bits of |r|/scale: non-negative doubles
 // order like their bit patterns) and its group; two stable LSD radix sorts (by
@@ -17,7 +17,8 @@
 namespace mvba {
 
 // Reprojection slots: group 2*cam + component; padding slots -> sentinel group.
-// Depth blocks: groups 2*ncam + k; XYZ priors (--tri_weight): 2*ncam + 3 + k.
+// Depth blocks: groups 2*ncam + k; XYZ priors (--tri_weight): 2*ncam + 3 + k;
+// depth_mesh 2*ncam + 6 + k; mesh_tri priors 2*ncam + 9 + k.
 __global__ void k_stats_keys_cam(const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
                                  const double* __restrict__ res, int64_t ld, int64_t nslots,
                                  uint64_t* __restrict__ keys, uint32_t* __restrict__ groups) {
@@ -36,36 +37,42 @@ __global__ void k_stats_keys_cam(const Segment* __restrict__ segs, int32_t nseg,
   }
 }
 
-// Depth slots: group g0 + component, value |r| / weight.
+// Depth slots: group g0 + component (depth_tri), g0 + 6 + component for the
+// BracketedDepthMeshError blocks (depth_mesh: their point is a virtual one,
+// index >= pid_mesh0); value |r| / weight.
 __global__ void k_stats_keys_depth(int64_t nslots, const int64_t* __restrict__ dorder,
+                                   const DepthDesc* __restrict__ dd, int32_t pid_mesh0,
                                    const double4* __restrict__ dmeas, const double* __restrict__ dres, int64_t ld,
                                    uint32_t g0, uint64_t* __restrict__ keys, uint32_t* __restrict__ groups) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nslots || dorder[i] < 0) return;
   const double w = dmeas[i].w;
+  const uint32_t gb = g0 + (dd[i].pid >= pid_mesh0 ? 6u : 0u);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const double v = fabs(dres[k * ld + i] / w);
     keys[k * nslots + i] = __double_as_longlong(v);
-    groups[k * nslots + i] = g0 + k;
+    groups[k * nslots + i] = gb + k;
   }
 }
 
 // XYZError prior blocks: group g0 + component, value |w (X - ref)| / w (the
 // reference divides the raw residual by its scale, rig_calibrator.cc:1172-1173).
+// mesh_tri priors (kind 1) go to g0 + 6 + component.
 __global__ void k_stats_keys_xyz(int64_t n, const int32_t* __restrict__ xpid, const double4* __restrict__ xref,
-                                 const double4* __restrict__ pts, uint32_t g0, uint64_t* __restrict__ keys,
-                                 uint32_t* __restrict__ groups) {
+                                 const uint8_t* __restrict__ xkind, const double4* __restrict__ pts, uint32_t g0,
+                                 uint64_t* __restrict__ keys, uint32_t* __restrict__ groups) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const double4 X = pts[xpid[j]];
   const double4 R = xref[j];
   const double d[3] = {X.x - R.x, X.y - R.y, X.z - R.z};
+  const uint32_t gb = g0 + (xkind[j] ? 6u : 0u);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const double v = fabs((R.w * d[k]) / R.w);
     keys[k * n + j] = __double_as_longlong(v);
-    groups[k * n + j] = g0 + k;
+    groups[k * n + j] = gb + k;
   }
 }
 
@@ -123,7 +130,7 @@ mvba_status mvba_residual_stats(mvba_handle* h, double* out, int64_t* counts, vo
     if (st != MVBA_OK) return st;
   }
   const int32_t ncam_groups = 2 * h->ncams;
-  const int32_t ngroups = ncam_groups + 6;
+  const int32_t ngroups = ncam_groups + 12;
   const uint32_t sentinel = (uint32_t)ngroups;
   const int64_t n_cam = 2 * h->nslots, n_dep = 3 * h->ndep_slots, n_xyz = 3 * h->nxyz, n = n_cam + n_dep + n_xyz;
   hipError_t e = hipSuccess;
@@ -158,11 +165,12 @@ mvba_status mvba_residual_stats(mvba_handle* h, double* out, int64_t* counts, vo
                          (int32_t)h->nsegs, h->d_fd, v.residuals, v.ld, h->nslots, k0, g0);
     if (h->ndep > 0)
       hipLaunchKernelGGL(mvba::k_stats_keys_depth, dim3((unsigned)((h->ndep_slots + 255) / 256)), dim3(256), 0, s,
-                         h->ndep_slots, h->d_dep_order, h->d_dep_meas, h->d_dres, h->dld, (uint32_t)ncam_groups,
+                         h->ndep_slots, h->d_dep_order, h->d_dep_desc, (int32_t)h->npts_user, h->d_dep_meas,
+                         h->d_dres, h->dld, (uint32_t)ncam_groups,
                          k0 + n_cam, g0 + n_cam);
     if (h->nxyz > 0)
       hipLaunchKernelGGL(mvba::k_stats_keys_xyz, dim3((unsigned)((h->nxyz + 255) / 256)), dim3(256), 0, s, h->nxyz,
-                         h->d_xpid, h->d_xref, h->d_pts, (uint32_t)(ncam_groups + 3), k0 + n_cam + n_dep,
+                         h->d_xpid, h->d_xref, h->d_xkind, h->d_pts, (uint32_t)(ncam_groups + 3), k0 + n_cam + n_dep,
                          g0 + n_cam + n_dep);
     size_t t1 = tb1, t2 = tb2;
     chk(hipcub::DeviceRadixSort::SortPairs(temp, t1, k0, k1, g0, g1, (int)n, 0, 64, s));   // by value

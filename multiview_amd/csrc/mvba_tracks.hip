@@ -37,6 +37,7 @@ struct TrackCams {
 // compute_rpc with n coefficients (degree from n = 2 (d+1)(d+2) - 2), in the
 // reference's accumulation order.
 __device__ void rpc_eval(const double* c, int n, double x, double y, double* ox, double* oy) {
+#pragma clang fp contract(off)
   const int d = (int)llround(sqrt(2.0 * n + 5.0) / 2.0 - 1.5);
   double px[kMaxRpcDegree + 1], py[kMaxRpcDegree + 1];
   double vx = 1.0, vy = 1.0;
@@ -64,6 +65,9 @@ __device__ void rpc_eval(const double* c, int n, double x, double y, double* ox,
 
 __global__ void k_undistort(int64_t nobs, const int32_t* __restrict__ img, const int32_t* __restrict__ image_cam,
                             const double* __restrict__ pix, TrackCams cams, double* __restrict__ upix) {
+  // no contraction: the oracle's oracle_undistort bit for bit (the mesh rays
+  // are rounded to float from these values)
+#pragma clang fp contract(off)
   const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= nobs) return;
   const int cam = image_cam[img[o]];
@@ -287,7 +291,103 @@ __global__ void k_flag_reproj(int64_t nobs, const double* __restrict__ res, doub
   }
 }
 
+// meshTriangulations' rays (texture_processing.cc:1448-1468), one thread per
+// feature, in double with the reference's operation order (no contraction):
+// cam_ray = normalize(u / f, v / f, 1); cam_to_world = world_to_cam^-1 (Eigen
+// Affine inverse); world_ray = R^-1 cam_ray; cam_ctr = -R^-1 t; float copies
+// for rayint's Ray with the direction normalised again in float. Outliers get a
+// zero direction (no ray).
+// inverse3 (mvba_depth.h) without contraction: the oracle's affine_inverse bit for bit
+__device__ __forceinline__ void inverse3_exact(const double* m, double* o) {
+#pragma clang fp contract(off)
+  const double c00 = m[4] * m[8] - m[5] * m[7];
+  const double c10 = m[5] * m[6] - m[3] * m[8];
+  const double c20 = m[3] * m[7] - m[4] * m[6];
+  const double det = c00 * m[0] + c10 * m[1] + c20 * m[2];
+  const double inv = 1.0 / det;
+  o[0] = c00 * inv;
+  o[1] = (m[2] * m[7] - m[1] * m[8]) * inv;
+  o[2] = (m[1] * m[5] - m[2] * m[4]) * inv;
+  o[3] = c10 * inv;
+  o[4] = (m[0] * m[8] - m[2] * m[6]) * inv;
+  o[5] = (m[2] * m[3] - m[0] * m[5]) * inv;
+  o[6] = c20 * inv;
+  o[7] = (m[1] * m[6] - m[0] * m[7]) * inv;
+  o[8] = (m[0] * m[4] - m[1] * m[3]) * inv;
+}
+
+__global__ void k_mesh_feature_rays(int64_t nobs, const int32_t* __restrict__ img,
+                                    const int32_t* __restrict__ image_cam, const double* __restrict__ wc,
+                                    const double* __restrict__ focal, const double* __restrict__ upix,
+                                    const uint8_t* __restrict__ inlier, float* __restrict__ orig,
+                                    float* __restrict__ dir, double* __restrict__ ctr, double* __restrict__ wray) {
+#pragma clang fp contract(off)
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= nobs) return;
+  if (!inlier[o]) {
+    for (int q = 0; q < 3; q++) {
+      orig[3 * o + q] = 0.0f;
+      dir[3 * o + q] = 0.0f;
+    }
+    return;
+  }
+  const int im = img[o];
+  const double f = focal[image_cam[im]];
+  double cr[3] = {upix[2 * o] / f, upix[2 * o + 1] / f, 1.0};
+  const double nrm = sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+  for (int q = 0; q < 3; q++) cr[q] = cr[q] / nrm;
+  const double* w = wc + 12 * im;
+  double Ri[9];
+  inverse3_exact(w, Ri);
+  float fd[3];
+  for (int r = 0; r < 3; r++) {
+    const double wr = Ri[3 * r] * cr[0] + Ri[3 * r + 1] * cr[1] + Ri[3 * r + 2] * cr[2];
+    const double c = -(Ri[3 * r] * w[9] + Ri[3 * r + 1] * w[10] + Ri[3 * r + 2] * w[11]);
+    wray[3 * o + r] = wr;
+    ctr[3 * o + r] = c;
+    orig[3 * o + r] = (float)c;
+    fd[r] = (float)wr;
+  }
+  float s = 0.0f;
+  s = s + fd[0] * fd[0];
+  s = s + fd[1] * fd[1];
+  s = s + fd[2] * fd[2];
+  const float dn = sqrtf(s);
+  for (int q = 0; q < 3; q++) dir[3 * o + q] = fd[q] / dn;
+}
+
+// Per track: intersection = cam_ctr + t * world_ray for every hit, summed in
+// feature order and divided by the count (bad = 1e100 otherwise).
+__global__ void k_mesh_points(int64_t npts, const int64_t* __restrict__ tb, const float* __restrict__ thit,
+                              const int32_t* __restrict__ fhit, const double* __restrict__ ctr,
+                              const double* __restrict__ wray, double* __restrict__ feat_xyz,
+                              double* __restrict__ pt_xyz) {
+#pragma clang fp contract(off)
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npts) return;
+  const double bad = 1.0e+100;
+  double avg[3] = {0.0, 0.0, 0.0};
+  int num = 0;
+  for (int64_t o = tb[p]; o < tb[p + 1]; o++) {
+    double X[3] = {bad, bad, bad};
+    if (fhit[o] >= 0) {
+      const double t = (double)thit[o];
+      for (int q = 0; q < 3; q++) X[q] = ctr[3 * o + q] + t * wray[3 * o + q];
+      for (int q = 0; q < 3; q++) avg[q] += X[q];
+      num++;
+    }
+    if (feat_xyz)
+      for (int q = 0; q < 3; q++) feat_xyz[3 * o + q] = X[q];
+  }
+  for (int q = 0; q < 3; q++) pt_xyz[3 * p + q] = num >= 1 ? avg[q] / (double)num : bad;
+}
+
 }  // namespace mvba
+
+extern "C" hipError_t mvba_launch_mesh_rays(const mvba_mesh* m, int64_t n, const int64_t* perm, const float* orig,
+                                            const float* dir, float tmin, float tmax, float* t_out,
+                                            int32_t* face_out, hipStream_t s);
+extern "C" int32_t mvba_mesh_device_ordinal(const mvba_mesh* m);
 
 namespace {
 
@@ -461,6 +561,62 @@ mvba_status mvba_flag_outliers(const mvba_tracks_desc* d, int32_t device, const 
   if (e == hipSuccess) e = hipMemcpy(hc, t.counts, sizeof(hc), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return fail(MVBA_E_HIP, std::string("HIP error: ") + hipGetErrorString(e));
   for (int q = 0; q < 4; q++) counts[q] = (int64_t)hc[q];
+  return MVBA_OK;
+}
+
+mvba_status mvba_mesh_triangulate(const mvba_tracks_desc* d, mvba_mesh* m, const uint8_t* inlier,
+                                  double min_ray_dist, double max_ray_dist, double* feature_xyz, double* point_xyz) {
+  g_tracks_error.clear();
+  if (!m) return fail(MVBA_E_INVALID, "null mesh handle");
+  if (d && d->num_points > 0 && (!inlier || !point_xyz)) return fail(MVBA_E_INVALID, "null array");
+  DevTracks t;
+  mvba_status st = load(d, mvba_mesh_device_ordinal(m), t);
+  if (st != MVBA_OK) return st;
+  if (t.npts == 0) return MVBA_OK;
+  const int64_t n = t.nobs;
+  float *orig = nullptr, *dir = nullptr, *thit = nullptr;
+  int32_t* fhit = nullptr;
+  double *ctr = nullptr, *wray = nullptr, *fx = nullptr;
+  int64_t* perm = nullptr;
+  hipError_t e = hipMemcpy(t.inlier, inlier, (size_t)n, hipMemcpyHostToDevice);
+  auto chk = [&](hipError_t x) {
+    if (e == hipSuccess && x != hipSuccess) e = x;
+  };
+  chk(dalloc(&t.upix, (size_t)2 * n));
+  chk(dalloc(&orig, (size_t)3 * n));
+  chk(dalloc(&dir, (size_t)3 * n));
+  chk(dalloc(&thit, (size_t)n));
+  chk(dalloc(&fhit, (size_t)n));
+  chk(dalloc(&ctr, (size_t)3 * n));
+  chk(dalloc(&wray, (size_t)3 * n));
+  chk(dalloc(&fx, (size_t)3 * n));
+  {
+    // image-major ray order (counting sort): a wave's rays share a camera centre
+    std::vector<int64_t> cnt((size_t)d->num_images + 1, 0), order((size_t)n);
+    for (int64_t o = 0; o < n; o++) cnt[(size_t)d->track_image[o] + 1]++;
+    for (int32_t i = 0; i < d->num_images; i++) cnt[(size_t)i + 1] += cnt[(size_t)i];
+    for (int64_t o = 0; o < n; o++) order[(size_t)cnt[(size_t)d->track_image[o]]++] = o;
+    chk(upload(&perm, order));
+  }
+  if (e == hipSuccess && n > 0) {
+    mvba::TrackCams cams{t.focal, t.center, t.K, t.doff, t.dist, t.dhalf, t.uhalf};
+    hipLaunchKernelGGL(mvba::k_undistort, dim3(grid(n)), dim3(256), 0, nullptr, n, t.img, t.image_cam, t.pix, cams,
+                       t.upix);
+    hipLaunchKernelGGL(mvba::k_mesh_feature_rays, dim3(grid(n)), dim3(256), 0, nullptr, n, t.img, t.image_cam, t.wc,
+                       t.focal, t.upix, t.inlier, orig, dir, ctr, wray);
+    chk(hipGetLastError());
+    chk(mvba_launch_mesh_rays(m, n, perm, orig, dir, (float)min_ray_dist, (float)max_ray_dist, thit, fhit, nullptr));
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(mvba::k_mesh_points, dim3(grid(t.npts)), dim3(256), 0, nullptr, t.npts, t.tb, thit, fhit, ctr,
+                       wray, fx, t.xyz);
+    chk(hipGetLastError());
+  }
+  if (e == hipSuccess) chk(hipMemcpy(point_xyz, t.xyz, (size_t)3 * t.npts * sizeof(double), hipMemcpyDeviceToHost));
+  if (e == hipSuccess && feature_xyz) chk(hipMemcpy(feature_xyz, fx, (size_t)3 * n * sizeof(double), hipMemcpyDeviceToHost));
+  for (void* p : {(void*)orig, (void*)dir, (void*)thit, (void*)fhit, (void*)ctr, (void*)wray, (void*)fx, (void*)perm})
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess) return fail(MVBA_E_HIP, std::string("HIP error: ") + hipGetErrorString(e));
   return MVBA_OK;
 }
 

@@ -248,12 +248,11 @@ class Evaluator:
         residual blocks."""
         ncam = len(self.problem.camera_dist_size)
         names = list(sensor_names or [f"cam{c}" for c in range(ncam)])
-        ng = 2 * ncam + 6
+        ng = 2 * ncam + 12
         out = np.empty(4 * ng)
         counts = np.empty(ng, dtype=np.int64)
         _lib.check(self.lib.mvba_residual_stats(self.h, out.ctypes.data, counts.ctypes.data, None), self.h)
-        labels = [f"{names[c]}_pix_{xy}" for c in range(ncam) for xy in "xy"] + \
-            [f"depth_tri_{a}_m" for a in "xyz"] + [f"tri_{a}_m" for a in "xyz"]
+        labels = stats_labels(names)
         rows = [(labels[g], *out[4 * g:4 * g + 4], int(counts[g])) for g in range(ng) if counts[g] > 0]
         return sorted(rows, key=lambda r: r[0])
 
@@ -305,6 +304,13 @@ class Evaluator:
 
     def __exit__(self, *a):
         self.close()
+
+
+def stats_labels(sensor_names) -> list:
+    """Residual names of the mvba_residual_stats groups (rig_calibrator.cc:1690-1691,
+    :1769-1771, :1818-1820, :1873-1875, :1893-1895)."""
+    return [f"{n}_pix_{xy}" for n in sensor_names for xy in "xy"] + \
+        [f"{kind}_{a}_m" for kind in ("depth_tri", "tri", "depth_mesh", "mesh_tri") for a in "xyz"]
 
 
 def default_solver_options(**kw) -> _lib.SolverOptions:

@@ -70,11 +70,15 @@ class CamProblem:
     depth_weight: np.ndarray = field(default_factory=lambda: np.zeros(0))
     depth_stamps: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
     depth_after: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int64))  # preceding cam block
+    # BracketedDepthMeshError blocks share the depth list: xyz block id -1 and the
+    # fixed mesh point in depth_mesh_xyz (rows of other blocks ignored); empty = none
+    depth_mesh_xyz: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
     # XYZError priors (optional): point block, reference xyz, weight, Cauchy threshold
     xyz_block: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.int32))
     xyz_ref: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
     xyz_weight: np.ndarray = field(default_factory=lambda: np.zeros(0))
     xyz_threshold: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    xyz_kind: np.ndarray = field(default_factory=lambda: np.zeros(0, dtype=np.uint8))  # 1 = mesh_tri prior
     _keep: list = field(default_factory=list, repr=False)
 
     @property
@@ -113,7 +117,13 @@ class CamProblem:
             np.ascontiguousarray(self.xyz_ref, dtype=np.float64).reshape(-1),
             np.ascontiguousarray(self.xyz_weight, dtype=np.float64).reshape(-1),
             np.ascontiguousarray(self.xyz_threshold, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.depth_mesh_xyz, dtype=np.float64).reshape(-1),
+            np.ascontiguousarray(self.xyz_kind, dtype=np.uint8).reshape(-1),
         ]
+        if arrs[17].size not in (0, 3 * self.num_depth_residuals):
+            raise ValueError("depth_mesh_xyz needs 3 values per depth residual block")
+        if arrs[18].size not in (0, self.num_xyz_residuals):
+            raise ValueError("xyz_kind needs one value per XYZ prior")
         self._keep = arrs
         d = _lib.ProblemDesc()
         d.num_blocks = len(arrs[0])
@@ -139,6 +149,8 @@ class CamProblem:
         d.xyz_ref = arrs[14].ctypes.data
         d.xyz_weight = arrs[15].ctypes.data
         d.xyz_threshold = arrs[16].ctypes.data
+        d.depth_mesh_xyz = arrs[17].ctypes.data if arrs[17].size else None
+        d.xyz_kind = arrs[18].ctypes.data if arrs[18].size else None
         return d
 
     def subset(self, idx: np.ndarray) -> "CamProblem":

@@ -256,14 +256,16 @@ def _sensor_yaw_deg(s: int, n_s: int) -> float:
 
 def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, models=None,
              seed=1001, point_range=None, window=20, noise_px=0.5, depth_sensors=(),
-             depth_noise=0.01, affine_depth=False) -> Rig:
+             depth_noise=0.01, affine_depth=False, surface=None) -> Rig:
     """Build a synthetic rig. ``point_range=(lo, hi)`` generates only points
     [lo, hi) of a larger problem (landmark-range sharding): the
     cameras are identical on every shard, points use a per-shard stream.
     ``depth_sensors``: sensors that also carry a depth cloud (config c5); every
     observation of such a sensor gets the cloud point of its landmark,
     depth_to_image^-1 (X_cam) + N(0, depth_noise^2), rounded to float32 (clouds
-    are float32, dense_map_utils.cc:1382)."""
+    are float32, dense_map_utils.cc:1382). ``surface="sphere"``: landmarks on the
+    sphere of radius SPHERE_RADIUS (the surface ``sphere_mesh`` triangulates, for
+    the --mesh constraints), observed only by cameras on their outer side."""
     models = list(models or ["radtan"] * num_sensors)
     assert len(models) == num_sensors
     rng = np.random.default_rng(seed)
@@ -330,7 +332,12 @@ def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, mode
     npts = hi - lo
     v = prng.normal(size=(npts, 3))
     v /= np.linalg.norm(v, axis=1, keepdims=True)
-    xyz = 4.0 * v * prng.random(npts)[:, None] ** (1 / 3)
+    if surface == "sphere":
+        xyz = SPHERE_RADIUS * v
+    elif surface is None:
+        xyz = 4.0 * v * prng.random(npts)[:, None] ** (1 / 3)
+    else:
+        raise ValueError(surface)
 
     # observations: candidates near an anchor reference index
     cid_of = -np.ones((nr, ns), dtype=np.int64)
@@ -352,6 +359,12 @@ def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, mode
     z = Xc[:, 2]
     pix = np.zeros((P.size, 2))
     ok &= z > 0.5
+    if surface == "sphere":
+        # visible side only, away from the silhouette: the viewing ray meets the
+        # surface normal at less than ~72 degrees
+        Cw = -np.einsum("nji,nj->ni", Rc[Cs], tc[Cs])
+        ray = Cw - xyz[P]
+        ok &= np.einsum("ni,ni->n", ray, xyz[P]) > 0.3 * SPHERE_RADIUS * np.linalg.norm(ray, axis=1)
     for s in range(ns):
         sel = ok & (cam_type[Cs] == s)
         if not sel.any():
@@ -453,6 +466,37 @@ def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, mode
                depth_obs=dsel, depth_meas=dmeas, depth_to_image=dti_true)
 
 
+SPHERE_RADIUS = 4.0
+
+
+def sphere_mesh(subdiv: int = 5, radius: float = SPHERE_RADIUS):
+    """Icosphere (float32 vertices on the sphere, uint32 faces, outward winding):
+    the synthetic stand-in for the --mesh PLY of a scene with surface="sphere"."""
+    t = (1.0 + 5.0 ** 0.5) / 2.0
+    V = [(-1, t, 0), (1, t, 0), (-1, -t, 0), (1, -t, 0), (0, -1, t), (0, 1, t), (0, -1, -t), (0, 1, -t),
+         (t, 0, -1), (t, 0, 1), (-t, 0, -1), (-t, 0, 1)]
+    F = [(0, 11, 5), (0, 5, 1), (0, 1, 7), (0, 7, 10), (0, 10, 11), (1, 5, 9), (5, 11, 4), (11, 10, 2), (10, 7, 6),
+         (7, 1, 8), (3, 9, 4), (3, 4, 2), (3, 2, 6), (3, 6, 8), (3, 8, 9), (4, 9, 5), (2, 4, 11), (6, 2, 10),
+         (8, 6, 7), (9, 8, 1)]
+    verts = [np.array(v, dtype=np.float64) / np.linalg.norm(v) for v in V]
+    for _ in range(subdiv):
+        mid = {}
+        nf = []
+
+        def m(a, b):
+            k = (min(a, b), max(a, b))
+            if k not in mid:
+                x = verts[a] + verts[b]
+                verts.append(x / np.linalg.norm(x))
+                mid[k] = len(verts) - 1
+            return mid[k]
+        for a, b, c in F:
+            ab, bc, ca = m(a, b), m(b, c), m(c, a)
+            nf += [(a, ab, ca), (b, bc, ab), (c, ca, bc), (ab, bc, ca)]
+        F = nf
+    return (radius * np.array(verts)).astype(np.float32), np.array(F, dtype=np.uint32)
+
+
 # ------------------------------------------------------------ problem assembly
 @dataclass
 class FloatFlags:
@@ -470,10 +514,17 @@ class FloatFlags:
     # XYZError prior on every point (rig_calibrator.cc:1889-1898)
     tri_weight: float = 0.0
     tri_robust_threshold: float = 0.0
+    # --mesh constraints (rig_calibrator.cc:1796-1877): BracketedDepthMeshError
+    # per depth observation with a mesh hit, XYZError to the track's mean hit
+    depth_mesh_weight: float = 0.0
+    mesh_tri_weight: float = 0.0
+    robust_threshold: float = 3.0
 
 
-def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = True) -> CamProblem:
+def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = True, mesh_xyz=None) -> CamProblem:
     """Assemble the BracketedCamError problem exactly as rig_calibrator.cc:1614-1752.
+    ``mesh_xyz = (feature_xyz [N_obs, 3], point_xyz [N_pts, 3])`` from
+    meshTriangulations (1e100 = no hit) enables the --mesh constraints.
 
     Packed parameter vector (DESIGN.md "Workloads"): world_to_ref | identity |
     ref_to_cam | xyz | offsets | focal | center | distortion | placeholder,
@@ -537,7 +588,12 @@ def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = Tr
             dist_b.append(-1)
     ph_b = add([0.0], True)  # distortion_placeholder (rig_calibrator.cc:1608)
     dist_b = [b if b >= 0 else ph_b for b in dist_b]
-    use_depth = flags.depth_tri_weight > 0 and rig.depth_obs is not None and rig.depth_obs.size > 0
+    has_depth = rig.depth_obs is not None and rig.depth_obs.size > 0
+    bad = 1.0e+100
+    mesh_dep = np.zeros(0, dtype=np.int64)
+    if mesh_xyz is not None and flags.depth_mesh_weight > 0 and has_depth:
+        mesh_dep = rig.depth_obs[mesh_xyz[0][rig.depth_obs, 0] != bad]
+    use_depth = (flags.depth_tri_weight > 0 and has_depth) or mesh_dep.size > 0
     if use_depth:
         dti_src = src.get("depth_to_image", rig.depth_to_image) if use_init else rig.depth_to_image
         want = 12 if flags.affine_depth_to_image else 7
@@ -590,9 +646,15 @@ def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = Tr
                    residual_stamps=stamps,
                    residual_names=None if n > 100000 else [names[t] for t in ct])
     if use_depth:
-        # one BracketedDepthError right after the observation's BracketedCamError
-        # (rig_calibrator.cc:1755-1791): same beg/end/ref_to_cam/offset/stamps
-        k = rig.depth_obs
+        # after the observation's BracketedCamError: its BracketedDepthError
+        # (rig_calibrator.cc:1755-1791), then its BracketedDepthMeshError
+        # (:1796-1834), with the same beg/end/ref_to_cam/offset/stamps
+        d_obs = rig.depth_obs if flags.depth_tri_weight > 0 else np.zeros(0, dtype=np.int64)
+        meas_of = {int(o): q for q, o in enumerate(rig.depth_obs)}
+        k = np.concatenate([d_obs, mesh_dep])
+        kind = np.concatenate([np.zeros(d_obs.size, dtype=np.int8), np.ones(mesh_dep.size, dtype=np.int8)])
+        o = np.lexsort((kind, k))
+        k, kind = k[o], kind[o]
         dct = ct[k]
         db = np.empty((k.size, 7), dtype=np.int32)
         db[:, 0] = blocks[k, 0]
@@ -600,22 +662,42 @@ def build_problem(rig: Rig, flags: FloatFlags | None = None, use_init: bool = Tr
         db[:, 2] = blocks[k, 2]
         db[:, 3] = dti_b0 + dct
         db[:, 4] = scl_b0 + dct
-        db[:, 5] = blocks[k, 3]
+        db[:, 5] = np.where(kind == 1, -1, blocks[k, 3])
         db[:, 6] = blocks[k, 4]
         P.depth_blocks = db
-        P.depth_meas = rig.depth_meas.copy()
-        P.depth_weight = np.full(k.size, float(flags.depth_tri_weight))
+        P.depth_meas = rig.depth_meas[[meas_of[int(x)] for x in k]].reshape(-1, 3).copy()
+        P.depth_weight = np.where(kind == 1, float(flags.depth_mesh_weight), float(flags.depth_tri_weight))
         P.depth_stamps = stamps[k].copy()
         P.depth_after = k.astype(np.int64)
+        if mesh_dep.size:
+            P.depth_mesh_xyz = np.where(kind[:, None] == 1, mesh_xyz[0][k], 0.0)
+    # per point: the mesh_tri prior (:1857-1877), then the tri prior (:1880-1898)
+    xb, xr, xw, xt, xk = [], [], [], [], []
+    if mesh_xyz is not None and flags.mesh_tri_weight > 0:
+        good = np.nonzero(mesh_xyz[1][:, 0] != bad)[0]
+        xb.append(xyz_b0 + good)
+        xr.append(np.asarray(mesh_xyz[1])[good])
+        xw.append(np.full(good.size, float(flags.mesh_tri_weight)))
+        xt.append(np.full(good.size, float(flags.robust_threshold)))
+        xk.append(np.ones(good.size, dtype=np.uint8))
     if flags.tri_weight > 0:
         # --tri_weight: keep points near their values before the optimisation
         # (xyz_vec_orig, :1571-1578), Cauchy(--tri_robust_threshold)
         if not flags.tri_robust_threshold > 0:
             raise ValueError("a positive --tri_robust_threshold is needed with --tri_weight")
-        P.xyz_block = (xyz_b0 + np.arange(npts)).astype(np.int32)
-        P.xyz_ref = np.asarray(src["xyz"], dtype=np.float64).reshape(-1, 3).copy()
-        P.xyz_weight = np.full(npts, float(flags.tri_weight))
-        P.xyz_threshold = np.full(npts, float(flags.tri_robust_threshold))
+        xb.append(xyz_b0 + np.arange(npts))
+        xr.append(np.asarray(src["xyz"], dtype=np.float64).reshape(-1, 3).copy())
+        xw.append(np.full(npts, float(flags.tri_weight)))
+        xt.append(np.full(npts, float(flags.tri_robust_threshold)))
+        xk.append(np.zeros(npts, dtype=np.uint8))
+    if xb:
+        b = np.concatenate(xb)
+        o = np.argsort(b, kind="stable")  # point-major, mesh_tri before tri
+        P.xyz_block = b[o].astype(np.int32)
+        P.xyz_ref = np.concatenate(xr)[o]
+        P.xyz_weight = np.concatenate(xw)[o]
+        P.xyz_threshold = np.concatenate(xt)[o]
+        P.xyz_kind = np.concatenate(xk)[o]
     return P
 
 

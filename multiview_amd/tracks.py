@@ -121,3 +121,69 @@ def from_rig(rig, world_to_cam, use_init: bool = True) -> Tracks:
                   focal=np.asarray(src["focal"], dtype=np.float64), center=np.asarray(src["center"], dtype=np.float64),
                   dist=dist, dist_half=half, undist_half=half.copy(), track_begin=tb,
                   track_image=rig.obs_cid.astype(np.int32), track_pix=rig.obs_pix.copy())
+
+
+# ---------------------------------------------------------------- mesh (--mesh)
+class Mesh:
+    """A triangle mesh on the GPU with its BVH (mvba_mesh_create; the reference's
+    loadMeshBuildTree, texture_processing.cc:264-285). ``vertices`` [V, 3]
+    float32, ``faces`` [F, 3] vertex indices."""
+
+    def __init__(self, vertices, faces, device: int = 0):
+        self.lib = _lib.load()
+        self.vertices = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+        self.faces = np.ascontiguousarray(faces, dtype=np.uint32).reshape(-1, 3)
+        d = _lib.MeshDesc()
+        d.num_vertices = self.vertices.shape[0]
+        d.vertices = self.vertices.ctypes.data
+        d.num_faces = self.faces.shape[0]
+        d.faces = self.faces.ctypes.data
+        self.h = C.c_void_p()
+        st = self.lib.mvba_mesh_create(C.byref(d), int(device), C.byref(self.h))
+        if st != _lib.MVBA_OK:
+            raise _lib.MvbaError(st, self.lib.mvba_mesh_error().decode())
+
+    def info(self) -> dict:
+        n, dp = C.c_int64(), C.c_int32()
+        self.lib.mvba_mesh_info(self.h, C.byref(n), C.byref(dp))
+        return {"num_nodes": n.value, "depth": dp.value}
+
+    def intersect_device(self, orig, dirs, tmin, tmax, t_out, face_out, stream=None):
+        """Closest hits of device rays (torch float32 [n, 3] tensors), rayint's Ray
+        semantics; t_out (float32, -1 = miss) and face_out (int32) [n]."""
+        n = int(orig.shape[0])
+        st = self.lib.mvba_mesh_intersect_device(self.h, n, C.c_void_p(orig.data_ptr()), C.c_void_p(dirs.data_ptr()),
+                                                 float(tmin), float(tmax), C.c_void_p(t_out.data_ptr()),
+                                                 C.c_void_p(face_out.data_ptr()), C.c_void_p(stream or 0))
+        if st != _lib.MVBA_OK:
+            raise _lib.MvbaError(st, self.lib.mvba_mesh_error().decode())
+
+    def close(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.mvba_mesh_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def mesh_triangulate(tracks: Tracks, mesh: Mesh, inlier, min_ray_dist: float = 0.0, max_ray_dist: float = 100.0):
+    """meshTriangulations (texture_processing.cc:1566-1625). Returns
+    (feature_xyz [N_obs, 3], point_xyz [N_pts, 3]); 1e100 marks no hit."""
+    lib = _lib.load()
+    inl = np.ascontiguousarray(inlier, dtype=np.uint8)
+    fx = np.zeros((tracks.num_obs, 3))
+    px = np.zeros((tracks.num_points, 3))
+    d = tracks.desc()
+    _check(lib.mvba_mesh_triangulate(C.byref(d), mesh.h, inl.ctypes.data, float(min_ray_dist), float(max_ray_dist),
+                                     fx.ctypes.data, px.ctypes.data))
+    return fx, px

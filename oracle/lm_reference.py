@@ -28,7 +28,8 @@ def _columns(P):
         used[P.residual_blocks[:, b]] = True
     used[P.residual_blocks[K_of > 0, 7]] = True
     if P.num_depth_residuals:
-        used[P.depth_blocks.reshape(-1)] = True
+        db = P.depth_blocks.reshape(-1)
+        used[db[db >= 0]] = True  # -1: the mesh point of a BracketedDepthMeshError block
     if P.num_xyz_residuals:
         used[P.xyz_block] = True
     free = np.nonzero(used & (P.block_constant == 0))[0]
@@ -73,6 +74,8 @@ def _jacobian(P, params, col, ncols, use_loss, thr):
         for j in range(nd):
             for b in range(7):
                 bid = int(P.depth_blocks[j, b])
+                if bid < 0:
+                    continue
                 c0 = col[bid]
                 if c0 < 0:
                     continue

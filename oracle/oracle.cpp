@@ -21,6 +21,10 @@
 //   BracketedCamError         rig_calibrator.cc:447-482
 //   BracketedDepthError       rig_calibrator.cc:547-583
 //   XYZError                  rig_calibrator.cc:721-727
+//   BracketedDepthMeshError   rig_calibrator.cc:641-673
+//   meshTriangulations        texture_processing.cc:1566-1625 (+ ray_mesh_intersect
+//                             :1436-1479; rayint's ray-triangle test [ext, absent]:
+//                             parity unpinned)
 //   DistortCentered           camera_params.cc:260-314 (+ Convert :412-415)
 //   SetDistortion precalcs    camera_params.cc:169-208
 //   compute_rpc               rpc_distortion.cc:116-160 (rpc_degree :43-49)
@@ -374,6 +378,25 @@ bool depth_error(const T* const* p, int dti_size, double weight, const double* m
   return true;
 }
 
+// rig_calibrator.cc:641-673 (BracketedDepthMeshError::operator()). p = [beg,
+// end, ref_to_cam, depth_to_image(7|12), scale, offset]; the mesh point is data.
+template <class T>
+bool depth_mesh_error(const T* const* p, int dti_size, double weight, const double* meas, const double* mesh,
+                      double sb, double se, double sc, T* r) {
+  Aff<T> wc;
+  if (!calc_world_to_cam_trans(p[0], p[1], p[2], sb, se, p[5][0], sc, &wc)) return false;
+  Aff<T> dti = (dti_size == 12) ? array_to_affine_transform(p[3]) : array_to_rigid_transform(p[3]);
+  T s = p[4][0];
+  for (int i = 0; i < 9; i++) dti.R[i] *= s;
+  T z[3] = {T(meas[0]), T(meas[1]), T(meas[2])};
+  T M[3], Mw[3];
+  apply(dti, z, M);
+  Aff<T> inv = affine_inverse(wc);
+  apply(inv, M, Mw);
+  for (int i = 0; i < 3; i++) r[i] = T(weight) * (T(mesh[i]) - Mw[i]);
+  return true;
+}
+
 // --------------------------------------------------------------- evaluation
 struct CamProblem {
   const mvba_problem_desc* d;
@@ -648,6 +671,60 @@ int oracle_depth_error(const double* const* blocks, int dti_size, const uint8_t*
   return off;
 }
 
+// BracketedDepthMeshError for one block set (6 pointers: beg, end, ref_to_cam,
+// depth_to_image, scale, offset); same modes and J layout rules as
+// oracle_depth_error (3 x size_b row-major per block, in block order).
+int oracle_depth_mesh_error(const double* const* blocks, int dti_size, const uint8_t* constant, double weight,
+                            const double* meas, const double* mesh, double sb, double se, double sc, int mode,
+                            double* r3, double* J) {
+  int sizes[6] = {7, 7, 7, dti_size, 1, 1};
+  if (dti_size != 7 && dti_size != 12) return -MVBA_E_DEPTH_BLOCK_SIZES;
+  std::vector<double> buf[6];
+  const double* pd[6];
+  for (int b = 0; b < 6; b++) {
+    buf[b].assign(blocks[b], blocks[b] + sizes[b]);
+    pd[b] = buf[b].data();
+  }
+  if (!depth_mesh_error<double>(pd, dti_size, weight, meas, mesh, sb, se, sc, r3)) return -MVBA_E_ALPHA_RANGE;
+  if (mode == 0 || !J) return 0;
+  int off = 0;
+  for (int b = 0; b < 6; b++) {
+    for (int j = 0; j < sizes[b]; j++) {
+      double jc[3] = {0, 0, 0};
+      if (!constant[b]) {
+        if (mode == 1) {
+          const double x = buf[b][j];
+          const double delta = std::max(std::sqrt(std::numeric_limits<double>::epsilon()), std::fabs(x) * 1e-6);
+          double rp[3], rm[3];
+          buf[b][j] = x + delta;
+          depth_mesh_error<double>(pd, dti_size, weight, meas, mesh, sb, se, sc, rp);
+          double ood = 1.0 / delta;
+          buf[b][j] = x - delta;
+          depth_mesh_error<double>(pd, dti_size, weight, meas, mesh, sb, se, sc, rm);
+          ood /= 2;
+          buf[b][j] = x;
+          for (int q = 0; q < 3; q++) jc[q] = (rp[q] - rm[q]) * ood;
+        } else {
+          std::vector<Dual> db[6];
+          const Dual* pdd[6];
+          for (int bb = 0; bb < 6; bb++) {
+            db[bb].resize(sizes[bb]);
+            for (int q = 0; q < sizes[bb]; q++) db[bb][q] = Dual(buf[bb][q], 0.0);
+            pdd[bb] = db[bb].data();
+          }
+          db[b][j].d = 1.0;
+          Dual rr[3];
+          depth_mesh_error<Dual>(pdd, dti_size, weight, meas, mesh, sb, se, sc, rr);
+          for (int q = 0; q < 3; q++) jc[q] = rr[q].d;
+        }
+      }
+      for (int q = 0; q < 3; q++) J[off + q * sizes[b] + j] = jc[q];
+    }
+    off += 3 * sizes[b];
+  }
+  return off;
+}
+
 // rig_calibrator.cc:753-789: 25/50/75/100th percentiles of |r| per name.
 // names: residual name id per residual (already mapped to sorted std::map order by
 // the caller), out: [num_names * 4] values and [num_names] counts.
@@ -860,6 +937,148 @@ void oracle_flag_outliers(int64_t npts, const int64_t* tb, const int32_t* img, c
         inlier[o] = 0;
       }
     }
+}
+
+// ---------------------------------------------------------------- mesh rays
+// rayint [ext, absent: the reference's rayint submodule is empty] — restated from
+// its published algorithm (acc/primitives.h intersect(Ray, Tri)): plane hit
+// t = -n.(o - a) / (n.d) with the unit normal n = normalize((c - a) x (b - a)),
+// rejected when |n| or |n.d| < FLT_EPSILON or t outside [tmin, tmax]; then the
+// barycentric coordinates of o + t d from the 2x2 normal equations (v, w, u =
+// 1 - v - w), inside when all three are >= 0. All in float, mve::math::Vec3f
+// operation order (dot = ((0 + x x') + y y') + z z', normalize = v / norm).
+// BVHTree::intersect returns the closest such hit; ties in t go to the lower
+// face index here (a BVH's visit order is not part of the result).
+static inline float dot3f(const float* a, const float* b) {
+  float s = 0.0f;
+  s = s + a[0] * b[0];
+  s = s + a[1] * b[1];
+  s = s + a[2] * b[2];
+  return s;
+}
+static bool ray_tri_f(const float* o, const float* d, float tmin, float tmax, const float* A, const float* B,
+                      const float* Cc, float* tout) {
+  const float v0[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
+  const float v1[3] = {Cc[0] - A[0], Cc[1] - A[1], Cc[2] - A[2]};
+  float n[3] = {v1[1] * v0[2] - v1[2] * v0[1], v1[2] * v0[0] - v1[0] * v0[2], v1[0] * v0[1] - v1[1] * v0[0]};
+  const float nn = std::sqrt(dot3f(n, n));
+  if (nn < std::numeric_limits<float>::epsilon()) return false;
+  for (int q = 0; q < 3; q++) n[q] = n[q] / nn;
+  const float cosine = dot3f(n, d);
+  if (std::fabs(cosine) < std::numeric_limits<float>::epsilon()) return false;
+  const float oa[3] = {o[0] - A[0], o[1] - A[1], o[2] - A[2]};
+  const float t = -dot3f(n, oa) / cosine;
+  if (t < tmin || tmax < t) return false;
+  const float v2[3] = {oa[0] + t * d[0], oa[1] + t * d[1], oa[2] + t * d[2]};
+  const float d00 = dot3f(v0, v0), d01 = dot3f(v0, v1), d11 = dot3f(v1, v1);
+  const float d20 = dot3f(v2, v0), d21 = dot3f(v2, v1);
+  const float denom = d00 * d11 - d01 * d01;
+  const float bv = (d11 * d20 - d01 * d21) / denom;
+  const float bw = (d00 * d21 - d01 * d20) / denom;
+  const float bu = 1.0f - bv - bw;
+  if (!(bu >= 0.0f && bv >= 0.0f && bw >= 0.0f)) return false;
+  *tout = t;
+  return true;
+}
+
+// Closest hit by brute force over every face (no BVH): t_out -1 / face_out -1 on a miss.
+void oracle_ray_mesh(int64_t nrays, const float* orig, const float* dir, float tmin, float tmax, int64_t nfaces,
+                     const float* verts, const uint32_t* faces, float* t_out, int32_t* face_out) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t r = 0; r < nrays; r++) {
+    float best = 0.0f;
+    int32_t bf = -1;
+    for (int64_t f = 0; f < nfaces; f++) {
+      float t;
+      if (!ray_tri_f(orig + 3 * r, dir + 3 * r, tmin, tmax, verts + 3 * faces[3 * f], verts + 3 * faces[3 * f + 1],
+                     verts + 3 * faces[3 * f + 2], &t))
+        continue;
+      if (bf < 0 || t < best) {
+        best = t;
+        bf = (int32_t)f;
+      }
+    }
+    t_out[r] = bf < 0 ? -1.0f : best;
+    face_out[r] = bf;
+  }
+}
+
+// meshTriangulations (texture_processing.cc:1566-1625) with ray_mesh_intersect
+// (:1436-1479): per inlier feature, undistort (Convert<DISTORTED, UNDISTORTED_C>),
+// cam_ray = normalize(u / f, v / f, 1) (double), cam_to_world = world_to_cam^-1,
+// world_ray = R^-1 cam_ray, ray origin / dir cast to float and dir normalised in
+// float, tmin/tmax = min/max_ray_dist; hit -> cam_ctr + t * world_ray (double).
+// Track mean over hits in feature (cid) order, then divided by the count; misses,
+// outliers and hitless tracks keep bad = 1e100.
+int oracle_mesh_triangulate(int64_t npts, const int64_t* tb, const int32_t* img, const int32_t* image_cam,
+                            const double* wc, const double* focal, const double* center, const int32_t* Ks,
+                            const int64_t* doff, const double* dist, const double* dhalf, const double* uhalf,
+                            const double* pix, const uint8_t* inlier, double min_ray_dist, double max_ray_dist,
+                            int64_t nfaces, const float* verts, const uint32_t* faces, double* feat_xyz,
+                            double* pt_xyz) {
+  const double bad = 1.0e+100;
+  const int64_t nobs = npts > 0 ? tb[npts] : 0;
+  std::vector<float> ro(3 * nobs), rd(3 * nobs), th(nobs);
+  std::vector<int32_t> fh(nobs, -1);
+  std::vector<double> ctr(3 * nobs), wray(3 * nobs);
+  std::vector<uint8_t> want(nobs, 0);
+  for (int64_t o = 0; o < nobs; o++) {
+    if (!inlier[o]) continue;
+    const int im = img[o], cam = image_cam[im];
+    double u[2];
+    const int st = oracle_undistort(focal[cam], center + 2 * cam, dist + doff[cam], Ks[cam], dhalf + 2 * cam,
+                                    uhalf + 2 * cam, pix + 2 * o, u);
+    if (st != MVBA_OK) return st;
+    double cr[3] = {u[0] / focal[cam], u[1] / focal[cam], 1.0};
+    const double nrm = std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+    for (int q = 0; q < 3; q++) cr[q] = cr[q] / nrm;
+    Aff<double> a;
+    for (int q = 0; q < 9; q++) a.R[q] = wc[12 * im + q];
+    for (int q = 0; q < 3; q++) a.t[q] = wc[12 * im + 9 + q];
+    Aff<double> inv = affine_inverse(a);
+    for (int r = 0; r < 3; r++) {
+      wray[3 * o + r] = inv.R[3 * r] * cr[0] + inv.R[3 * r + 1] * cr[1] + inv.R[3 * r + 2] * cr[2];
+      ctr[3 * o + r] = inv.t[r];
+      ro[3 * o + r] = (float)inv.t[r];
+      rd[3 * o + r] = (float)wray[3 * o + r];
+    }
+    const float dn = std::sqrt(dot3f(&rd[3 * o], &rd[3 * o]));
+    for (int q = 0; q < 3; q++) rd[3 * o + q] = rd[3 * o + q] / dn;
+    want[o] = 1;
+  }
+  std::vector<int64_t> idx;
+  for (int64_t o = 0; o < nobs; o++)
+    if (want[o]) idx.push_back(o);
+  std::vector<float> ro2(3 * idx.size()), rd2(3 * idx.size()), t2(idx.size());
+  std::vector<int32_t> f2(idx.size());
+  for (size_t k = 0; k < idx.size(); k++)
+    for (int q = 0; q < 3; q++) {
+      ro2[3 * k + q] = ro[3 * idx[k] + q];
+      rd2[3 * k + q] = rd[3 * idx[k] + q];
+    }
+  oracle_ray_mesh((int64_t)idx.size(), ro2.data(), rd2.data(), (float)min_ray_dist, (float)max_ray_dist, nfaces, verts,
+                  faces, t2.data(), f2.data());
+  for (size_t k = 0; k < idx.size(); k++) {
+    th[idx[k]] = t2[k];
+    fh[idx[k]] = f2[k];
+  }
+  for (int64_t p = 0; p < npts; p++) {
+    double avg[3] = {0.0, 0.0, 0.0};
+    int num = 0;
+    for (int64_t o = tb[p]; o < tb[p + 1]; o++) {
+      double X[3] = {bad, bad, bad};
+      if (want[o] && fh[o] >= 0) {
+        const double t = (double)th[o];
+        for (int q = 0; q < 3; q++) X[q] = ctr[3 * o + q] + t * wray[3 * o + q];
+        for (int q = 0; q < 3; q++) avg[q] += X[q];
+        num++;
+      }
+      if (feat_xyz)
+        for (int q = 0; q < 3; q++) feat_xyz[3 * o + q] = X[q];
+    }
+    for (int q = 0; q < 3; q++) pt_xyz[3 * p + q] = num >= 1 ? avg[q] / (double)num : bad;
+  }
+  return MVBA_OK;
 }
 
 }  // extern "C"

@@ -52,6 +52,15 @@ def load():
     lib.oracle_distort.restype = C.c_int
     lib.oracle_distort.argtypes = [C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                                    C.c_void_p, C.c_int, C.c_double, C.c_double, C.c_void_p]
+    lib.oracle_depth_mesh_error.restype = C.c_int
+    lib.oracle_depth_mesh_error.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_double, C.c_void_p, C.c_void_p,
+                                            C.c_double, C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_void_p]
+    lib.oracle_ray_mesh.restype = None
+    lib.oracle_ray_mesh.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_float, C.c_float, C.c_int64,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.oracle_mesh_triangulate.restype = C.c_int
+    lib.oracle_mesh_triangulate.argtypes = [C.c_int64] + [C.c_void_p] * 13 + [C.c_double, C.c_double, C.c_int64] + \
+        [C.c_void_p] * 4
     lib.oracle_depth_error.restype = C.c_int
     lib.oracle_depth_error.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_double, C.c_void_p,
                                        C.c_double, C.c_double, C.c_double, C.c_int, C.c_void_p,
@@ -151,6 +160,24 @@ def depth_error(blocks, constant, weight, meas, sb, se, sc, mode=ANALYTIC):
     return r, J
 
 
+def depth_mesh_error(blocks, constant, weight, meas, mesh, sb, se, sc, mode=ANALYTIC):
+    """BracketedDepthMeshError (rig_calibrator.cc:641-673). blocks: 6 arrays (beg,
+    end, ref_to_cam, depth_to_image, scale, offset); J rows 3 x size_b per block."""
+    lib = load()
+    arrs = [np.ascontiguousarray(b, dtype=np.float64) for b in blocks]
+    ptrs = (C.c_void_p * 6)(*[a.ctypes.data for a in arrs])
+    const = np.ascontiguousarray(constant, dtype=np.uint8)
+    m = np.ascontiguousarray(meas, dtype=np.float64)
+    x = np.ascontiguousarray(mesh, dtype=np.float64)
+    r = np.empty(3)
+    J = np.zeros(3 * sum(a.size for a in arrs))
+    st = lib.oracle_depth_mesh_error(ptrs, arrs[3].size, const.ctypes.data, float(weight), m.ctypes.data,
+                                     x.ctypes.data, sb, se, sc, mode, r.ctypes.data, J.ctypes.data)
+    if st < 0:
+        raise OracleError(-st, "depth mesh error")
+    return r, J
+
+
 def residual_stats(residuals, name_ids, num_names):
     lib = load()
     r = np.ascontiguousarray(residuals, dtype=np.float64)
@@ -175,12 +202,22 @@ def evaluate_depth(problem, mode=ANALYTIC, apply_loss=False, robust_threshold=3.
     J = np.zeros((n, DJAC_ROWS)) if mode != RESIDUAL else None
     b = robust_threshold * robust_threshold
     cost = 0.0
+    mesh_xyz = getattr(problem, "depth_mesh_xyz", np.zeros((0, 3)))
     for j in range(n):
         blk = problem.depth_blocks[j]
-        blocks = [problem.block_values(int(x)) for x in blk]
-        const = problem.block_constant[blk]
-        rj, Jj = depth_error(blocks, const, problem.depth_weight[j], problem.depth_meas[j],
-                             *problem.depth_stamps[j], mode=mode)
+        if blk[5] == -1:
+            # BracketedDepthMeshError: blocks without xyz; the xyz rows stay zero
+            ids = [int(blk[q]) for q in (0, 1, 2, 3, 4, 6)]
+            six = [problem.block_values(x) for x in ids]
+            rj, J6 = depth_mesh_error(six, problem.block_constant[ids], problem.depth_weight[j],
+                                      problem.depth_meas[j], mesh_xyz[j], *problem.depth_stamps[j], mode=mode)
+            blocks = six[:5] + [np.zeros(3)] + six[5:]
+            Jj = np.concatenate([J6[:3 * (21 + six[3].size + 1)], np.zeros(9), J6[3 * (21 + six[3].size + 1):]])
+        else:
+            blocks = [problem.block_values(int(x)) for x in blk]
+            const = problem.block_constant[blk]
+            rj, Jj = depth_error(blocks, const, problem.depth_weight[j], problem.depth_meas[j],
+                                 *problem.depth_stamps[j], mode=mode)
         s2 = float(rj @ rj)
         sr = 1.0
         if apply_loss:
@@ -256,3 +293,42 @@ def flag_outliers(tracks, xyz, residuals, min_angle, max_err, inlier):
                              inl.ctypes.data, counts.ctypes.data)
     del d
     return inl, counts
+
+
+def ray_mesh(orig, dir, tmin, tmax, verts, faces):
+    """Closest hit of each ray, brute force over every face (rayint's test restated,
+    float). Returns (t [n] float32, -1 = miss; face [n] int32, -1 = miss)."""
+    lib = load()
+    o = np.ascontiguousarray(orig, dtype=np.float32).reshape(-1)
+    d = np.ascontiguousarray(dir, dtype=np.float32).reshape(-1)
+    v = np.ascontiguousarray(verts, dtype=np.float32).reshape(-1)
+    f = np.ascontiguousarray(faces, dtype=np.uint32).reshape(-1)
+    n = o.size // 3
+    t = np.empty(n, dtype=np.float32)
+    face = np.empty(n, dtype=np.int32)
+    lib.oracle_ray_mesh(C.c_int64(n), o.ctypes.data, d.ctypes.data, C.c_float(tmin), C.c_float(tmax),
+                        C.c_int64(f.size // 3), v.ctypes.data, f.ctypes.data, t.ctypes.data, face.ctypes.data)
+    return t, face
+
+
+def mesh_triangulate(tracks, inlier, min_ray_dist, max_ray_dist, verts, faces):
+    """meshTriangulations restated (oracle.cpp). Returns (feature_xyz [n_obs,3],
+    point_xyz [n_pts,3]) with bad = 1e100."""
+    lib = load()
+    d = tracks.desc()
+    ar = tracks._keep
+    inl = np.ascontiguousarray(inlier, dtype=np.uint8)
+    v = np.ascontiguousarray(verts, dtype=np.float32).reshape(-1)
+    f = np.ascontiguousarray(faces, dtype=np.uint32).reshape(-1)
+    fx = np.zeros((tracks.num_obs, 3))
+    px = np.zeros((tracks.num_points, 3))
+    st = lib.oracle_mesh_triangulate(C.c_int64(tracks.num_points), ar[9].ctypes.data, ar[10].ctypes.data,
+                                     ar[1].ctypes.data, ar[0].ctypes.data, ar[2].ctypes.data, ar[3].ctypes.data,
+                                     ar[4].ctypes.data, ar[5].ctypes.data, ar[6].ctypes.data, ar[7].ctypes.data,
+                                     ar[8].ctypes.data, ar[11].ctypes.data, inl.ctypes.data,
+                                     C.c_double(min_ray_dist), C.c_double(max_ray_dist), C.c_int64(f.size // 3),
+                                     v.ctypes.data, f.ctypes.data, fx.ctypes.data, px.ctypes.data)
+    if st != 0:
+        raise OracleError(st, "mesh_triangulate")
+    del d
+    return fx, px
