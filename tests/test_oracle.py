@@ -192,3 +192,40 @@ def test_oracle_depth_matches_mpmath_golden(oracle, ci):
         scale = max(np.abs(Jg).max(), 1e-300)
         assert np.abs(J[off:off + n] - Jg).max() <= 1e-8 * scale, (b, np.abs(J[off:off + n] - Jg).max() / scale)
         off += n
+
+
+# ------------------------------------------------------- depth-mesh golden vectors
+def _depth_mesh_golden():
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "depth_mesh_error_golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+DEPTH_MESH_CASES = _depth_mesh_golden()
+
+
+@pytest.mark.parametrize("ci", range(len(DEPTH_MESH_CASES)))
+def test_oracle_depth_mesh_matches_mpmath_golden(oracle, ci):
+    """BracketedDepthMeshError (rig_calibrator.cc:641-673): the oracle against the
+    50-digit mpmath restatement (tests/golden/make_golden_depth_mesh.py), rigid and
+    affine depth_to_image, reference / interpolated frames, scale != 1. Residuals
+    1e-12 relative, Jacobian 1e-8 of each block's largest entry; the numeric-diff
+    mode (the reference's own Jacobian) within 1e-6 of it."""
+    import numpy as np
+
+    c = DEPTH_MESH_CASES[ci]
+    blocks = [np.array(b) for b in c["blocks"]]
+    rg = np.array(c["residual"])
+    for mode, tol in ((oracle.ANALYTIC, 1e-8), (oracle.NUMDIFF, 1e-6)):
+        r, J = oracle.depth_mesh_error(blocks, np.zeros(6, np.uint8), c["weight"], c["meas"], c["mesh"],
+                                       *c["stamps"], mode=mode)
+        assert np.abs(r - rg).max() <= 1e-12 * max(np.abs(rg).max(), 1.0)
+        off = 0
+        for b, blk in enumerate(blocks):
+            n = 3 * blk.size
+            Jg = np.array(c["jacobian"][b])
+            scale = max(np.abs(Jg).max(), 1e-300)
+            assert np.abs(J[off:off + n] - Jg).max() <= tol * scale, (mode, b)
+            off += n
