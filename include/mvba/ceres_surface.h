@@ -5,6 +5,8 @@
 //   BracketedCamError::Create(meas, left, right, cam_stamp, block_sizes, cam_params)   :485-505
 //   BracketedDepthError::Create(weight, meas_depth_xyz, left, right, cam_stamp,
 //                               block_sizes)                                           :586-600
+//   BracketedDepthMeshError::Create(weight, meas_depth_xyz, mesh_xyz, left, right,
+//                                   cam_stamp, block_sizes)                            :677-693
 //   XYZError::Create(ref_xyz, block_sizes, weight)                                     :728-741
 //   problem.AddResidualBlock(cost, loss, <blocks>...)      :1695-1699, :1779-1785, :1869-1894
 //
@@ -13,7 +15,7 @@
 //       cam_params.GetDistortion().size(), cam_params.GetDistortedHalfSize().data(),
 //       {beg, end, ref_to_cam, xyz, offset, focal, center, dist});
 //   problem.AddResidualBlock(cost, loss, beg, end, ref_to_cam, xyz, offset, focal, center, dist);
-//   ... batch.CreateDepth(...), batch.CreateXyz(...) likewise ...
+//   ... batch.CreateDepth(...), batch.CreateDepthMesh(...), batch.CreateXyz(...) likewise ...
 //   options.evaluation_callback = batch.callback();   // Ceres 1.14 (2.x: Problem::Options)
 //
 // Semantics: Evaluate() returns what the reference functor + numeric
@@ -167,6 +169,35 @@ class BracketedCamBatch {
     return new GpuBatchCost(this, kDepth, (int64_t)res_[kDepth].size() - 1, 3, block_sizes);
   }
 
+  // Mirror of BracketedDepthMeshError::Create (rig_calibrator.cc:677-693) with the
+  // AddResidualBlock blocks (:1824-1828): beg, end, ref_to_cam, depth_to_image (7
+  // or 12), scale, offset; the mesh point is data (no point block).
+  ceres::CostFunction* CreateDepthMesh(double weight, const double meas_depth_xyz[3], const double mesh_xyz[3],
+                                       double left_ref_stamp, double right_ref_stamp, double cam_stamp,
+                                       const std::vector<int>& block_sizes, const std::array<double*, 6>& blocks) {
+    if (block_sizes.size() != 6 || block_sizes[0] != 7 || block_sizes[1] != 7 || block_sizes[2] != 7 ||
+        (block_sizes[3] != 7 && block_sizes[3] != 12) || block_sizes[4] != 1 || block_sizes[5] != 1)
+      throw std::runtime_error("BracketedDepthMeshError: The block sizes were not set up properly.");
+    check_open();
+    Residual r;
+    r.nblocks = 6;
+    for (int b = 0; b < 6; b++) {
+      r.block[b] = register_block(blocks[b], block_sizes[b]);
+      r.width[b] = block_sizes[b];
+    }
+    r.weight = weight;
+    r.mesh = true;
+    for (int k = 0; k < 3; k++) {
+      r.xyz[k] = meas_depth_xyz[k];
+      r.mesh_xyz[k] = mesh_xyz[k];
+    }
+    r.stamps[0] = left_ref_stamp;
+    r.stamps[1] = right_ref_stamp;
+    r.stamps[2] = cam_stamp;
+    res_[kDepth].push_back(r);
+    return new GpuBatchCost(this, kDepth, (int64_t)res_[kDepth].size() - 1, 3, block_sizes);
+  }
+
   // Mirror of XYZError::Create (rig_calibrator.cc:728-741) on one point block.
   ceres::CostFunction* CreateXyz(const double ref_xyz[3], const std::vector<int>& block_sizes, double weight,
                                  double* xyz) {
@@ -237,6 +268,8 @@ class BracketedCamBatch {
     double stamps[3] = {0, 0, 0};
     double weight = 0;
     double xyz[3] = {0, 0, 0};
+    bool mesh = false;            // BracketedDepthMeshError (kDepth family, 6 blocks)
+    double mesh_xyz[3] = {0, 0, 0};
   };
   struct Callback : public ceres::EvaluationCallback {
     explicit Callback(BracketedCamBatch* b) : batch(b) {}
@@ -284,6 +317,8 @@ class BracketedCamBatch {
     const int64_t n = (int64_t)C.size(), nd = (int64_t)D.size(), nx = (int64_t)X.size();
     std::vector<int32_t> rb(8 * n), rc(n), db(7 * nd), xb(nx);
     std::vector<double> rm(2 * n), rs(3 * n), dm(3 * nd), dw(nd), ds(3 * nd), xr(3 * nx), xw(nx), xt(nx, 1.0);
+    std::vector<double> dmesh(3 * nd, 0.0);
+    bool any_mesh = false;
     for (int64_t i = 0; i < n; i++) {
       for (int b = 0; b < 8; b++) rb[8 * i + b] = C[i].block[b];
       rc[i] = C[i].cam;
@@ -292,7 +327,14 @@ class BracketedCamBatch {
       for (int k = 0; k < 3; k++) rs[3 * i + k] = C[i].stamps[k];
     }
     for (int64_t j = 0; j < nd; j++) {
-      for (int b = 0; b < 7; b++) db[7 * j + b] = D[j].block[b];
+      if (D[j].mesh) {  // 6 blocks: the MVBA_DBLK_XYZ slot is -1
+        for (int b = 0; b < 7; b++)
+          db[7 * j + b] = b < MVBA_DBLK_XYZ ? D[j].block[b] : b == MVBA_DBLK_XYZ ? -1 : D[j].block[b - 1];
+        for (int k = 0; k < 3; k++) dmesh[3 * j + k] = D[j].mesh_xyz[k];
+        any_mesh = true;
+      } else {
+        for (int b = 0; b < 7; b++) db[7 * j + b] = D[j].block[b];
+      }
       for (int k = 0; k < 3; k++) {
         dm[3 * j + k] = D[j].xyz[k];
         ds[3 * j + k] = D[j].stamps[k];
@@ -332,6 +374,7 @@ class BracketedCamBatch {
     d.xyz_ref = xr.data();
     d.xyz_weight = xw.data();
     d.xyz_threshold = xt.data();
+    d.depth_mesh_xyz = any_mesh ? dmesh.data() : nullptr;
     mvba_options o;
     std::memset(&o, 0, sizeof(o));
     o.device = device_;
@@ -435,8 +478,10 @@ class BracketedCamBatch {
                                   MVBA_DJAC_BASE_DEPTH_TO_IMAGE, MVBA_DJAC_BASE_SCALE, MVBA_DJAC_BASE_XYZ,
                                   MVBA_DJAC_BASE_OFFSET};
       const double* src = J_[kDepth].data() + (size_t)i * MVBA_DJAC_ROWS;
-      for (int b = 0; b < 7; b++)
-        if (jacobians[b]) std::memcpy(jacobians[b], src + base[b], sizeof(double) * 3 * r.width[b]);
+      for (int b = 0; b < r.nblocks; b++) {
+        const int row = base[r.mesh && b >= MVBA_DBLK_XYZ ? b + 1 : b];  // mesh blocks skip the xyz rows
+        if (jacobians[b]) std::memcpy(jacobians[b], src + row, sizeof(double) * 3 * r.width[b]);
+      }
     } else {
       if (jacobians[0]) std::memcpy(jacobians[0], J_[kXyz].data() + (size_t)i * 9, sizeof(double) * 9);
     }

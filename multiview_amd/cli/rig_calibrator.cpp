@@ -12,10 +12,14 @@
 // every per-observation and per-track computation runs through libmvba. There
 // is no CPU compute path: --device=cpu is refused, and a missing GPU is an error.
 //
+// --mesh (a PLY file): after each triangulation the inlier rays are intersected
+// with the mesh on the GPU (meshTriangulations, mvba_mesh_triangulate), which
+// feeds --depth_mesh_weight (BracketedDepthMeshError) and --mesh_tri_weight
+// (XYZError to the track's mean hit) blocks.
 // Out of scope: feature detection/matching (--num_overlaps > 0),
-// meshes (--mesh, --mesh_tri_weight, --depth_mesh_weight, --out_texture_dir),
-// registration, voxblox export, saving transformed clouds and match files. These
-// flags are parsed and rejected unless left at their defaults.
+// texturing (--out_texture_dir), registration, voxblox export, saving transformed
+// clouds and match files. These flags are parsed and rejected unless left at
+// their defaults.
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -51,6 +55,9 @@ namespace rigcal {
 [[noreturn]] static void fatal(const std::string& msg) { throw std::runtime_error(msg); }
 
 // ---------------------------------------------------------------- flags
+// meshTriangulations' marker for "no intersection" (rig_calibrator.cc:1546)
+constexpr double kBadXyz = 1.0e+100;
+
 struct Flags {
   double robust_threshold = 3.0;
   int num_iterations = 20;
@@ -107,9 +114,12 @@ static std::vector<FlagDef> flag_table(Flags& F) {
       {"timestamp_offsets_max_change", 'd', &F.timestamp_offsets_max_change,
        "Maximum change of a floated timestamp offset."},
       {"depth_tri_weight", 'd', &F.depth_tri_weight, "Weight of the depth-to-triangulated-point constraint."},
-      {"mesh", 's', &F.mesh, "(not supported in this build) mesh constraint."},
-      {"mesh_tri_weight", 'd', &F.mesh_tri_weight, "(not supported in this build)"},
-      {"depth_mesh_weight", 'd', &F.depth_mesh_weight, "(not supported in this build)"},
+      {"mesh", 's', &F.mesh, "Use this mesh to help constrain the calibration (in .ply format). Must use a "
+                             "positive --mesh_tri_weight."},
+      {"mesh_tri_weight", 'd', &F.mesh_tri_weight, "Weight of the constraint that triangulated points stay close "
+                                                  "to a preexisting mesh."},
+      {"depth_mesh_weight", 'd', &F.depth_mesh_weight, "Weight of the constraint that the depth clouds stay close "
+                                                      "to the mesh."},
       {"tri_weight", 'd', &F.tri_weight, "Weight keeping triangulated points near their initial values."},
       {"tri_robust_threshold", 'd', &F.tri_robust_threshold, "Cauchy threshold of the --tri_weight constraint."},
       {"affine_depth_to_image", 'b', &F.affine_depth_to_image, "Model depth-to-image as a general affine map."},
@@ -119,8 +129,10 @@ static std::vector<FlagDef> flag_table(Flags& F) {
       {"max_reprojection_error", 'd', &F.max_reprojection_error, "Outlier reprojection error after a pass (pixels)."},
       {"min_triangulation_angle", 'd', &F.min_triangulation_angle, "Minimum ray convergence angle (degrees)."},
       {"out_texture_dir", 's', &F.out_texture_dir, "(not supported in this build)"},
-      {"min_ray_dist", 'd', &F.min_ray_dist, "(mesh only)"},
-      {"max_ray_dist", 'd', &F.max_ray_dist, "(mesh only)"},
+      {"min_ray_dist", 'd', &F.min_ray_dist, "Minimum search distance along a ray when intersecting it with "
+                                             "the mesh, in meters."},
+      {"max_ray_dist", 'd', &F.max_ray_dist, "Maximum search distance along a ray when intersecting it with "
+                                             "the mesh, in meters."},
       {"registration", 'b', &F.registration, "(not supported in this build)"},
       {"hugin_file", 's', &F.hugin_file, "(registration only)"},
       {"xyz_file", 's', &F.xyz_file, "(registration only)"},
@@ -261,12 +273,11 @@ static void parameter_validation(const Flags& F) {
     fatal(what + " is outside this build's scope (SURVEY.md §8(b)); leave it at its default.");
   };
   if (F.num_overlaps > 0) unsupported("--num_overlaps > 0 (feature detection and matching)");
-  if (F.mesh != "") unsupported("--mesh");
-  if (F.mesh_tri_weight > 0 || F.depth_mesh_weight > 0) unsupported("--mesh_tri_weight / --depth_mesh_weight");
   if (F.registration) unsupported("--registration");
   if (F.export_to_voxblox) unsupported("--export_to_voxblox");
   if (F.save_transformed_depth_clouds) unsupported("--save_transformed_depth_clouds");
   if (F.save_matches) unsupported("--save_matches");
+  if (F.out_texture_dir != "") unsupported("--out_texture_dir (texturing)");
   if (F.device.rfind("gpu", 0) != 0)
     fatal("--device=" + F.device + ": this build has no CPU compute path; use --device=gpu or gpu:<ordinal>.");
   if (F.num_gpus < 1) fatal("--num_gpus must be positive.");
@@ -577,10 +588,15 @@ struct DepthRes {
   double meas[3];
   double stamps[3];
   int pid;
+  double weight;
+  bool mesh;           // BracketedDepthMeshError (no point block)
+  double mesh_xyz[3];
 };
 struct XyzRes {
   int pid;
   double ref[3];
+  double weight, threshold;
+  uint8_t kind;  // 0 tri, 1 mesh_tri
 };
 
 struct Plan {
@@ -599,6 +615,9 @@ struct Shard {
   BlockSet blocks;
   std::vector<int32_t> res_blocks, res_cam, dep_blocks, xyz_block;
   std::vector<double> res_meas, res_stamps, dep_meas, dep_weight, dep_stamps, xyz_ref, xyz_weight, xyz_thr;
+  std::vector<double> dep_mesh;     // [3 per depth block] mesh point (BracketedDepthMeshError rows)
+  std::vector<uint8_t> dep_is_mesh, xyz_kind;
+  bool any_mesh = false;
   std::vector<int32_t> cam_dist_size;
   std::vector<double> cam_half;
   std::vector<int64_t> res_feature;  // residual -> feature
@@ -646,8 +665,9 @@ static std::vector<std::string> group_labels(const std::vector<std::string>& nam
     labels.push_back(n + "_pix_x");
     labels.push_back(n + "_pix_y");
   }
-  for (const char* a : {"x", "y", "z"}) labels.push_back(std::string("depth_tri_") + a + "_m");
-  for (const char* a : {"x", "y", "z"}) labels.push_back(std::string("tri_") + a + "_m");
+  // mvba_residual_stats groups: depth_tri, tri, depth_mesh, mesh_tri
+  for (const char* kind : {"depth_tri_", "tri_", "depth_mesh_", "mesh_tri_"})
+    for (const char* a : {"x", "y", "z"}) labels.push_back(std::string(kind) + a + "_m");
   return labels;
 }
 
@@ -656,7 +676,7 @@ static std::vector<std::string> group_labels(const std::vector<std::string>& nam
 // and the percentiles picked on the host (percentiles do not merge).
 static void residual_stats(std::vector<Shard>& shards, const std::vector<std::string>& names,
                            const std::string& tag) {
-  const size_t ng = 2 * names.size() + 6;
+  const size_t ng = 2 * names.size() + 12;
   const auto labels = group_labels(names);
   std::vector<StatRow> rows;
   if (shards.size() == 1) {
@@ -678,10 +698,12 @@ static void residual_stats(std::vector<Shard>& shards, const std::vector<std::st
         for (int k = 0; k < 2; k++) vals[2 * (size_t)s.res_cam[(size_t)i] + (size_t)k].push_back(std::fabs(r[2 * (size_t)i + (size_t)k]));
       for (int64_t i = 0; i < nd; i++)
         for (int k = 0; k < 3; k++)
-          vals[2 * names.size() + (size_t)k].push_back(std::fabs(rd[3 * (size_t)i + (size_t)k] / s.dep_weight[(size_t)i]));
+          vals[2 * names.size() + (s.dep_is_mesh[(size_t)i] ? 6 : 0) + (size_t)k].push_back(
+              std::fabs(rd[3 * (size_t)i + (size_t)k] / s.dep_weight[(size_t)i]));
       for (int64_t i = 0; i < nx; i++)
         for (int k = 0; k < 3; k++)
-          vals[2 * names.size() + 3 + (size_t)k].push_back(std::fabs(rx[3 * (size_t)i + (size_t)k] / s.xyz_weight[(size_t)i]));
+          vals[2 * names.size() + (s.xyz_kind[(size_t)i] ? 9 : 3) + (size_t)k].push_back(
+              std::fabs(rx[3 * (size_t)i + (size_t)k] / s.xyz_weight[(size_t)i]));
     }
     for (size_t g = 0; g < ng; g++) {
       auto& v = vals[g];
@@ -922,6 +944,27 @@ static int run(int argc, char** argv) {
   if (F.calibrator_num_passes > 0 && (mvba_device_count(&ndev) != MVBA_OK || ndev < 1))
     fatal("No HIP device is available (this build has no CPU compute path).");
   double placeholder = 0.0;  // distortion_placeholder (:1608)
+  // --mesh: loadMeshBuildTree (texture_processing.cc:264-285) -> BVH on the GPU
+  mvba_mesh* mesh = nullptr;
+  std::vector<double> mesh_feat_xyz, mesh_pt_xyz;
+  if (F.mesh != "" && F.calibrator_num_passes > 0) {
+    std::cout << "Loading mesh: " << F.mesh << std::endl;
+    std::vector<float> mv;
+    std::vector<uint32_t> mf;
+    std::string err;
+    if (!read_ply_mesh(F.mesh, mv, mf, err)) fatal(err);
+    std::cout << "Number of faces: " << mf.size() / 3 << " faces.\n";
+    const auto tb = Clock::now();
+    mvba_mesh_desc md{};
+    md.num_vertices = (int64_t)(mv.size() / 3);
+    md.vertices = mv.data();
+    md.num_faces = (int64_t)(mf.size() / 3);
+    md.faces = mf.data();
+    if (mvba_mesh_create(&md, device0, &mesh) != MVBA_OK) fatal(std::string("mesh: ") + mvba_mesh_error());
+    std::cout << "Building the tree took: " << secs(tb) << " seconds\n";
+    mesh_feat_xyz.assign(3 * (size_t)nobs, kBadXyz);
+    mesh_pt_xyz.assign(3 * (size_t)npid, kBadXyz);
+  }
   double t_tri = 0, t_build = 0, t_create = 0, t_stats = 0, t_solve = 0, t_flag = 0;
   std::vector<double> residuals_after;  // per feature, [2*nobs]
   for (int pass = 0; pass < F.calibrator_num_passes; pass++) {
@@ -932,6 +975,13 @@ static int run(int argc, char** argv) {
       mvba_tracks_desc d = tracks_desc();
       if (mvba_triangulate(&d, device0, inlier.data(), xyz_vec.data()) != MVBA_OK)
         fatal(std::string("triangulation: ") + mvba_tracks_error());
+    }
+    // where each inlier ray meets the mesh (meshTriangulations, :1581-1588)
+    if (mesh) {
+      mvba_tracks_desc d = tracks_desc();
+      if (mvba_mesh_triangulate(&d, mesh, inlier.data(), F.min_ray_dist, F.max_ray_dist, mesh_feat_xyz.data(),
+                                mesh_pt_xyz.data()) != MVBA_OK)
+        fatal(std::string("mesh intersection: ") + mvba_tracks_error() + mvba_mesh_error());
     }
     t_tri += secs(t0);
     t0 = Clock::now();
@@ -1003,15 +1053,48 @@ static int run(int argc, char** argv) {
           std::memcpy(dr.meas, dxyz, sizeof(dxyz));
           std::memcpy(dr.stamps, r.stamps, sizeof(dr.stamps));
           dr.pid = pid;
+          dr.weight = F.depth_tri_weight;
+          plan.depth.push_back(dr);
+          if (!F.float_scale || F.affine_depth_to_image) plan.constant.insert(&depth_scales[(size_t)t]);
+          if (!dti_to_float.count(cam_names[(size_t)t])) plan.constant.insert(dti);
+        }
+        // depth-to-mesh constraint (:1796-1834): the feature's mesh hit vs its depth point
+        if (mesh && F.depth_mesh_weight > 0 && mesh_feat_xyz[3 * (size_t)o] != kBadXyz &&
+            depth_value(cam.cloud.get(), r.meas[0], r.meas[1], dxyz)) {
+          DepthRes dr{};
+          double* dti = &depth_to_image_vec[(size_t)num_depth_params * (size_t)t];
+          double* dblk[7] = {beg, end, r2c, dti, &depth_scales[(size_t)t], nullptr, &offsets[(size_t)t]};
+          const int dbs[7] = {7, 7, 7, num_depth_params, 1, 0, 1};
+          std::memcpy(dr.blk, dblk, sizeof(dblk));
+          std::memcpy(dr.bsize, dbs, sizeof(dbs));
+          std::memcpy(dr.meas, dxyz, sizeof(dxyz));
+          std::memcpy(dr.stamps, r.stamps, sizeof(dr.stamps));
+          std::memcpy(dr.mesh_xyz, &mesh_feat_xyz[3 * (size_t)o], sizeof(dr.mesh_xyz));
+          dr.pid = pid;
+          dr.weight = F.depth_mesh_weight;
+          dr.mesh = true;
           plan.depth.push_back(dr);
           if (!F.float_scale || F.affine_depth_to_image) plan.constant.insert(&depth_scales[(size_t)t]);
           if (!dti_to_float.count(cam_names[(size_t)t])) plan.constant.insert(dti);
         }
       }
+      // mesh-to-triangulated-point constraint (:1857-1877), then --tri_weight (:1880-1898)
+      if (mesh && tri_inlier && F.mesh_tri_weight > 0 && mesh_pt_xyz[3 * (size_t)pid] != kBadXyz) {
+        XyzRes x{};
+        x.pid = pid;
+        std::memcpy(x.ref, &mesh_pt_xyz[3 * (size_t)pid], sizeof(x.ref));
+        x.weight = F.mesh_tri_weight;
+        x.threshold = F.robust_threshold;
+        x.kind = 1;
+        plan.xyz.push_back(x);
+      }
       if (F.tri_weight > 0.0 && tri_inlier) {
         XyzRes x{};
         x.pid = pid;
         std::memcpy(x.ref, &xyz_orig[3 * (size_t)pid], sizeof(x.ref));
+        x.weight = F.tri_weight;
+        x.threshold = F.tri_robust_threshold;
+        x.kind = 0;
         plan.xyz.push_back(x);
       }
     }
@@ -1079,17 +1162,22 @@ static int run(int argc, char** argv) {
       }
       for (const auto& r : plan.depth) {
         if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
-        for (int b = 0; b < 7; b++) S.dep_blocks.push_back(b == MVBA_DBLK_XYZ ? point(r.pid) : r.id[b]);
+        for (int b = 0; b < 7; b++)
+          S.dep_blocks.push_back(b == MVBA_DBLK_XYZ ? (r.mesh ? -1 : point(r.pid)) : r.id[b]);
         S.dep_meas.insert(S.dep_meas.end(), r.meas, r.meas + 3);
-        S.dep_weight.push_back(F.depth_tri_weight);
+        S.dep_weight.push_back(r.weight);
         S.dep_stamps.insert(S.dep_stamps.end(), r.stamps, r.stamps + 3);
+        S.dep_mesh.insert(S.dep_mesh.end(), r.mesh_xyz, r.mesh_xyz + 3);
+        S.dep_is_mesh.push_back(r.mesh ? 1 : 0);
+        S.any_mesh = S.any_mesh || r.mesh;
       }
       for (const auto& r : plan.xyz) {
         if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
         S.xyz_block.push_back(point(r.pid));
         S.xyz_ref.insert(S.xyz_ref.end(), r.ref, r.ref + 3);
-        S.xyz_weight.push_back(F.tri_weight);
-        S.xyz_thr.push_back(F.tri_robust_threshold);
+        S.xyz_weight.push_back(r.weight);
+        S.xyz_thr.push_back(r.threshold);
+        S.xyz_kind.push_back(r.kind);
       }
       for (int t = 0; t < ncam; t++) {
         S.cam_dist_size.push_back((int32_t)dist[(size_t)t].size());
@@ -1120,6 +1208,8 @@ static int run(int argc, char** argv) {
       d.xyz_ref = S.xyz_ref.data();
       d.xyz_weight = S.xyz_weight.data();
       d.xyz_threshold = S.xyz_thr.data();
+      d.depth_mesh_xyz = S.any_mesh ? S.dep_mesh.data() : nullptr;
+      d.xyz_kind = S.xyz_kind.data();
       mvba_options o{};
       o.device = S.device;
       const auto tc = Clock::now();
@@ -1274,6 +1364,8 @@ static int run(int argc, char** argv) {
     }
     t_flag += secs(t0);
   }
+
+  if (mesh) mvba_mesh_destroy(mesh);
 
   // outputs (:1989-2038)
   for (int t = 0; t < ncam; t++) {

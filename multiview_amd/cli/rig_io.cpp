@@ -1,7 +1,9 @@
 // rig_io.cpp — see rig_io.h for the reference functions each routine follows.
 #include "rig_io.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <cstdint>
 #include <cstdlib>
 #include <filesystem>
@@ -403,6 +405,173 @@ void save_camera_poses(const std::string& out_dir, const std::vector<std::string
   f << "# image_file world_to_image_transform\n";
   for (size_t it = 0; it < image_names.size(); it++)
     f << image_names[it] << " " << affine_to_str(world_to_cam[it]) << "\n";
+}
+
+// ---------------------------------------------------------------- PLY meshes
+namespace {
+
+struct PlyProp {
+  std::string name, type, count_type;  // count_type non-empty: list property
+};
+struct PlyElem {
+  std::string name;
+  int64_t count = 0;
+  std::vector<PlyProp> props;
+};
+
+int ply_type_size(const std::string& t) {
+  if (t == "char" || t == "uchar" || t == "int8" || t == "uint8") return 1;
+  if (t == "short" || t == "ushort" || t == "int16" || t == "uint16") return 2;
+  if (t == "int" || t == "uint" || t == "float" || t == "int32" || t == "uint32" || t == "float32") return 4;
+  if (t == "double" || t == "float64") return 8;
+  return 0;
+}
+
+// One scalar of type t from a binary stream (swapping bytes when big endian).
+bool ply_read_bin(std::istream& in, const std::string& t, bool big, double* out) {
+  unsigned char b[8];
+  const int n = ply_type_size(t);
+  if (n == 0 || !in.read(reinterpret_cast<char*>(b), n)) return false;
+  if (big) std::reverse(b, b + n);
+  if (t == "char" || t == "int8") *out = (double)(int8_t)b[0];
+  else if (t == "uchar" || t == "uint8") *out = (double)b[0];
+  else if (t == "short" || t == "int16") { int16_t v; std::memcpy(&v, b, 2); *out = v; }
+  else if (t == "ushort" || t == "uint16") { uint16_t v; std::memcpy(&v, b, 2); *out = v; }
+  else if (t == "int" || t == "int32") { int32_t v; std::memcpy(&v, b, 4); *out = v; }
+  else if (t == "uint" || t == "uint32") { uint32_t v; std::memcpy(&v, b, 4); *out = v; }
+  else if (t == "float" || t == "float32") { float v; std::memcpy(&v, b, 4); *out = v; }
+  else { double v; std::memcpy(&v, b, 8); *out = v; }
+  return true;
+}
+
+}  // namespace
+
+bool read_ply_mesh(const std::string& path, std::vector<float>& vertices, std::vector<uint32_t>& faces,
+                   std::string& err) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) {
+    err = "Cannot open mesh file: " + path;
+    return false;
+  }
+  std::string line;
+  std::getline(in, line);
+  if (line.rfind("ply", 0) != 0) {
+    err = "Not a PLY file: " + path;
+    return false;
+  }
+  std::string format;
+  std::vector<PlyElem> elems;
+  while (std::getline(in, line)) {
+    if (!line.empty() && line.back() == '\r') line.pop_back();
+    std::istringstream is(line);
+    std::string key;
+    is >> key;
+    if (key == "format") {
+      is >> format;
+    } else if (key == "element") {
+      PlyElem e;
+      is >> e.name >> e.count;
+      elems.push_back(e);
+    } else if (key == "property") {
+      if (elems.empty()) {
+        err = "PLY property before any element: " + path;
+        return false;
+      }
+      PlyProp p;
+      std::string t;
+      is >> t;
+      if (t == "list") {
+        is >> p.count_type >> p.type >> p.name;
+      } else {
+        p.type = t;
+        is >> p.name;
+      }
+      elems.back().props.push_back(p);
+    } else if (key == "end_header") {
+      break;
+    }
+  }
+  const bool ascii = format == "ascii", big = format == "binary_big_endian";
+  if (!ascii && format != "binary_little_endian" && !big) {
+    err = "Unsupported PLY format '" + format + "': " + path;
+    return false;
+  }
+  vertices.clear();
+  faces.clear();
+  for (const PlyElem& e : elems) {
+    const bool is_vertex = e.name == "vertex", is_face = e.name == "face";
+    int ix = -1, iy = -1, iz = -1, iface = -1;
+    for (size_t k = 0; k < e.props.size(); k++) {
+      if (e.props[k].name == "x") ix = (int)k;
+      if (e.props[k].name == "y") iy = (int)k;
+      if (e.props[k].name == "z") iz = (int)k;
+      if (!e.props[k].count_type.empty() && (e.props[k].name == "vertex_indices" || e.props[k].name == "vertex_index"))
+        iface = (int)k;
+    }
+    if (is_vertex && (ix < 0 || iy < 0 || iz < 0)) {
+      err = "PLY vertices without x, y, z: " + path;
+      return false;
+    }
+    if (is_face && iface < 0) {
+      err = "PLY faces without vertex_indices: " + path;
+      return false;
+    }
+    std::vector<double> row;
+    for (int64_t r = 0; r < e.count; r++) {
+      std::istringstream ls;
+      if (ascii) {
+        if (!std::getline(in, line)) {
+          err = "Truncated PLY file: " + path;
+          return false;
+        }
+        ls.str(line);
+      }
+      auto scalar = [&](const std::string& t, double* v) -> bool {
+        if (ascii) return static_cast<bool>(ls >> *v);
+        return ply_read_bin(in, t, big, v);
+      };
+      float xyz[3] = {0, 0, 0};
+      for (size_t k = 0; k < e.props.size(); k++) {
+        const PlyProp& p = e.props[k];
+        if (p.count_type.empty()) {
+          double v;
+          if (!scalar(p.type, &v)) {
+            err = "Truncated PLY file: " + path;
+            return false;
+          }
+          if ((int)k == ix) xyz[0] = (float)v;
+          if ((int)k == iy) xyz[1] = (float)v;
+          if ((int)k == iz) xyz[2] = (float)v;
+          continue;
+        }
+        double cnt;
+        if (!scalar(p.count_type, &cnt)) {
+          err = "Truncated PLY file: " + path;
+          return false;
+        }
+        row.assign((size_t)cnt, 0.0);
+        for (size_t q = 0; q < row.size(); q++)
+          if (!scalar(p.type, &row[q])) {
+            err = "Truncated PLY file: " + path;
+            return false;
+          }
+        if (is_face && (int)k == iface) {
+          if (row.size() != 3) {
+            err = "Only triangle faces are supported in " + path;
+            return false;
+          }
+          for (double v : row) faces.push_back((uint32_t)v);
+        }
+      }
+      if (is_vertex) vertices.insert(vertices.end(), xyz, xyz + 3);
+    }
+  }
+  for (uint32_t f : faces)
+    if ((size_t)f >= vertices.size() / 3) {
+      err = "PLY face index out of range in " + path;
+      return false;
+    }
+  return true;
 }
 
 }  // namespace rigcal

@@ -104,6 +104,14 @@ void save_camera_poses(const std::string& out_dir, const std::vector<std::string
 
 void create_dir(const std::string& dir);
 
+// mve::geom::load_ply_mesh as loadMeshBuildTree uses it (texture_processing.cc:268):
+// "ply" header, format ascii 1.0 / binary_little_endian 1.0 / binary_big_endian
+// 1.0; element vertex with float/double x y z (other properties skipped); element
+// face with a list property vertex_indices (or vertex_index) of triangles; other
+// elements skipped. False with a message on anything else.
+bool read_ply_mesh(const std::string& path, std::vector<float>& vertices, std::vector<uint32_t>& faces,
+                   std::string& err);
+
 }  // namespace rigcal
 
 #endif  // MVBA_CLI_RIG_IO_H_

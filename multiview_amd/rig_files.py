@@ -153,3 +153,26 @@ def write_dataset(rig: Rig, out_dir: str, depth_to_image=None) -> dict:
     write_nvm(rig, nvm, names, init_world_to_cam(rig))
     nclouds = write_depth_clouds(rig, names, depth_to_image)
     return {"rig_config": cfg, "nvm": nvm, "images": names, "num_clouds": nclouds}
+
+
+def write_ply(path: str, vertices, faces, binary: bool = True) -> None:
+    """A triangle mesh as PLY (what --mesh reads, mve::geom::load_ply_mesh):
+    float x y z per vertex, "list uchar int vertex_indices" per face."""
+    V = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    F = np.ascontiguousarray(faces, dtype=np.int64).reshape(-1, 3)
+    head = ("ply\nformat {} 1.0\nelement vertex {}\nproperty float x\nproperty float y\nproperty float z\n"
+            "element face {}\nproperty list uchar int vertex_indices\nend_header\n").format(
+                "binary_little_endian" if binary else "ascii", V.shape[0], F.shape[0])
+    with open(path, "wb") as f:
+        f.write(head.encode())
+        if binary:
+            f.write(V.astype("<f4").tobytes())
+            rec = np.zeros(F.shape[0], dtype=[("n", "u1"), ("v", "<i4", 3)])
+            rec["n"] = 3
+            rec["v"] = F
+            f.write(rec.tobytes())
+        else:
+            for v in V:
+                f.write(("%.9g %.9g %.9g\n" % tuple(v)).encode())
+            for q in F:
+                f.write(("3 %d %d %d\n" % tuple(q)).encode())

@@ -125,11 +125,49 @@ def _load_cloud(path):
     return data.reshape(int(rows), int(cols), int(ch))
 
 
+def read_ply(path):
+    """Vertices (float32 x y z) and triangle faces of an ascii or binary
+    little-endian PLY with float x, y, z vertex properties and a uchar/int list
+    of int/uint vertex indices (what tests write)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    end = data.index(b"end_header") + len(b"end_header")
+    end = data.index(b"\n", end) + 1
+    head = data[:end].decode().splitlines()
+    fmt = next(ln.split()[1] for ln in head if ln.startswith("format"))
+    elems = []
+    for ln in head:
+        w = ln.split()
+        if w[:1] == ["element"]:
+            elems.append([w[1], int(w[2]), []])
+        elif w[:1] == ["property"]:
+            elems[-1][2].append(w[1:])
+    nv = next(e[1] for e in elems if e[0] == "vertex")
+    nf = next(e[1] for e in elems if e[0] == "face")
+    vprops = next(e[2] for e in elems if e[0] == "vertex")
+    if fmt == "ascii":
+        rows = data[end:].decode().split("\n")
+        V = np.array([[float(x) for x in rows[i].split()[:len(vprops)]] for i in range(nv)])
+        names = [q[-1] for q in vprops]
+        V = V[:, [names.index("x"), names.index("y"), names.index("z")]].astype(np.float32)
+        F = np.array([[int(x) for x in rows[nv + i].split()[1:4]] for i in range(nf)], dtype=np.uint32)
+        return V, F
+    tmap = {"float": "<f4", "float32": "<f4", "double": "<f8", "float64": "<f8", "uchar": "u1", "uint8": "u1",
+            "int": "<i4", "int32": "<i4", "uint": "<u4", "uint32": "<u4"}
+    vt = np.dtype([(q[-1], tmap[q[0]]) for q in vprops])
+    V = np.frombuffer(data, dtype=vt, count=nv, offset=end)
+    fp = next(e[2] for e in elems if e[0] == "face")[0]  # list <count> <index> vertex_indices
+    ft = np.dtype([("n", tmap[fp[1]]), ("v", tmap[fp[2]], 3)])
+    F = np.frombuffer(data, dtype=ft, count=nf, offset=end + nv * vt.itemsize)
+    return np.stack([V["x"], V["y"], V["z"]], 1).astype(np.float32), F["v"].astype(np.uint32)
+
+
 def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_threshold=3.0, bracket_len=0.6,
         intrinsics_to_float="", rig_transforms_to_float="", camera_poses_to_float="", no_rig=False,
         depth_tri_weight=0.0, depth_to_image_transforms_to_float="", float_scale=False, tri_weight=0.0,
         tri_robust_threshold=0.0, min_triangulation_angle=0.5, max_reprojection_error=25.0,
-        parameter_tolerance=1e-12, timestamp_offsets_max_change=1.0):
+        parameter_tolerance=1e-12, timestamp_offsets_max_change=1.0, mesh="", mesh_tri_weight=0.0,
+        depth_mesh_weight=0.0, min_ray_dist=0.0, max_ray_dist=100.0):
     sensors = _read_config(rig_config)
     names = [s["name"] for s in sensors]
     ns = len(sensors)
@@ -300,10 +338,14 @@ def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_thre
 
     stats_log = []
     xyz = np.zeros((npid, 3))
+    BAD = 1.0e100
+    mesh_vf = read_ply(mesh) if mesh else None  # loadMeshBuildTree (texture_processing.cc:264-285)
     for _ in range(calibrator_num_passes):
         w2c = world_to_cam_all()
         inlier, xyz = oracle_py.triangulate(tracks_obj(w2c), inlier)
         xyz_orig = xyz.copy()
+        if mesh_vf is not None:  # meshTriangulations (:1581-1588)
+            mfx, mpx = oracle_py.mesh_triangulate(tracks_obj(w2c), inlier, min_ray_dist, max_ray_dist, *mesh_vf)
         # problem assembly with lazily registered blocks (Ceres Problem semantics)
         reg, sizes, vals, const = {}, [], [], set()
 
@@ -363,13 +405,28 @@ def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_thre
                     col, row = int(round(tpix[o, 0])), int(round(tpix[o, 1]))
                     if col < cl.shape[1] and row < cl.shape[0] and np.any(cl[row, col] != 0):
                         dk = [kb, ke, ("r2c", t), ("dti", t), ("sc", t), ("xyz", p), ("off", t)]
-                        dres.append(([blk(k, get(k)) for k in dk], cl[row, col].astype(np.float64), stamps))
+                        dres.append(([blk(k, get(k)) for k in dk], cl[row, col].astype(np.float64), stamps,
+                                     depth_tri_weight, None))
                         if not float_scale:
                             const.add(("sc", t))
                         if names[t] not in dtf:
                             const.add(("dti", t))
+                if mesh_vf is not None and depth_mesh_weight > 0 and mfx[o, 0] != BAD and c["cloud"] is not None:
+                    # BracketedDepthMeshError (:1796-1834): no point block
+                    cl = c["cloud"]
+                    col, row = int(round(tpix[o, 0])), int(round(tpix[o, 1]))
+                    if col < cl.shape[1] and row < cl.shape[0] and np.any(cl[row, col] != 0):
+                        dk = [kb, ke, ("r2c", t), ("dti", t), ("sc", t), None, ("off", t)]
+                        dres.append(([blk(k, get(k)) if k else -1 for k in dk], cl[row, col].astype(np.float64),
+                                     stamps, depth_mesh_weight, mfx[o].copy()))
+                        if not float_scale:
+                            const.add(("sc", t))
+                        if names[t] not in dtf:
+                            const.add(("dti", t))
+            if mesh_vf is not None and tri_inl and mesh_tri_weight > 0 and mpx[p, 0] != BAD:
+                xres.append((blk(("xyz", p), get(("xyz", p))), mpx[p].copy(), mesh_tri_weight, robust_threshold, 1))
             if tri_weight > 0 and tri_inl:
-                xres.append((blk(("xyz", p), get(("xyz", p))), xyz_orig[p]))
+                xres.append((blk(("xyz", p), get(("xyz", p))), xyz_orig[p], tri_weight, tri_robust_threshold, 0))
         sizes_a = np.array(sizes, dtype=np.int32)
         offs = np.zeros(len(sizes), dtype=np.int64)
         offs[1:] = np.cumsum(sizes_a[:-1])
@@ -387,13 +444,16 @@ def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_thre
         if dres:
             P.depth_blocks = np.array([d[0] for d in dres], dtype=np.int32)
             P.depth_meas = np.array([d[1] for d in dres])
-            P.depth_weight = np.full(len(dres), float(depth_tri_weight))
+            P.depth_weight = np.array([float(d[3]) for d in dres])
             P.depth_stamps = np.array([d[2] for d in dres])
+            if any(d[4] is not None for d in dres):
+                P.depth_mesh_xyz = np.array([d[4] if d[4] is not None else np.zeros(3) for d in dres])
         if xres:
             P.xyz_block = np.array([x[0] for x in xres], dtype=np.int32)
             P.xyz_ref = np.array([x[1] for x in xres])
-            P.xyz_weight = np.full(len(xres), float(tri_weight))
-            P.xyz_threshold = np.full(len(xres), float(tri_robust_threshold))
+            P.xyz_weight = np.array([float(x[2]) for x in xres])
+            P.xyz_threshold = np.array([float(x[3]) for x in xres])
+            P.xyz_kind = np.array([x[4] for x in xres], dtype=np.uint8)
 
         def stats():
             _, r, _ = oracle_py.evaluate(P, oracle_py.RESIDUAL)
@@ -402,15 +462,17 @@ def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_thre
             if dres:
                 _, rd, _ = oracle_py.evaluate_depth(P, oracle_py.RESIDUAL)
                 v.append((rd / P.depth_weight[:, None]).reshape(-1))
-                ids.append(2 * ns + np.tile(np.arange(3), len(dres)))
+                g0 = np.where(P.depth_blocks[:, 5] == -1, 2 * ns + 6, 2 * ns)
+                ids.append((g0[:, None] + np.arange(3)).reshape(-1))
             if xres:
                 _, rx, _ = oracle_py.evaluate_xyz(P)
                 v.append((rx.reshape(-1, 3) / P.xyz_weight[:, None]).reshape(-1))
-                ids.append(2 * ns + 3 + np.tile(np.arange(3), len(xres)))
-            ng = 2 * ns + 6
+                g0 = np.where(P.xyz_kind == 1, 2 * ns + 9, 2 * ns + 3)
+                ids.append((g0[:, None] + np.arange(3)).reshape(-1))
+            ng = 2 * ns + 12
             out, cnt = oracle_py.residual_stats(np.concatenate(v), np.concatenate(ids).astype(np.int32), ng)
-            labels = [f"{n}_pix_{a}" for n in names for a in "xy"] + [f"depth_tri_{a}_m" for a in "xyz"] + \
-                [f"tri_{a}_m" for a in "xyz"]
+            labels = [f"{n}_pix_{a}" for n in names for a in "xy"] + \
+                [f"{k}_{a}_m" for k in ("depth_tri", "tri", "depth_mesh", "mesh_tri") for a in "xyz"]
             return sorted([(labels[g], *out[g], int(cnt[g])) for g in range(ng) if cnt[g] > 0])
 
         before = stats()

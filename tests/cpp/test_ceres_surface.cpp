@@ -55,6 +55,7 @@ int main(int argc, char** argv) {
   auto xblock = read_vec<int32_t>(in);   // xyz priors
   auto xref = read_vec<double>(in);
   auto xweight = read_vec<double>(in);
+  auto dmesh = read_vec<double>(in);     // [3 nd] mesh point of BracketedDepthMeshError rows (xyz block -1)
   const int64_t n = (int64_t)rcam.size();
 
   std::vector<double> user = params;  // the integrator's parameter arrays
@@ -186,6 +187,7 @@ int main(int argc, char** argv) {
   {
     mvba::BracketedCamBatch b7(0);
     std::vector<std::unique_ptr<ceres::CostFunction>> c7, d7, x7;
+    auto is_mesh = [&](int64_t j) { return dblocks[7 * j + 5] == -1; };
     for (int64_t i = 0; i < n; i++) {
       std::array<double*, 8> ptr;
       for (int b = 0; b < 8; b++) ptr[b] = &user[(size_t)block_offset[rblocks[8 * i + b]]];
@@ -194,6 +196,14 @@ int main(int argc, char** argv) {
                                 &cam_half[2 * c], ptr));
     }
     for (int64_t j = 0; j < nd; j++) {
+      if (is_mesh(j)) {  // BracketedDepthMeshError: beg, end, ref_to_cam, depth_to_image, scale, offset
+        std::array<double*, 6> ptr;
+        for (int b = 0; b < 6; b++) ptr[b] = &user[(size_t)block_offset[dblocks[7 * j + (b < 5 ? b : 6)]]];
+        const std::vector<int> dbs = {7, 7, 7, dsizes[j], 1, 1};
+        d7.emplace_back(b7.CreateDepthMesh(dweight[j], &dmeas[3 * j], &dmesh[3 * j], dstamps[3 * j],
+                                           dstamps[3 * j + 1], dstamps[3 * j + 2], dbs, ptr));
+        continue;
+      }
       std::array<double*, 7> ptr;
       for (int b = 0; b < 7; b++) ptr[b] = &user[(size_t)block_offset[dblocks[7 * j + b]]];
       const std::vector<int> dbs = {7, 7, 7, dsizes[j], 1, 3, 1};
@@ -209,9 +219,11 @@ int main(int argc, char** argv) {
     for (int64_t j = 0; j < nd; j++) {
       const double* p[7];
       double* jp[7];
+      int q = 0;
       for (int b = 0; b < 7; b++) {
-        p[b] = &user[(size_t)block_offset[dblocks[7 * j + b]]];
-        jp[b] = &JD[114 * j + dbase[b]];
+        if (is_mesh(j) && b == 5) continue;  // no point block: its rows stay zero
+        p[q] = &user[(size_t)block_offset[dblocks[7 * j + b]]];
+        jp[q++] = &JD[114 * j + dbase[b]];
       }
       ok &= d7[j]->Evaluate(p, &RD[3 * j], jp);
     }

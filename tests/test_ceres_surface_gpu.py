@@ -34,12 +34,18 @@ def test_ceres_adapter(tmp_path, oracle):
 def run_adapter_case(binary, tmp_path, oracle, env=None):
     """Drive the adapter binary on a dumped problem and check every case;
     returns the binary's stderr (the sanitizer build checks it is clean)."""
-    R = rig.make_rig(num_sensors=3, num_ref=12, num_points=150, obs_per_point=5,
-                     models=["radtan", "rpc1", "fov"], seed=31, depth_sensors=(2,), affine_depth=False)
+    from test_mesh import _oracle_mesh_xyz
+
+    # sphere-surface scene: depth, depth-mesh (BracketedDepthMeshError), mesh_tri
+    # and tri blocks beside the reprojection blocks
+    R = rig.make_rig(num_sensors=3, num_ref=30, num_points=300, obs_per_point=5,
+                     models=["radtan", "rpc1", "fov"], seed=31, depth_sensors=(2,), affine_depth=False,
+                     surface="sphere")
     F = rig.FloatFlags(depth_tri_weight=10.0, depth_to_image_transforms_to_float=("cam2",), float_scale=True,
-                       tri_weight=0.5, tri_robust_threshold=0.1)
-    P = rig.build_problem(R, F)
-    assert P.num_depth_residuals > 0 and P.num_xyz_residuals > 0
+                       tri_weight=0.5, tri_robust_threshold=0.1, depth_mesh_weight=5.0, mesh_tri_weight=2.0)
+    mxyz = _oracle_mesh_xyz(R)
+    P = rig.build_problem(R, F, mesh_xyz=mxyz)
+    assert P.num_depth_residuals > 0 and P.num_xyz_residuals > 0 and (P.depth_blocks[:, 5] == -1).any()
     params2 = P.params.copy()
     params2 += np.random.default_rng(1).normal(0, 1e-4, params2.shape) * (P.params != 0)
     src = tmp_path / "prob.bin"
@@ -62,6 +68,7 @@ def run_adapter_case(binary, tmp_path, oracle, env=None):
         _write(fh, P.xyz_block, np.int32)
         _write(fh, P.xyz_ref, np.float64)
         _write(fh, P.xyz_weight, np.float64)
+        _write(fh, P.depth_mesh_xyz, np.float64)
     out = tmp_path / "out.bin"
     p = subprocess.run([binary, str(src), str(out)], capture_output=True, text=True, timeout=300, env=env)
     assert p.returncode == 0, p.stderr[-4000:]
@@ -79,10 +86,10 @@ def run_adapter_case(binary, tmp_path, oracle, env=None):
         RD, JD, RX, JX = (_read(fh, np.float64) for _ in range(4))
         flags = _read(fh, np.int32)
     # full Jacobians: the adapter evaluates every block (all free)
-    Pf = rig.build_problem(R, F)
+    Pf = rig.build_problem(R, F, mesh_xyz=mxyz)
     Pf.block_constant[:] = 0
     _, r_o, J_o = oracle.evaluate(Pf, oracle.ANALYTIC)
-    P2 = rig.build_problem(R, F)
+    P2 = rig.build_problem(R, F, mesh_xyz=mxyz)
     P2.block_constant[:] = 0
     P2.params = params2
     _, r_o2, J_o2 = oracle.evaluate(P2, oracle.ANALYTIC)

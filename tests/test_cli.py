@@ -63,7 +63,10 @@ VALIDATION = [
     (["--no_rig", "--use_initial_rig_transforms"], "Cannot use initial rig transforms if not modeling the rig."),
     (["--rig_config="], "Must specify the initial rig configuration via --rig_config."),
     (["--camera_poses=x.txt"], "Cannot specify both --nvm and --camera_poses."),
-    (["--mesh=m.ply"], "--mesh is outside this build's scope"),
+    (["--mesh_tri_weight=-1"], "The mesh weight must non-negative."),
+    (["--depth_mesh_weight=-1"], "The depth mesh weight must non-negative."),
+    (["--out_texture_dir=t"], "Cannot project camera images onto a mesh if a mesh was not provided."),
+    (["--out_texture_dir=t", "--mesh=m.ply"], "--out_texture_dir (texturing) is outside this build's scope"),
     (["--num_overlaps=3"], "feature detection and matching"),
     (["--device=cpu"], "no CPU compute path"),
 ]
@@ -223,6 +226,11 @@ CASES = {
     "depth": dict(rig=dict(depth_sensors=(2,)),
                   flags=dict(rig_transforms_to_float="cam1 cam2", depth_tri_weight=10.0,
                              depth_to_image_transforms_to_float="cam2", float_scale=True)),
+    # --mesh (PLY icosphere of the sphere-surface scene): meshTriangulations each
+    # pass, BracketedDepthMeshError + mesh_tri priors beside the depth blocks
+    "mesh": dict(rig=dict(depth_sensors=(2,), surface="sphere", num_ref=30, num_points=300),
+                 flags=dict(rig_transforms_to_float="cam1 cam2", depth_tri_weight=10.0, depth_mesh_weight=5.0,
+                            mesh_tri_weight=2.0, depth_to_image_transforms_to_float="cam2", float_scale=True)),
 }
 
 
@@ -247,6 +255,11 @@ def test_cli_matches_oracle_pipeline(cli, tmp_path, name):
     name = name.replace("_2shards", "")
     flags = dict(CASES[name]["flags"])
     R, info = _dataset(tmp_path, seed=11 + len(name), **CASES[name].get("rig", {}))
+    if "mesh_tri_weight" in flags:
+        from multiview_amd import rig_files
+
+        flags["mesh"] = str(tmp_path / "data" / "mesh.ply")
+        rig_files.write_ply(flags["mesh"], *rig.sphere_mesh(5))
     out_dir = tmp_path / "out"
     common = dict(num_iterations=100, parameter_tolerance=1e-12)
     code, out, err = _run(cli, "--rig_config", info["rig_config"], "--nvm", info["nvm"], "--out_dir", str(out_dir),
@@ -294,6 +307,8 @@ def test_cli_matches_oracle_pipeline(cli, tmp_path, name):
             Rr, tr = _array_to_rigid(ref["ref_to_cam"][t])
             T = np.array(r["ref_to_sensor_transform"])
             assert np.allclose(T[:9], Rr.reshape(-1), atol=1e-6) and np.allclose(T[9:], tr, atol=1e-6)
+    if flags.get("mesh"):
+        assert "depth_mesh_x_m" in before0 and "mesh_tri_x_m" in before0
     if flags.get("depth_tri_weight"):
         assert info["num_clouds"] > 0 and "depth_tri_x_m" in before0
         for t, r in enumerate(rows):
