@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba-iters", type=int, default=5, help="LM iterations timed in phase C (0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=0, help="residuals in the CPU sample (0 = auto)")
+    ap.add_argument("--mesh-subdiv", type=int, default=7,
+                    help="icosphere level of the --mesh ray-intersection line (0 = skip; 7 = 327,680 faces)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (rehearsal of the multi-rank path on one GPU)")
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
@@ -255,6 +257,58 @@ def ceres_surface(ev, P, torch, args):
         "pageable_full_layout": {"evals_per_s": n / full_dt, "ms": 1e3 * full_dt,
                                  "note": "mvba_evaluate into pageable numpy arrays (Ceres jac_stride "
                                          "layout, zero-filled), staged through two pinned 32 MB buffers"},
+    }
+
+
+def mesh_bench(torch, stream, nrays, args):
+    """--mesh path (meshTriangulations -> ray_mesh_intersect, texture_processing.cc:
+    1436-1479, 1566-1625): closest hits of one ray per observation against an
+    icosphere of the scene's size (subdivision level --mesh-subdiv), rays grouped
+    by camera as meshTriangulations issues them (image-major order), timed on the
+    launch stream; the host BVH build (loadMeshBuildTree's tree) timed beside."""
+    from multiview_amd import rig
+    from multiview_amd.tracks import Mesh
+
+    V, F = rig.sphere_mesh(args.mesh_subdiv)
+    t0 = time.perf_counter()
+    M = Mesh(V, F)
+    build_s = time.perf_counter() - t0
+    info = M.info()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    ncam = 3000
+    per = (nrays + ncam - 1) // ncam
+    phi = torch.rand(ncam, device="cuda", generator=g, dtype=torch.float64) * 2 * np.pi
+    C = torch.stack([8 * torch.cos(phi), 0.3 * torch.sin(3 * phi), 8 * torch.sin(phi)], 1)
+    v = torch.randn(ncam, per, 3, device="cuda", generator=g, dtype=torch.float64)
+    v = v / v.norm(dim=2, keepdim=True)
+    v = torch.where(((v * C[:, None, :]).sum(2, keepdim=True) < 0), -v, v)  # the side the camera sees
+    d = rig.SPHERE_RADIUS * v - C[:, None, :]
+    d = d / d.norm(dim=2, keepdim=True)
+    o = C[:, None, :].expand(ncam, per, 3).reshape(-1, 3)[:nrays].float().contiguous()
+    d = d.reshape(-1, 3)[:nrays].float().contiguous()
+    t = torch.empty(nrays, dtype=torch.float32, device="cuda")
+    f = torch.empty(nrays, dtype=torch.int32, device="cuda")
+    sh = stream.cuda_stream
+    for _ in range(args.warmup):
+        M.intersect_device(o, d, 0.0, 100.0, t, f, stream=sh)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        M.intersect_device(o, d, 0.0, 100.0, t, f, stream=sh)
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    hit = float((f >= 0).float().mean().item())
+    M.close()
+    return {
+        "what": "closest-hit ray-mesh intersection (BVH traversal, rayint's float triangle test), one ray per "
+                "observation, 3000 cameras",
+        "rays": nrays, "faces": int(F.shape[0]), "bvh_nodes": info["num_nodes"], "bvh_depth": info["depth"],
+        "rays_per_s": nrays / (ms * 1e-3), "kernel_ms": ms, "hit_fraction": hit,
+        "bvh_build_s": build_s,
+        "bound": "latency (dependent node loads per ray; node + triangle sets of "
+                 f"{(32 * info['num_nodes'] + 48 * int(F.shape[0])) / 1e6:.1f} MB stay in the on-die caches)",
     }
 
 
@@ -693,6 +747,8 @@ def main():
             "kernel_ms": w_obs_ms,
         }
 
+    if rank == 0 and world == 1 and args.mesh_subdiv > 0:
+        line["mesh"] = mesh_bench(torch, stream, ev.num_residuals, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(P, args.cpu_sample)
     if rank == 0:
