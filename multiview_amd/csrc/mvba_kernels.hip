@@ -344,7 +344,10 @@ __global__ void __launch_bounds__(256) k_obs(
 // The Gram entries stay in the accumulator layout: pair p = (ti, tj), ti <= tj,
 // lane l and register r hold G[16 ti + (l >> 4) + 4 r][16 tj + (l & 15)].
 constexpr int kGramLd = 66;  // 64 rows + 2 pad doubles: bank-conflict-free reads
-constexpr int kLinReplicas = 8;
+#ifndef MVBA_LIN_REPLICAS
+#define MVBA_LIN_REPLICAS 8
+#endif
+constexpr int kLinReplicas = MVBA_LIN_REPLICAS;  // power of two
 #ifndef MVBA_FLIN_WAVES
 #define MVBA_FLIN_WAVES 2
 #endif
