@@ -43,7 +43,7 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                                     const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
                                     const double2* obs_meas, const int32_t* slot_po, const double* dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
-                                    const double* prec, const double4* obsX, mvba::PointFuse pf, hipStream_t s);
+                                    const double* prec, const double4* obsX, hipStream_t s);
 hipError_t mvba_launch_gather_obs_pts(int64_t nslots, const int32_t* obs_pid, const double4* pts, double4* out,
                                       hipStream_t s);
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
@@ -133,8 +133,6 @@ struct SolverState {
   double* partial = nullptr;  // [npartial]
   double* scal = nullptr;     // [32] device scalars
   unsigned* cnt = nullptr;    // [8] grid-reduction counters (kept zero between kernels)
-  unsigned* pcnt = nullptr;   // [np] per-point arrival counters of the fused pass A (kept zero)
-  bool fuse_w = false;        // every point has a reprojection observation: k_point_w folds into pass A
   double* hscal = nullptr;    // [32] pinned host mirror
   mvba::CgCtl* ctl = nullptr; // device CG control (single-rank solves)
   double* prec = nullptr;     // [nframes * kProjDoubles] projection records
@@ -151,7 +149,7 @@ void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
                   S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du,
-                  S->cnt, S->pcnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
+                  S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (S->hscal) (void)hipHostFree(S->hscal);
@@ -210,20 +208,6 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
     HCHK(dalloc(&S->cnt, 8));
     HCHK(hipMemset(S->cnt, 0, 8 * sizeof(unsigned)));
-    HCHK(dalloc(&S->pcnt, (size_t)std::max<int64_t>(S->np, 1)));
-    HCHK(hipMemset(S->pcnt, 0, (size_t)std::max<int64_t>(S->np, 1) * sizeof(unsigned)));
-    {
-      // the fused pass A computes w_p at a point's last observation: every point
-      // needs one (points seen only by depth / prior blocks keep k_point_w)
-      static const char* env = std::getenv("MVBA_FUSE_POINT_W");
-      if (env && env[0] == '1' && S->np > 0) {
-        std::vector<int64_t> pb((size_t)S->np + 1);
-        HCHK(hipMemcpy(pb.data(), h->d_pt_begin, pb.size() * sizeof(int64_t), hipMemcpyDeviceToHost));
-        S->fuse_w = true;
-        for (int64_t q = 0; q < S->np; q++)
-          if (pb[(size_t)q + 1] == pb[(size_t)q]) S->fuse_w = false;
-      }
-    }
     int64_t ncost = 0;
     for (const Group& G : h->groups) ncost = std::max<int64_t>(ncost, (G.seg_count + 3) / 4);
     // k_cg_update: 3 partials per 256-entry block; k_vec_rep_reduce / k_add_diag one
@@ -424,20 +408,15 @@ class Solver {
     else {
       // one segment per wave (MVBA_PASS_A_CHUNKS=1: the 4-segment solver chunks, for A/B timing)
       static const bool chunked = std::getenv("MVBA_PASS_A_CHUNKS") && std::getenv("MVBA_PASS_A_CHUNKS")[0] == '1';
-      // fused: the point solve at each point's last arriving observation (no k_point_w)
-      const bool fuse = dir && S_->fuse_w;
-      const mvba::PointFuse pf{fuse ? S_->pcnt : nullptr, h_->d_pt_begin, tinit, S_->phess, S_->dmp + S_->ng,
-                               S_->wbuf, 4};
       if (dir)
         for (const Group& G : h_->groups)
           HCHK(mvba_launch_pass_a_frame(G.model, G.deg,
                                         chunked ? h_->d_chunks + G.chunk_begin : h_->d_segchunks + G.seg_begin,
                                         chunked ? G.chunk_count : G.seg_count, h_->d_segs,
                                         h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dir, (double4*)S_->cbuf, flags_,
-                                        cauchy_c_, gate, S_->prec, obsx(), pf, s_));
-      if (!fuse)
-        HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, h_->d_po_slot, dir ? (const double4*)S_->cbuf : nullptr,
-                                 tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate, s_));
+                                        cauchy_c_, gate, S_->prec, obsx(), s_));
+      HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, h_->d_po_slot, dir ? (const double4*)S_->cbuf : nullptr,
+                               tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate, s_));
     }
   }
 

@@ -413,8 +413,7 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
     const int32_t* __restrict__ slot_po, const double* __restrict__ dir, double4* __restrict__ cbuf, int32_t flags,
     double cauchy_c,
-    const int32_t* __restrict__ gate, const double* __restrict__ prec, const double4* __restrict__ obsX,
-    PointFuse pf) {
+    const int32_t* __restrict__ gate, const double* __restrict__ prec, const double4* __restrict__ obsX) {
   const int lane = threadIdx.x & 63;
   const int ch = blockIdx.x * kPassAWaves + (threadIdx.x >> 6);
   if (ch >= nchunks || (gate && *gate)) return;
@@ -429,44 +428,10 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
       const int64_t i = (int64_t)sg.begin + lane;
       double z[2], P0[3], P1[3];
       pass_a_obs<MODEL, DEG>(rec, d, obsX ? obsX[i] : pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
-      const double c0 = P0[0] * z[0] + P1[0] * z[1], c1 = P0[1] * z[0] + P1[1] * z[1],
-                   c2 = P0[2] * z[0] + P1[2] * z[1];
-      if (!pf.cnt) {
-        // plain store: a nontemporal store of these scattered 32-B records
-        // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM)
-        cbuf[slot_po[i]] = make_double4(c0, c1, c2, 0.0);
-      } else {
-        // k_point_w folded in: c_o handed over at the coherence point
-        // (partial_put / arrive_last, as the grid reductions), the point's last
-        // arriving observation sums its c_o in slot order and solves for w_p
-        double* cr = reinterpret_cast<double*>(cbuf + slot_po[i]);
-        partial_put(cr, c0);
-        partial_put(cr + 1, c1);
-        partial_put(cr + 2, c2);
-        const int32_t p = obs_pid[i];
-        const int64_t pb = pf.pt_begin[p], pe = pf.pt_begin[p + 1];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned prev = __hip_atomic_fetch_add(pf.cnt + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (prev == (unsigned)(pe - pb - 1)) {
-          double t[3] = {0.0, 0.0, 0.0};
-          for (int64_t j = pb; j < pe; j++) {
-            double* cj = reinterpret_cast<double*>(cbuf + j);
-#pragma unroll
-            for (int q = 0; q < 3; q++) t[q] += partial_get(cj + q);
-          }
-          pf.cnt[p] = 0u;
-          double w[3] = {0.0, 0.0, 0.0};
-          if (pts[p].w != 0.0) {
-            if (pf.tinit)
-#pragma unroll
-              for (int q = 0; q < 3; q++) t[q] += pf.tinit[3 * p + q];
-            solve3(pf.V + 6 * p, pf.dp + 3 * p, t, w);
-          }
-#pragma unroll
-          for (int q = 0; q < 3; q++) pf.wout[pf.wstride * p + q] = w[q];
-        }
-      }
+      // plain store: a nontemporal store of these scattered 32-B records
+      // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM)
+      cbuf[slot_po[i]] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
+                                      P0[2] * z[0] + P1[2] * z[1], 0.0);
     }
   }
 }
@@ -1299,12 +1264,12 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                                     const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
                                     const double2* obs_meas, const int32_t* slot_po, const double* dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
-                                    const double* prec, const double4* obsX, mvba::PointFuse pf, hipStream_t s) {
+                                    const double* prec, const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PAF(M, D)                                                                                      \
   hipLaunchKernelGGL((mvba::k_pass_a_frame<M, D>), dim3((unsigned)((nchunks + mvba::kPassAWaves - 1) /        \
                      mvba::kPassAWaves)), dim3(64 * mvba::kPassAWaves), 0, s, chunks, nchunks,                 \
-                     segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec, obsX, pf)
+                     segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec, obsX)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PAF)
 #undef MVBA_PAF
   return hipGetLastError();

@@ -164,18 +164,6 @@ struct CgEntry {
   int64_t moff;
 };
 
-// k_point_w folded into the frame-order pass A (per-point arrival counters):
-// cnt == nullptr selects the separate point kernel.
-struct PointFuse {
-  unsigned* cnt;            // [num_points], zero between launches (the last arriver resets)
-  const int64_t* pt_begin;  // CSR point -> point-order slots
-  const double* tinit;      // right-hand side term (nullable)
-  const double* V;          // packed 3x3 point blocks
-  const double* dp;         // LM damping of the point entries
-  double* wout;
-  int32_t wstride;
-};
-
 // The CG search direction formed where it is first read (k_frame_dir):
 // p_new = z (first) or z + beta p_old, with first/beta from ctl when set.
 struct LazyDir {
