@@ -12,6 +12,28 @@
 
 namespace mvba {
 
+// ------------------------------------------------------------ XCD-aware block order
+// Workgroups are dealt round-robin over the 8 XCDs (block b -> XCD b % 8), each
+// XCD with its own L2. Frame-ordered kernels renumber their blocks so that XCD
+// x runs the contiguous range [x per, (x + 1) per) of logical blocks: a frame's
+// records (K0 output, projection and direction records) and the landmarks its
+// window of frames observes are then fetched into one XCD's L2 instead of all
+// eight. Launch xcd_grid(nb) blocks; xcd_block returns -1 for the few surplus
+// blocks. MVBA_XCD_MAP=0 keeps the plain order (A/B builds).
+#ifndef MVBA_XCD_MAP
+#define MVBA_XCD_MAP 1
+#endif
+constexpr int kXcds = 8;
+__host__ __device__ __forceinline__ unsigned xcd_grid(int64_t nb) {
+  return MVBA_XCD_MAP ? (unsigned)(((nb + kXcds - 1) / kXcds) * kXcds) : (unsigned)nb;
+}
+__device__ __forceinline__ int64_t xcd_block_of(int64_t b, int64_t nb) {
+  if (!MVBA_XCD_MAP) return b < nb ? b : -1;
+  const int64_t per = (nb + kXcds - 1) / kXcds;
+  const int64_t l = (b % kXcds) * per + b / kXcds;
+  return l < nb ? l : -1;
+}
+__device__ __forceinline__ int64_t xcd_block(int64_t nb) { return xcd_block_of(blockIdx.x, nb); }
 
 // ------------------------------------------------------------ small helpers
 __device__ __forceinline__ void quat_to_rot(double x, double y, double z, double w, double* R) {

@@ -219,7 +219,9 @@ __global__ void __launch_bounds__(256) k_obs(
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
     const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
     int64_t ld, int32_t flags, double cauchy_c) {
-  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int64_t blk = xcd_block((nseg + 3) / 4);  // 4 segments per block, XCD-contiguous
+  if (blk < 0) return;
+  const int wave = (int)((blk * blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   if (wave >= nseg) return;
   const Segment sg = segs[wave];
@@ -850,7 +852,7 @@ hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_
                            void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
                            hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
-  const unsigned blocks = (unsigned)((nseg + 3) / 4);
+  const unsigned blocks = mvba::xcd_grid((nseg + 3) / 4);
 #define MVBA_OBS(M, D)                                                                                     \
   if (out_f32)                                                                                           \
     hipLaunchKernelGGL((mvba::k_obs<M, D, float>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec,    \
