@@ -25,27 +25,35 @@ constexpr int kDJacBase[7] = {MVBA_DJAC_BASE_BEG, MVBA_DJAC_BASE_END, MVBA_DJAC_
 // column planes; constant blocks are not written. flags & APPLY_LOSS applies the
 // corrector in-kernel.
 // OT: double (fp64 output) or float (fp32 output of the same fp64 arithmetic).
+// A segment's blocks share one image: their descriptors differ only in the
+// point (and its free bit, the point record's w), so the descriptor is read once
+// per wave (scalar loads) and the point index per lane from the dense dpid array
+// (4 B per block instead of a 64-B descriptor); blocks in XCD-contiguous order.
 template <class OT>
 __global__ void __launch_bounds__(64) k_depth_obs(const Segment* __restrict__ segs, int32_t nseg,
-                                                  const DepthDesc* __restrict__ dd, const double4* __restrict__ dmeas,
+                                                  const DepthDesc* __restrict__ dd, const int32_t* __restrict__ dpid,
+                                                  const double4* __restrict__ dmeas,
                                                   const FrameDesc* __restrict__ fd, const double* __restrict__ frec,
                                                   const double* __restrict__ params, const double4* __restrict__ pts,
                                                   OT* __restrict__ res, OT* __restrict__ J, int64_t ld,
                                                   int32_t flags, double cauchy_c) {
-  const int seg = blockIdx.x;
-  if (seg >= nseg) return;
+  const int64_t seg = xcd_block(nseg);
+  if (seg < 0) return;
   const Segment sg = segs[seg];
   const int lane = threadIdx.x;
   // padding lanes up to the next 128-B line of OT recompute the last block
   // into their padding slots (whole-line stores, as in k_obs)
   constexpr int kLine = 128 / (int)sizeof(OT);
-  const int count = sg.count;
+  const int count = __builtin_amdgcn_readfirstlane(sg.count);
+  const int begin = __builtin_amdgcn_readfirstlane(sg.begin);
   if (lane >= ((count + kLine - 1) & ~(kLine - 1))) return;
-  const int64_t i = (int64_t)sg.begin + lane;
-  const int64_t isrc = (int64_t)sg.begin + min(lane, count - 1);
-  const DepthDesc d = dd[isrc];
+  const int64_t i = (int64_t)begin + lane;
+  const int64_t isrc = (int64_t)begin + min(lane, count - 1);
+  DepthDesc d = dd[begin];
+  d.pid = dpid[isrc];
   const double* rec = frec + (int64_t)d.frame * kFrameRecDoubles;
   const double4 X = pts[d.pid];
+  d.free_mask = (d.free_mask & ~(1 << MVBA_DBLK_XYZ)) | (X.w != 0.0 ? (1 << MVBA_DBLK_XYZ) : 0);
   DepthRows o;
   depth_rows(d, rec, params, dmeas[isrc], X.x, X.y, X.z, flags, cauchy_c, o);
   const bool loss = (flags & MVBA_EVAL_APPLY_LOSS) != 0;
@@ -374,15 +382,16 @@ extern "C" {
 size_t mvba_depth_desc_size(void) { return sizeof(mvba::DepthDesc); }
 
 hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
-                                 const double4* dmeas, const mvba::FrameDesc* fd, const double* frec,
-                                 const double* params, const double4* pts, void* res, void* J, int64_t ld,
-                                 int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s) {
+                                 const int32_t* dpid, const double4* dmeas, const mvba::FrameDesc* fd,
+                                 const double* frec, const double* params, const double4* pts, void* res, void* J,
+                                 int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
+  const unsigned grid = mvba::xcd_grid(nseg);
   if (out_f32)
-    hipLaunchKernelGGL(mvba::k_depth_obs<float>, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, fd, frec,
+    hipLaunchKernelGGL(mvba::k_depth_obs<float>, dim3(grid), dim3(64), 0, s, segs, nseg, dd, dpid, dmeas, fd, frec,
                        params, pts, (float*)res, (float*)J, ld, flags, cauchy_c);
   else
-    hipLaunchKernelGGL(mvba::k_depth_obs<double>, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, fd,
+    hipLaunchKernelGGL(mvba::k_depth_obs<double>, dim3(grid), dim3(64), 0, s, segs, nseg, dd, dpid, dmeas, fd,
                        frec, params, pts, (double*)res, (double*)J, ld, flags, cauchy_c);
   return hipGetLastError();
 }

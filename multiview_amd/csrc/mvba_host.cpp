@@ -36,7 +36,7 @@ static void free_all(mvba_handle* h) {
                   h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
-                  h->d_dep_desc, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
+                  h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
                   h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xkind, h->d_xpid,
                   h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt, h->d_varsize, h->d_tres, h->d_tcost,
                   h->d_trows, h->d_xmask, h->d_xoff, h->d_dwritten, h->d_dvarsize, h->d_tdres,
@@ -723,6 +723,11 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_slot_po, slot_po));
   chk(upload(&h->d_po_slot, po_slot));
   chk(upload(&h->d_dep_desc, ddesc));
+  {
+    std::vector<int32_t> dpid(ddesc.size());
+    for (size_t q = 0; q < ddesc.size(); q++) dpid[q] = ddesc[q].pid;
+    chk(upload(&h->d_dep_pid, dpid));
+  }
   chk(upload(&h->d_dep_meas, dmeas));
   chk(upload(&h->d_dep_segs, dsegs));
   chk(upload(&h->d_dep_order, h->dep_order));
@@ -1040,7 +1045,7 @@ static mvba_status evaluate_depth_device_impl(mvba_handle* h, int32_t flags, dou
     return h->fail(MVBA_E_INVALID, "MVBA_EVAL_SKIP_PREP before any full evaluation");
   }
   if (e == hipSuccess && !(flags & MVBA_EVAL_PREP_ONLY))
-    e = mvba_launch_depth_obs(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_fd, h->d_frec,
+    e = mvba_launch_depth_obs(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_fd, h->d_frec,
                               h->d_params, h->d_pts, d_res, d_J, ld, flags & (MVBA_EVAL_APPLY_LOSS), cauchy_c,
                               out_f32, s);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_depth_device launch");

@@ -58,9 +58,9 @@ hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg
 extern "C" {
 size_t mvba_depth_desc_size(void);
 hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
-                                 const double4* dmeas, const mvba::FrameDesc* fd, const double* frec,
-                                 const double* params, const double4* pts, void* res, void* J, int64_t ld,
-                                 int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s);
+                                 const int32_t* dpid, const double4* dmeas, const mvba::FrameDesc* fd,
+                                 const double* frec, const double* params, const double4* pts, void* res, void* J,
+                                 int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s);
 hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
@@ -335,6 +335,7 @@ struct mvba_handle {
   double bytes_dep = 0.0;
   std::vector<int64_t> dep_order;         // depth slot -> depth insertion index (-1 = padding)
   mvba::DepthDesc* d_dep_desc = nullptr;
+  int32_t* d_dep_pid = nullptr;           // depth slot -> point index (dense, for K1-depth)
   double4* d_dep_meas = nullptr;          // (x, y, z, weight)
   Segment* d_dep_segs = nullptr;
   int64_t* d_dep_order = nullptr;
