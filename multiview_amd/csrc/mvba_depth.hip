@@ -121,7 +121,7 @@ constexpr int kDLd = kDStage + 2; // LDS leading dimension (doubles)
 constexpr int kDReplicas = kDepthReplicas;
 
 __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ segs, int32_t nseg,
-                                                   const DepthDesc* __restrict__ dd,
+                                                   const DepthDesc* __restrict__ dd, const int32_t* __restrict__ dpid,
                                                    const double4* __restrict__ dmeas, const double* __restrict__ frec,
                                                    const double* __restrict__ params,
                                                    const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
@@ -144,7 +144,8 @@ __global__ void __launch_bounds__(64) k_depth_gram(const Segment* __restrict__ s
   DepthDesc d0 = dd[sg.begin];
   if (lane < sg.count) {
     const int64_t i = (int64_t)sg.begin + lane;
-    const DepthDesc d = dd[i];
+    DepthDesc d = d0;  // one image per segment: only the point differs (as k_depth_obs)
+    d.pid = dpid[i];
     const double4 X = pts[d.pid];
     DepthRows o;
     depth_rows(d, rec, params, dmeas[i], X.x, X.y, X.z, flags, cauchy_c, o);
@@ -397,11 +398,11 @@ hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const 
 }
 
 hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
-                                  const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                  const int32_t* dpid, const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
                                   mvba::Slab sl, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_depth_gram, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params,
+  hipLaunchKernelGGL(mvba::k_depth_gram, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dpid, dmeas, frec, params,
                      pts, (const mvba::FrameLin*)fl, rep, ng, nh, flags, cauchy_c, sl);
   return hipGetLastError();
 }

@@ -975,7 +975,7 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
                                h->npts, h->d_po_frame, h->d_po_meas, h->d_fd, h->d_frec, h->d_params, h->d_pts,
                                d_pt_grad, d_pt_hess, lflags, cauchy_c, dc, s);
   if (cam_side && e == hipSuccess && h->ndep_segs > 0)
-    e = mvba_launch_depth_gram(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_meas, h->d_frec, h->d_params,
+    e = mvba_launch_depth_gram(h->d_dep_segs, h->ndep_segs, h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_frec, h->d_params,
                                h->d_pts, h->d_frame_lin, h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags,
                                cauchy_c, det ? D.slab(h->nparts) : no_slab(), s);
   if (det && e == hipSuccess && !D.ready) e = det_plan_finish(D, s);

@@ -62,7 +62,7 @@ hipError_t mvba_launch_depth_obs(const mvba::Segment* segs, int32_t nseg, const 
                                  const double* frec, const double* params, const double4* pts, void* res, void* J,
                                  int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s);
 hipError_t mvba_launch_depth_gram(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
-                                  const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                  const int32_t* dpid, const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   const void* fl, double* rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c,
                                   mvba::Slab sl, hipStream_t s);
 hipError_t mvba_launch_xyz_cost(int64_t n, const int32_t* xpid, const double4* xref, const double* xcc,
