@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
                                                  const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
                                                  const double* __restrict__ du, double* __restrict__ yrep, int64_t ng,
                                                  int32_t flags, double cauchy_c, const int32_t* __restrict__ gate,
-                                                 Slab sl) {
+                                                 Slab sl, const double4* __restrict__ wbuf) {
   if (gate && *gate) return;
   constexpr int NA = 6 + 12 + 1;
   const int seg = blockIdx.x;
@@ -302,7 +302,14 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
     const double4 m = dmeas[i];
     DepthCore c;
     depth_core(d, rec, params, m, X.x, X.y, X.z, flags, cauchy_c, c);
-    const double u[3] = {du[3 * i], du[3 * i + 1], du[3 * i + 2]};
+    // du: u_d (point-order pass A), or z_d with wbuf (frame-order k_depth_pa): u_d = z_d - P w_p
+    double u[3] = {du[3 * i], du[3 * i + 1], du[3 * i + 2]};
+    if (wbuf) {
+      const double4 w = wbuf[d.pid];
+      u[0] -= c.P * w.x;
+      u[1] -= c.P * w.y;
+      u[2] -= c.P * w.z;
+    }
     depth_jtu(c, m, u, acc, acc + 6, acc + 18);
   }
   {
@@ -422,10 +429,11 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
-                                double cauchy_c, const int32_t* gate, mvba::Slab sl, hipStream_t s) {
+                                double cauchy_c, const int32_t* gate, mvba::Slab sl, const double4* wbuf,
+                                hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params, pts,
-                     (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c, gate, sl);
+                     (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c, gate, sl, wbuf);
   return hipGetLastError();
 }
 

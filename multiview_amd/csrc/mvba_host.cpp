@@ -37,7 +37,7 @@ static void free_all(mvba_handle* h) {
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
-                  h->d_dpt_begin, h->d_dpo_slot, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xkind, h->d_xpid,
+                  h->d_dpt_begin, h->d_dpo_slot, h->d_dslot_po, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xkind, h->d_xpid,
                   h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt, h->d_varsize, h->d_tres, h->d_tcost,
                   h->d_trows, h->d_xmask, h->d_xoff, h->d_dwritten, h->d_dvarsize, h->d_tdres,
                   h->d_tdcost, h->d_tdrows};
@@ -733,6 +733,11 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_dep_order, h->dep_order));
   chk(upload(&h->d_dpt_begin, dpt_begin));
   chk(upload(&h->d_dpo_slot, dpo_slot));
+  {
+    std::vector<int32_t> dslot_po((size_t)std::max<int64_t>(h->ndep_slots, 1), -1);
+    for (size_t k = 0; k < dpo_slot.size(); k++) dslot_po[(size_t)dpo_slot[k]] = (int32_t)k;
+    chk(upload(&h->d_dslot_po, dslot_po));
+  }
   chk(upload(&h->d_xpt_begin, xpt_begin));
   chk(upload(&h->d_xref, xref));
   chk(upload(&h->d_xcc, xcc));

@@ -341,6 +341,7 @@ struct mvba_handle {
   int64_t* d_dep_order = nullptr;
   int64_t* d_dpt_begin = nullptr;         // CSR point -> depth slots
   int32_t* d_dpo_slot = nullptr;
+  int32_t* d_dslot_po = nullptr;          // depth slot -> point-order index (inverse of d_dpo_slot)
   mvba::PointExtra point_extra() const {
     mvba::PointExtra c;
     c.begin = ndep > 0 ? d_dpt_begin : nullptr;

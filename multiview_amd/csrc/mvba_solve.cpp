@@ -48,13 +48,20 @@ hipError_t mvba_launch_gather_obs_pts(int64_t nslots, const int32_t* obs_pid, co
                                       hipStream_t s);
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
                                const double* tinit, const double* V, const double* dp, const double4* pts,
-                               double* wout, int32_t wstride, const int32_t* gate, hipStream_t s);
+                               double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
+                               const double4* dcbuf, hipStream_t s);
+hipError_t mvba_launch_depth_pa(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
+                                const int32_t* dpid, const double4* dmeas, const double* frec, const double* params,
+                                const double4* pts, const double* dir, const double* xcam, double* du,
+                                const int32_t* dslot_po, double4* dcbuf, int32_t flags, double cauchy_c,
+                                const int32_t* gate, hipStream_t s);
 hipError_t mvba_launch_frame_proj(int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
                                   const double* params, double* prec, hipStream_t s);
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
-                                double cauchy_c, const int32_t* gate, mvba::Slab sl, hipStream_t s);
+                                double cauchy_c, const int32_t* gate, mvba::Slab sl, const double4* wbuf,
+                                hipStream_t s);
 hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nchunks, int32_t chunk_base,
                               const Segment* segs, const FrameDesc* fd, const void* fl, const double* frec,
                               const double* params, const double4* pts, const int32_t* obs_pid,
@@ -129,7 +136,8 @@ struct SolverState {
   double* wbuf = nullptr;     // [4 np] w_p of the last pass A (double4 per point)
   double* cbuf = nullptr;     // [4 slots] frame-order pass A: J_pt^T z per slot
   double* obsX = nullptr;     // [4 slots] landmark of each slot (fixed during a linear solve)
-  double* du = nullptr;       // [3 depth slots] u_d of the depth blocks (pass A -> k_depth_sb)
+  double* du = nullptr;       // [3 depth slots] u_d (point-order pass A) or z_d (k_depth_pa) -> k_depth_sb
+  double* dcbuf = nullptr;    // [4 depth blocks] P z_d at the point-order position (k_depth_pa -> k_point_w)
   double* partial = nullptr;  // [npartial]
   double* scal = nullptr;     // [32] device scalars
   unsigned* cnt = nullptr;    // [8] grid-reduction counters (kept zero between kernels)
@@ -148,7 +156,7 @@ struct SolverState {
 void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
-                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du,
+                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du, S->dcbuf,
                   S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -206,6 +214,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->cbuf, (size_t)(4 * std::max<int64_t>(N, 1))));
     HCHK(dalloc(&S->obsX, (size_t)(4 * std::max<int64_t>(h->nslots, 1))));
     HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
+    HCHK(dalloc(&S->dcbuf, (size_t)(4 * std::max<int64_t>(h->ndep, 1))));
     HCHK(dalloc(&S->cnt, 8));
     HCHK(hipMemset(S->cnt, 0, 8 * sizeof(unsigned)));
     int64_t ncost = 0;
@@ -378,7 +387,8 @@ class Solver {
     if (h_->ndep > 0)
       HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
                                 h_->d_params, h_->d_pts, h_->d_frame_lin, S_->du, S_->yrep, S_->ng, flags_, cauchy_c_,
-                                gate, det ? D.slab(h_->nchunks) : no_slab(), s_));
+                                gate, det ? D.slab(h_->nchunks) : no_slab(),
+                                dir ? (const double4*)S_->wbuf : nullptr, s_));  // dir: du holds z_d (k_depth_pa)
     if (det && !D.ready) HCHK(det_plan_finish(D, s_));
     const bool fuse = xv && !o_.allreduce;
     if (det)
@@ -400,24 +410,32 @@ class Solver {
   // directions of x, null for x = 0). Depth blocks need the point-lane kernel
   // (it also forms their u_d); otherwise the frame-order sweep + point solve.
   void pass_a_w(const double* dir, const double* tinit, const double* xv, const int32_t* gate) {
-    if (h_->ndep > 0)
+    if (h_->ndep > 0 && !dir) {
+      // right-hand side (x = 0): the point-order kernel also forms u_d = -P w_p
       HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas,
                               h_->d_fd, h_->d_frec, h_->d_params, h_->d_pts, dir, tinit, S_->phess,
                               S_->dmp + S_->ng, S_->zbuf, S_->wbuf, 4, nullptr, nullptr, nullptr, flags_, cauchy_c_,
                               h_->point_extra(), xv, S_->du, gate, S_->prec, s_));
-    else {
-      // one segment per wave (MVBA_PASS_A_CHUNKS=1: the 4-segment solver chunks, for A/B timing)
-      static const bool chunked = std::getenv("MVBA_PASS_A_CHUNKS") && std::getenv("MVBA_PASS_A_CHUNKS")[0] == '1';
-      if (dir)
-        for (const Group& G : h_->groups)
-          HCHK(mvba_launch_pass_a_frame(G.model, G.deg,
-                                        chunked ? h_->d_chunks + G.chunk_begin : h_->d_segchunks + G.seg_begin,
-                                        chunked ? G.chunk_count : G.seg_count, h_->d_segs,
-                                        h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dir, (double4*)S_->cbuf, flags_,
-                                        cauchy_c_, gate, S_->prec, obsx(), s_));
-      HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, h_->d_po_slot, dir ? (const double4*)S_->cbuf : nullptr,
-                               tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate, s_));
+      return;
     }
+    // one segment per wave (MVBA_PASS_A_CHUNKS=1: the 4-segment solver chunks, for A/B timing)
+    static const bool chunked = std::getenv("MVBA_PASS_A_CHUNKS") && std::getenv("MVBA_PASS_A_CHUNKS")[0] == '1';
+    if (dir)
+      for (const Group& G : h_->groups)
+        HCHK(mvba_launch_pass_a_frame(G.model, G.deg,
+                                      chunked ? h_->d_chunks + G.chunk_begin : h_->d_segchunks + G.seg_begin,
+                                      chunked ? G.chunk_count : G.seg_count, h_->d_segs,
+                                      h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dir, (double4*)S_->cbuf, flags_,
+                                      cauchy_c_, gate, S_->prec, obsx(), s_));
+    // depth blocks in frame order (z_d into du, P z_d per block for the point solve)
+    const bool dep = dir && h_->ndep > 0;
+    if (dep)
+      HCHK(mvba_launch_depth_pa(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_pid, h_->d_dep_meas,
+                                h_->d_frec, h_->d_params, h_->d_pts, dir, xv, S_->du, h_->d_dslot_po,
+                                (double4*)S_->dcbuf, flags_, cauchy_c_, gate, s_));
+    HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, h_->d_po_slot, dir ? (const double4*)S_->cbuf : nullptr,
+                             tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate,
+                             dep ? h_->d_dpt_begin : nullptr, dep ? (const double4*)S_->dcbuf : nullptr, s_));
   }
 
   // y = S x (implicit Schur complement with damping); x.y -> scal[dot_slot].

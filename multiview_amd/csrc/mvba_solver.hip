@@ -445,6 +445,42 @@ __global__ void k_gather_obs_pts(int64_t nslots, const int32_t* __restrict__ obs
   if (i < nslots) out[i] = pts[obs_pid[i]];
 }
 
+// BracketedDepthError / BracketedDepthMeshError blocks in the frame-order CG
+// product: one wave per depth segment (one image: the descriptor is read once,
+// the point per lane), z_d = J_cam,d x into du (slot order; k_depth_sb forms
+// u_d = z_d - P w_p once w is known) and c_d = P z_d at the block's point-order
+// position for k_point_w. Replaces the point-order k_pass_a (4 lanes per point
+// gathering per-frame data) inside CG iterations.
+__global__ void __launch_bounds__(64) k_depth_pa(const Segment* __restrict__ segs, int32_t nseg,
+                                                 const DepthDesc* __restrict__ dd, const int32_t* __restrict__ dpid,
+                                                 const double4* __restrict__ dmeas, const double* __restrict__ frec,
+                                                 const double* __restrict__ params, const double4* __restrict__ pts,
+                                                 const double* __restrict__ dir, const double* __restrict__ xcam,
+                                                 double* __restrict__ du, const int32_t* __restrict__ dslot_po,
+                                                 double4* __restrict__ dcbuf, int32_t flags, double cauchy_c,
+                                                 const int32_t* __restrict__ gate) {
+  if (gate && *gate) return;
+  const int seg = blockIdx.x;
+  if (seg >= nseg) return;
+  const Segment sg = segs[seg];
+  const int lane = threadIdx.x;
+  const int count = __builtin_amdgcn_readfirstlane(sg.count);
+  const int begin = __builtin_amdgcn_readfirstlane(sg.begin);
+  if (lane >= count) return;
+  const int64_t i = (int64_t)begin + lane;
+  DepthDesc d = dd[begin];
+  d.pid = dpid[i];
+  const double4 X = pts[d.pid];
+  const double4 m = dmeas[i];
+  DepthCore c;
+  depth_core(d, frec + (int64_t)d.frame * kFrameRecDoubles, params, m, X.x, X.y, X.z, flags, cauchy_c, c);
+  double z[3];
+  depth_jx(d, c, m, dir + (int64_t)d.frame * kDirStride, xcam, z);
+#pragma unroll
+  for (int q = 0; q < 3; q++) du[3 * i + q] = z[q];
+  dcbuf[dslot_po[i]] = make_double4(c.P * z[0], c.P * z[1], c.P * z[2], 0.0);
+}
+
 // w_p = (V + D)^-1 (tinit + sum_o c_o), kLanesW lanes per point gathering its
 // c_o (lane-strided, then a butterfly sum); cbuf null: x = 0
 constexpr int kLanesW = 8;
@@ -453,7 +489,8 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
                                                  const double* __restrict__ tinit, const double* __restrict__ V,
                                                  const double* __restrict__ dp, const double4* __restrict__ pts,
                                                  double* __restrict__ wout, int32_t wstride,
-                                                 const int32_t* __restrict__ gate) {
+                                                 const int32_t* __restrict__ gate, const int64_t* __restrict__ dbegin,
+                                                 const double4* __restrict__ dcbuf) {
   if (gate && *gate) return;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t p = t0 / kLanesW;
@@ -463,6 +500,13 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
   if (valid && cbuf)
     for (int64_t j = pt_begin[p] + sub; j < pt_begin[p + 1]; j += kLanesW) {
       const double4 cv = cbuf[j];
+      t[0] += cv.x;
+      t[1] += cv.y;
+      t[2] += cv.z;
+    }
+  if (valid && dcbuf)  // depth blocks of the point (k_depth_pa), point order
+    for (int64_t j = dbegin[p] + sub; j < dbegin[p + 1]; j += kLanesW) {
+      const double4 cv = dcbuf[j];
       t[0] += cv.x;
       t[1] += cv.y;
       t[2] += cv.z;
@@ -1285,11 +1329,23 @@ hipError_t mvba_launch_gather_obs_pts(int64_t nslots, const int32_t* obs_pid, co
 
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
                                const double* tinit, const double* V, const double* dp, const double4* pts,
-                               double* wout, int32_t wstride, const int32_t* gate, hipStream_t s) {
+                               double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
+                               const double4* dcbuf, hipStream_t s) {
   if (npts <= 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_point_w, dim3((unsigned)((npts * mvba::kLanesW + 255) / 256)), dim3(256), 0, s, npts,
                      pt_begin, po_slot,
-                     cbuf, tinit, V, dp, pts, wout, wstride, gate);
+                     cbuf, tinit, V, dp, pts, wout, wstride, gate, dbegin, dcbuf);
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_depth_pa(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
+                                const int32_t* dpid, const double4* dmeas, const double* frec, const double* params,
+                                const double4* pts, const double* dir, const double* xcam, double* du,
+                                const int32_t* dslot_po, double4* dcbuf, int32_t flags, double cauchy_c,
+                                const int32_t* gate, hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_depth_pa, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dpid, dmeas, frec, params,
+                     pts, dir, xcam, du, dslot_po, dcbuf, flags, cauchy_c, gate);
   return hipGetLastError();
 }
 
