@@ -278,7 +278,8 @@ __global__ void __launch_bounds__(256) k_depth_cost(int64_t nslots, const DepthD
 // y += J_cam,d^T u_d, wave-reduced per segment, mapped through the generators,
 // added into replica (segment mod 32) of the camera-side vector.
 __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ segs, int32_t nseg,
-                                                 const DepthDesc* __restrict__ dd, const double4* __restrict__ dmeas,
+                                                 const DepthDesc* __restrict__ dd, const int32_t* __restrict__ dpid,
+                                                 const double4* __restrict__ dmeas,
                                                  const double* __restrict__ frec, const double* __restrict__ params,
                                                  const double4* __restrict__ pts, const FrameLin* __restrict__ fl,
                                                  const double* __restrict__ du, double* __restrict__ yrep, int64_t ng,
@@ -297,7 +298,8 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
   const DepthDesc d0 = dd[sg.begin];
   if (lane < sg.count) {
     const int64_t i = (int64_t)sg.begin + lane;
-    const DepthDesc d = dd[i];
+    DepthDesc d = d0;  // one image per segment: only the point differs
+    d.pid = dpid[i];
     const double4 X = pts[d.pid];
     const double4 m = dmeas[i];
     DepthCore c;
@@ -427,12 +429,12 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
 }
 
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
-                                const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                const int32_t* dpid, const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
                                 double cauchy_c, const int32_t* gate, mvba::Slab sl, const double4* wbuf,
                                 hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dmeas, frec, params, pts,
+  hipLaunchKernelGGL(mvba::k_depth_sb, dim3((unsigned)nseg), dim3(64), 0, s, segs, nseg, dd, dpid, dmeas, frec, params, pts,
                      (const mvba::FrameLin*)fl, du, yrep, ng, flags, cauchy_c, gate, sl, wbuf);
   return hipGetLastError();
 }

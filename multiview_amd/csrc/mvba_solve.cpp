@@ -58,7 +58,7 @@ hipError_t mvba_launch_depth_pa(const mvba::Segment* segs, int32_t nseg, const m
 hipError_t mvba_launch_frame_proj(int32_t nframes, const mvba::FrameDesc* fd, const double* frec,
                                   const double* params, double* prec, hipStream_t s);
 hipError_t mvba_launch_depth_sb(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
-                                const double4* dmeas, const double* frec, const double* params, const double4* pts,
+                                const int32_t* dpid, const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                 const void* fl, const double* du, double* yrep, int64_t ng, int32_t flags,
                                 double cauchy_c, const int32_t* gate, mvba::Slab sl, const double4* wbuf,
                                 hipStream_t s);
@@ -385,7 +385,7 @@ class Solver {
                               h_->d_obs_pid, h_->d_obs_meas, dir, (const double4*)S_->wbuf, S_->yrep, S_->ng, flags_,
                               cauchy_c_, gate, det ? D.slab(0) : no_slab(), obsx(), s_));
     if (h_->ndep > 0)
-      HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_meas, h_->d_frec,
+      HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_pid, h_->d_dep_meas, h_->d_frec,
                                 h_->d_params, h_->d_pts, h_->d_frame_lin, S_->du, S_->yrep, S_->ng, flags_, cauchy_c_,
                                 gate, det ? D.slab(h_->nchunks) : no_slab(),
                                 dir ? (const double4*)S_->wbuf : nullptr, s_));  // dir: du holds z_d (k_depth_pa)
