@@ -359,6 +359,40 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     return res_frame[a] < res_frame[b];
   });
 
+  // Point numbering in order of first use in DEVICE order (frame order), not in
+  // AddResidualBlock order: a frame's landmarks then have nearby indices, so K1's
+  // landmark gathers, the solver's point-order scatters (c_o) and gathers
+  // (k_point_w) touch a cache-sized window instead of the whole table (tables of
+  // 10M+ observations exceed the 256 MB Infinity Cache). Points without a
+  // reprojection residual keep their relative order after those; the virtual
+  // mesh points stay last. mvba_point_block_map reports the numbering.
+  {
+    const int64_t np = (int64_t)pt_off.size();
+    std::vector<int32_t> perm((size_t)np, -1);
+    int32_t next = 0;
+    for (int64_t p = 0; p < N; p++) {
+      const int32_t q = res_pt[idx[p]];
+      if (perm[q] < 0) perm[q] = next++;
+    }
+    for (int64_t q = 0; q < h->npts_user; q++)
+      if (perm[q] < 0) perm[q] = next++;
+    for (int64_t q = h->npts_user; q < np; q++) perm[q] = (int32_t)q;  // mesh points: unchanged, last
+    std::vector<int64_t> off2((size_t)np);
+    std::vector<uint8_t> free2((size_t)np);
+    for (int64_t q = 0; q < np; q++) {
+      off2[perm[q]] = pt_off[q];
+      free2[perm[q]] = pt_free[q];
+    }
+    pt_off.swap(off2);
+    pt_free.swap(free2);
+    for (auto& v : res_pt) v = perm[v];
+    for (auto& v : dep_pt) v = perm[v];
+    for (auto& v : xyz_pt) v = perm[v];
+    for (auto& kv : pt_index) kv.second = perm[kv.second];
+    h->res_pt = res_pt;
+    h->pt_free_h = pt_free;
+  }
+
   // Device slots: every frame's residuals start on a 128-byte line (16 doubles,
   // 32 floats), so each wavefront's 64-element store chunk per Jacobian plane is
   // line-aligned (misaligned chunks write at ~60% of the aligned rate:

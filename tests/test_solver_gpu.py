@@ -315,6 +315,13 @@ def _cam_values(ev, P):
     return np.concatenate(out)
 
 
+def _points_by_block(ev, P):
+    """Point values in parameter-block order (the library numbers points by first
+    use in device order; block ids follow the landmark index)."""
+    ids = np.sort(ev.lin_layout()["point_block_ids"])
+    return np.concatenate([P.block_values(int(b)) for b in ids if b >= 0])
+
+
 def _shard_worker(rank, world, port, out_dir):
     import sys
 
@@ -336,7 +343,7 @@ def _shard_worker(rank, world, port, out_dir):
         s = ev.solve(max_num_iterations=100, allreduce=ex, **TOL)
         P.params = ev.get_params()
         cam = _cam_values(ev, P)
-        pts = np.concatenate([P.block_values(int(b)) for b in ev.lin_layout()["point_block_ids"]])
+        pts = _points_by_block(ev, P)
     np.save(os.path.join(out_dir, f"cam{rank}.npy"), cam)
     np.save(os.path.join(out_dir, f"pts{rank}.npy"), pts)
     np.save(os.path.join(out_dir, f"cost{rank}.npy"), np.array([s["final_cost"], s["termination_type"]]))
@@ -384,11 +391,11 @@ def test_sharded_solve_matches_unsharded(tmp_path):
         s = ev.solve(max_num_iterations=100, **TOL)
         P.params = ev.get_params()
         cam = _cam_values(ev, P)
-        pts_ref = np.concatenate([P.block_values(int(b)) for b in ev.lin_layout()["point_block_ids"]])
+        pts_ref = _points_by_block(ev, P)
     assert s["termination_type"] == 0
     assert np.isclose(costs[0][0], s["final_cost"], rtol=1e-9)
     assert _close(cams[0], cam, 1e-6)
-    # point order: first use in residual order = shard 0's points then shard 1's
+    # points by block id = landmark order: shard 0's landmarks, then shard 1's
     assert _close(pts, pts_ref, 1e-6)
 
 
@@ -437,7 +444,7 @@ def test_local_comm_sharded_solve_device_resident():
     for r in range(world):
         probs[r].params = evs[r].get_params()
         cams.append(_cam_values(evs[r], probs[r]))
-        pts.append(np.concatenate([probs[r].block_values(int(b)) for b in evs[r].lin_layout()["point_block_ids"]]))
+        pts.append(_points_by_block(evs[r], probs[r]))
     assert out[0]["termination_type"] == 0, out[0]["message"]
     assert out[0]["final_cost"] == out[1]["final_cost"]
     assert out[0]["num_linear_iterations"] == out[1]["num_linear_iterations"]
@@ -452,7 +459,7 @@ def test_local_comm_sharded_solve_device_resident():
         s = ev.solve(max_num_iterations=100, **TOL)
         P.params = ev.get_params()
         cam = _cam_values(ev, P)
-        pts_ref = np.concatenate([P.block_values(int(b)) for b in ev.lin_layout()["point_block_ids"]])
+        pts_ref = _points_by_block(ev, P)
     assert np.isclose(out[0]["final_cost"], s["final_cost"], rtol=1e-9)
     assert _close(cams[0], cam, 1e-6)
     assert _close(np.concatenate(pts), pts_ref, 1e-6)
