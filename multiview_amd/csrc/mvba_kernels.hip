@@ -190,14 +190,15 @@ __global__ void __launch_bounds__(kPrepBlock) k_prep(const FrameDesc* __restrict
                                                      double* __restrict__ frec, const int64_t* __restrict__ pt_off,
                                                      const uint8_t* __restrict__ pt_free, int64_t npts,
                                                      double4* __restrict__ pts, int gen, int* __restrict__ err) {
-  if ((int)blockIdx.x < frame_blocks) {
-    const int64_t t = (int64_t)blockIdx.x * kPrepBlock + threadIdx.x;
+  const int bid = (int)blockIdx.x;
+  if (bid < frame_blocks) {
+    const int64_t t = (int64_t)bid * kPrepBlock + threadIdx.x;
     const int64_t f = t / kThreadsPerFrame;
     if (f >= nframes) return;
     const FrameDesc F = fd[f];
     frame_columns(F, params, frec + f * kFrameRecDoubles, (int)(t % kThreadsPerFrame), gen, err);
   } else {
-    const int64_t p = (int64_t)(blockIdx.x - frame_blocks) * kPrepBlock + threadIdx.x;
+    const int64_t p = (int64_t)(bid - frame_blocks) * kPrepBlock + threadIdx.x;
     if (p >= npts) return;
     const int64_t o = pt_off[p];
     pts[p] = make_double4(params[o], params[o + 1], params[o + 2], pt_free[p] ? 1.0 : 0.0);

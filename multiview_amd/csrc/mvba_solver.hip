@@ -15,7 +15,10 @@
 namespace mvba {
 
 constexpr int kDirStride = 128;    // per-frame direction record: u (6) | x_intr (<= 122: RPC degree 6 has 113)
-constexpr int kVecReplicas = 32;
+#ifndef MVBA_VEC_REPLICAS
+#define MVBA_VEC_REPLICAS 32
+#endif
+constexpr int kVecReplicas = MVBA_VEC_REPLICAS;  // power of two
 
 // Camera-side columns of one observation at a frame, as a row pair:
 // Z (6), intrinsics (focal, center 2, live distortion nd), J_pt (3), corrected r.

@@ -19,7 +19,7 @@ import json,sys
 for ln in open(sys.argv[1]):
     if ln.startswith("{"):
         d=json.loads(ln); L=d.get("linearize",{})
-        print("    lin kernel %.1f us, camera side %.1f us, point side %.1f us" % (1e3*L.get("kernel_ms",0), 1e3*L.get("camera_side_ms",0), 1e3*L.get("point_side_ms",0)))
+        print("    step %.1f us, prep %.1f us | lin kernel %.1f us, camera side %.1f us, point side %.1f us" % (1e3*d["ms_per_step"], 1e3*d["roofline"].get("prep_ms",0), 1e3*L.get("kernel_ms",0), 1e3*L.get("camera_side_ms",0), 1e3*L.get("point_side_ms",0)))
 PY
   done
 done
