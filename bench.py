@@ -55,6 +55,8 @@ def parse():
                     help="icosphere level of the --mesh ray-intersection line (0 = skip; 7 = 327,680 faces)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, default) or gloo (rehearsal of the multi-rank path on one GPU)")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="single-process rehearsal: run rank 0's shard of an N-way strong split (timing only)")
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
                     help="strong (default): the config is the whole job, split over the ranks; "
                          "weak: every rank owns a config-sized shard")
@@ -347,7 +349,8 @@ def main():
         if strong_split:
             # the config's landmark count is the whole problem, split into
             # contiguous landmark ranges
-            c["point_range"] = (rank * npts // world, (rank + 1) * npts // world)
+            split = world if world > 1 else max(1, args.shard_of)
+            c["point_range"] = (rank * npts // split, (rank + 1) * npts // split)
         else:
             # each rank owns a config-sized shard of an N x larger problem
             c["point_range"] = (rank * npts, (rank + 1) * npts)
@@ -383,18 +386,26 @@ def main():
         for _ in range(args.warmup):
             step()
         ev.sync(sh)
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(args.steps):
-            step(evs[k])
+            step()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
         ev.sync(sh)  # raises on device-side errors (alpha out of range)
+        # Per-kernel times: the same K steps again, each split into its prep and
+        # K1 launches with HIP events on the launch stream between them. Events
+        # between kernels cost the step ~10 us (c2: 114 vs 104 us per step;
+        # tools/step_overhead.py), so the timed loop above carries none.
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize()
+        ev.sync(sh)
         prep_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
         obs_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
@@ -410,6 +421,8 @@ def main():
     n = ev.num_residuals
     dt_max, total_evals, prep_ms, obs_ms = time_eval(ev)
 
+    if world == 1 and args.shard_of > 1:  # timing rehearsal, not a bench line
+        cfg["shard_rehearsal"] = f"rank 0's shard of a {args.shard_of}-way landmark split, one process"
     bytes_eval = ev.eval_bytes(True)                 # algorithmic bytes of K1 per launch set
     achieved = bytes_eval / (obs_ms * 1e-3) / 1e9    # GB/s
     line = {
@@ -435,6 +448,7 @@ def main():
             "num_frames": ev.num_frames,
             "num_points_per_gpu": ev.num_points,
             "parallelism": f"landmark-range shards x{world}",
+            **({"shard_rehearsal": cfg["shard_rehearsal"]} if "shard_rehearsal" in cfg else {}),
         },
         "roofline": {
             "bound": "hbm",
@@ -447,6 +461,9 @@ def main():
             "bytes_per_launch": bytes_eval,
             "kernel_ms": obs_ms,
             "prep_ms": prep_ms,
+            "kernel_timing": "HIP events on the launch stream around the prep and K1 launches of K "
+                             "instrumented steps run right after the timed loop (the timed loop has no "
+                             "events: they add ~10 us per step)",
         },
         "gen_s": t_gen,
     }
