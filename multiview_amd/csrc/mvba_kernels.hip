@@ -213,8 +213,8 @@ __device__ __forceinline__ void stj(OT* J, int64_t ld, int row, int64_t i, doubl
   __builtin_nontemporal_store((OT)v, J + (int64_t)row * ld + i);
 }
 
-template <int MODEL, int DEG, class OT>
-__global__ void __launch_bounds__(256) k_obs(
+template <int MODEL, int DEG, class OT, bool JAC>
+__device__ __forceinline__ void obs_body(
     const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(256) k_obs(
     __builtin_nontemporal_store((OT)r0, res + i);
     __builtin_nontemporal_store((OT)r1, res + ld + i);
   }
-  if (!(flags & MVBA_EVAL_JACOBIAN)) return;
+  if (!JAC) return;
 
   // G = A * du/dXc, du/dXc = (f/z) [[1, 0, -nx], [0, 1, -ny]]; scaled by the loss.
   const double fz = f / o.Xc[2] * sr;
@@ -334,6 +334,27 @@ __global__ void __launch_bounds__(256) k_obs(
 // (2 rows per observation): B^T B holds Z^T Z, Z^T J_intr, J_intr^T J_intr and
 // the gradients Z^T r, J_intr^T r; the expansion applies w.
 //
+// K1 with the Jacobian planes, and the residual-only evaluation under its own
+// name (k_obs_res) so kernel statistics never mix the two.
+template <int MODEL, int DEG, class OT>
+__global__ void __launch_bounds__(256) k_obs(
+    const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
+    const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
+    int64_t ld, int32_t flags, double cauchy_c) {
+  obs_body<MODEL, DEG, OT, true>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld, flags, cauchy_c);
+}
+template <int MODEL, int DEG, class OT>
+__global__ void __launch_bounds__(256) k_obs_res(
+    const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
+    const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
+    int64_t ld, int32_t flags, double cauchy_c) {
+  obs_body<MODEL, DEG, OT, false>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld, flags, cauchy_c);
+}
+
 // k_frame_lin: one block per frame part (<= kPartSegs segments of ONE frame),
 // WAVES waves per block. Each wave builds the Gram of its segments' rows (a
 // K = 128-deep GEMM per segment on fp64 MFMA v_mfma_f64_16x16x4, B staged in
@@ -854,15 +875,20 @@ hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_
                            hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   const unsigned blocks = mvba::xcd_grid((nseg + 3) / 4);
-#define MVBA_OBS(M, D)                                                                                     \
-  if (out_f32)                                                                                           \
-    hipLaunchKernelGGL((mvba::k_obs<M, D, float>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec,    \
-                       params, pts, obs_pid, obs_meas, (float*)res, (float*)J, ld, flags, cauchy_c);       \
-  else                                                                                                   \
-    hipLaunchKernelGGL((mvba::k_obs<M, D, double>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec,   \
-                       params, pts, obs_pid, obs_meas, (double*)res, (double*)J, ld, flags, cauchy_c)
+#define MVBA_OBS_K(KER, M, D, OT)                                                                            \
+  hipLaunchKernelGGL((mvba::KER<M, D, OT>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec, params, pts, \
+                     obs_pid, obs_meas, (OT*)res, (OT*)J, ld, flags, cauchy_c)
+#define MVBA_OBS(M, D)                                                                                   \
+  if (flags & MVBA_EVAL_JACOBIAN) {                                                                      \
+    if (out_f32) MVBA_OBS_K(k_obs, M, D, float);                                                         \
+    else MVBA_OBS_K(k_obs, M, D, double);                                                                \
+  } else {                                                                                               \
+    if (out_f32) MVBA_OBS_K(k_obs_res, M, D, float);                                                     \
+    else MVBA_OBS_K(k_obs_res, M, D, double);                                                            \
+  }
   MVBA_SWITCH_MODEL(model, deg, MVBA_OBS)
 #undef MVBA_OBS
+#undef MVBA_OBS_K
   return hipGetLastError();
 }
 
