@@ -463,3 +463,62 @@ def test_local_comm_sharded_solve_device_resident():
     assert np.isclose(out[0]["final_cost"], s["final_cost"], rtol=1e-9)
     assert _close(cams[0], cam, 1e-6)
     assert _close(np.concatenate(pts), pts_ref, 1e-6)
+
+
+def _rccl_world1_worker(port, out):
+    """One rank: torch.distributed over RCCL (world 1), the library's RCCL
+    communicator joined from the broadcast unique id (dist.Comm.rccl, the path
+    bench.py takes at N > 1), a solve exchanging through it."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from multiview_amd.dist import Comm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    try:
+        comm = Comm.rccl(0)
+        P = rig.build_problem(rig.make_rig(**CFG), FLAGS)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(max_num_iterations=20, comm=comm, **TOL)
+            np.save(out, ev.get_params())
+            np.save(out + ".cost.npy", np.array([s["final_cost"], s["termination_type"]]))
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_comm_world1_solve(tmp_path):
+    """mvba_comm_init_rccl + mvba_comm_allreduce (RCCL) at world size 1 in a
+    child process: the communicator bench.py builds for N > 1 initialises from
+    the torch.distributed-broadcast unique id, and a solve exchanging through it
+    converges to the unsharded solve's point (the exchange is an identity at
+    world 1, so only the plumbing is under test)."""
+    import multiprocessing as mpc
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "rccl_params.npy")
+    ctx = mpc.get_context("spawn")
+    p = ctx.Process(target=_rccl_world1_worker, args=(port, out))
+    p.start()
+    p.join(240)
+    assert p.exitcode == 0, p.exitcode
+    P = rig.build_problem(rig.make_rig(**CFG), FLAGS)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s_ref = ev.solve(max_num_iterations=20, **TOL)
+        ref = ev.get_params()
+    got = np.load(out)
+    cost, term = np.load(out + ".cost.npy")
+    assert int(term) == s_ref["termination_type"]
+    assert np.isclose(cost, s_ref["final_cost"], rtol=1e-9)
+    assert _close(got, ref, 1e-6)
