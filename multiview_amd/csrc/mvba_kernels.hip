@@ -29,6 +29,10 @@ namespace mvba {
 // 22 pose columns); the remaining blocks gather the points.
 constexpr int kThreadsPerFrame = 16;
 constexpr int kPrepBlock = 256;
+#ifndef MVBA_PREP_POINTS
+#define MVBA_PREP_POINTS 4
+#endif
+constexpr int kPrepPoints = MVBA_PREP_POINTS;  // landmarks gathered per thread
 
 __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ params, double* rec,
                               int sub, int gen, int* err) {
@@ -198,10 +202,29 @@ __global__ void __launch_bounds__(kPrepBlock) k_prep(const FrameDesc* __restrict
     const FrameDesc F = fd[f];
     frame_columns(F, params, frec + f * kFrameRecDoubles, (int)(t % kThreadsPerFrame), gen, err);
   } else {
-    const int64_t p = (int64_t)(bid - frame_blocks) * kPrepBlock + threadIdx.x;
-    if (p >= npts) return;
-    const int64_t o = pt_off[p];
-    pts[p] = make_double4(params[o], params[o + 1], params[o + 2], pt_free[p] ? 1.0 : 0.0);
+    // kPrepPoints landmarks per thread, all loads in flight before the stores
+    const int64_t p0 = (int64_t)(bid - frame_blocks) * kPrepBlock * kPrepPoints + threadIdx.x;
+    int64_t o[kPrepPoints];
+#pragma unroll
+    for (int j = 0; j < kPrepPoints; j++) {
+      const int64_t p = p0 + (int64_t)j * kPrepBlock;
+      o[j] = p < npts ? pt_off[p] : -1;
+    }
+    double v[kPrepPoints][3];
+    bool fr[kPrepPoints];
+#pragma unroll
+    for (int j = 0; j < kPrepPoints; j++) {
+      const int64_t p = p0 + (int64_t)j * kPrepBlock;
+      if (o[j] >= 0) {
+        v[j][0] = params[o[j]];
+        v[j][1] = params[o[j] + 1];
+        v[j][2] = params[o[j] + 2];
+        fr[j] = pt_free[p] != 0;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kPrepPoints; j++)
+      if (o[j] >= 0) pts[p0 + (int64_t)j * kPrepBlock] = make_double4(v[j][0], v[j][1], v[j][2], fr[j] ? 1.0 : 0.0);
   }
 }
 
@@ -841,7 +864,7 @@ hipError_t mvba_launch_prep(const mvba::FrameDesc* fd, int64_t nframes, const do
                             double* frec, const int64_t* pt_off, const uint8_t* pt_free, int64_t npts,
                             double4* pts, int gen, int* err, hipStream_t s) {
   const int64_t fb = (nframes * mvba::kThreadsPerFrame + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
-  const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
+  const int64_t pb = (npts + mvba::kPrepBlock * mvba::kPrepPoints - 1) / (mvba::kPrepBlock * mvba::kPrepPoints);
   if (fb + pb == 0) return hipSuccess;
   hipLaunchKernelGGL(mvba::k_prep, dim3((unsigned)(fb + pb)), dim3(mvba::kPrepBlock), 0, s, fd, nframes,
                      (int32_t)fb, params, frec, pt_off, pt_free, npts, pts, gen, err);
