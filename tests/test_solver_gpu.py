@@ -511,6 +511,9 @@ def test_rccl_comm_world1_solve(tmp_path):
     p = ctx.Process(target=_rccl_world1_worker, args=(port, out))
     p.start()
     p.join(240)
+    if p.is_alive():  # never leave a rank holding the GPU behind
+        p.kill()
+        p.join()
     assert p.exitcode == 0, p.exitcode
     P = rig.build_problem(rig.make_rig(**CFG), FLAGS)
     with Evaluator(P) as ev:
