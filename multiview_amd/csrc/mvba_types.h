@@ -57,7 +57,10 @@ enum ModelKind : int32_t {
 constexpr int kMaxRpcDegree = 6;
 constexpr int kMaxLinRpcDegree = 6;
 constexpr int kChunkSegs = 4;       // segments per solver chunk (one wave)
-constexpr int kPartSegs = 16;       // segments per K2 frame part (one block)
+#ifndef MVBA_PART_SEGS
+#define MVBA_PART_SEGS 16
+#endif
+constexpr int kPartSegs = MVBA_PART_SEGS;  // segments per K2 frame part (one block)
 constexpr int kDepthReplicas = 32;  // replicas the depth Gram adds into (frame-segment mod 32)
 
 // Deterministic accumulation (mvba_solver_options.deterministic,
