@@ -1006,7 +1006,7 @@ mvba_status mvba_linearize_device(mvba_handle* h, int32_t flags, double cauchy_t
                                 h->d_frame_lin, h->d_frec, h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas,
                                 h->d_rep, h->cam_grad_size, h->cam_hess_size, lflags, cauchy_c,
                                 pts_here ? h->d_pt_begin : nullptr, h->npts, h->d_po_frame, h->d_po_meas, d_pt_grad,
-                                d_pt_hess, dc, det ? D.slab(0) : no_slab(), G.part_begin, s);
+                                d_pt_hess, dc, det ? D.slab(0) : no_slab(), G.part_begin, h->lin_obsx, s);
     }
   }
   if (pt_side && (!single || !cam_side) && e == hipSuccess)

@@ -36,7 +36,7 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
                                  int64_t ng, int64_t nh, int32_t flags, double cauchy_c, const int64_t* pt_begin,
                                  int64_t npts, const int32_t* po_frame, const double2* po_meas, double* pgrad,
                                  double* phess, mvba::PointExtra dc, mvba::Slab sl, int32_t part_base,
-                                 hipStream_t s);
+                                 double4* obsx_out, hipStream_t s);
 hipError_t mvba_launch_slab_lin(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
                                 const double* val, int64_t ng, int64_t nh, double* grad, double* hess, double* cost,
                                 hipStream_t s);
@@ -266,6 +266,10 @@ struct mvba_handle {
   int64_t* d_pt_off = nullptr;
   uint8_t* d_pt_free = nullptr;
   double4* d_pts = nullptr;
+  // set by mvba_solve for its duration: K2 also writes every reprojection
+  // slot's (landmark xyz, Cauchy weight sqrt(rho')) here, the record the
+  // frame-order CG passes read instead of the landmark + measurement
+  double4* lin_obsx = nullptr;
   int32_t* d_obs_pid = nullptr;
   double2* d_obs_meas = nullptr;
   Segment* d_segs = nullptr;

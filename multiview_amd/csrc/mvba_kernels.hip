@@ -464,7 +464,7 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
     const double* __restrict__ params, const double4* __restrict__ pts,
     const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
     double* __restrict__ rep, int64_t ng, int64_t nh, int32_t flags, double cauchy_c, PointLinArgs pa, Slab sl,
-    int32_t part_base) {
+    int32_t part_base, double4* __restrict__ obsx_out) {
   using S = GramShape<MODEL, DEG>;
   constexpr int T = S::kTiles;
   constexpr int NP = S::kPairs;
@@ -510,6 +510,7 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
     double half_rho;
     const double sr = loss_scale(r0, r1, flags, cauchy_c, &half_rho);
     cost += half_rho;
+    if (obsx_out) obsx_out[i] = make_double4(P.x, P.y, P.z, sr);  // the CG passes' per-slot record
     const double fz = f / o.Xc[2] * sr;
     const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
     const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
@@ -944,7 +945,7 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
                                  int64_t ng, int64_t nh, int32_t flags, double cauchy_c, const int64_t* pt_begin,
                                  int64_t npts, const int32_t* po_frame, const double2* po_meas, double* pgrad,
                                  double* phess, mvba::PointExtra dc, mvba::Slab sl, int32_t part_base,
-                                 hipStream_t s) {
+                                 double4* obsx_out, hipStream_t s) {
   const bool with_pts = pt_begin != nullptr && npts > 0;
   if (nparts <= 0 && !with_pts) return hipSuccess;
   const mvba::PointLinArgs pa{pt_begin, npts, po_frame, po_meas, pgrad, phess, dc};
@@ -957,11 +958,11 @@ hipError_t mvba_launch_frame_lin(int model, int deg, const int4* parts, int32_t 
       hipLaunchKernelGGL((mvba::k_frame_lin<M, D, true>), dim3((unsigned)(nparts + pblocks)),             \
                          dim3((unsigned)threads), GS::kLdsBytes, s, parts, nparts, segs, fd,               \
                          (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas, rep, ng, nh, flags, \
-                         cauchy_c, pa, sl, part_base);                                                     \
+                         cauchy_c, pa, sl, part_base, obsx_out);                                           \
     else                                                                                                   \
       hipLaunchKernelGGL((mvba::k_frame_lin<M, D, false>), dim3((unsigned)nparts), dim3((unsigned)threads), \
                          GS::kLdsBytes, s, parts, nparts, segs, fd, (const mvba::FrameLin*)fl, frec, params, \
-                         pts, obs_pid, obs_meas, rep, ng, nh, flags, cauchy_c, pa, sl, part_base);         \
+                         pts, obs_pid, obs_meas, rep, ng, nh, flags, cauchy_c, pa, sl, part_base, obsx_out); \
   }
   switch (model) {
     case mvba::kModelNone: MVBA_FLIN(mvba::kModelNone, 0); break;

@@ -261,6 +261,8 @@ class Solver {
   }
 
   void run(mvba_solver_summary* sum);
+  // the frame-order passes' per-slot records (null with MVBA_NO_OBSX=1)
+  double4* obsx_records() const { return const_cast<double4*>(obsx()); }
 
  private:
   mvba_handle* h_;
@@ -452,7 +454,10 @@ class Solver {
   // records for pass A are built here (parameters fixed until the next step).
   void schur_rhs() {
     HCHK(mvba_launch_frame_proj((int32_t)h_->nframes, h_->d_fd, h_->d_frec, h_->d_params, S_->prec, s_));
-    HCHK(mvba_launch_gather_obs_pts(h_->nslots, h_->d_obs_pid, h_->d_pts, (double4*)S_->obsX, s_));
+    // the per-slot records (landmark + Cauchy weight) were written by K2 at
+    // this linearization point (h_->lin_obsx); without them, landmarks only
+    if (!h_->lin_obsx && obsx())
+      HCHK(mvba_launch_gather_obs_pts(h_->nslots, h_->d_obs_pid, h_->d_pts, (double4*)S_->obsX, s_));
     pass_a_w(nullptr, S_->G + S_->ng, nullptr, nullptr);
     reduce_frames(S_->tmp, nullptr, 0, nullptr);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
@@ -1001,6 +1006,12 @@ mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver
   try {
     if (!h->solver) h->solver = alloc_state(h);
     Solver sv(h, *o, (hipStream_t)stream);
+    // K2 writes the CG passes' per-slot records for the duration of the solve
+    struct ObsxScope {
+      mvba_handle* h;
+      ~ObsxScope() { h->lin_obsx = nullptr; }
+    } scope{h};
+    h->lin_obsx = sv.obsx_records();
     sv.run(summary);
   } catch (const HipErr& e) {
     std::snprintf(summary->message, sizeof(summary->message), "HIP error");

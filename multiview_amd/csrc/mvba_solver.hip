@@ -23,20 +23,25 @@ constexpr int kVecReplicas = MVBA_VEC_REPLICAS;  // power of two
 // Camera-side columns of one observation at a frame, as a row pair:
 // Z (6), intrinsics (focal, center 2, live distortion nd), J_pt (3), corrected r.
 template <int MODEL, int DEG>
+// sr_given >= 0: the Cauchy weight K2 stored with the slot's landmark (the
+// residual and the loss are not recomputed; r and half_rho are then not set).
 __device__ __forceinline__ void obs_rows(const FrameDesc& F, const double* __restrict__ rec,
                                          const double* __restrict__ params, double X0, double X1,
                                          double X2, double2 meas, int32_t flags, double cauchy_c,
                                          double* Z0, double* Z1, double* I0, double* I1, double* P0,
-                                         double* P1, double* r, double* half_rho) {
+                                         double* P1, double* r, double* half_rho, double sr_given = -1.0) {
   const double f = params[F.off[MVBA_BLK_FOCAL]];
   const double c0 = params[F.off[MVBA_BLK_CENTER]];
   const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
   Proj o;
   project<MODEL, DEG>(rec, X0, X1, X2, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
-  const double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
-  const double sr = loss_scale(r0, r1, flags, cauchy_c, half_rho);
-  r[0] = r0 * sr;
-  r[1] = r1 * sr;
+  double sr = sr_given;
+  if (sr < 0.0) {
+    const double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
+    sr = loss_scale(r0, r1, flags, cauchy_c, half_rho);
+    r[0] = r0 * sr;
+    r[1] = r1 * sr;
+  }
   const double fz = f / o.Xc[2] * sr;
   const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
   const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
@@ -169,13 +174,13 @@ __device__ __forceinline__ void solve3(const double* V, const double* dp, const 
 template <int MODEL, int DEG>
 __device__ __forceinline__ void pass_a_obs(const double* __restrict__ rec, const double* dirf,
                                            double4 X, double2 m, int32_t flags, double cauchy_c,
-                                           double* z, double* P0, double* P1) {
+                                           double* z, double* P0, double* P1, double sr_given = -1.0) {
   const double f = rec[12];
   const int K = (int)rec[17];
   Proj o;
   project<MODEL, DEG>(rec, X.x, X.y, X.z, f, rec[13], rec[14], rec + 18, K, rec[15], rec[16], o);
   double hr;
-  const double sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
+  const double sr = sr_given >= 0.0 ? sr_given : loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
   const double fz = f / o.Xc[2] * sr;
   const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
   const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
@@ -430,7 +435,11 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
     if (lane < count) {
       const int64_t i = (int64_t)sg.begin + lane;
       double z[2], P0[3], P1[3];
-      pass_a_obs<MODEL, DEG>(rec, d, obsX ? obsX[i] : pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
+      // obsX (K2's per-slot record): landmark + Cauchy weight, no measurement read
+      if (obsX)
+        pass_a_obs<MODEL, DEG>(rec, d, obsX[i], double2{0.0, 0.0}, flags, cauchy_c, z, P0, P1, obsX[i].w);
+      else
+        pass_a_obs<MODEL, DEG>(rec, d, pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
       // plain store: a nontemporal store of these scattered 32-B records
       // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM)
       cbuf[slot_po[i]] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
@@ -575,11 +584,16 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
           const int64_t i = (int64_t)sg.begin + lane;
           const int32_t pid = obs_pid[i];
           const double4 X = obsX ? obsX[i] : pts[pid];
-          const double2 m = obs_meas[i];
           Proj o;
           project<MODEL, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
           double hr;
-          const double sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
+          double sr;
+          if (obsX) {
+            sr = X.w;  // K2's Cauchy weight
+          } else {
+            const double2 m = obs_meas[i];
+            sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
+          }
           const double fz = f / o.Xc[2] * sr;
           const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
           const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
@@ -703,8 +717,9 @@ __global__ void __launch_bounds__(64) k_pass_b(
       double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], P0[3], P1[3], r[2], hr;
 #pragma unroll
       for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;
-      obs_rows<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, obs_meas[i], flags, cauchy_c, Z0, Z1, I0, I1, P0,
-                           P1, r, &hr);
+      // obsX: the Cauchy weight rides in .w (K2), no measurement read
+      obs_rows<MODEL, DEG>(F, rec, params, X.x, X.y, X.z, obsX ? double2{0.0, 0.0} : obs_meas[i], flags,
+                           cauchy_c, Z0, Z1, I0, I1, P0, P1, r, &hr, obsX ? X.w : -1.0);
       double z0 = 0.0, z1 = 0.0;
       if (d) {
 #pragma unroll
