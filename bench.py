@@ -63,6 +63,59 @@ def parse():
     return ap.parse_args()
 
 
+def launch_plan(gpus, environ, device_count, backend, script, argv, port):
+    """How `bench.py --gpus N` runs. Returns None when this process is itself a
+    rank (a launcher set WORLD_SIZE, or N == 1), else the command that starts
+    the N ranks as a child (torch.distributed.run on 127.0.0.1). Raises
+    SystemExit for an impossible request, before anything touches the GPU:
+    RCCL needs N distinct devices; the gloo rehearsal may share them."""
+    if gpus < 1:
+        raise SystemExit(f"--gpus {gpus}: need at least one GPU")
+    world = environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"--gpus {gpus} but the launcher set WORLD_SIZE {world}")
+        return None
+    if gpus == 1:
+        return None
+    if device_count < 1:
+        raise SystemExit(f"--gpus {gpus}: no GPU visible")
+    if backend == "nccl" and device_count < gpus:
+        raise SystemExit(f"--gpus {gpus}: only {device_count} GPU(s) visible (RCCL needs one GPU per rank; "
+                         f"--dist-backend gloo rehearses the multi-rank path on fewer)")
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), script] + list(argv)
+
+
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def maybe_launch(args):
+    """Start the ranks as a child process when --gpus N > 1 was given without a
+    launcher; returns its exit code, or None to run here. torch.cuda.device_count()
+    does not initialise the GPU, so no GPU state exists in this parent."""
+    import subprocess
+
+    if args.gpus == 1 and "WORLD_SIZE" not in os.environ:
+        return None
+    import torch
+
+    cmd = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), args.dist_backend,
+                      os.path.abspath(__file__), sys.argv[1:], _free_port())
+    if cmd is None:
+        return None
+    env = dict(os.environ)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    env.setdefault("OMP_NUM_THREADS", "4")
+    print(f"bench.py: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def _time_numdiff(oracle_py, problem, n, threads, min_seconds):
     """Whole passes of the oracle's numeric differentiation over the first n
     blocks until >= min_seconds (at most 64 passes). Returns (evals/s, passes, s)."""
@@ -316,6 +369,9 @@ def mesh_bench(torch, stream, nrays, args):
 
 def main():
     args = parse()
+    rc = maybe_launch(args)
+    if rc is not None:
+        raise SystemExit(rc)
     import torch
     import torch.distributed as dist
 
@@ -410,16 +466,24 @@ def main():
         obs_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         tot = torch.tensor([float(n)], dtype=torch.float64, device="cuda")
+        per_rank = None
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+            mine = torch.tensor([1e3 * dt / args.steps, prep_ms, obs_ms, float(n)], dtype=torch.float64,
+                                device="cuda")
+            allr = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(allr, mine)
+            rows = [r.cpu().tolist() for r in allr]
+            per_rank = {"ms_per_step": [r[0] for r in rows], "prep_ms": [r[1] for r in rows],
+                        "kernel_ms": [r[2] for r in rows], "num_residuals": [int(r[3]) for r in rows]}
         del res, jac
-        return float(t.item()), float(tot.item()) * args.steps, prep_ms, obs_ms
+        return float(t.item()), float(tot.item()) * args.steps, prep_ms, obs_ms, per_rank
 
     ev = Evaluator(P, device=dev)
     ev.set_params()
     n = ev.num_residuals
-    dt_max, total_evals, prep_ms, obs_ms = time_eval(ev)
+    dt_max, total_evals, prep_ms, obs_ms, per_rank = time_eval(ev)
 
     if world == 1 and args.shard_of > 1:  # timing rehearsal, not a bench line
         cfg["shard_rehearsal"] = f"rank 0's shard of a {args.shard_of}-way landmark split, one process"
@@ -430,6 +494,7 @@ def main():
         "value": total_evals / dt_max,
         "unit": "evals/s",
         "n_gpus": world,
+        "devices": min(world, torch.cuda.device_count()),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1e3 * dt_max / args.steps,
@@ -467,6 +532,8 @@ def main():
         },
         "gen_s": t_gen,
     }
+    if per_rank is not None:
+        line["per_rank"] = per_rank
     # achievable HBM bandwidth on this box ("measure achieved peak
     # with a STREAM-like copy kernel ... and report against both")
     stream_gbs = _stream_copy_gbs(torch, stream)
@@ -726,6 +793,35 @@ def main():
                          "gloo (host-staged callback)" if ex else "none (single rank)"),
             "exchange_calls": ex.calls if ex else None,
         }
+        if world > 1:
+            # the per-CG-iteration exchange alone: one all-reduce of the
+            # camera-side product vector (cam_grad_size doubles), on the solver's
+            # stream, HIP events around K of them
+            ng = int(L["cam_grad_size"])
+            vbuf = torch.ones(ng, dtype=torch.float64, device="cuda")
+
+            def xchg():
+                if comm is not None:
+                    comm.allreduce(vbuf.data_ptr(), ng, 0, sh)
+                else:
+                    ex(vbuf.data_ptr(), ng, 0, sh)
+
+            for _ in range(args.warmup):
+                xchg()
+            torch.cuda.synchronize()
+            dist.barrier()
+            xe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            t0 = time.perf_counter()
+            xe[0].record(stream)
+            for _ in range(args.steps):
+                xchg()
+            xe[1].record(stream)
+            xe[1].synchronize()
+            host_us = 1e6 * (time.perf_counter() - t0) / args.steps
+            line["ba"]["exchange_us_per_cg_iteration"] = 1e3 * xe[0].elapsed_time(xe[1]) / args.steps
+            line["ba"]["exchange_host_us_per_call"] = host_us
+            line["ba"]["exchange_bytes_per_cg_iteration"] = 8 * ng
+            del vbuf
         if world == 1:
             # deterministic mode (fixed-order slab gathers instead of fp64 atomics):
             # same LM iterations, reproducible CG count; its cost per CG iteration
@@ -755,13 +851,14 @@ def main():
         Pw = rig.build_problem(Rw, flags)
         ev = Evaluator(Pw, device=dev)
         ev.set_params()
-        wdt, wtot, _, w_obs_ms = time_eval(ev)
+        wdt, wtot, _, w_obs_ms, w_per_rank = time_eval(ev)
         line["weak"] = {
             "what": f"weak scaling: every rank owns a {args.config}-sized shard of a {world} x larger problem",
             "value": wtot / wdt,
             "ms_per_step": 1e3 * wdt / args.steps,
             "num_residuals_per_gpu": ev.num_residuals,
             "kernel_ms": w_obs_ms,
+            "per_rank": w_per_rank,
         }
 
     if rank == 0 and world == 1 and args.mesh_subdiv > 0:

@@ -940,20 +940,23 @@ static int run(int argc, char** argv) {
   };
 
   const int ngpu = F.num_gpus;
+  // --mesh: loadMeshBuildTree (texture_processing.cc:264-285): the PLY file is
+  // read (host) before the device check, the BVH is built on the GPU below
+  std::vector<float> mv;
+  std::vector<uint32_t> mf;
+  if (F.mesh != "" && F.calibrator_num_passes > 0) {
+    std::cout << "Loading mesh: " << F.mesh << std::endl;
+    std::string err;
+    if (!read_ply_mesh(F.mesh, mv, mf, err)) fatal(err);
+    std::cout << "Number of faces: " << mf.size() / 3 << " faces.\n";
+  }
   int32_t ndev = 0;
   if (F.calibrator_num_passes > 0 && (mvba_device_count(&ndev) != MVBA_OK || ndev < 1))
     fatal("No HIP device is available (this build has no CPU compute path).");
   double placeholder = 0.0;  // distortion_placeholder (:1608)
-  // --mesh: loadMeshBuildTree (texture_processing.cc:264-285) -> BVH on the GPU
   mvba_mesh* mesh = nullptr;
   std::vector<double> mesh_feat_xyz, mesh_pt_xyz;
   if (F.mesh != "" && F.calibrator_num_passes > 0) {
-    std::cout << "Loading mesh: " << F.mesh << std::endl;
-    std::vector<float> mv;
-    std::vector<uint32_t> mf;
-    std::string err;
-    if (!read_ply_mesh(F.mesh, mv, mf, err)) fatal(err);
-    std::cout << "Number of faces: " << mf.size() / 3 << " faces.\n";
     const auto tb = Clock::now();
     mvba_mesh_desc md{};
     md.num_vertices = (int64_t)(mv.size() / 3);

@@ -470,7 +470,10 @@ bool read_ply_mesh(const std::string& path, std::vector<float>& vertices, std::v
       is >> format;
     } else if (key == "element") {
       PlyElem e;
-      is >> e.name >> e.count;
+      if (!(is >> e.name >> e.count) || e.count < 0) {
+        err = "Bad PLY element count in " + path;
+        return false;
+      }
       elems.push_back(e);
     } else if (key == "property") {
       if (elems.empty()) {
@@ -547,6 +550,12 @@ bool read_ply_mesh(const std::string& path, std::vector<float>& vertices, std::v
         double cnt;
         if (!scalar(p.count_type, &cnt)) {
           err = "Truncated PLY file: " + path;
+          return false;
+        }
+        // list lengths: faces must be triangles; anything else is read and
+        // dropped, but a negative, fractional or absurd count is corruption
+        if (!(cnt >= 0.0) || cnt > 1024.0 || cnt != (double)(int64_t)cnt) {
+          err = "Bad PLY list count in " + path;
           return false;
         }
         row.assign((size_t)cnt, 0.0);

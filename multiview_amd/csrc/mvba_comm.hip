@@ -63,13 +63,13 @@ struct LocalGroup {
   int arrived = 0;
   uint64_t gen = 0;
   bool aborted = false;
-  int64_t count[2] = {0, 0};
   struct Rank {
     int device = 0;
     hipEvent_t ready[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
     double* slot[2] = {nullptr, nullptr};
     int64_t cap[2] = {0, 0};
+    int64_t count[2] = {0, 0};  // this rank's element count of its current use of slot p
   };
   std::vector<Rank> ranks;
   int refs = 0;
@@ -142,12 +142,21 @@ int32_t local_allreduce(mvba_comm* c, double* buf, int64_t n, int32_t op, hipStr
   if (hipEventRecord(me.ready[p], s) != hipSuccess) return 1;
   {
     std::lock_guard<std::mutex> lk(G.m);
-    G.count[p] = n;  // every rank stores the same n (checked after the barrier)
+    me.count[p] = n;
   }
   if (!G.barrier()) return 1;
-  if (G.count[p] != n) {
-    G.abort();
-    return 1;
+  // every rank compares every rank's count (a rank cannot overwrite count[p]
+  // before all ranks passed the next barrier, on the other slot), so a
+  // mismatch fails all of them before any reduce over a smaller peer slot
+  {
+    std::lock_guard<std::mutex> lk(G.m);
+    for (int j = 0; j < G.nranks; j++)
+      if (G.ranks[(size_t)j].count[p] != n) {
+        comm_fail("mvba_comm_allreduce: ranks passed different element counts");
+        G.aborted = true;
+        G.cv.notify_all();
+        return 1;
+      }
   }
   SlotArgs a{};
   for (int j = 0; j < G.nranks; j++) {

@@ -44,8 +44,6 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                                     const double2* obs_meas, const int32_t* slot_po, const double* dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
                                     const double* prec, const double4* obsX, hipStream_t s);
-hipError_t mvba_launch_gather_obs_pts(int64_t nslots, const int32_t* obs_pid, const double4* pts, double4* out,
-                                      hipStream_t s);
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
                                const double* tinit, const double* V, const double* dp, const double4* pts,
                                double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
@@ -454,10 +452,12 @@ class Solver {
   // records for pass A are built here (parameters fixed until the next step).
   void schur_rhs() {
     HCHK(mvba_launch_frame_proj((int32_t)h_->nframes, h_->d_fd, h_->d_frec, h_->d_params, S_->prec, s_));
-    // the per-slot records (landmark + Cauchy weight) were written by K2 at
-    // this linearization point (h_->lin_obsx); without them, landmarks only
-    if (!h_->lin_obsx && obsx())
-      HCHK(mvba_launch_gather_obs_pts(h_->nslots, h_->d_obs_pid, h_->d_pts, (double4*)S_->obsX, s_));
+    // the per-slot records (landmark + Cauchy weight sqrt(rho')) were written
+    // by K2 at this linearization point (h_->lin_obsx). A landmark-only copy
+    // would carry the prep kernel's free flag in .w, which the frame-order
+    // passes would take as the Cauchy weight: never fall back to one.
+    if (obsx() && h_->lin_obsx != obsx())
+      throw StatusErr{MVBA_E_INVALID, "internal: CG slot records were not written by the linearization"};
     pass_a_w(nullptr, S_->G + S_->ng, nullptr, nullptr);
     reduce_frames(S_->tmp, nullptr, 0, nullptr);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));

@@ -448,15 +448,6 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
   }
 }
 
-// Landmark of every observation slot, in slot order: the points are fixed for
-// a whole linear solve, so the frame-order passes read them coalesced instead
-// of gathering pts[obs_pid[i]] behind the index load every CG iteration.
-__global__ void k_gather_obs_pts(int64_t nslots, const int32_t* __restrict__ obs_pid,
-                                 const double4* __restrict__ pts, double4* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nslots) out[i] = pts[obs_pid[i]];
-}
-
 // BracketedDepthError / BracketedDepthMeshError blocks in the frame-order CG
 // product: one wave per depth segment (one image: the descriptor is read once,
 // the point per lane), z_d = J_cam,d x into du (slot order; k_depth_sb forms
@@ -1334,14 +1325,6 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                      segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec, obsX)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PAF)
 #undef MVBA_PAF
-  return hipGetLastError();
-}
-
-hipError_t mvba_launch_gather_obs_pts(int64_t nslots, const int32_t* obs_pid, const double4* pts, double4* out,
-                                      hipStream_t s) {
-  if (nslots <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_gather_obs_pts, dim3((unsigned)((nslots + 255) / 256)), dim3(256), 0, s, nslots, obs_pid,
-                     pts, out);
   return hipGetLastError();
 }
 

@@ -210,6 +210,14 @@ class Comm:
             raise _lib.MvbaError(st, lib.mvba_comm_error().decode())
         return [cls(C.c_void_p(out[i])) for i in range(len(dev))]
 
+    def allreduce(self, ptr: int, count: int, op: int = 0, stream: int = 0):
+        """mvba_comm_allreduce on a device buffer, enqueued on `stream` (the
+        solver's exchange, callable on its own for timing)."""
+        import ctypes as C
+
+        if self.lib.mvba_comm_allreduce(C.c_void_p(ptr), count, op, C.c_void_p(stream), self.h) != 0:
+            raise RuntimeError("mvba_comm_allreduce failed: " + self.lib.mvba_comm_error().decode())
+
     def abort(self):
         if self.h is not None and self.h.value:
             self.lib.mvba_comm_abort(self.h)

@@ -313,6 +313,13 @@ def stats_labels(sensor_names) -> list:
         [f"{kind}_{a}_m" for kind in ("depth_tri", "tri", "depth_mesh", "mesh_tri") for a in "xyz"]
 
 
+def _hip_sync(stream) -> int:
+    """hipStreamSynchronize on a raw stream handle (libamdhip64, loaded by torch)."""
+    from .dist import _hip
+
+    return _hip().hipStreamSynchronize(stream or None)
+
+
 def default_solver_options(**kw) -> _lib.SolverOptions:
     """mvba_solver_default_options, then overrides (lower_bounds/upper_bounds as
     numpy arrays over the packed parameter vector; allreduce as a Python callable
@@ -349,6 +356,11 @@ def default_solver_options(**kw) -> _lib.SolverOptions:
                     if _n >= 4:
                         _f(ptr, count, op, stream or 0)
                     else:
+                        # a 3-argument callback predates the stream-ordered
+                        # contract: it reads and writes the buffer on the host
+                        # side, so the solver's stream must have drained first
+                        if _hip_sync(stream) != 0:
+                            raise RuntimeError("hipStreamSynchronize failed")
                         _f(ptr, count, op)
                     return 0
                 except Exception as e:  # noqa: BLE001 - reported as a failed status

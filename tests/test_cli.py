@@ -129,6 +129,33 @@ def test_image_lookup_and_bracketing(cli, tmp_path):
     assert code == 1 and "Could not find images for all sensors" in err
 
 
+@pytest.mark.parametrize("body,msg", [
+    ("element vertex -1\nproperty float x\nproperty float y\nproperty float z\nend_header\n",
+     "Bad PLY element count"),
+    ("element vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+     "element face 1\nproperty list uchar int vertex_indices\nend_header\n"
+     "0 0 0\n1 0 0\n0 1 0\n-1 0 1 2\n", "Bad PLY list count"),
+    ("element vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+     "element face 1\nproperty list int int vertex_indices\nend_header\n"
+     "0 0 0\n1 0 0\n0 1 0\n2000000000 0 1 2\n", "Bad PLY list count"),
+    ("element vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+     "element face 1\nproperty list uchar int vertex_indices\nend_header\n"
+     "0 0 0\n1 0 0\n0 1 0\n4 0 1 2 0\n", "Only triangle faces are supported"),
+    ("element vertex 3\nproperty float x\nproperty float y\nproperty float z\n"
+     "element face 1\nproperty list uchar int vertex_indices\nend_header\n"
+     "0 0 0\n1 0 0\n0 1 0\n3 0 1 7\n", "PLY face index out of range"),
+])
+def test_corrupt_ply_is_a_clean_error(cli, tmp_path, body, msg):
+    """--mesh files are read on the host before the first GPU call: a corrupt
+    count is reported through the CLI's error path, not a bad_alloc abort."""
+    R, info = _dataset(tmp_path)
+    ply = tmp_path / "bad.ply"
+    ply.write_text("ply\nformat ascii 1.0\n" + body)
+    code, out, err = _run(cli, "--rig_config", info["rig_config"], "--nvm", info["nvm"], "--out_dir",
+                          str(tmp_path / "o"), "--mesh", str(ply), "--mesh_tri_weight", "1")
+    assert code == 1 and msg in err, (code, out, err)
+
+
 def test_rig_config_round_trip(cli, tmp_path):
     """With no passes and --use_initial_rig_transforms the written rig_config.txt
     holds the configuration read in."""

@@ -277,6 +277,34 @@ def test_bounded_offsets_and_callback_path():
     assert np.all(x0 >= lo) and np.all(x0 <= hi)
 
 
+def test_legacy_three_arg_callback_host_roundtrip():
+    """A 3-argument allreduce callback (the pre-stream-ordered contract) reads
+    the device buffer to the host and writes it back. The wrapper drains the
+    solver's stream before calling it, so the round trip sees finished data and
+    the solve reaches the same point as the unsharded one."""
+    from multiview_amd.dist import _hip
+
+    R, P = _problem(["radtan", "radtan", "fov"], seed=56)
+    hip = _hip()
+
+    def roundtrip(ptr, n, op):
+        host = np.empty(n, dtype=np.float64)
+        assert hip.hipMemcpy(host.ctypes.data, ptr, 8 * n, 2) == 0
+        assert np.all(np.isfinite(host))
+        assert hip.hipMemcpy(ptr, host.ctypes.data, 8 * n, 1) == 0
+
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s0 = ev.solve(max_num_iterations=100, **TOL)
+        x0 = ev.get_params()
+        ev.set_params()
+        s1 = ev.solve(max_num_iterations=100, allreduce=roundtrip, **TOL)
+        x1 = ev.get_params()
+    assert s0["termination_type"] == 0 and s1["termination_type"] == 0
+    assert np.isclose(s0["final_cost"], s1["final_cost"], rtol=1e-10)
+    assert np.abs(_poses(P, x0) - _poses(P, x1)).max() <= 1e-7
+
+
 def test_solver_rejects_bad_options():
     from multiview_amd._lib import MvbaError
 

@@ -28,11 +28,14 @@ def main():
     TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
     _, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
     print("cpu LM", s_ref["final_cost"], flush=True)
-    for k in range(int(sys.argv[1]) if len(sys.argv) > 1 else 8):
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    for det in (0, 1):
+      for k in range(reps):
         with Evaluator(P) as ev:
             ev.set_params()
-            s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, **TOL)
-        print(k, s["termination_type"], s["num_iterations"], "%.12g" % s["final_cost"],
+            s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, deterministic=det, **TOL)
+        print("det" if det else "atomic", k, s["termination_type"], s["num_iterations"],
+              s["num_successful_steps"], s["num_linear_iterations"], "%.17g" % s["final_cost"],
               "rel %.2e" % abs(s["final_cost"] / s_ref["final_cost"] - 1), s["message"][:70], flush=True)
 
 
