@@ -10,13 +10,23 @@
 //   XYZError::Create(ref_xyz, block_sizes, weight)                                     :728-741
 //   problem.AddResidualBlock(cost, loss, <blocks>...)      :1695-1699, :1779-1785, :1869-1894
 //
-// Usage: one BracketedCamBatch per ceres::Problem;
-//   ceres::CostFunction* cost = batch.Create(meas, left, right, cam, block_sizes,
-//       cam_params.GetDistortion().size(), cam_params.GetDistortedHalfSize().data(),
-//       {beg, end, ref_to_cam, xyz, offset, focal, center, dist});
-//   problem.AddResidualBlock(cost, loss, beg, end, ref_to_cam, xyz, offset, focal, center, dist);
-//   ... batch.CreateDepth(...), batch.CreateDepthMesh(...), batch.CreateXyz(...) likewise ...
+// Usage: one BracketedCamBatch per ceres::Problem,
+// declared right after the problem; the reference's own statements then change
+// only in their namespace qualifier (dense_map:: -> mvba::):
+//   ceres::Problem problem;
+//   mvba::BracketedCamBatch batch(problem);             // the batch in scope
+//   ceres::CostFunction* cost = mvba::BracketedCamError::Create(dist_ip, beg_ref_timestamp,
+//       end_ref_timestamp, cam_timestamp, bracketed_cam_block_sizes, cam_params[cam_type]);
+//   problem.AddResidualBlock(cost, loss, beg_cam_ptr, end_cam_ptr, ref_to_cam_ptr, &xyz_vec[pid][0],
+//       &ref_to_cam_timestamp_offsets[cam_type], &focal_lengths[cam_type],
+//       &optical_centers[cam_type][0], distortion_ptr);             // unchanged
+//   ... mvba::BracketedDepthError / BracketedDepthMeshError / XYZError::Create likewise ...
 //   options.evaluation_callback = batch.callback();   // Ceres 1.14 (2.x: Problem::Options)
+// The factories do not see the parameter blocks (the reference passes them to
+// AddResidualBlock only): at the first evaluation the batch reads them back from
+// the problem (Problem::GetResidualBlocks / GetCostFunctionForResidualBlock /
+// GetParameterBlocksForResidualBlock). The member factories below
+// (batch.Create(..., blocks)) take the block pointers directly instead.
 //
 // Semantics: Evaluate() returns what the reference functor + numeric
 // differentiation return (raw residuals; row-major num_residuals x size_b
@@ -52,6 +62,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "mvba.h"
@@ -102,9 +113,25 @@ class PinnedDoubles {
 
 class BracketedCamBatch {
  public:
-  explicit BracketedCamBatch(int device = 0) : device_(device), callback_(this) {}
+  // A batch fed through the member factories (block pointers given).
+  explicit BracketedCamBatch(int device = 0) : device_(device), callback_(this) { push_current(); }
+  // A batch bound to the problem its residual blocks are added to: the static
+  // reference-signature factories (mvba::BracketedCamError::Create, ...) feed the
+  // batch in scope on this thread, i.e. the most recently constructed one.
+  explicit BracketedCamBatch(ceres::Problem& problem, int device = 0)
+      : device_(device), problem_(&problem), callback_(this) {
+    push_current();
+  }
   ~BracketedCamBatch() {
     if (h_) mvba_destroy(h_);
+    if (current_slot() == this) current_slot() = prev_;
+  }
+
+  // The batch the static factories feed (throws if none is in scope).
+  static BracketedCamBatch& Current() {
+    BracketedCamBatch* b = current_slot();
+    if (!b) throw std::runtime_error("mvba: no BracketedCamBatch in scope (construct one with the ceres::Problem)");
+    return *b;
   }
   BracketedCamBatch(const BracketedCamBatch&) = delete;
   BracketedCamBatch& operator=(const BracketedCamBatch&) = delete;
@@ -116,6 +143,15 @@ class BracketedCamBatch {
   ceres::CostFunction* Create(const double meas_dist_pix[2], double left_ref_stamp, double right_ref_stamp,
                               double cam_stamp, const std::vector<int>& block_sizes, int dist_size,
                               const double dist_half_size[2], const std::array<double*, 8>& blocks) {
+    return CreateCam(meas_dist_pix, left_ref_stamp, right_ref_stamp, cam_stamp, block_sizes, dist_size,
+                     dist_half_size, blocks.data());
+  }
+
+  // blocks == nullptr: the pointers are read back from the problem at the first
+  // evaluation (the reference-signature factory's path).
+  ceres::CostFunction* CreateCam(const double meas_dist_pix[2], double left_ref_stamp, double right_ref_stamp,
+                                 double cam_stamp, const std::vector<int>& block_sizes, int dist_size,
+                                 const double dist_half_size[2], double* const* blocks) {
     static const int kFixed[8] = {7, 7, 7, 3, 1, 1, 2, 1};
     if (block_sizes.size() != 8)
       throw std::runtime_error("BracketedCamError: The block sizes were not set up properly.");
@@ -129,8 +165,8 @@ class BracketedCamBatch {
     Residual r;
     r.nblocks = 8;
     for (int b = 0; b < 8; b++) {
-      r.block[b] = register_block(blocks[b], b == 7 ? std::max(dist_size, 1) : sizes[b]);
       r.width[b] = sizes[b];
+      r.block[b] = blocks ? register_block(blocks[b], b == 7 ? std::max(dist_size, 1) : sizes[b]) : -1;
     }
     r.cam = cam;
     r.meas[0] = meas_dist_pix[0];
@@ -138,8 +174,7 @@ class BracketedCamBatch {
     r.stamps[0] = left_ref_stamp;
     r.stamps[1] = right_ref_stamp;
     r.stamps[2] = cam_stamp;
-    res_[kCam].push_back(r);
-    return new GpuBatchCost(this, kCam, (int64_t)res_[kCam].size() - 1, 2, sizes);
+    return add(kCam, r, 2, sizes, blocks == nullptr);
   }
 
   // Mirror of BracketedDepthError::Create (rig_calibrator.cc:586-600) with the
@@ -149,6 +184,12 @@ class BracketedCamBatch {
   ceres::CostFunction* CreateDepth(double weight, const double meas_depth_xyz[3], double left_ref_stamp,
                                    double right_ref_stamp, double cam_stamp, const std::vector<int>& block_sizes,
                                    const std::array<double*, 7>& blocks) {
+    return CreateDepthBlocks(weight, meas_depth_xyz, left_ref_stamp, right_ref_stamp, cam_stamp, block_sizes,
+                             blocks.data());
+  }
+  ceres::CostFunction* CreateDepthBlocks(double weight, const double meas_depth_xyz[3], double left_ref_stamp,
+                                         double right_ref_stamp, double cam_stamp,
+                                         const std::vector<int>& block_sizes, double* const* blocks) {
     if (block_sizes.size() != 7 || block_sizes[0] != 7 || block_sizes[1] != 7 || block_sizes[2] != 7 ||
         (block_sizes[3] != 7 && block_sizes[3] != 12) || block_sizes[4] != 1 || block_sizes[5] != 3 ||
         block_sizes[6] != 1)
@@ -157,7 +198,7 @@ class BracketedCamBatch {
     Residual r;
     r.nblocks = 7;
     for (int b = 0; b < 7; b++) {
-      r.block[b] = register_block(blocks[b], block_sizes[b]);
+      r.block[b] = blocks ? register_block(blocks[b], block_sizes[b]) : -1;
       r.width[b] = block_sizes[b];
     }
     r.weight = weight;
@@ -165,8 +206,7 @@ class BracketedCamBatch {
     r.stamps[0] = left_ref_stamp;
     r.stamps[1] = right_ref_stamp;
     r.stamps[2] = cam_stamp;
-    res_[kDepth].push_back(r);
-    return new GpuBatchCost(this, kDepth, (int64_t)res_[kDepth].size() - 1, 3, block_sizes);
+    return add(kDepth, r, 3, block_sizes, blocks == nullptr);
   }
 
   // Mirror of BracketedDepthMeshError::Create (rig_calibrator.cc:677-693) with the
@@ -175,6 +215,13 @@ class BracketedCamBatch {
   ceres::CostFunction* CreateDepthMesh(double weight, const double meas_depth_xyz[3], const double mesh_xyz[3],
                                        double left_ref_stamp, double right_ref_stamp, double cam_stamp,
                                        const std::vector<int>& block_sizes, const std::array<double*, 6>& blocks) {
+    return CreateDepthMeshBlocks(weight, meas_depth_xyz, mesh_xyz, left_ref_stamp, right_ref_stamp, cam_stamp,
+                                 block_sizes, blocks.data());
+  }
+  ceres::CostFunction* CreateDepthMeshBlocks(double weight, const double meas_depth_xyz[3],
+                                             const double mesh_xyz[3], double left_ref_stamp,
+                                             double right_ref_stamp, double cam_stamp,
+                                             const std::vector<int>& block_sizes, double* const* blocks) {
     if (block_sizes.size() != 6 || block_sizes[0] != 7 || block_sizes[1] != 7 || block_sizes[2] != 7 ||
         (block_sizes[3] != 7 && block_sizes[3] != 12) || block_sizes[4] != 1 || block_sizes[5] != 1)
       throw std::runtime_error("BracketedDepthMeshError: The block sizes were not set up properly.");
@@ -182,7 +229,7 @@ class BracketedCamBatch {
     Residual r;
     r.nblocks = 6;
     for (int b = 0; b < 6; b++) {
-      r.block[b] = register_block(blocks[b], block_sizes[b]);
+      r.block[b] = blocks ? register_block(blocks[b], block_sizes[b]) : -1;
       r.width[b] = block_sizes[b];
     }
     r.weight = weight;
@@ -194,8 +241,7 @@ class BracketedCamBatch {
     r.stamps[0] = left_ref_stamp;
     r.stamps[1] = right_ref_stamp;
     r.stamps[2] = cam_stamp;
-    res_[kDepth].push_back(r);
-    return new GpuBatchCost(this, kDepth, (int64_t)res_[kDepth].size() - 1, 3, block_sizes);
+    return add(kDepth, r, 3, block_sizes, blocks == nullptr);
   }
 
   // Mirror of XYZError::Create (rig_calibrator.cc:728-741) on one point block.
@@ -206,12 +252,11 @@ class BracketedCamBatch {
     check_open();
     Residual r;
     r.nblocks = 1;
-    r.block[0] = register_block(xyz, 3);
+    r.block[0] = xyz ? register_block(xyz, 3) : -1;
     r.width[0] = 3;
     r.weight = weight;
     for (int k = 0; k < 3; k++) r.xyz[k] = ref_xyz[k];
-    res_[kXyz].push_back(r);
-    return new GpuBatchCost(this, kXyz, (int64_t)res_[kXyz].size() - 1, 3, block_sizes);
+    return add(kXyz, r, 3, block_sizes, xyz == nullptr);
   }
 
   ceres::EvaluationCallback* callback() { return &callback_; }
@@ -284,6 +329,54 @@ class BracketedCamBatch {
     if (finalized_) throw std::runtime_error("mvba: Create() after the batch was evaluated");
   }
 
+  static BracketedCamBatch*& current_slot() {
+    static thread_local BracketedCamBatch* cur = nullptr;
+    return cur;
+  }
+  void push_current() {
+    prev_ = current_slot();
+    current_slot() = this;
+  }
+
+  ceres::CostFunction* add(Family f, const Residual& r, int nres, const std::vector<int>& sizes, bool deferred) {
+    res_[f].push_back(r);
+    const int64_t index = (int64_t)res_[f].size() - 1;
+    GpuBatchCost* cost = new GpuBatchCost(this, f, index, nres, sizes);
+    if (deferred) {
+      if (!problem_)
+        throw std::runtime_error("mvba: the reference-signature factories need a BracketedCamBatch constructed "
+                                 "with the ceres::Problem the residual blocks are added to");
+      deferred_.emplace(static_cast<const ceres::CostFunction*>(cost), std::make_pair(f, index));
+    }
+    return cost;
+  }
+
+  // Parameter blocks of the residuals created without them: read back from the
+  // problem, in its residual-block order (= AddResidualBlock order).
+  void resolve_deferred_locked() {
+    if (deferred_.empty()) return;
+    std::vector<ceres::ResidualBlockId> ids;
+    problem_->GetResidualBlocks(&ids);
+    std::vector<double*> ptrs;
+    size_t resolved = 0;
+    for (ceres::ResidualBlockId id : ids) {
+      auto it = deferred_.find(problem_->GetCostFunctionForResidualBlock(id));
+      if (it == deferred_.end()) continue;
+      Residual& r = res_[it->second.first][(size_t)it->second.second];
+      problem_->GetParameterBlocksForResidualBlock(id, &ptrs);
+      if ((int)ptrs.size() != r.nblocks)
+        throw std::runtime_error("mvba: a residual block was added with the wrong number of parameter blocks");
+      for (int b = 0; b < r.nblocks; b++) {
+        const bool dist = it->second.first == kCam && b == 7;
+        r.block[b] = register_block(ptrs[(size_t)b], dist ? std::max(r.width[b], 1) : r.width[b]);
+      }
+      resolved++;
+    }
+    if (resolved != deferred_.size())
+      throw std::runtime_error("mvba: a cost function from the batch was never added to its ceres::Problem");
+    deferred_.clear();
+  }
+
   int register_block(double* p, int size) {
     auto it = block_index_.find(p);
     if (it != block_index_.end()) {
@@ -311,6 +404,7 @@ class BracketedCamBatch {
 
   void finalize_locked() {
     if (finalized_) return;
+    resolve_deferred_locked();
     const std::vector<Residual>& C = res_[kCam];
     const std::vector<Residual>& D = res_[kDepth];
     const std::vector<Residual>& X = res_[kXyz];
@@ -497,7 +591,10 @@ class BracketedCamBatch {
   };
 
   int device_;
+  ceres::Problem* problem_ = nullptr;
+  BracketedCamBatch* prev_ = nullptr;
   Callback callback_;
+  std::unordered_map<const ceres::CostFunction*, std::pair<Family, int64_t>> deferred_;
   mvba_handle* h_ = nullptr;
   bool finalized_ = false, valid_ = false, have_jac_ = false, xfer_set_ = false;
   int64_t num_params_ = 0;
@@ -521,6 +618,53 @@ class BracketedCamBatch {
 inline bool GpuBatchCost::Evaluate(double const* const* parameters, double* residuals, double** jacobians) const {
   return batch_->Serve(fam_, index_, parameters, residuals, jacobians);
 }
+
+// ---- The reference's factories, same signatures (rig_calibrator.cc:485-488,
+// :586-588, :677-681, :728-730), feeding the batch in scope. Vec2 / Vec3 are
+// Eigen::Vector2d / Vector3d (anything indexable); CamParams is
+// camera::CameraParameters (GetDistortion().size(), GetDistortedHalfSize()).
+struct BracketedCamError {
+  template <class Vec2, class CamParams>
+  static ceres::CostFunction* Create(Vec2 const& meas_dist_pix, double left_ref_stamp, double right_ref_stamp,
+                                     double cam_stamp, std::vector<int> const& block_sizes,
+                                     CamParams const& cam_params) {
+    const double meas[2] = {meas_dist_pix[0], meas_dist_pix[1]};
+    const auto& half = cam_params.GetDistortedHalfSize();
+    const double h[2] = {half[0], half[1]};
+    return BracketedCamBatch::Current().CreateCam(meas, left_ref_stamp, right_ref_stamp, cam_stamp, block_sizes,
+                                                  (int)cam_params.GetDistortion().size(), h, nullptr);
+  }
+};
+
+struct BracketedDepthError {
+  template <class Vec3>
+  static ceres::CostFunction* Create(double weight, Vec3 const& meas_depth_xyz, double left_ref_stamp,
+                                     double right_ref_stamp, double cam_stamp, std::vector<int> const& block_sizes) {
+    const double m[3] = {meas_depth_xyz[0], meas_depth_xyz[1], meas_depth_xyz[2]};
+    return BracketedCamBatch::Current().CreateDepthBlocks(weight, m, left_ref_stamp, right_ref_stamp, cam_stamp,
+                                                          block_sizes, nullptr);
+  }
+};
+
+struct BracketedDepthMeshError {
+  template <class Vec3>
+  static ceres::CostFunction* Create(double weight, Vec3 const& meas_depth_xyz, Vec3 const& mesh_xyz,
+                                     double left_ref_stamp, double right_ref_stamp, double cam_stamp,
+                                     std::vector<int> const& block_sizes) {
+    const double m[3] = {meas_depth_xyz[0], meas_depth_xyz[1], meas_depth_xyz[2]};
+    const double x[3] = {mesh_xyz[0], mesh_xyz[1], mesh_xyz[2]};
+    return BracketedCamBatch::Current().CreateDepthMeshBlocks(weight, m, x, left_ref_stamp, right_ref_stamp,
+                                                              cam_stamp, block_sizes, nullptr);
+  }
+};
+
+struct XYZError {
+  template <class Vec3>
+  static ceres::CostFunction* Create(Vec3 const& ref_xyz, std::vector<int> const& block_sizes, double weight) {
+    const double x[3] = {ref_xyz[0], ref_xyz[1], ref_xyz[2]};
+    return BracketedCamBatch::Current().CreateXyz(x, block_sizes, weight, nullptr);
+  }
+};
 
 // The reprojection cost's previous name.
 using GpuBracketedCamCost = GpuBatchCost;

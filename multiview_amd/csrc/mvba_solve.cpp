@@ -540,8 +540,10 @@ class Solver {
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);
     dot(S_->ng, S_->G, S_->delta, 2);  // g_c' delta_c (global already)
     const double* hs = fetch(3);
+    for (int k = 0; k < 3; k++) last_mc_[k] = hs[k];
     return -(hs[1] + hs[2] + 0.5 * hs[0]);
   }
+  double last_mc_[3] = {0, 0, 0};  // |J delta|^2, g_p'delta_p, g_c'delta_c of the last step
 
   // max |x - P(x - g)| and |x - P(x - g)|, over ranks
   double grad_max_norm() {
@@ -885,6 +887,12 @@ void Solver::run(mvba_solver_summary* sum) {
       valid = std::isfinite(mcc) && mcc > 0.0;
     }
     sum->linear_solver_time_s += now_s() - ts;
+    static const bool trace = std::getenv("MVBA_SOLVER_TRACE") && std::getenv("MVBA_SOLVER_TRACE")[0] == '1';
+    if (trace)
+      std::fprintf(stderr,
+                   "mvba trace: it %d cg status %d iters %d | model change %.6e (|Jd|^2 %.6e, gp'dp %.6e, "
+                   "gc'dc %.6e) | gmax %.3e radius %.3e\n",
+                   iteration, cgr.status, cgr.iters, mcc, last_mc_[0], last_mc_[1], last_mc_[2], gmax, radius);
     if (!valid) {
       // HandleInvalidStep
       if (++invalid >= o_.max_num_consecutive_invalid_steps) {
@@ -928,6 +936,9 @@ void Solver::run(mvba_solver_summary* sum) {
       break;
     }
     const double change = x_cost - cand;
+    if (trace)
+      std::fprintf(stderr, "mvba trace:   step %.6e (x %.6e) cost %.17g -> %.17g change %.6e ratio %.6e\n",
+                   step_norm, x_norm, x_cost, cand, change, change / mcc);
     if (std::fabs(change) <= o_.function_tolerance * x_cost) {
       std::snprintf(buf, sizeof(buf), "Function tolerance reached. |cost_change|/cost: %e <= %e",
                     std::fabs(change) / x_cost, o_.function_tolerance);

@@ -7,7 +7,11 @@
 // (4) callback path, (5) 8 threads evaluating concurrently,
 // (6) packed transfer: blocks Ceres never asks for stop crossing PCIe after the
 //     first Jacobian pass, and asking for one later extends the set,
-// (7) BracketedDepthError + XYZError blocks served from the same batch.
+// (7) BracketedDepthError + XYZError blocks served from the same batch,
+// (8) the reference's own statements (rig_calibrator.cc:1674-1677, :1695-1699,
+//     :1762-1785, :1816-1828, :1868-1873) with only the namespace qualifier
+//     changed: static Create factories of the batch in scope, blocks read back
+//     from the ceres::Problem at the first evaluation.
 #include <array>
 #include <atomic>
 #include <cstdio>
@@ -18,6 +22,27 @@
 #include <vector>
 
 #include "mvba/ceres_surface.h"
+
+// Test stand-ins for the reference's value types (Eigen::Vector2d / Vector3d
+// and camera::CameraParameters): the factories only index the vectors and call
+// GetDistortion().size() / GetDistortedHalfSize().
+struct Vec {
+  double v[3] = {0, 0, 0};
+  Vec(double a, double b, double c = 0) : v{a, b, c} {}
+  double operator[](int i) const { return v[i]; }
+};
+namespace camera {
+class CameraParameters {
+ public:
+  CameraParameters(int K, const double* half) : dist_((size_t)K, 0.0), half_{half[0], half[1]} {}
+  const std::vector<double>& GetDistortion() const { return dist_; }
+  const std::array<double, 2>& GetDistortedHalfSize() const { return half_; }
+
+ private:
+  std::vector<double> dist_;
+  std::array<double, 2> half_;
+};
+}  // namespace camera
 
 template <class T>
 static std::vector<T> read_vec(std::ifstream& f) {
@@ -235,6 +260,127 @@ int main(int argc, char** argv) {
     flags.push_back(ok);
     flags.push_back((int32_t)b7.gpu_evaluations());
     write_vec(out, RD); write_vec(out, JD); write_vec(out, RX); write_vec(out, JX);
+  }
+  // (8) the reference's statements; parameter blocks as in the reference's
+  // arrays (here: slices of `user`), loss functions owned by the problem
+  {
+    ceres::Problem problem;
+    mvba::BracketedCamBatch batch8(problem);
+    std::vector<camera::CameraParameters> cam_params;
+    for (size_t c = 0; c < cam_K.size(); c++) cam_params.emplace_back(cam_K[c], &cam_half[2 * c]);
+    const std::vector<int> bracketed_cam_block_sizes = {7, 7, 7, 3, 1, 1, 2, 1};
+    const double FLAGS_robust_threshold = 3.0;
+    std::vector<ceres::CostFunction*> c8, d8, x8;
+    for (int64_t i = 0; i < n; i++) {
+      auto blk = [&](int b) { return &user[(size_t)block_offset[rblocks[8 * i + b]]]; };
+      double *beg_cam_ptr = blk(0), *end_cam_ptr = blk(1), *ref_to_cam_ptr = blk(2), *xyz_ptr = blk(3),
+             *offset_ptr = blk(4), *focal_ptr = blk(5), *center_ptr = blk(6), *distortion_ptr = blk(7);
+      const int cam_type = rcam[i];
+      double beg_ref_timestamp = rstamps[3 * i], end_ref_timestamp = rstamps[3 * i + 1],
+             cam_timestamp = rstamps[3 * i + 2];
+      Vec dist_ip(rmeas[2 * i], rmeas[2 * i + 1]);
+
+      ceres::CostFunction* bracketed_cost_function =
+        mvba::BracketedCamError::Create(dist_ip, beg_ref_timestamp, end_ref_timestamp,
+                                        cam_timestamp, bracketed_cam_block_sizes,
+                                        cam_params[cam_type]);
+      ceres::LossFunction* bracketed_loss_function = new ceres::CauchyLoss(FLAGS_robust_threshold);
+      problem.AddResidualBlock
+        (bracketed_cost_function, bracketed_loss_function,
+         beg_cam_ptr, end_cam_ptr, ref_to_cam_ptr, xyz_ptr,
+         offset_ptr, focal_ptr, center_ptr, distortion_ptr);
+      c8.push_back(bracketed_cost_function);
+    }
+    auto is_mesh = [&](int64_t j) { return dblocks[7 * j + 5] == -1; };
+    for (int64_t j = 0; j < nd; j++) {
+      auto blk = [&](int b) { return &user[(size_t)block_offset[dblocks[7 * j + b]]]; };
+      double *beg_cam_ptr = blk(0), *end_cam_ptr = blk(1), *ref_to_cam_ptr = blk(2);
+      double beg_ref_timestamp = dstamps[3 * j], end_ref_timestamp = dstamps[3 * j + 1],
+             cam_timestamp = dstamps[3 * j + 2];
+      Vec depth_xyz(dmeas[3 * j], dmeas[3 * j + 1], dmeas[3 * j + 2]);
+      ceres::LossFunction* loss = new ceres::CauchyLoss(FLAGS_robust_threshold);
+      if (is_mesh(j)) {
+        const std::vector<int> bracketed_depth_mesh_block_sizes = {7, 7, 7, dsizes[j], 1, 1};
+        Vec mesh_xyz(dmesh[3 * j], dmesh[3 * j + 1], dmesh[3 * j + 2]);
+        ceres::CostFunction* bracketed_depth_mesh_cost_function
+          = mvba::BracketedDepthMeshError::Create
+          (dweight[j], depth_xyz, mesh_xyz, beg_ref_timestamp,
+           end_ref_timestamp, cam_timestamp, bracketed_depth_mesh_block_sizes);
+        problem.AddResidualBlock
+          (bracketed_depth_mesh_cost_function, loss,
+           beg_cam_ptr, end_cam_ptr, ref_to_cam_ptr, blk(3), blk(4), blk(6));
+        d8.push_back(bracketed_depth_mesh_cost_function);
+        continue;
+      }
+      const std::vector<int> bracketed_depth_block_sizes = {7, 7, 7, dsizes[j], 1, 3, 1};
+      ceres::CostFunction* bracketed_depth_cost_function
+        = mvba::BracketedDepthError::Create(dweight[j], depth_xyz, beg_ref_timestamp,
+                                            end_ref_timestamp, cam_timestamp,
+                                            bracketed_depth_block_sizes);
+      problem.AddResidualBlock
+        (bracketed_depth_cost_function, loss,
+         beg_cam_ptr, end_cam_ptr, ref_to_cam_ptr, blk(3), blk(4), blk(5), blk(6));
+      d8.push_back(bracketed_depth_cost_function);
+    }
+    const std::vector<int> xyz_block_sizes = {3};
+    for (int64_t j = 0; j < nx; j++) {
+      Vec avg_mesh_xyz(xref[3 * j], xref[3 * j + 1], xref[3 * j + 2]);
+      ceres::CostFunction* mesh_cost_function =
+        mvba::XYZError::Create(avg_mesh_xyz, xyz_block_sizes, xweight[j]);
+      problem.AddResidualBlock(mesh_cost_function, new ceres::CauchyLoss(FLAGS_robust_threshold),
+                               &user[(size_t)block_offset[xblock[j]]]);
+      x8.push_back(mesh_cost_function);
+    }
+    // Problem::Evaluate-style lazy pass (no callback), then the callback pass
+    std::vector<double> R8, J8;
+    bool ok = true;
+    R8.assign(2 * n, 0.0);
+    J8.assign(n * stride, 0.0);
+    for (int64_t i = 0; i < n; i++) {
+      const double* p[8];
+      double* jp[8];
+      for (int b = 0; b < 8; b++) {
+        p[b] = &user[(size_t)block_offset[rblocks[8 * i + b]]];
+        jp[b] = &J8[i * stride + base[b]];
+      }
+      ok &= c8[(size_t)i]->Evaluate(p, &R8[2 * i], jp);
+    }
+    static const int dbase[7] = {0, 21, 42, 63, 99, 102, 111};
+    std::vector<double> RD(3 * nd), JD(114 * nd, 0.0), RX(3 * nx), JX(9 * nx);
+    batch8.callback()->PrepareForEvaluation(true, true);
+    for (int64_t j = 0; j < nd; j++) {
+      const double* p[7];
+      double* jp[7];
+      int q = 0;
+      for (int b = 0; b < 7; b++) {
+        if (is_mesh(j) && b == 5) continue;
+        p[q] = &user[(size_t)block_offset[dblocks[7 * j + b]]];
+        jp[q++] = &JD[114 * j + dbase[b]];
+      }
+      ok &= d8[(size_t)j]->Evaluate(p, &RD[3 * j], jp);
+    }
+    for (int64_t j = 0; j < nx; j++) {
+      const double* p[1] = {&user[(size_t)block_offset[xblock[j]]]};
+      double* jp[1] = {&JX[9 * j]};
+      ok &= x8[(size_t)j]->Evaluate(p, &RX[3 * j], jp);
+    }
+    flags.push_back(ok);
+    flags.push_back((int32_t)batch8.gpu_evaluations());
+    flags.push_back((int32_t)problem.NumResidualBlocks());
+    write_vec(out, R8); write_vec(out, J8);
+    write_vec(out, RD); write_vec(out, JD); write_vec(out, RX); write_vec(out, JX);
+  }
+  // a static factory whose batch in scope is not bound to a problem (here the
+  // first, explicit-pointer batch, already evaluated) throws, not crashes
+  {
+    camera::CameraParameters cp(0, &cam_half[0]);
+    int32_t threw = 0;
+    try {
+      mvba::BracketedCamError::Create(Vec(1, 2), 0.0, 1.0, 0.5, {7, 7, 7, 3, 1, 1, 2, 1}, cp);
+    } catch (const std::runtime_error&) {
+      threw = 1;
+    }
+    flags.push_back(threw);
   }
   write_vec(out, flags);
   return 0;

@@ -84,6 +84,7 @@ def run_adapter_case(binary, tmp_path, oracle, env=None):
         J6b = _read(fh, np.float64)
         sizes6 = _read(fh, np.int64)
         RD, JD, RX, JX = (_read(fh, np.float64) for _ in range(4))
+        R8, J8, RD8, JD8, RX8, JX8 = (_read(fh, np.float64) for _ in range(6))
         flags = _read(fh, np.int32)
     # full Jacobians: the adapter evaluates every block (all free)
     Pf = rig.build_problem(R, F, mesh_xyz=mxyz)
@@ -139,4 +140,16 @@ def run_adapter_case(binary, tmp_path, oracle, env=None):
     w = P.xyz_weight[:, None]
     assert np.allclose(RX.reshape(-1, 3), w * (X - P.xyz_ref), rtol=0, atol=1e-12)
     assert np.allclose(JX.reshape(-1, 3, 3), P.xyz_weight[:, None, None] * np.eye(3), rtol=0, atol=0)
+    # (8) the reference's own Create / AddResidualBlock statements (only the
+    # namespace qualifier changed): blocks read back from the ceres::Problem,
+    # same residuals and Jacobians as the explicit-pointer batch and the oracle
+    nx = P.num_xyz_residuals
+    assert flags[14] == 1, "case 8: an Evaluate() failed"
+    assert flags[15] == 2  # the lazy pass, then the callback's pass
+    assert flags[16] == n + nd + nx
+    assert flags[17] == 1  # a static factory without a problem-bound batch throws
+    assert close(R8, J8, r_o, J_o)
+    assert np.array_equal(R8, R0) and np.array_equal(J8, J0)
+    assert np.array_equal(RD8, RD) and np.array_equal(JD8, JD.ravel())
+    assert np.array_equal(RX8, RX) and np.array_equal(JX8, JX)
     return p.stderr

@@ -118,17 +118,32 @@ def test_single_observation_points_and_frames():
     assert (counts == 1).sum() > 20
     TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
     x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
-    with Evaluator(P) as ev:
-        ev.set_params()
-        s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, **TOL)
-        x = ev.get_params()
-    assert np.isfinite(x).all()
-    # at these tolerances (1e-16) the run ends at the optimum either by a
-    # tolerance or, when the remaining model cost changes are rounding noise
-    # (the fp64 atomics make them differ run to run), by Ceres' "consecutive
-    # invalid steps" rule; both must sit at the CPU LM's cost
-    assert s["termination_type"] != _lib.FAILURE or "consecutive invalid steps" in s["message"], s["message"]
-    assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
+    runs = []
+    for det in (1, 1, 0):
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, deterministic=det, **TOL)
+            x = ev.get_params()
+        assert np.isfinite(x).all()
+        # every run sits at the CPU LM's cost
+        assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
+        runs.append((s, x))
+    # Deterministic mode pins the termination. Near the optimum the trust region
+    # radius grows to ~1e15 (LM diagonal ~1e-15 after Jacobi scaling), so the
+    # single-observation points' V_p + D is singular to rounding and the model
+    # cost change -(g'd + |J d|^2/2) of the next steps is rounding noise <= 0:
+    # Ceres 1.14 calls such a step invalid (TrustRegionMinimizer::
+    # ComputeTrustRegionStep, step_is_valid = model_cost_change > 0), divides the
+    # radius by a doubling factor (LevenbergMarquardtStrategy::StepIsInvalid) and
+    # stops with FAILURE after max_num_consecutive_invalid_steps = 5 of them.
+    # MVBA_SOLVER_TRACE=1 prints those steps (profiles/r03/edge_trace_r03b.log).
+    (a, xa), (b, xb) = runs[0], runs[1]
+    assert a["termination_type"] == _lib.FAILURE, a["message"]
+    assert "consecutive invalid steps" in a["message"] and "5" in a["message"], a["message"]
+    for k in ("termination_type", "num_iterations", "num_successful_steps", "num_unsuccessful_steps",
+              "num_linear_iterations", "final_cost"):
+        assert a[k] == b[k], (k, a[k], b[k])
+    assert np.array_equal(xa, xb)
 
 
 @pytest.mark.gpu
