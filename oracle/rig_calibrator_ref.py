@@ -167,7 +167,7 @@ def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_thre
         depth_tri_weight=0.0, depth_to_image_transforms_to_float="", float_scale=False, tri_weight=0.0,
         tri_robust_threshold=0.0, min_triangulation_angle=0.5, max_reprojection_error=25.0,
         parameter_tolerance=1e-12, timestamp_offsets_max_change=1.0, mesh="", mesh_tri_weight=0.0,
-        depth_mesh_weight=0.0, min_ray_dist=0.0, max_ray_dist=100.0):
+        depth_mesh_weight=0.0, min_ray_dist=0.0, max_ray_dist=100.0, use_initial_rig_transforms=False):
     sensors = _read_config(rig_config)
     names = [s["name"] for s in sensors]
     ns = len(sensors)
@@ -256,6 +256,9 @@ def run(rig_config, nvm, num_iterations=20, calibrator_num_passes=2, robust_thre
         tr.setdefault(c["type"], []).append(Mc @ np.linalg.inv(Mi))
     r2c_vec = np.zeros((ns, 7))
     for t in range(ns):
+        if use_initial_rig_transforms:  # the configuration's ref_to_sensor_transform (rig_calibrator.cc:1347-1355)
+            r2c_vec[t] = _rigid_to_array(*sensors[t]["ref_to_cam"])
+            continue
         v = tr[t][len(tr[t]) // 2]
         L = v[:3, :3] / np.cbrt(np.linalg.det(v[:3, :3]))
         r2c_vec[t] = _rigid_to_array(L, v[:3, 3])
