@@ -476,6 +476,211 @@ static int eval_one(const mvba_problem_desc* d, const double* params, int64_t i,
   return MVBA_OK;
 }
 
+// ------------------------------------------- mode 3: the reference's per-call work
+// Same numbers as mode 1 (central differences over the same functor arithmetic),
+// with the work the reference does around them on every call kept, for the CPU
+// baseline (bench.py cpu_baseline):
+//   * the functor's deep copy of its CameraParameters, a heap VectorXd for the
+//     distortion, SetFocalLength / SetOpticalOffset / SetDistortion on the copy
+//     (rig_calibrator.cc:460-467; camera_params.cc:169-208: RPC reset, coefficient
+//     assignment, FOV precalcs, RPC set_dist_undist_params with its validation
+//     and four vectors, rpc_distortion.cc:229-293);
+//   * compute_rpc's validation (sqrt, round) and two std::vector per call
+//     (rpc_distortion.cc:116-124);
+//   * Ceres 1.14 [ext, absent] DynamicNumericDiffCostFunction::Evaluate: the
+//     parameter copy (vector<double> + vector<double*>), per differentiated
+//     block the x and step_size vectors (numeric_diff.h
+//     EvaluateJacobianForParameterBlock), and ResidualBlock::Evaluate's
+//     InvalidateEvaluation / IsEvaluationValid sweeps over residuals and
+//     Jacobian blocks (residual_block.cc, residual_block_utils.cc).
+struct RpcF {  // dense_map::RPCLensDistortion (rpc_distortion.h:33-39)
+  int deg = 0;
+  std::vector<double> dist, undist;
+  bool can_undistort = false;
+};
+struct CamParamsF {  // camera::CameraParameters (camera_params.h:127-181)
+  double focal[2] = {0, 0}, center[2] = {0, 0};
+  int dist_size[2] = {0, 0}, undist_size[2] = {0, 0}, crop_size[2] = {0, 0};
+  double dhalf[2] = {0, 0}, uhalf[2] = {0, 0}, crop_offset[2] = {0, 0};
+  RpcF rpc;
+  std::vector<double> coeffs;
+  double pc1 = 0, pc2 = 0, pc3 = 0;
+};
+
+static int rpc_num_dist(int deg) { return 2 * (deg + 1) * (deg + 2) - 2; }
+static int rpc_deg_of(int n) { return (int)std::round(std::sqrt(2.0 * n + 5.0) / 2.0 - 1.5); }
+static bool rpc_validate(int n) {  // validate_distortion_params (rpc_distortion.cc:52-57)
+  const int deg = rpc_deg_of(n);
+  return rpc_num_dist(deg) == n && deg > 0;
+}
+
+// SetDistortion (camera_params.cc:169-208) on a copy; false = the LOG(FATAL).
+static bool set_distortion_f(CamParamsF& c, const std::vector<double>& distortion) {
+  c.rpc = RpcF();
+  c.coeffs = distortion;
+  c.pc1 = c.pc2 = c.pc3 = 0;
+  switch (c.coeffs.size()) {
+    case 0:
+      break;
+    case 1:
+      c.pc1 = 1 / distortion[0];
+      c.pc2 = 2 * std::tan(distortion[0] / 2);
+      break;
+    case 4:
+    case 5:
+      break;
+    default: {  // set_dist_undist_params (rpc_distortion.cc:272-293)
+      const int num = (int)c.coeffs.size();
+      if (num % 2 != 0) return false;
+      std::vector<double> dp(num / 2), up(num / 2);
+      for (int i = 0; i < num / 2; i++) dp[i] = c.coeffs[i];
+      for (int i = 0; i < num / 2; i++) up[i] = c.coeffs[i + num / 2];
+      if (!rpc_validate((int)dp.size())) return false;  // set_distortion_parameters (:229-246)
+      if (dp.size() != c.rpc.dist.size()) {
+        c.rpc.can_undistort = false;
+      } else {
+        for (size_t i = 0; i < dp.size(); i++)
+          if (c.rpc.dist[i] != dp[i]) c.rpc.can_undistort = false;
+      }
+      c.rpc.dist = dp;
+      c.rpc.deg = rpc_deg_of((int)dp.size());
+      if (up.size() != c.rpc.dist.size()) return false;  // set_undistortion_parameters (:248-253)
+      c.rpc.undist = up;
+      c.rpc.can_undistort = true;
+    }
+  }
+  return true;
+}
+
+// BracketedCamError::operator() with the per-call copies (rig_calibrator.cc:447-482).
+static bool cam_error_faithful(const CamParamsF& m_cam_params, int K, const double* const* p, double m0, double m1,
+                               double sb, double se, double sc, double* r) {
+  Aff<double> wc;
+  if (!calc_world_to_cam_trans(p[0], p[1], p[2], sb, se, p[4][0], sc, &wc)) return false;
+  double X[3] = {p[3][0], p[3][1], p[3][2]};
+  CamParamsF cam_params = m_cam_params;  // "Make a deep copy which we will modify"
+  const double focal_vector[2] = {p[5][0], p[5][0]};
+  const double optical_center[2] = {p[6][0], p[6][1]};
+  std::vector<double> distortion(K);
+  for (int i = 0; i < K; i++) distortion[i] = p[7][i];
+  cam_params.focal[0] = focal_vector[0];
+  cam_params.focal[1] = focal_vector[1];
+  cam_params.center[0] = optical_center[0];
+  cam_params.center[1] = optical_center[1];
+  if (!set_distortion_f(cam_params, distortion)) return false;
+  double Xc[3];
+  apply(wc, X, Xc);
+  const double f = cam_params.focal[0];
+  const double u0 = f * (Xc[0] / Xc[2]);
+  const double u1 = f * (Xc[1] / Xc[2]);
+  double d0, d1;
+  if (K > 5) {  // compute_rpc's own validation before the polynomial (rpc_distortion.cc:117)
+    if (!rpc_validate((int)cam_params.rpc.dist.size())) return false;
+    compute_rpc(u0, u1, cam_params.rpc.dist.data(), (int)cam_params.rpc.dist.size(), &d0, &d1);
+    d0 += cam_params.dhalf[0];
+    d1 += cam_params.dhalf[1];
+  } else {
+    distort(u0, u1, f, cam_params.center[0], cam_params.center[1], cam_params.coeffs.data(), K,
+            cam_params.dhalf[0], cam_params.dhalf[1], &d0, &d1);
+  }
+  r[0] = d0 - m0;
+  r[1] = d1 - m1;
+  return true;
+}
+
+static const double kImpossibleValue = 1e302;  // Ceres residual_block_utils.cc [ext]
+
+// One ResidualBlock::Evaluate of a DynamicNumericDiffCostFunction<CENTRAL>.
+static int eval_one_faithful(const mvba_problem_desc* d, const CamParamsF& cam_params, const double* params,
+                             int64_t i, double* r, double* J) {
+  const int32_t* blk = d->residual_blocks + 8 * i;
+  const int cam = d->residual_camera[i];
+  const int K = d->camera_dist_size[cam];
+  const double m0 = d->residual_meas[2 * i], m1 = d->residual_meas[2 * i + 1];
+  const double sb = d->residual_stamps[3 * i], se = d->residual_stamps[3 * i + 1], sc = d->residual_stamps[3 * i + 2];
+  int sizes[8];
+  for (int b = 0; b < 7; b++) sizes[b] = kFixedSize[b];
+  sizes[7] = K;
+  const double* state[8];
+  for (int b = 0; b < 8; b++) state[b] = params + d->block_offset[blk[b]];
+  double* jac[8];
+  for (int b = 0; b < 8; b++) jac[b] = (J && !d->block_constant[blk[b]]) ? J + kBase[b] : nullptr;
+  // InvalidateEvaluation
+  r[0] = r[1] = kImpossibleValue;
+  for (int b = 0; b < 8; b++)
+    if (jac[b])
+      for (int k = 0; k < 2 * sizes[b]; k++) jac[b][k] = kImpossibleValue;
+  // DynamicNumericDiffCostFunction::Evaluate: residuals at the point
+  if (!cam_error_faithful(cam_params, K, state, m0, m1, sb, se, sc, r)) return MVBA_E_ALPHA_RANGE;
+  if (J) {
+    int total = 0;
+    for (int b = 0; b < 8; b++) total += sizes[b];
+    std::vector<double> parameters_copy(total);
+    std::vector<double*> refs(8);
+    int off = 0;
+    for (int b = 0; b < 8; b++) {
+      refs[b] = parameters_copy.data() + off;
+      for (int j = 0; j < sizes[b]; j++) refs[b][j] = state[b][j];
+      off += sizes[b];
+    }
+    const double min_step = std::sqrt(std::numeric_limits<double>::epsilon());
+    for (int b = 0; b < 8; b++) {
+      if (!jac[b]) continue;
+      // EvaluateJacobianForParameterBlock: x, step_size (dynamic Eigen vectors)
+      std::vector<double> x(refs[b], refs[b] + sizes[b]);
+      std::vector<double> step(sizes[b]);
+      for (int j = 0; j < sizes[b]; j++) step[j] = std::fabs(x[j]) * 1e-6;
+      for (int j = 0; j < sizes[b]; j++) {
+        const double delta = std::max(min_step, step[j]);
+        double res[2], tmp[2];
+        refs[b][j] = x[j] + delta;
+        if (!cam_error_faithful(cam_params, K, refs.data(), m0, m1, sb, se, sc, res)) return MVBA_E_ALPHA_RANGE;
+        double one_over_delta = 1.0 / delta;
+        refs[b][j] = x[j] - delta;
+        if (!cam_error_faithful(cam_params, K, refs.data(), m0, m1, sb, se, sc, tmp)) return MVBA_E_ALPHA_RANGE;
+        res[0] -= tmp[0];
+        res[1] -= tmp[1];
+        one_over_delta /= 2;
+        refs[b][j] = x[j];
+        jac[b][0 * sizes[b] + j] = res[0] * one_over_delta;
+        jac[b][1 * sizes[b] + j] = res[1] * one_over_delta;
+      }
+    }
+  }
+  // IsEvaluationValid
+  bool ok = std::isfinite(r[0]) && std::isfinite(r[1]) && r[0] != kImpossibleValue && r[1] != kImpossibleValue;
+  for (int b = 0; b < 8; b++)
+    if (jac[b])
+      for (int k = 0; k < 2 * sizes[b]; k++) ok = ok && std::isfinite(jac[b][k]) && jac[b][k] != kImpossibleValue;
+  return ok ? MVBA_OK : MVBA_E_INVALID;
+}
+
+// Per camera: the CameraParameters each functor of that camera holds (built as
+// readRigConfig + SetDistortion build it; the copies are made per call).
+static std::vector<CamParamsF> camera_params_f(const mvba_problem_desc* d, const double* params) {
+  std::vector<CamParamsF> out(d->num_cameras);
+  std::vector<int> seen(d->num_cameras, 0);
+  for (int64_t i = 0; i < d->num_residuals; i++) {
+    const int c = d->residual_camera[i];
+    if (seen[c]) continue;
+    seen[c] = 1;
+    const int32_t* blk = d->residual_blocks + 8 * i;
+    CamParamsF& cp = out[c];
+    cp.dhalf[0] = cp.uhalf[0] = d->camera_half_size[2 * c];
+    cp.dhalf[1] = cp.uhalf[1] = d->camera_half_size[2 * c + 1];
+    for (int a = 0; a < 2; a++) {
+      cp.dist_size[a] = cp.undist_size[a] = cp.crop_size[a] = (int)(2 * cp.dhalf[a]);
+    }
+    cp.focal[0] = cp.focal[1] = params[d->block_offset[blk[5]]];
+    cp.center[0] = params[d->block_offset[blk[6]]];
+    cp.center[1] = params[d->block_offset[blk[6]] + 1];
+    const int K = d->camera_dist_size[c];
+    std::vector<double> dist(params + d->block_offset[blk[7]], params + d->block_offset[blk[7]] + K);
+    set_distortion_f(cp, dist);
+  }
+  return out;
+}
+
 }  // namespace oracle
 
 using namespace oracle;
@@ -576,6 +781,8 @@ int oracle_evaluate_mt(const mvba_problem_desc* d, const double* params, int mod
   const int stride = oracle_jacobian_stride(d);
   if (end < 0 || end > d->num_residuals) end = d->num_residuals;
   int bad = 0;
+  // mode 3: the reference's per-call copies and checks around mode 1's numbers
+  const std::vector<CamParamsF> cams = mode == 3 ? camera_params_f(d, params) : std::vector<CamParamsF>();
 #pragma omp parallel for schedule(dynamic, 64) num_threads(threads) reduction(| : bad)
   for (int64_t i = begin; i < end; i++) {
     double r[2];
@@ -584,7 +791,9 @@ int oracle_evaluate_mt(const mvba_problem_desc* d, const double* params, int mod
       J = jacobian + (i - begin) * stride;
       std::fill(J, J + stride, 0.0);
     }
-    if (eval_one(d, params, i, mode, r, J) != MVBA_OK) bad |= 1;
+    const int st = mode == 3 ? eval_one_faithful(d, cams[d->residual_camera[i]], params, i, r, J)
+                             : eval_one(d, params, i, mode, r, J);
+    if (st != MVBA_OK) bad |= 1;
     residuals[2 * (i - begin)] = r[0];
     residuals[2 * (i - begin) + 1] = r[1];
   }

@@ -16,6 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle_mvba.so")
 
 RESIDUAL, NUMDIFF, ANALYTIC = 0, 1, 2
+# evaluate_mt only: mode 1 numbers with the reference's per-call copies and checks
+# (CameraParameters deep copy, SetDistortion, compute_rpc vectors, Ceres 1.14
+# DynamicNumericDiffCostFunction / ResidualBlock::Evaluate bookkeeping)
+NUMDIFF_FAITHFUL = 3
 _lib = None
 
 

@@ -229,3 +229,18 @@ def test_oracle_depth_mesh_matches_mpmath_golden(oracle, ci):
             scale = max(np.abs(Jg).max(), 1e-300)
             assert np.abs(J[off:off + n] - Jg).max() <= tol * scale, (mode, b)
             off += n
+
+
+@pytest.mark.parametrize("models", [["radtan", "fov", "none"], ["rpc2", "radtan4", "rpc1"], ["rpc3", "none"]])
+def test_faithful_numdiff_is_bit_identical(oracle, models):
+    """Mode NUMDIFF_FAITHFUL (bench.py's cpu_baseline) keeps the reference's
+    per-call work (CameraParameters deep copy + SetDistortion,
+    rig_calibrator.cc:460-467; compute_rpc's validation, rpc_distortion.cc:116-124;
+    Ceres' parameter copies and evaluation checks) around the same arithmetic:
+    residuals and Jacobians equal mode NUMDIFF bit for bit, constant blocks
+    included."""
+    R = rig.make_rig(num_sensors=len(models), num_ref=10, num_points=120, obs_per_point=4, models=models, seed=17)
+    P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=()))
+    r1, J1 = oracle.evaluate_mt(P, oracle.NUMDIFF, threads=2)
+    r3, J3 = oracle.evaluate_mt(P, oracle.NUMDIFF_FAITHFUL, threads=2)
+    assert np.array_equal(r1, r3) and np.array_equal(J1, J3)
