@@ -491,11 +491,12 @@ __device__ __forceinline__ void partial_put(double* p, double v) {
 __device__ __forceinline__ double partial_get(double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool arrive_last(unsigned* counter) {
+// nb: the blocks that take part (the grid's first nb; 0 = the whole grid)
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned nb = 0) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial stores above have completed
   const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __atomic_signal_fence(__ATOMIC_SEQ_CST);  // partial loads of the last block stay below the add
-  return prev == gridDim.x - 1;
+  return prev == (nb ? nb : gridDim.x) - 1;
 }
 
 __device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__ partial,
@@ -520,20 +521,22 @@ __device__ __forceinline__ bool grid_sum_finalize(double v, double* __restrict__
 
 // Three sums in one last-block finalisation (block partials interleaved as
 // partial[3 b + k]); the last block also returns the sums in res[0..2].
+// nb: blocks [0, nb) take part (0 = the whole grid); later blocks must not call it
 __device__ __forceinline__ bool grid_sum3_finalize(double a, double b, double c, double* __restrict__ partial,
                                                    unsigned* __restrict__ counter, double* __restrict__ out,
-                                                   double* res) {
+                                                   double* res, unsigned nb = 0) {
   __shared__ bool last;
   double v[3] = {a, b, c};
   block_sum<3>(v);
   if (threadIdx.x == 0) {
     for (int k = 0; k < 3; k++) partial_put(&partial[3 * blockIdx.x + k], v[k]);
-    last = arrive_last(counter);
+    last = arrive_last(counter, nb);
   }
   __syncthreads();
   if (!last) return false;
   double acc[3] = {0.0, 0.0, 0.0};
-  for (unsigned e = threadIdx.x; e < gridDim.x; e += blockDim.x)
+  const unsigned nblk = nb ? nb : gridDim.x;
+  for (unsigned e = threadIdx.x; e < nblk; e += blockDim.x)
     for (int k = 0; k < 3; k++) acc[k] += partial_get(&partial[3 * e + k]);
   block_sum<3>(acc);
   for (int k = 0; k < 3; k++) res[k] = acc[k];

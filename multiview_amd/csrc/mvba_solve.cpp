@@ -41,7 +41,7 @@ hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64
                               const double* prec, hipStream_t s);
 hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int32_t nchunks,
                                     const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
-                                    const double2* obs_meas, const int32_t* slot_po, const double* dir,
+                                    const double2* obs_meas, const int32_t* slot_po, mvba::DirPair dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
                                     const double* prec, const double4* obsX, hipStream_t s);
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
@@ -69,18 +69,18 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
 hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
                                        const double* val, const double* diag, const double* x, double* y,
                                        double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                       mvba::CgCtl* ctl, hipStream_t s);
+                                       mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, hipStream_t s);
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s);
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
                                 unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
-                                hipStream_t s);
+                                const mvba::LazyDir* lz, hipStream_t s);
 hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const double* minv, int32_t mode, double alpha,
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
-                                 int32_t iter, hipStream_t s);
+                                 int32_t iter, const mvba::FrameDirZ* fz, hipStream_t s);
 hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
                              hipStream_t s);
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, unsigned* counter, double* out,
@@ -130,6 +130,8 @@ struct SolverState {
          *tmp = nullptr;  // [ng]; p, p2: the CG direction, double-buffered
   double* yrep = nullptr;     // [replicas * ng], kept zero between products
   double* dir = nullptr;      // [nframes * dir stride]
+  double* dirz = nullptr;     // [nframes * dir stride] W z, by the CG update's frame blocks
+  double* dirp[2] = {nullptr, nullptr};  // W p_old / W p_new, alternating CG products
   double* zbuf = nullptr;     // [8 N] point-order z_o | J_pt rows
   double* wbuf = nullptr;     // [4 np] w_p of the last pass A (double4 per point)
   double* cbuf = nullptr;     // [4 slots] frame-order pass A: J_pt^T z per slot
@@ -154,7 +156,7 @@ struct SolverState {
 void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
-                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du, S->dcbuf,
+                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->dirz, S->dirp[0], S->dirp[1], S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du, S->dcbuf,
                   S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -206,6 +208,8 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->yrep, nrep));
     HCHK(hipMemset(S->yrep, 0, nrep * sizeof(double)));
     HCHK(dalloc(&S->dir, (size_t)(h->nframes * mvba_solver_dir_stride())));
+    for (double** v : {&S->dirz, &S->dirp[0], &S->dirp[1]})
+      HCHK(dalloc(v, (size_t)(h->nframes * mvba_solver_dir_stride())));
     HCHK(dalloc(&S->prec, (size_t)(h->nframes * mvba::kProjDoubles)));
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
     HCHK(dalloc(&S->wbuf, (size_t)(4 * std::max<int64_t>(S->np, 1))));
@@ -370,9 +374,10 @@ class Solver {
   // (dot -> scal[dot_slot]); sharded: cross-rank sum of y first (stream-ordered),
   // then damping + dot. gate: device CG stop flag (nullptr: always run); ctl:
   // CG step-length logic in the finalising block of the x.y reduction
-  // dir: the frame directions of xv (null: pass B with x = 0, u_o = -J_pt w_p)
+  // dir: the frame directions of xv (null: pass B with x = 0, u_o = -J_pt w_p);
+  // lz: xv is the CG direction, formed (and stored) by the reduction that damps it
   void reduce_frames(double* y, const double* xv, int dot_slot, const double* dir, const int32_t* gate = nullptr,
-                     mvba::CgCtl* ctl = nullptr) {
+                     mvba::CgCtl* ctl = nullptr, const mvba::LazyDir* lz = nullptr) {
     // deterministic mode: slab rows per chunk / depth segment and a fixed-order
     // gather instead of replica atomics (the first product records the plan)
     DetPlan& D = S_->b_det;
@@ -395,21 +400,24 @@ class Solver {
       HCHK(mvba_launch_slab_reduce_vec(D.tier_view(), D.grid(), D.begin, D.pos, D.val,
                                        fuse ? S_->dmp : nullptr, fuse ? xv : nullptr,
                                        y, S_->partial, S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate,
-                                       fuse ? ctl : nullptr, s_));
+                                       fuse ? ctl : nullptr, fuse ? lz : nullptr, s_));
     else
       HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr, y,
                                       S_->partial, S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate,
-                                      fuse ? ctl : nullptr, s_));
+                                      fuse ? ctl : nullptr, fuse ? lz : nullptr, s_));
     exchange(y, S_->ng, MVBA_REDUCE_SUM);
     if (xv && !fuse)
       HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, gate, ctl,
-                                s_));
+                                lz, s_));
   }
 
-  // w_p = (V + D)^-1 (tinit + sum J_pt^T J_cam x) into wbuf (dir: frame
-  // directions of x, null for x = 0). Depth blocks need the point-lane kernel
+  static mvba::DirPair plain_dir(const double* dir) { return mvba::DirPair{dir, nullptr, nullptr, nullptr}; }
+
+  // w_p = (V + D)^-1 (tinit + sum J_pt^T J_cam x) into wbuf (dr: frame
+  // directions of x, dr.dz null for x = 0). Depth blocks need the point-lane kernel
   // (it also forms their u_d); otherwise the frame-order sweep + point solve.
-  void pass_a_w(const double* dir, const double* tinit, const double* xv, const int32_t* gate) {
+  void pass_a_w(const mvba::DirPair& dr, const double* tinit, const double* xv, const int32_t* gate) {
+    const double* dir = dr.dz;
     if (h_->ndep > 0 && !dir) {
       // right-hand side (x = 0): the point-order kernel also forms u_d = -P w_p
       HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas,
@@ -425,8 +433,8 @@ class Solver {
         HCHK(mvba_launch_pass_a_frame(G.model, G.deg,
                                       chunked ? h_->d_chunks + G.chunk_begin : h_->d_segchunks + G.seg_begin,
                                       chunked ? G.chunk_count : G.seg_count, h_->d_segs,
-                                      h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dir, (double4*)S_->cbuf, flags_,
-                                      cauchy_c_, gate, S_->prec, obsx(), s_));
+                                      h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dr, (double4*)S_->cbuf,
+                                      flags_, cauchy_c_, gate, S_->prec, obsx(), s_));
     // depth blocks in frame order (z_d into du, P z_d per block for the point solve)
     const bool dep = dir && h_->ndep > 0;
     if (dep)
@@ -444,8 +452,19 @@ class Solver {
                    mvba::CgCtl* ctl = nullptr, const mvba::LazyDir* lz = nullptr) {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, xv, S_->dir, gate, lz,
                                s_));
-    pass_a_w(S_->dir, nullptr, xv, gate);
+    pass_a_w(plain_dir(S_->dir), nullptr, xv, gate);
     reduce_frames(y, xv, dot_slot, S_->dir, gate, ctl);
+  }
+
+  // y = S p_new for the CG direction p_new = z (+ beta p_old) with no direction
+  // kernel: pass A forms the frame records dz + beta dp (dz = W z, written by the
+  // CG update's frame blocks; dp = the previous product's, DirPair) and keeps
+  // them in dr.dp_out, which pass B then reads; p_new itself is formed by the
+  // reduction that damps it (lz). Reprojection-only problems.
+  void apply_schur_cg(double* y, const int32_t* gate, mvba::CgCtl* ctl, const mvba::LazyDir& lz,
+                      const mvba::DirPair& dr) {
+    pass_a_w(dr, nullptr, lz.p_new, gate);
+    reduce_frames(y, lz.p_new, 0, dr.dp_out, gate, ctl, &lz);
   }
 
   // b = -(g_c - W (V+D)^-1 g_p). Starts every linear solve: the projection
@@ -458,7 +477,7 @@ class Solver {
     // passes would take as the Cauchy weight: never fall back to one.
     if (obsx() && h_->lin_obsx != obsx())
       throw StatusErr{MVBA_E_INVALID, "internal: CG slot records were not written by the linearization"};
-    pass_a_w(nullptr, S_->G + S_->ng, nullptr, nullptr);
+    pass_a_w(plain_dir(nullptr), S_->G + S_->ng, nullptr, nullptr);
     reduce_frames(S_->tmp, nullptr, 0, nullptr);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
   }
@@ -489,14 +508,22 @@ class Solver {
     *S_->hctl = c;
     HCHK(hipMemcpyAsync(S_->ctl, S_->hctl, sizeof(mvba::CgCtl), hipMemcpyHostToDevice, s_));
     const int32_t* gate = &S_->ctl->done;
+    // Reprojection-only problems: the CG update's frame blocks form W z and the
+    // products combine it with the previous product's records (no direction
+    // kernel per iteration). Depth blocks read the direction in more kernels:
+    // they keep the direction kernel (MVBA_CG_DIR_KERNEL=1 forces it, for A/B).
+    static const bool dir_kernel = std::getenv("MVBA_CG_DIR_KERNEL") && std::getenv("MVBA_CG_DIR_KERNEL")[0] == '1';
+    const bool fused_dir = h_->ndep == 0 && !dir_kernel;
+    const mvba::FrameDirZ fz{h_->d_frame_lin, h_->d_fd, h_->d_frec, S_->dirz, (int32_t)h_->nframes, 0};
     auto upd = [&](int32_t mode, const double* q, int32_t iter, bool end_logic) {
       HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, 0.0, S_->p, q, S_->b, xv,
                                  S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl,
-                                 end_logic ? iter : -1, s_));
+                                 end_logic ? iter : -1, fused_dir ? &fz : nullptr, s_));
       std::swap(S_->r, S_->r2);
     };
     upd(4 | 8, nullptr, 0, true);  // r = b, z = M^-1 r, rho
     int i = 1;
+    int pp = 0;  // dirp[pp] holds W p_old
     // Batch sizes only decide where the host looks at the control block (gated
     // iterations past the stop are no-ops): the first batch runs to just short
     // of the previous solve's iteration count, later ones are short, so most
@@ -506,7 +533,12 @@ class Solver {
       for (int k = 0; k < batch && i <= std::max(o_.max_linear_solver_iterations, 1); k++, i++) {
         const mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, S_->ctl, 0, 0.0};
         std::swap(S_->p, S_->p2);
-        apply_schur(S_->p, S_->q, 0, gate, S_->ctl, &lz);
+        if (fused_dir) {
+          apply_schur_cg(S_->q, gate, S_->ctl, lz, mvba::DirPair{S_->dirz, S_->dirp[pp], S_->dirp[pp ^ 1], S_->ctl});
+          pp ^= 1;
+        } else {
+          apply_schur(S_->p, S_->q, 0, gate, S_->ctl, &lz);
+        }
         if (i % 10 == 0) {  // residual reset: r = b - A x
           upd(1, S_->q, i, false);
           apply_schur(xv, S_->tmp, 1, gate, nullptr);

@@ -82,8 +82,72 @@ __device__ __forceinline__ double lazy_p(const LazyDir& lz, int32_t first, doubl
   return first ? lz.z[e] : __fma_rn(beta, lz.p_old[e], lz.z[e]);
 }
 
+// The first N entries of frame `frame`'s direction record into this wave's LDS
+// area sd: d = dz, or inside CG iterations d = dz + beta dp (dp ignored on the
+// first iteration, as lazy_p ignores p_old); the writer wave also stores d into
+// dp_out for the next product. Wave-local: no block barrier.
+template <int N>
+__device__ __forceinline__ void stage_dir(const DirPair& D, int frame, double* sd, bool writer) {
+  const int lane = threadIdx.x & 63;
+  const int64_t base = (int64_t)frame * kDirStride;
+  int32_t first = 1;
+  double beta = 0.0;
+  if (D.dp) {
+    first = D.ctl->first;
+    beta = D.ctl->beta;
+  }
+  for (int m = lane; m < N; m += 64) {
+    double v = D.dz[base + m];
+    if (!first) v = __fma_rn(beta, D.dp[base + m], v);
+    sd[m] = v;
+    if (writer) D.dp_out[base + m] = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // One wave per frame: lane k < 22 takes pose column k (w_k x_k, butterfly-summed
-// over the wave), lanes 22.. copy the intrinsic entries.
+// over the wave), lanes 22.. copy the intrinsic entries. X(e): entry e of x.
+template <class XF>
+__device__ __forceinline__ void frame_dir_body(const FrameLin& L, int32_t K, const double* __restrict__ frec_f,
+                                               int lane, XF X, double* __restrict__ d) {
+  double u[6] = {0, 0, 0, 0, 0, 0};
+  if (lane < kPoseCols) {
+    const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
+    const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+    if (L.goff[b] >= 0) {
+      const double xv = X(L.goff[b] + (lane - 7 * blk));
+      const double* wk = frec_f + 12 + 6 * lane;
+#pragma unroll
+      for (int a = 0; a < 6; a++) u[a] = wk[a] * xv;
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 6; a++)
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) u[a] += __shfl_xor(u[a], off, 64);  // lanes 0..31 hold all columns
+  if (lane < 6) {
+    double v = u[0];
+#pragma unroll
+    for (int a = 1; a < 6; a++)
+      if (lane == a) v = u[a];
+    d[lane] = v;
+  }
+  // lanes 22.. copy the intrinsic entries: 0 focal, 1..2 centre, 3.. distortion
+  const int nd = L.width - 10;
+  for (int m = lane - kPoseCols; m >= 0 && m < 3 + nd; m += 64 - kPoseCols) {
+    double v = 0.0;
+    if (m == 0) {
+      if (L.goff[MVBA_BLK_FOCAL] >= 0) v = X(L.goff[MVBA_BLK_FOCAL]);
+    } else if (m < 3) {
+      if (L.goff[MVBA_BLK_CENTER] >= 0) v = X(L.goff[MVBA_BLK_CENTER] + (m - 1));
+    } else if (L.goff[MVBA_BLK_DIST] >= 0 && m - 3 < K) {
+      v = X(L.goff[MVBA_BLK_DIST] + (m - 3));
+    }
+    d[6 + m] = v;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_frame_dir(const FrameLin* __restrict__ fl, int32_t nframes,
                                                   const FrameDesc* __restrict__ fd,
                                                   const double* __restrict__ frec,
@@ -104,43 +168,7 @@ __global__ void __launch_bounds__(64) k_frame_dir(const FrameLin* __restrict__ f
   }
   const int f = blockIdx.x;
   auto X = [&](int64_t e) { return lz.z ? lazy_p(lz, first, beta, e) : x[e]; };
-  const FrameLin& L = fl[f];
-  double u[6] = {0, 0, 0, 0, 0, 0};
-  if (lane < kPoseCols) {
-    const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
-    const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
-    if (L.goff[b] >= 0) {
-      const double xv = X(L.goff[b] + (lane - 7 * blk));
-      const double* wk = frec + (int64_t)f * kFrameRecDoubles + 12 + 6 * lane;
-#pragma unroll
-      for (int a = 0; a < 6; a++) u[a] = wk[a] * xv;
-    }
-  }
-#pragma unroll
-  for (int a = 0; a < 6; a++)
-#pragma unroll
-    for (int off = 16; off > 0; off >>= 1) u[a] += __shfl_xor(u[a], off, 64);  // lanes 0..31 hold all columns
-  double* d = dir + (int64_t)f * kDirStride;
-  if (lane < 6) {
-    double v = u[0];
-#pragma unroll
-    for (int a = 1; a < 6; a++)
-      if (lane == a) v = u[a];
-    d[lane] = v;
-  }
-  // lanes 22.. copy the intrinsic entries: 0 focal, 1..2 centre, 3.. distortion
-  const int nd = L.width - 10;
-  for (int m = lane - kPoseCols; m >= 0 && m < 3 + nd; m += 64 - kPoseCols) {
-    double v = 0.0;
-    if (m == 0) {
-      if (L.goff[MVBA_BLK_FOCAL] >= 0) v = X(L.goff[MVBA_BLK_FOCAL]);
-    } else if (m < 3) {
-      if (L.goff[MVBA_BLK_CENTER] >= 0) v = X(L.goff[MVBA_BLK_CENTER] + (m - 1));
-    } else if (L.goff[MVBA_BLK_DIST] >= 0 && m - 3 < fd[f].K) {
-      v = X(L.goff[MVBA_BLK_DIST] + (m - 3));
-    }
-    d[6 + m] = v;
-  }
+  frame_dir_body(fl[f], fd[f].K, frec + (int64_t)f * kFrameRecDoubles, lane, X, dir + (int64_t)f * kDirStride);
 }
 
 // ------------------------------------------------------------ pass A (point order)
@@ -419,16 +447,22 @@ template <int MODEL, int DEG>
 __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
     const int4* __restrict__ chunks, int32_t nchunks, const Segment* __restrict__ segs,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
-    const int32_t* __restrict__ slot_po, const double* __restrict__ dir, double4* __restrict__ cbuf, int32_t flags,
+    const int32_t* __restrict__ slot_po, DirPair dr, double4* __restrict__ cbuf, int32_t flags,
     double cauchy_c,
     const int32_t* __restrict__ gate, const double* __restrict__ prec, const double4* __restrict__ obsX) {
+  constexpr int ND = 6 + RowShape<MODEL, DEG>::kIntr;  // direction entries the rows read
+  __shared__ double sdir[kPassAWaves][ND];
   const int lane = threadIdx.x & 63;
   const int ch = blockIdx.x * kPassAWaves + (threadIdx.x >> 6);
   if (ch >= nchunks || (gate && *gate)) return;
   const int4 c = chunks[ch];
   const int frame = __builtin_amdgcn_readfirstlane(c.z);
   const double* __restrict__ rec = prec + (int64_t)frame * kProjDoubles;
-  const double* __restrict__ d = dir + (int64_t)frame * kDirStride;
+  // the frame's direction (combined from dz and dp inside CG iterations); the
+  // wave of the frame's first segment keeps it for the next product
+  double* d = sdir[threadIdx.x >> 6];
+  const bool writer = dr.dp_out && (c.x == 0 || segs[c.x - 1].frame != frame);
+  stage_dir<ND>(dr, frame, d, writer);
   for (int sidx = 0; sidx < c.y; sidx++) {
     const Segment sg = segs[c.x + sidx];
     const int count = __builtin_amdgcn_readfirstlane(sg.count);
@@ -789,16 +823,26 @@ __device__ __forceinline__ void cg_step_length(CgCtl* ctl, double pq) {
   }
 }
 
+// With lz.z set, x is the CG direction p_new = z (+ beta p_old): formed here
+// (first / beta from lz.ctl) and stored to lz.p_new for the update kernel.
+__device__ __forceinline__ double x_entry(const double* __restrict__ x, const LazyDir& lz, int64_t e) {
+  if (!lz.z) return x[e];
+  const double v = lazy_p(lz, lz.ctl->first, lz.ctl->beta, e);
+  lz.p_new[e] = v;
+  return v;
+}
+
 __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yrep, int64_t n,
                                                         const double* __restrict__ diag,
                                                         const double* __restrict__ x, double* __restrict__ y,
                                                         double* __restrict__ partial, unsigned* __restrict__ counter,
                                                         double* __restrict__ dot_out, const int32_t* __restrict__ gate,
-                                                        CgCtl* __restrict__ ctl) {
+                                                        CgCtl* __restrict__ ctl, LazyDir lz) {
   if (gate && *gate) return;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double d = 0.0;
   if (e < n) {
+    const double xe = (x || lz.z) ? x_entry(x, lz, e) : 0.0;
     // all replica loads in flight before the first add / zeroing store (the
     // stores go through the same pointer, so a fused loop serialises them)
     double v[kVecReplicas];
@@ -809,9 +853,9 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
     for (int r = 0; r < kVecReplicas; r++) acc += v[r];
 #pragma unroll
     for (int r = 0; r < kVecReplicas; r++) yrep[r * n + e] = 0.0;
-    if (diag) acc += diag[e] * x[e];
+    if (diag) acc += diag[e] * xe;
     y[e] = acc;
-    d = x ? x[e] * acc : 0.0;
+    d = xe * acc;
   }
   if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
     cg_step_length(ctl, dot_out[0]);
@@ -827,15 +871,17 @@ __global__ void __launch_bounds__(256) k_vec_slab_reduce(SlabTiers tiers, const 
                                                          const double* __restrict__ x, double* __restrict__ y,
                                                          double* __restrict__ partial, unsigned* __restrict__ counter,
                                                          double* __restrict__ dot_out,
-                                                         const int32_t* __restrict__ gate, CgCtl* __restrict__ ctl) {
+                                                         const int32_t* __restrict__ gate, CgCtl* __restrict__ ctl,
+                                                         LazyDir lz) {
   if (gate && *gate) return;
   int64_t e;
   double acc;
   double d = 0.0;
   if (slab_gather(tiers, begin, pos, val, &e, &acc)) {
-    if (diag) acc += diag[e] * x[e];
+    const double xe = (x || lz.z) ? x_entry(x, lz, e) : 0.0;
+    if (diag) acc += diag[e] * xe;
     y[e] = acc;
-    d = x ? x[e] * acc : 0.0;
+    d = xe * acc;
   }
   if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
     cg_step_length(ctl, dot_out[0]);
@@ -848,23 +894,45 @@ __global__ void __launch_bounds__(256) k_add_diag(int64_t n, const double* __res
                                                   const double* __restrict__ x, double* __restrict__ y,
                                                   double* __restrict__ partial, unsigned* __restrict__ counter,
                                                   double* __restrict__ dot_out, const int32_t* __restrict__ gate,
-                                                  CgCtl* __restrict__ ctl) {
+                                                  CgCtl* __restrict__ ctl, LazyDir lz) {
   if (gate && *gate) return;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double d = 0.0;
   if (e < n) {
-    const double v = y[e] + diag[e] * x[e];
+    const double xe = x_entry(x, lz, e);
+    const double v = y[e] + diag[e] * xe;
     y[e] = v;
-    d = x[e] * v;
+    d = xe * v;
   }
   if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
     cg_step_length(ctl, dot_out[0]);
+}
+
+// r_new(k) and z_i = (M^-1 r_new)_i as the CG update forms them (shared by the
+// entry threads and the frame blocks, so both see the same values)
+__device__ __forceinline__ double cg_rnew(int32_t mode, double alpha, const double* __restrict__ q,
+                                          const double* __restrict__ b, const double* __restrict__ r_in, int64_t k) {
+  if (mode & 2) return r_in[k] - alpha * q[k];
+  if (mode & 4) return q ? b[k] - q[k] : b[k];
+  return r_in[k];
+}
+__device__ __forceinline__ double cg_zentry(const CgEntry& E, const double* __restrict__ minv, int32_t mode,
+                                            double alpha, const double* __restrict__ q, const double* __restrict__ b,
+                                            const double* __restrict__ r_in) {
+  const double* M = minv + E.moff;
+  double zi = 0.0;
+  for (int k = 0; k < E.nb; k++) zi += M[k] * cg_rnew(mode, alpha, q, b, r_in, E.o + k);
+  return zi;
 }
 
 // One CG step on the camera side, one thread per camera entry
 // (conjugate_gradients_solver.cc [ext]); r is double-buffered (r_in -> r_out):
 //   mode & 1: x += alpha p;  & 2: r = r_in - alpha q;  & 4: r = b - q (q null: r = b);
 //   mode & 8: z = M^-1 r (explicit block inverses) and out = [x.b, x.r, r.z].
+// With fz.dz (mode & 8), blocks from fz.owner_blocks on are frame blocks, one
+// wave per frame: dz_f = W_f z from z recomputed for the frame's camera entries
+// (the next product's direction is then dz + beta dp, DirPair): the separate
+// direction kernel between this update and pass A is gone.
 __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __restrict__ ent,
                                                    const double* __restrict__ minv,
                                                    int32_t mode, double alpha, const double* __restrict__ p,
@@ -872,33 +940,33 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
                                                    double* __restrict__ x, const double* __restrict__ r_in,
                                                    double* __restrict__ r_out, double* __restrict__ z,
                                                    double* __restrict__ partial, unsigned* __restrict__ counters,
-                                                   double* __restrict__ out, CgCtl* __restrict__ ctl, int32_t iter) {
+                                                   double* __restrict__ out, CgCtl* __restrict__ ctl, int32_t iter,
+                                                   FrameDirZ fz) {
   if (ctl) {
     if (ctl->done) return;
     alpha = ctl->alpha;
+  }
+  if (fz.dz && (int32_t)blockIdx.x >= fz.owner_blocks) {
+    const int f = ((int32_t)blockIdx.x - fz.owner_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+    if (f >= fz.nframes) return;
+    auto Z = [&](int64_t e) { return cg_zentry(ent[e], minv, mode, alpha, q, b, r_in); };
+    frame_dir_body(((const FrameLin*)fz.fl)[f], fz.fd[f].K, fz.frec + (int64_t)f * kFrameRecDoubles,
+                   (int)(threadIdx.x & 63), Z, fz.dz + (int64_t)f * kDirStride);
+    return;
   }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double xb = 0.0, xr = 0.0, rz = 0.0;
   if (i < n) {
     const CgEntry E = ent[i];
-    const int64_t o = E.o;
-    const int nb = E.nb;
-    auto rnew = [&](int64_t k) -> double {
-      if (mode & 2) return r_in[k] - alpha * q[k];
-      if (mode & 4) return q ? b[k] - q[k] : b[k];
-      return r_in[k];
-    };
     double xi = x[i];
     if (mode & 1) {
       xi += alpha * p[i];
       x[i] = xi;
     }
-    const double ri = rnew(i);
+    const double ri = cg_rnew(mode, alpha, q, b, r_in, i);
     r_out[i] = ri;
     if (mode & 8) {
-      const double* M = minv + E.moff;
-      double zi = 0.0;
-      for (int k = 0; k < nb; k++) zi += M[k] * rnew(o + k);
+      const double zi = cg_zentry(E, minv, mode, alpha, q, b, r_in);
       z[i] = zi;
       xb = xi * b[i];
       xr = xi * ri;
@@ -907,7 +975,8 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
   }
   if (mode & 8) {
     double sums[3];
-    if (grid_sum3_finalize(xb, xr, rz, partial, counters, out, sums) && ctl && threadIdx.x == 0) {
+    const unsigned nb = fz.dz ? (unsigned)fz.owner_blocks : 0u;
+    if (grid_sum3_finalize(xb, xr, rz, partial, counters, out, sums, nb) && ctl && threadIdx.x == 0) {
       const double sxb = sums[0], sxr = sums[1];
       const double rho_next = sums[2];
       auto bad = [](double v) { return v == 0.0 || isinf(v) || isnan(v); };
@@ -1315,7 +1384,7 @@ hipError_t mvba_launch_pass_a(int model, int deg, const int64_t* pt_begin, int64
 // Frame-order pass A (no depth blocks, no |u|^2 sweep) for one model group
 hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int32_t nchunks,
                                     const mvba::Segment* segs, const double4* pts, const int32_t* obs_pid,
-                                    const double2* obs_meas, const int32_t* slot_po, const double* dir,
+                                    const double2* obs_meas, const int32_t* slot_po, mvba::DirPair dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
                                     const double* prec, const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
@@ -1382,28 +1451,31 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
 hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
                                        const double* val, const double* diag, const double* x, double* y,
                                        double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                       mvba::CgCtl* ctl, hipStream_t s) {
+                                       mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
+  const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
   hipLaunchKernelGGL(mvba::k_vec_slab_reduce, dim3((unsigned)grid), dim3(256), 0, s, t, begin, pos, val, diag, x, y,
-                     partial, counter, dot_out, gate, ctl);
+                     partial, counter, dot_out, gate, ctl, l);
   return hipGetLastError();
 }
 
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, hipStream_t s) {
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s) {
   if (ng <= 0) return hipSuccess;
+  const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
   hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, diag, x,
-                     y, partial, counter, dot_out, gate, ctl);
+                     y, partial, counter, dot_out, gate, ctl, l);
   return hipGetLastError();
 }
 
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
                                 unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
-                                hipStream_t s) {
+                                const mvba::LazyDir* lz, hipStream_t s) {
   if (n <= 0) return hipSuccess;
+  const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
   hipLaunchKernelGGL(mvba::k_add_diag, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, diag, x, y, partial,
-                     counter, dot_out, gate, ctl);
+                     counter, dot_out, gate, ctl, l);
   return hipGetLastError();
 }
 
@@ -1412,11 +1484,18 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
-                                 int32_t iter, hipStream_t s) {
+                                 int32_t iter, const mvba::FrameDirZ* fz, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 255) / 256);
-  hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks), dim3(256), 0, s, n, ent, minv, mode, alpha,
-                     p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter);
+  mvba::FrameDirZ f{};
+  unsigned fblocks = 0;
+  if (fz && fz->dz && (mode & 8) && fz->nframes > 0) {
+    f = *fz;
+    f.owner_blocks = (int32_t)blocks;
+    fblocks = (unsigned)((fz->nframes + 3) / 4);  // 4 frame waves per 256-thread block
+  }
+  hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks + fblocks), dim3(256), 0, s, n, ent, minv, mode, alpha,
+                     p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter, f);
   return hipGetLastError();
 }
 

@@ -179,6 +179,30 @@ struct LazyDir {
   double beta;
 };
 
+// The frame direction records the CG passes read (dir[frame * kDirStride]: the
+// frame's 6 pose sums w x | intrinsic entries). Outside CG iterations d = dz.
+// Inside them d = W p_new with p_new = z (first) or z + beta p_old, formed as
+// d = dz + beta dp from dz = W z (the CG update kernel's frame blocks) and
+// dp = W p_old (the previous product's records, stored by pass A into dp_out),
+// so no separate direction kernel runs between the update and pass A.
+struct DirPair {
+  const double* dz;
+  const double* dp;  // null: d = dz
+  double* dp_out;    // pass A: d stored here by one wave per frame (null: not stored)
+  const CgCtl* ctl;  // first / beta
+};
+
+// Frame blocks of the CG update kernel: dz = W z for every frame, z = M^-1 r_new
+// recomputed from the same inputs as the entry blocks (owner_blocks of them).
+struct FrameDirZ {
+  const void* fl;  // FrameLin
+  const FrameDesc* fd;
+  const double* frec;
+  double* dz;
+  int32_t nframes;
+  int32_t owner_blocks;
+};
+
 }  // namespace mvba
 
 #endif  // MVBA_TYPES_H_

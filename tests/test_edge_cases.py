@@ -97,13 +97,7 @@ def test_all_constant_problem(oracle):
     assert np.array_equal(x, P.params)
 
 
-@pytest.mark.gpu
-def test_single_observation_points_and_frames():
-    """Points seen once have a rank-2 block V_p; with LM damping the step is
-    defined and the solve reaches the CPU LM's cost (the points' positions along
-    their rays are a null direction, so only the cost is compared)."""
-    from oracle import lm_reference
-
+def _single_observation_problem():
     R = rig.make_rig(num_sensors=3, num_ref=8, num_points=150, obs_per_point=2.0, models=["radtan", "fov", "none"],
                      seed=21)
     P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=()))
@@ -116,34 +110,64 @@ def test_single_observation_points_and_frames():
     P.residual_names = None
     counts = np.bincount(R.obs_pid[keep])
     assert (counts == 1).sum() > 20
-    TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
-    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
-    runs = []
-    for det in (1, 1, 0):
-        with Evaluator(P) as ev:
-            ev.set_params()
-            s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, deterministic=det, **TOL)
-            x = ev.get_params()
-        assert np.isfinite(x).all()
-        # every run sits at the CPU LM's cost
-        assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
-        runs.append((s, x))
-    # Deterministic mode pins the termination. Near the optimum the trust region
-    # radius grows to ~1e15 (LM diagonal ~1e-15 after Jacobi scaling), so the
-    # single-observation points' V_p + D is singular to rounding and the model
-    # cost change -(g'd + |J d|^2/2) of the next steps is rounding noise <= 0:
-    # Ceres 1.14 calls such a step invalid (TrustRegionMinimizer::
-    # ComputeTrustRegionStep, step_is_valid = model_cost_change > 0), divides the
-    # radius by a doubling factor (LevenbergMarquardtStrategy::StepIsInvalid) and
-    # stops with FAILURE after max_num_consecutive_invalid_steps = 5 of them.
-    # MVBA_SOLVER_TRACE=1 prints those steps (profiles/r03/edge_trace_r03b.log).
-    (a, xa), (b, xb) = runs[0], runs[1]
-    assert a["termination_type"] == _lib.FAILURE, a["message"]
-    assert "consecutive invalid steps" in a["message"] and "5" in a["message"], a["message"]
+    return P
+
+
+def _solve(P, det, max_it, **tol):
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=max_it, use_loss=1, robust_threshold=3.0, deterministic=det, **tol)
+        x = ev.get_params()
+    assert np.isfinite(x).all()
+    return s, x
+
+
+def _same_run(a, b):
+    (sa, xa), (sb, xb) = a, b
     for k in ("termination_type", "num_iterations", "num_successful_steps", "num_unsuccessful_steps",
               "num_linear_iterations", "final_cost"):
-        assert a[k] == b[k], (k, a[k], b[k])
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
     assert np.array_equal(xa, xb)
+
+
+@pytest.mark.gpu
+def test_single_observation_points_and_frames():
+    """Points seen once have a rank-2 block V_p; with LM damping the step is
+    defined and the solve reaches the CPU LM's cost (the points' positions along
+    their rays are a null direction, so only the cost is compared), at the
+    reference CLI's tolerances (function and gradient 1e-16,
+    rig_calibrator.cc:1915-1916).
+
+    The inexact Schur-CG steps (ITERATIVE_SCHUR, eta = 0.1) converge slowly
+    along the null directions: the CPU LM (exact steps) stops after ~60
+    iterations, the GPU LM keeps making small successful steps for ~160 and
+    then reaches the rounding-noise regime: the trust-region radius has grown to
+    ~1e15 (LM diagonal ~1e-15 after Jacobi scaling), V_p + D of the
+    single-observation points is singular to rounding and the model cost change
+    -(g'd + |J d|^2/2) of the next steps is noise. Ceres 1.14 calls a step with
+    model cost change <= 0 invalid (TrustRegionMinimizer::ComputeTrustRegionStep),
+    divides the radius (LevenbergMarquardtStrategy::StepIsInvalid) and stops with
+    FAILURE after max_num_consecutive_invalid_steps = 5; noise steps that come
+    out "valid" keep the solve going to max_num_iterations (NO_CONVERGENCE).
+    Which of the two ends the solve is decided by rounding, i.e. by the build
+    (the CG passes' FMA contraction and summation order): round 2's build ended
+    with FAILURE, the fused-direction CG of round 3 with NO_CONVERGENCE at 200.
+    Pinned here: every run is at the CPU LM's cost within 1e-6, ends in one of
+    those two noise-regime terminations, and two deterministic solves are
+    bit-identical (termination, iteration counts, cost, parameters).
+    MVBA_SOLVER_TRACE=1 prints the steps (profiles/r03/edge_trace_r03b.log)."""
+    from oracle import lm_reference
+
+    P = _single_observation_problem()
+    TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
+    runs = [_solve(P, det, 200, **TOL) for det in (1, 1, 0)]
+    for s, _ in runs:
+        assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
+        noise_end = (s["termination_type"] == _lib.FAILURE and "consecutive invalid steps" in s["message"]) or \
+            (s["termination_type"] == _lib.NO_CONVERGENCE and "Maximum number of iterations" in s["message"])
+        assert noise_end, s["message"]
+    _same_run(runs[0], runs[1])
 
 
 @pytest.mark.gpu
