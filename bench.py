@@ -207,7 +207,7 @@ def _stream_copy_gbs(torch, stream, nbytes=1 << 30, reps=10):
     return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
-PROFILE_ROUNDS = ("r02", "r01")  # newest first: committed PMC summaries are read from here
+PROFILE_ROUNDS = ("r03", "r02", "r01")  # newest first: committed PMC summaries are read from here
 
 
 def _profile_path(name):
@@ -246,6 +246,44 @@ def _pmc_flops(config):
 def _flops_of(table, prefixes):
     tot = [v["fp64_flops"] for k, v in table.items() if any(k.startswith(p) for p in prefixes)]
     return sum(tot) if tot else None
+
+
+def cg_bytes(num_obs, num_points, num_frames, ng, dist_sizes):
+    """Algorithmic bytes of one CG iteration (one implicit-Schur product + the
+    vector updates) of a reprojection-only problem, DESIGN.md §5 "BA roofline":
+      per observation  136 B  pass A: slot record (landmark + Cauchy weight) 32,
+                              point-order slot 4, c_o store 32; k_point_w: c_o 32;
+                              pass B: point index 4, slot record 32
+      per point        152 B  k_point_w: CSR start 8, V 48, D 24, free flag 8,
+                              w store 32; pass B: w read once 32
+      per frame               pass B: world_to_cam + 22 generators (144 doubles);
+                              update frame blocks: the 22 generators (132 doubles);
+                              pass A: projection record (18 + K doubles); direction
+                              records dz, dp (read) and the combined one (written,
+                              read by pass B): 4 x (9 + live distortion) doubles
+      per camera entry 704 B  replica sum: 32 replicas read + re-zeroed (512),
+                              damping, z, p_old, p_new, y (48); update: entry
+                              descriptor 16, x r/w 16, p, q, b, r_in, r_out, z (48),
+                              block-inverse row (8 per block entry, ~7)
+    Gathers that re-read L2-resident tables (the w of a point per observation,
+    the frame records per wave) are counted once."""
+    k = max(int(x) for x in dist_sizes) if len(dist_sizes) else 0
+    live = k // 2 if k > 5 else k
+    per_frame = 8 * (144 + 132 + (18 + k) + 4 * (9 + live))
+    return 136 * num_obs + 152 * num_points + per_frame * num_frames + 704 * ng
+
+
+def _ba_summary(config):
+    """Committed CG-iteration summary of this config (tools/ba_roofline.py over a
+    rocprofv3 kernel trace + FETCH/WRITE/SQ passes of this same command), or {}."""
+    path = _profile_path(f"ba_{config}.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        d["path"] = os.path.relpath(path, os.path.dirname(os.path.abspath(__file__)))
+        return d
+    except (OSError, ValueError):
+        return {}
 
 
 def ceres_surface(ev, P, torch, args):
@@ -796,6 +834,32 @@ def main():
                          "gloo (host-staged callback)" if ex else "none (single rank)"),
             "exchange_calls": ex.calls if ex else None,
         }
+        if ev.num_depth == 0:
+            cgb = cg_bytes(ev.num_residuals, int(L["num_points"]), ev.num_frames, int(L["cam_grad_size"]),
+                           P.camera_dist_size)
+            wall_ms = line["ba"]["ms_per_cg_iteration"]
+            roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                    "bytes_per_cg_iteration": cgb,
+                    "achieved_wall": cgb / (wall_ms * 1e-3) / 1e9,
+                    "frac_wall": cgb / (wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "wall_note": "algorithmic bytes / (linear-solver wall time / CG iterations): includes the "
+                                 "residual-reset products (every 10th), the per-solve setup and host reads"}
+            summ = _ba_summary(args.config)
+            if summ and world == 1:
+                kus = summ["kernel_us_per_cg_iteration"]
+                roof.update({
+                    "kernel_us": kus,
+                    "achieved": cgb / (kus * 1e-6) / 1e9,
+                    "frac": cgb / (kus * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                    "traffic": summ["traffic_bytes_per_cg_iteration"],
+                    "traffic_ratio": summ["traffic_bytes_per_cg_iteration"] / cgb,
+                    "valu_floor_us": summ["valu_floor_us"],
+                    "valu_frac": summ["valu_floor_us"] / kus,
+                    "source": summ["path"] + " (rocprofv3 kernel trace: median span of non-gated iterations "
+                              "pass A -> update, boundaries included; FETCH_SIZE x2 + WRITE_SIZE and "
+                              "SQ_INSTS_VALU per kernel, median of non-gated launches)",
+                })
+            line["ba"]["roofline"] = roof
         if world > 1:
             # the per-CG-iteration exchange alone: one all-reduce of the
             # camera-side product vector (cam_grad_size doubles), on the solver's
