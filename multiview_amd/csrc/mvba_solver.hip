@@ -107,7 +107,8 @@ __device__ __forceinline__ void stage_dir(const DirPair& D, int frame, double* s
 }
 
 // One wave per frame: lane k < 22 takes pose column k (w_k x_k, butterfly-summed
-// over the wave), lanes 22.. copy the intrinsic entries. X(e): entry e of x.
+// over the wave), lanes 22.. copy the intrinsic entries. X(b, j): entry j of the
+// frame's camera block b (MVBA_BLK_*) of x; called only for floating blocks.
 template <class XF>
 __device__ __forceinline__ void frame_dir_body(const FrameLin& L, int32_t K, const double* __restrict__ frec_f,
                                                int lane, XF X, double* __restrict__ d) {
@@ -116,7 +117,7 @@ __device__ __forceinline__ void frame_dir_body(const FrameLin& L, int32_t K, con
     const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
     if (L.goff[b] >= 0) {
-      const double xv = X(L.goff[b] + (lane - 7 * blk));
+      const double xv = X(b, lane - 7 * blk);
       const double* wk = frec_f + 12 + 6 * lane;
 #pragma unroll
       for (int a = 0; a < 6; a++) u[a] = wk[a] * xv;
@@ -138,11 +139,11 @@ __device__ __forceinline__ void frame_dir_body(const FrameLin& L, int32_t K, con
   for (int m = lane - kPoseCols; m >= 0 && m < 3 + nd; m += 64 - kPoseCols) {
     double v = 0.0;
     if (m == 0) {
-      if (L.goff[MVBA_BLK_FOCAL] >= 0) v = X(L.goff[MVBA_BLK_FOCAL]);
+      if (L.goff[MVBA_BLK_FOCAL] >= 0) v = X(MVBA_BLK_FOCAL, 0);
     } else if (m < 3) {
-      if (L.goff[MVBA_BLK_CENTER] >= 0) v = X(L.goff[MVBA_BLK_CENTER] + (m - 1));
+      if (L.goff[MVBA_BLK_CENTER] >= 0) v = X(MVBA_BLK_CENTER, m - 1);
     } else if (L.goff[MVBA_BLK_DIST] >= 0 && m - 3 < K) {
-      v = X(L.goff[MVBA_BLK_DIST] + (m - 3));
+      v = X(MVBA_BLK_DIST, m - 3);
     }
     d[6 + m] = v;
   }
@@ -167,8 +168,12 @@ __global__ void __launch_bounds__(64) k_frame_dir(const FrameLin* __restrict__ f
     return;
   }
   const int f = blockIdx.x;
-  auto X = [&](int64_t e) { return lz.z ? lazy_p(lz, first, beta, e) : x[e]; };
-  frame_dir_body(fl[f], fd[f].K, frec + (int64_t)f * kFrameRecDoubles, lane, X, dir + (int64_t)f * kDirStride);
+  const FrameLin& L = fl[f];
+  auto X = [&](int b, int j) {
+    const int64_t e = L.goff[b] + j;
+    return lz.z ? lazy_p(lz, first, beta, e) : x[e];
+  };
+  frame_dir_body(L, fd[f].K, frec + (int64_t)f * kFrameRecDoubles, lane, X, dir + (int64_t)f * kDirStride);
 }
 
 // ------------------------------------------------------------ pass A (point order)
@@ -608,6 +613,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
         if (lane < count) {
           const int64_t i = (int64_t)sg.begin + lane;
           const int32_t pid = obs_pid[i];
+          const double4 w = wbuf[pid];
           const double4 X = obsX ? obsX[i] : pts[pid];
           Proj o;
           project<MODEL, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
@@ -649,7 +655,6 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
             P0[q] = G0[0] * rec[q] + G0[1] * rec[3 + q] + G0[2] * rec[6 + q];
             P1[q] = G1[0] * rec[q] + G1[1] * rec[3 + q] + G1[2] * rec[6 + q];
           }
-          const double4 w = wbuf[pid];
           const double ux = z0 - (P0[0] * w.x + P0[1] * w.y + P0[2] * w.z);
           const double uy = z1 - (P1[0] * w.x + P1[1] * w.y + P1[2] * w.z);
           *(dbl2v*)&st[NA * kWideLd + slot] = dbl2v{ux, uy};
@@ -738,6 +743,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     if (lane < count) {
       const int64_t i = (int64_t)sg.begin + lane;
       const int32_t pid = obs_pid[i];
+      const double4 w = wbuf[pid];
       const double4 X = obsX ? obsX[i] : pts[pid];
       double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], P0[3], P1[3], r[2], hr;
 #pragma unroll
@@ -758,7 +764,6 @@ __global__ void __launch_bounds__(64) k_pass_b(
           z1 += I1[q] * d[6 + q];
         }
       }
-      const double4 w = wbuf[pid];
       double2 u;
       u.x = z0 - (P0[0] * w.x + P0[1] * w.y + P0[2] * w.z);
       u.y = z1 - (P1[0] * w.x + P1[1] * w.y + P1[2] * w.z);
@@ -949,9 +954,18 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
   if (fz.dz && (int32_t)blockIdx.x >= fz.owner_blocks) {
     const int f = ((int32_t)blockIdx.x - fz.owner_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
     if (f >= fz.nframes) return;
-    auto Z = [&](int64_t e) { return cg_zentry(ent[e], minv, mode, alpha, q, b, r_in); };
-    frame_dir_body(((const FrameLin*)fz.fl)[f], fz.fd[f].K, fz.frec + (int64_t)f * kFrameRecDoubles,
-                   (int)(threadIdx.x & 63), Z, fz.dz + (int64_t)f * kDirStride);
+    const FrameLin& L = ((const FrameLin*)fz.fl)[f];
+    const int32_t K = fz.fd[f].K;
+    // z_j of camera block b straight from the frame's block offsets (the same
+    // entries and block-inverse row the entry threads use, without their
+    // CgEntry descriptor load)
+    auto Z = [&](int blk, int j) {
+      const int nb = blk <= MVBA_BLK_REF_TO_CAM ? 7 : blk == MVBA_BLK_CENTER ? 2 : blk == MVBA_BLK_DIST ? K : 1;
+      return cg_zentry(CgEntry{(int32_t)L.goff[blk], nb, L.hoff[blk] + (int64_t)j * nb}, minv, mode, alpha, q, b,
+                       r_in);
+    };
+    frame_dir_body(L, K, fz.frec + (int64_t)f * kFrameRecDoubles, (int)(threadIdx.x & 63), Z,
+                   fz.dz + (int64_t)f * kDirStride);
     return;
   }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
