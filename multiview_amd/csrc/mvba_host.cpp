@@ -33,7 +33,7 @@ static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
-                  h->d_row_written, h->d_err, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
+                  h->d_row_written, h->d_err, h->d_ready, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
@@ -728,6 +728,11 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_varsize, h->pos_K));
   chk(dalloc(&h->d_err, 1));
   if (e == hipSuccess) chk(hipMemset(h->d_err, 0, sizeof(int)));
+  {
+    const int64_t nw = std::max<int64_t>(mvba_eval_ready_words(h->nframes), 1);
+    chk(dalloc(&h->d_ready, (size_t)nw));
+    if (e == hipSuccess) chk(hipMemset(h->d_ready, 0, (size_t)nw * sizeof(unsigned)));
+  }
   chk(upload(&h->d_chunks, chunks));
   {
     // one-segment chunks: the solver's frame-order pass A takes one segment per
@@ -879,6 +884,26 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
     cauchy_c = 1.0 / (cauchy_threshold * cauchy_threshold);
   }
   hipError_t e = hipSuccess;
+  // One model group with at least two segments per frame: prep and K1 in one
+  // launch (K0 blocks hand their frame records to the K1 waves of the same grid;
+  // c2 101.8 vs 104.5 us, c3 2.16 vs 2.24 ms per step, same box). Thin shards
+  // (about one segment per frame: c2 split 8 ways) keep two launches, where the
+  // fused kernel's K0-sized register file (156 VGPRs, 3 waves per SIMD) costs
+  // more than the boundary it saves (27.9 vs 24.1 us). MVBA_SPLIT_PREP=1 forces
+  // two launches, for A/B timing.
+  static const bool split = std::getenv("MVBA_SPLIT_PREP") && std::getenv("MVBA_SPLIT_PREP")[0] == '1';
+  if (!split && h->groups.size() == 1 && h->groups[0].seg_count >= 2 * h->nframes &&
+      !(flags & (MVBA_EVAL_SKIP_PREP | MVBA_EVAL_PREP_ONLY))) {
+    h->gen++;
+    const Group& G = h->groups[0];
+    e = mvba_launch_eval_fused(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->nframes,
+                               h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts, h->d_obs_pid,
+                               h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen, h->d_err,
+                               h->d_ready, s);
+    h->prep_done = true;
+    if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
+    return MVBA_OK;
+  }
   if (!(flags & MVBA_EVAL_SKIP_PREP)) {
     // The error word is never reset: K0 raises it to this evaluation's
     // generation (atomicMax), so a stale error from an earlier call is ignored.

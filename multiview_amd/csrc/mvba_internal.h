@@ -53,6 +53,13 @@ hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg
                            const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
                            void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
                            hipStream_t s);
+int64_t mvba_eval_ready_words(int64_t nframes);
+hipError_t mvba_launch_eval_fused(int model, int deg, const Segment* segs, int32_t nseg, const FrameDesc* fd,
+                                  int64_t nframes, double* frec, const double* params, const int64_t* pt_off,
+                                  const uint8_t* pt_free, int64_t npts, double4* pts, const int32_t* obs_pid,
+                                  const double2* obs_meas, void* res, void* J, int64_t ld, int32_t flags,
+                                  double cauchy_c, int32_t out_f32, int gen, int* err, unsigned* ready,
+                                  hipStream_t s);
 }
 
 extern "C" {
@@ -276,6 +283,7 @@ struct mvba_handle {
   int64_t* d_order = nullptr;
   uint8_t* d_row_written = nullptr;
   int* d_err = nullptr;
+  unsigned* d_ready = nullptr;  // fused evaluation: per-K0-block ready words (zeroed at creation)
   double* d_res = nullptr;  // library-owned outputs, allocated lazily
   double* d_J = nullptr;
   int64_t ld = 0;

@@ -34,7 +34,25 @@ constexpr int kPrepBlock = 256;
 #endif
 constexpr int kPrepPoints = MVBA_PREP_POINTS;  // landmarks gathered per thread
 
-__device__ void frame_columns(const FrameDesc& F, const double* __restrict__ params, double* rec,
+// WT: every store of the record write-through (agent-scope relaxed atomic
+// store, `global_store ... sc1`): the fused evaluation hands the record to K1
+// waves of the same launch (k_eval; MI355X_MICROARCH.md visibility, valid forms).
+template <bool WT>
+__device__ __forceinline__ void wr(double* p, double v) {
+  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool WT>
+__device__ __forceinline__ void put_col_wt(double* rec, int k, const double* om, const double* dt, const double* t) {
+  double c[3];
+  cross(om, t, c);
+  double* o = rec + 12 + 6 * k;
+  wr<WT>(o + 0, om[0]); wr<WT>(o + 1, om[1]); wr<WT>(o + 2, om[2]);
+  wr<WT>(o + 3, dt[0] - c[0]); wr<WT>(o + 4, dt[1] - c[1]); wr<WT>(o + 5, dt[2] - c[2]);
+}
+
+template <bool WT>
+__device__ __forceinline__ void frame_columns(const FrameDesc& F, const double* __restrict__ params, double* rec,
                               int sub, int gen, int* err) {
   const double* p0 = params + F.off[MVBA_BLK_BEG];
   double R0[9], qh0[4], in0;
@@ -44,8 +62,8 @@ __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ par
   if (F.sb == F.se) {
     // rig_calibrator.cc:371-374 — reference camera or --no_rig: T = rigid(p0).
     if (sub == 0) {
-      for (int k = 0; k < 9; k++) rec[k] = R0[k];
-      rec[9] = t0[0]; rec[10] = t0[1]; rec[11] = t0[2];
+      for (int k = 0; k < 9; k++) wr<WT>(rec + k, R0[k]);
+      wr<WT>(rec + 9, t0[0]); wr<WT>(rec + 10, t0[1]); wr<WT>(rec + 11, t0[2]);
     }
     for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
       double om[3] = {0.0, 0.0, 0.0};
@@ -56,7 +74,7 @@ __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ par
       } else if (k < 7) {
         quat_generator(qh0, 2.0 * in0, k - 3, om);
       }
-      put_col(rec, k, om, dt, t0);
+      put_col_wt<WT>(rec, k, om, dt, t0);
     }
     return;
   }
@@ -123,8 +141,8 @@ __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ par
     tw[r] = R2[3 * r + 0] * ti[0] + R2[3 * r + 1] * ti[1] + R2[3 * r + 2] * ti[2] + t2[r];
   }
   if (sub == 0) {
-    for (int k = 0; k < 9; k++) rec[k] = Rw[k];
-    rec[9] = tw[0]; rec[10] = tw[1]; rec[11] = tw[2];
+    for (int k = 0; k < 9; k++) wr<WT>(rec + k, Rw[k]);
+    wr<WT>(rec + 9, tw[0]); wr<WT>(rec + 10, tw[1]); wr<WT>(rec + 11, tw[2]);
   }
 
   for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
@@ -185,7 +203,7 @@ __device__ void frame_columns(const FrameDesc& F, const double* __restrict__ par
       const double dti[3] = {(t1[0] - t0[0]) * da, (t1[1] - t0[1]) * da, (t1[2] - t0[2]) * da};
       matvec(R2, dti, dt);
     }
-    put_col(rec, k, om, dt, tw);
+    put_col_wt<WT>(rec, k, om, dt, tw);
   }
 }
 
@@ -200,7 +218,7 @@ __global__ void __launch_bounds__(kPrepBlock) k_prep(const FrameDesc* __restrict
     const int64_t f = t / kThreadsPerFrame;
     if (f >= nframes) return;
     const FrameDesc F = fd[f];
-    frame_columns(F, params, frec + f * kFrameRecDoubles, (int)(t % kThreadsPerFrame), gen, err);
+    frame_columns<false>(F, params, frec + f * kFrameRecDoubles, (int)(t % kThreadsPerFrame), gen, err);
   } else {
     // kPrepPoints landmarks per thread, all loads in flight before the stores
     const int64_t p0 = (int64_t)(bid - frame_blocks) * kPrepBlock * kPrepPoints + threadIdx.x;
@@ -236,14 +254,24 @@ __device__ __forceinline__ void stj(OT* J, int64_t ld, int row, int64_t i, doubl
   __builtin_nontemporal_store((OT)v, J + (int64_t)row * ld + i);
 }
 
-template <int MODEL, int DEG, class OT, bool JAC>
+// The fused evaluation's hand-off from its K0 blocks to its K1 waves.
+struct FusedIn {
+  const int64_t* pt_off;   // landmark offsets in the parameter vector
+  const uint8_t* pt_free;  // landmark floats
+  const unsigned* ready;   // one word per K0 block: = epoch once its 16 frame records are stored
+  unsigned epoch;
+  int64_t k1_block0;       // first K1 block of the grid (a multiple of 8: XCD order kept)
+};
+
+template <int MODEL, int DEG, class OT, bool JAC, bool FUSED = false>
 __device__ __forceinline__ void obs_body(
     const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
     const double* __restrict__ frec, const double* __restrict__ params,
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
     const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
-    int64_t ld, int32_t flags, double cauchy_c) {
-  const int64_t blk = xcd_block((nseg + 3) / 4);  // 4 segments per block, XCD-contiguous
+    int64_t ld, int32_t flags, double cauchy_c, const FusedIn& fu = FusedIn{}) {
+  // 4 segments per block, XCD-contiguous
+  const int64_t blk = xcd_block_of((int64_t)blockIdx.x - (FUSED ? fu.k1_block0 : 0), (nseg + 3) / 4);
   if (blk < 0) return;
   const int wave = (int)((blk * blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
@@ -259,12 +287,12 @@ __device__ __forceinline__ void obs_body(
   // partly written line costs HBM a read-modify-write: 110 -> 98 us at c2).
   // No reader looks at padding slots.
   constexpr int kLine = 128 / (int)sizeof(OT);
-  if (lane >= ((count + kLine - 1) & ~(kLine - 1))) return;
+  const bool active = lane < ((count + kLine - 1) & ~(kLine - 1));
+  if (!FUSED && !active) return;
   const int64_t i = (int64_t)begin + lane;
   const int64_t isrc = (int64_t)begin + min(lane, count - 1);
 
   const FrameDesc& F = fd[frame];
-  const double* __restrict__ rec = frec + (int64_t)frame * kFrameRecDoubles;
   const double f = params[F.off[MVBA_BLK_FOCAL]];
   const double c0 = params[F.off[MVBA_BLK_CENTER]];
   const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
@@ -272,7 +300,39 @@ __device__ __forceinline__ void obs_body(
   const int free_mask = F.free_mask;
   const int K = F.K;
 
-  const double4 P = pts[obs_pid[isrc]];
+  double4 P;
+  const double* rec;
+  if constexpr (FUSED) {
+    // landmark straight from the parameter vector (this launch's gather blocks
+    // fill pts for later launches only), issued before the wait
+    const int32_t pid = obs_pid[isrc];
+    const int64_t po = fu.pt_off[pid];
+    P = make_double4(params[po], params[po + 1], params[po + 2], fu.pt_free[pid] ? 1.0 : 0.0);
+    // Wait for the frame's K0 block, then read its record: one lane polls the
+    // ready word (relaxed agent load, sc1), every record load is an sc1 load to
+    // registers (the record was stored write-through), staged in this wave's
+    // LDS area (MI355X_MICROARCH.md, visibility: valid forms, first row).
+    __shared__ double srec[4][kFrameRecDoubles];
+    double* sr = srec[threadIdx.x >> 6];
+    if (lane == 0) {
+      const unsigned* w = fu.ready + (frame >> 4);  // 16 frames per K0 block
+      for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != fu.epoch; n++) {
+        if (n > (1u << 24)) break;  // bounded (~0.5 s): never reached with K0 blocks dispatched first
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the record loads below the poll
+    const double* g = frec + (int64_t)frame * kFrameRecDoubles;
+    for (int m = lane; m < kFrameRecDoubles; m += 64)
+      sr[m] = __hip_atomic_load(const_cast<double*>(g + m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (!active) return;
+    rec = sr;
+  } else {
+    P = pts[obs_pid[isrc]];
+    rec = frec + (int64_t)frame * kFrameRecDoubles;
+  }
   const double2 meas = obs_meas[isrc];
   Proj o;
   project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, kd, K, F.h0, F.h1, o);
@@ -376,6 +436,45 @@ __global__ void __launch_bounds__(256) k_obs_res(
     const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
     int64_t ld, int32_t flags, double cauchy_c) {
   obs_body<MODEL, DEG, OT, false>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld, flags, cauchy_c);
+}
+
+// Fused evaluation (one model group): prep and K1 in one launch. Blocks
+// [0, fb) run K0 for 16 frames each, storing the records write-through, and
+// publish ready[block] = epoch behind every storing wave's vmcnt(0) wait and a
+// block barrier; blocks [fb, fb + pb) gather the landmarks into pts (for later
+// launches: the solver, SKIP_PREP evaluations); blocks from fu.k1_block0 run K1,
+// whose waves issue their landmark loads, then wait for their frame's ready
+// word. K0 blocks never wait and precede every K1 block in dispatch order, so
+// every wait ends; the frame arithmetic overlaps the K1 waves' loads instead of
+// a kernel boundary.
+template <int MODEL, int DEG, class OT, bool JAC>
+__global__ void __launch_bounds__(256) k_eval(
+    const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd, int64_t nframes,
+    int32_t fb, int32_t pb, double* __restrict__ frec, const double* __restrict__ params, int64_t npts,
+    double4* __restrict__ pts, const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
+    OT* __restrict__ res, OT* __restrict__ J, int64_t ld, int32_t flags, double cauchy_c, int gen,
+    int* __restrict__ err, unsigned* __restrict__ ready, FusedIn fu) {
+  const int bid = (int)blockIdx.x;
+  if (bid < fb) {
+    const int64_t t = (int64_t)bid * kPrepBlock + threadIdx.x;
+    const int64_t f = t / kThreadsPerFrame;
+    if (f < nframes) frame_columns<true>(fd[f], params, frec + f * kFrameRecDoubles, (int)(t % kThreadsPerFrame),
+                                         gen, err);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(ready + bid, fu.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if ((int64_t)bid < fu.k1_block0) {
+    const int64_t p = (int64_t)(bid - fb) * kPrepBlock + threadIdx.x;
+    if (bid - fb < pb && p < npts) {
+      const int64_t o = fu.pt_off[p];
+      pts[p] = make_double4(params[o], params[o + 1], params[o + 2], fu.pt_free[p] ? 1.0 : 0.0);
+    }
+    return;
+  }
+  obs_body<MODEL, DEG, OT, JAC, true>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld, flags,
+                                      cauchy_c, fu);
 }
 
 // k_frame_lin: one block per frame part (<= kPartSegs segments of ONE frame),
@@ -913,6 +1012,44 @@ hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_
   MVBA_SWITCH_MODEL(model, deg, MVBA_OBS)
 #undef MVBA_OBS
 #undef MVBA_OBS_K
+  return hipGetLastError();
+}
+
+// Prep + K1 in one launch (k_eval): K0 blocks, landmark-gather blocks (one
+// landmark per thread), then the K1 blocks from a multiple of 8 on. ready:
+// >= mvba_eval_ready_words(nframes) words, zero before the first launch; epoch:
+// a value no earlier launch on these words used (the handle's generation).
+int64_t mvba_eval_ready_words(int64_t nframes) {
+  return (nframes * mvba::kThreadsPerFrame + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
+}
+
+hipError_t mvba_launch_eval_fused(int model, int deg, const mvba::Segment* segs, int32_t nseg,
+                                  const mvba::FrameDesc* fd, int64_t nframes, double* frec, const double* params,
+                                  const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts,
+                                  const int32_t* obs_pid, const double2* obs_meas, void* res, void* J, int64_t ld,
+                                  int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err,
+                                  unsigned* ready, hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
+  const int64_t fb = mvba_eval_ready_words(nframes);
+  const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
+  const int64_t k1 = (fb + pb + mvba::kXcds - 1) / mvba::kXcds * mvba::kXcds;
+  const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((nseg + 3) / 4));
+  const mvba::FusedIn fu{pt_off, pt_free, ready, (unsigned)gen, k1};
+#define MVBA_EVF_K(M, D, OT, JC)                                                                              \
+  hipLaunchKernelGGL((mvba::k_eval<M, D, OT, JC>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, nframes,      \
+                     (int32_t)fb, (int32_t)pb, frec, params, npts, pts, obs_pid, obs_meas, (OT*)res, (OT*)J, ld, \
+                     flags, cauchy_c, gen, err, ready, fu)
+#define MVBA_EVF(M, D)                                                                                   \
+  if (flags & MVBA_EVAL_JACOBIAN) {                                                                      \
+    if (out_f32) MVBA_EVF_K(M, D, float, true);                                                          \
+    else MVBA_EVF_K(M, D, double, true);                                                                 \
+  } else {                                                                                               \
+    if (out_f32) MVBA_EVF_K(M, D, float, false);                                                         \
+    else MVBA_EVF_K(M, D, double, false);                                                                \
+  }
+  MVBA_SWITCH_MODEL(model, deg, MVBA_EVF)
+#undef MVBA_EVF
+#undef MVBA_EVF_K
   return hipGetLastError();
 }
 
