@@ -538,6 +538,22 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
   const int64_t p = t0 / kLanesW;
   const int sub = (int)(t0 % kLanesW);
   const bool valid = p < npts;
+  // the solving lane's point data (free flag, right-hand side, V, damping)
+  // loaded before the c_o gathers, so the gathers are its only dependent
+  // round trip
+  const bool solver = valid && sub == 0;
+  double Vp[6], dpp[3], ti[3] = {0.0, 0.0, 0.0};
+  double freep = 0.0;
+  if (solver) {
+    freep = pts[p].w;
+#pragma unroll
+    for (int q = 0; q < 6; q++) Vp[q] = V[6 * p + q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) dpp[q] = dp[3 * p + q];
+    if (tinit)
+#pragma unroll
+      for (int q = 0; q < 3; q++) ti[q] = tinit[3 * p + q];
+  }
   double t[3] = {0.0, 0.0, 0.0};
   if (valid && cbuf)
     for (int64_t j = pt_begin[p] + sub; j < pt_begin[p + 1]; j += kLanesW) {
@@ -557,13 +573,13 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
   for (int off = 1; off < kLanesW; off <<= 1)
 #pragma unroll
     for (int q = 0; q < 3; q++) t[q] += __shfl_xor(t[q], off, 64);
-  if (!valid || sub != 0) return;
+  if (!solver) return;
   double w[3] = {0.0, 0.0, 0.0};
-  if (pts[p].w != 0.0) {
+  if (freep != 0.0) {
     if (tinit)
 #pragma unroll
-      for (int q = 0; q < 3; q++) t[q] += tinit[3 * p + q];
-    solve3(V + 6 * p, dp + 3 * p, t, w);
+      for (int q = 0; q < 3; q++) t[q] += ti[q];
+    solve3(Vp, dpp, t, w);
   }
 #pragma unroll
   for (int q = 0; q < 3; q++) wout[wstride * p + q] = w[q];
