@@ -489,6 +489,7 @@ def main():
         t0 = time.perf_counter()
         for k in range(args.steps):
             step()
+        t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -511,14 +512,16 @@ def main():
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-            mine = torch.tensor([1e3 * dt / args.steps, prep_ms, obs_ms, float(n)], dtype=torch.float64,
-                                device="cuda")
+            mine = torch.tensor([1e3 * dt / args.steps, prep_ms, obs_ms, float(n), 1e3 * t_issue / args.steps],
+                                dtype=torch.float64, device="cuda")
             allr = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(allr, mine)
             rows = [r.cpu().tolist() for r in allr]
             per_rank = {"ms_per_step": [r[0] for r in rows], "prep_ms": [r[1] for r in rows],
-                        "kernel_ms": [r[2] for r in rows], "num_residuals": [int(r[3]) for r in rows]}
+                        "kernel_ms": [r[2] for r in rows], "num_residuals": [int(r[3]) for r in rows],
+                        "host_issue_ms_per_step": [r[4] for r in rows]}
         del res, jac
+        time_eval.host_issue_ms = 1e3 * t_issue / args.steps
         return float(t.item()), float(tot.item()) * args.steps, prep_ms, obs_ms, per_rank
 
     ev = Evaluator(P, device=dev)
@@ -572,6 +575,9 @@ def main():
                              "events: they add ~10 us per step)",
         },
         "gen_s": t_gen,
+        # host time to enqueue one step (Python + ctypes + the launches): when it
+        # approaches ms_per_step the step is launch-bound, not GPU-bound
+        "host_issue_ms_per_step": time_eval.host_issue_ms,
     }
     if per_rank is not None:
         line["per_rank"] = per_rank

@@ -33,7 +33,7 @@ static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
-                  h->d_row_written, h->d_err, h->d_ready, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
+                  h->d_row_written, h->d_err, h->d_ready, h->d_lone_frames, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
@@ -733,12 +733,34 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     chk(dalloc(&h->d_ready, (size_t)nw));
     if (e == hipSuccess) chk(hipMemset(h->d_ready, 0, (size_t)nw * sizeof(unsigned)));
   }
-  chk(upload(&h->d_chunks, chunks));
   {
+    // frames without a reprojection segment: k_eval_local's K0 blocks store
+    // their records (the K1 waves store the others)
+    std::vector<uint8_t> has_seg(h->nframes, 0);
+    for (const Segment& sg : segs) has_seg[sg.frame] = 1;
+    std::vector<int32_t> lone;
+    for (int64_t f = 0; f < h->nframes; f++)
+      if (!has_seg[f]) lone.push_back((int32_t)f);
+    h->nlone = (int32_t)lone.size();
+    chk(upload(&h->d_lone_frames, lone));
+  }
+  {
+    // The CG passes' chunk records carry the slot range directly: (first slot,
+    // observations, frame, first chunk of the frame). A chunk's segments are
+    // consecutive 64-slot runs of one frame, so the passes load no Segment.
+    auto direct = [&](int32_t sidx, int32_t nseg, bool first) {
+      int32_t n = 0;
+      for (int32_t k = sidx; k < sidx + nseg; k++) n += segs[k].count;
+      return make_int4(segs[sidx].begin, n, segs[sidx].frame, first ? 1 : 0);
+    };
+    std::vector<int4> dc(chunks.size());
+    for (size_t k = 0; k < chunks.size(); k++)
+      dc[k] = direct(chunks[k].x, chunks[k].y, k == 0 || chunks[k - 1].z != chunks[k].z);
+    chk(upload(&h->d_chunks, dc));
     // one-segment chunks: the solver's frame-order pass A takes one segment per
     // wave (it writes per-observation records, nothing per frame to reduce)
     std::vector<int4> sc(segs.size());
-    for (size_t k = 0; k < segs.size(); k++) sc[k] = make_int4((int32_t)k, 1, segs[k].frame, 0);
+    for (size_t k = 0; k < segs.size(); k++) sc[k] = direct((int32_t)k, 1, k == 0 || segs[k - 1].frame != segs[k].frame);
     chk(upload(&h->d_segchunks, sc));
   }
   {
@@ -886,20 +908,33 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
   hipError_t e = hipSuccess;
   // One model group with at least two segments per frame: prep and K1 in one
   // launch (K0 blocks hand their frame records to the K1 waves of the same grid;
-  // c2 101.8 vs 104.5 us, c3 2.16 vs 2.24 ms per step, same box). Thin shards
-  // (about one segment per frame: c2 split 8 ways) keep two launches, where the
-  // fused kernel's K0-sized register file (156 VGPRs, 3 waves per SIMD) costs
-  // more than the boundary it saves (27.9 vs 24.1 us). MVBA_SPLIT_PREP=1 forces
-  // two launches, for A/B timing.
+  // c2 101.8 vs 104.5 us, c3 2.16 vs 2.24 ms per step, same box). For thin
+  // shards (about one segment per frame: c2 split 8 ways) the hand-off measured
+  // slower than two launches (27.9 vs 24.1 us: the fused kernel's K0-sized
+  // register file, 156 VGPRs, 3 waves per SIMD). MVBA_SPLIT_PREP=1 forces two
+  // launches, for A/B timing.
+  // Thinner shards (fewer than two segments per frame) run k_eval_local: every
+  // K1 wave computes its own frame's record in LDS, so neither a prep launch
+  // nor a hand-off sits in front of K1. MVBA_EVAL_MODE=split|fused|local forces
+  // one form, for A/B timing.
   static const bool split = std::getenv("MVBA_SPLIT_PREP") && std::getenv("MVBA_SPLIT_PREP")[0] == '1';
-  if (!split && h->groups.size() == 1 && h->groups[0].seg_count >= 2 * h->nframes &&
-      !(flags & (MVBA_EVAL_SKIP_PREP | MVBA_EVAL_PREP_ONLY))) {
+  static const char* mode_env = std::getenv("MVBA_EVAL_MODE");
+  static const int forced = !mode_env ? -1 : !std::strcmp(mode_env, "split") ? 0
+                            : !std::strcmp(mode_env, "fused") ? 1 : !std::strcmp(mode_env, "local") ? 2 : -1;
+  if (!split && forced != 0 && h->groups.size() == 1 && !(flags & (MVBA_EVAL_SKIP_PREP | MVBA_EVAL_PREP_ONLY))) {
     h->gen++;
     const Group& G = h->groups[0];
-    e = mvba_launch_eval_fused(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->nframes,
-                               h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts, h->d_obs_pid,
-                               h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen, h->d_err,
-                               h->d_ready, s);
+    const bool fused = forced == 1 || (forced < 0 && G.seg_count >= 2 * h->nframes);
+    if (fused)
+      e = mvba_launch_eval_fused(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->nframes,
+                                 h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,
+                                 h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen,
+                                 h->d_err, h->d_ready, s);
+    else
+      e = mvba_launch_eval_local(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_lone_frames, h->nlone,
+                                 h->d_fd, h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,
+                                 h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen,
+                                 h->d_err, s);
     h->prep_done = true;
     if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
     return MVBA_OK;

@@ -460,19 +460,20 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
   const int lane = threadIdx.x & 63;
   const int ch = blockIdx.x * kPassAWaves + (threadIdx.x >> 6);
   if (ch >= nchunks || (gate && *gate)) return;
+  // (first slot, observations, frame, first chunk of the frame): the chunk's
+  // segments are consecutive 64-slot runs of one frame, so no segment loads
   const int4 c = chunks[ch];
   const int frame = __builtin_amdgcn_readfirstlane(c.z);
+  const int nobs = __builtin_amdgcn_readfirstlane(c.y);
   const double* __restrict__ rec = prec + (int64_t)frame * kProjDoubles;
   // the frame's direction (combined from dz and dp inside CG iterations); the
   // wave of the frame's first segment keeps it for the next product
   double* d = sdir[threadIdx.x >> 6];
-  const bool writer = dr.dp_out && (c.x == 0 || segs[c.x - 1].frame != frame);
+  const bool writer = dr.dp_out && c.w;
   stage_dir<ND>(dr, frame, d, writer);
-  for (int sidx = 0; sidx < c.y; sidx++) {
-    const Segment sg = segs[c.x + sidx];
-    const int count = __builtin_amdgcn_readfirstlane(sg.count);
-    if (lane < count) {
-      const int64_t i = (int64_t)sg.begin + lane;
+  for (int s0 = 0; s0 < nobs; s0 += 64) {
+    if (lane < nobs - s0) {
+      const int64_t i = (int64_t)c.x + s0 + lane;
       double z[2], P0[3], P1[3];
       // obsX (K2's per-slot record): landmark + Cauchy weight, no measurement read
       if (obsX)
@@ -620,14 +621,14 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
   const double c0 = params[F.off[MVBA_BLK_CENTER]];
   const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
   double acc0 = 0.0, acc1 = 0.0;  // columns lane, lane + 64
-  for (int sidx = 0; sidx < c.y; sidx++) {
-    const Segment sg = segs[c.x + sidx];
-    const int count = __builtin_amdgcn_readfirstlane(sg.count);
+  const int nobs = __builtin_amdgcn_readfirstlane(c.y);
+  for (int s0 = 0; s0 < nobs; s0 += 64) {
+    const int count = min(64, nobs - s0);
     for (int half = 0; half < 2 && 32 * half < count; half++) {
       if ((lane >> 5) == half) {
         const int slot = 2 * (lane & 31);
         if (lane < count) {
-          const int64_t i = (int64_t)sg.begin + lane;
+          const int64_t i = (int64_t)c.x + s0 + lane;
           const int32_t pid = obs_pid[i];
           const double4 w = wbuf[pid];
           const double4 X = obsX ? obsX[i] : pts[pid];
@@ -753,11 +754,10 @@ __global__ void __launch_bounds__(64) k_pass_b(
   double acc[NA];
 #pragma unroll
   for (int q = 0; q < NA; q++) acc[q] = 0.0;
-  for (int sidx = 0; sidx < c.y; sidx++) {
-    const Segment sg = segs[c.x + sidx];
-    const int count = __builtin_amdgcn_readfirstlane(sg.count);
-    if (lane < count) {
-      const int64_t i = (int64_t)sg.begin + lane;
+  const int nobs = __builtin_amdgcn_readfirstlane(c.y);
+  for (int s0 = 0; s0 < nobs; s0 += 64) {
+    if (lane < nobs - s0) {
+      const int64_t i = (int64_t)c.x + s0 + lane;
       const int32_t pid = obs_pid[i];
       const double4 w = wbuf[pid];
       const double4 X = obsX ? obsX[i] : pts[pid];

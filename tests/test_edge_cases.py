@@ -140,33 +140,40 @@ def test_single_observation_points_and_frames():
 
     The inexact Schur-CG steps (ITERATIVE_SCHUR, eta = 0.1) converge slowly
     along the null directions: the CPU LM (exact steps) stops after ~60
-    iterations, the GPU LM keeps making small successful steps for ~160 and
-    then reaches the rounding-noise regime: the trust-region radius has grown to
-    ~1e15 (LM diagonal ~1e-15 after Jacobi scaling), V_p + D of the
-    single-observation points is singular to rounding and the model cost change
-    -(g'd + |J d|^2/2) of the next steps is noise. Ceres 1.14 calls a step with
+    iterations, the GPU LM keeps making small successful steps until iteration
+    ~160 and then reaches the rounding-noise regime: the trust-region radius has
+    grown to ~1e15 (LM diagonal ~1e-15 after Jacobi scaling), V_p + D of the
+    single-observation points is singular to rounding, CG reports an indefinite
+    matrix and the model cost change -(g'd + |J d|^2/2) of the next steps is
+    noise (profiles/r03/edge_trace_r03b.log). Ceres 1.14 calls a step with
     model cost change <= 0 invalid (TrustRegionMinimizer::ComputeTrustRegionStep),
     divides the radius (LevenbergMarquardtStrategy::StepIsInvalid) and stops with
     FAILURE after max_num_consecutive_invalid_steps = 5; noise steps that come
     out "valid" keep the solve going to max_num_iterations (NO_CONVERGENCE).
-    Which of the two ends the solve is decided by rounding, i.e. by the build
-    (the CG passes' FMA contraction and summation order): round 2's build ended
-    with FAILURE, the fused-direction CG of round 3 with NO_CONVERGENCE at 200.
-    Pinned here: every run is at the CPU LM's cost within 1e-6, ends in one of
-    those two noise-regime terminations, and two deterministic solves are
-    bit-identical (termination, iteration counts, cost, parameters).
-    MVBA_SOLVER_TRACE=1 prints the steps (profiles/r03/edge_trace_r03b.log)."""
+    Which of the two ends a solve that enters that regime is decided by
+    rounding, i.e. by the build (the CG passes' FMA contraction and summation
+    order).
+
+    Pinned: (1) with max_num_iterations = 120 (before the noise regime) every
+    run, deterministic or atomic, ends with exactly NO_CONVERGENCE ("Maximum
+    number of iterations") at the CPU LM's cost within 1e-6 -- the LM control
+    flow up to there does not depend on arrival order; (2) run into the noise
+    regime (200 iterations), two deterministic solves are bit-identical
+    (termination, iteration counts, cost, parameters) and still at that cost.
+    MVBA_SOLVER_TRACE=1 prints the steps."""
     from oracle import lm_reference
 
     P = _single_observation_problem()
     TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
     x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
-    runs = [_solve(P, det, 200, **TOL) for det in (1, 1, 0)]
+    for det in (1, 0):
+        s, _ = _solve(P, det, 120, **TOL)
+        assert s["termination_type"] == _lib.NO_CONVERGENCE, (det, s["message"])
+        assert "Maximum number of iterations" in s["message"]
+        assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
+    runs = [_solve(P, 1, 200, **TOL) for _ in range(2)]
     for s, _ in runs:
         assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
-        noise_end = (s["termination_type"] == _lib.FAILURE and "consecutive invalid steps" in s["message"]) or \
-            (s["termination_type"] == _lib.NO_CONVERGENCE and "Maximum number of iterations" in s["message"])
-        assert noise_end, s["message"]
     _same_run(runs[0], runs[1])
 
 
