@@ -913,10 +913,13 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
   // slower than two launches (27.9 vs 24.1 us: the fused kernel's K0-sized
   // register file, 156 VGPRs, 3 waves per SIMD). MVBA_SPLIT_PREP=1 forces two
   // launches, for A/B timing.
-  // Thinner shards (fewer than two segments per frame) run k_eval_local: every
-  // K1 wave computes its own frame's record in LDS, so neither a prep launch
-  // nor a hand-off sits in front of K1. MVBA_EVAL_MODE=split|fused|local forces
-  // one form, for A/B timing.
+  // Fewer than four segments per frame (shards of a landmark split) run
+  // k_eval_local: every K1 wave computes its own frame's record in LDS, so
+  // neither a prep launch nor a hand-off sits in front of K1 (same box, rank 0's
+  // shard of c2: 2-way 56.1-56.5 vs fused 61.2-61.8 us, 8-way 19.1-20.6 vs
+  // split 22.1-23.6 us; whole c2 98.4-101.1 vs fused 100.3-102.0 us;
+  // profiles/r03/ab_eval_local/). MVBA_EVAL_MODE=split|fused|local forces one
+  // form, for A/B timing.
   static const bool split = std::getenv("MVBA_SPLIT_PREP") && std::getenv("MVBA_SPLIT_PREP")[0] == '1';
   static const char* mode_env = std::getenv("MVBA_EVAL_MODE");
   static const int forced = !mode_env ? -1 : !std::strcmp(mode_env, "split") ? 0
@@ -924,7 +927,7 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
   if (!split && forced != 0 && h->groups.size() == 1 && !(flags & (MVBA_EVAL_SKIP_PREP | MVBA_EVAL_PREP_ONLY))) {
     h->gen++;
     const Group& G = h->groups[0];
-    const bool fused = forced == 1 || (forced < 0 && G.seg_count >= 2 * h->nframes);
+    const bool fused = forced == 1 || (forced < 0 && G.seg_count >= 4 * h->nframes);
     if (fused)
       e = mvba_launch_eval_fused(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->nframes,
                                  h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,

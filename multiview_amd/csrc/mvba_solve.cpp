@@ -213,7 +213,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->prec, (size_t)(h->nframes * mvba::kProjDoubles)));
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
     HCHK(dalloc(&S->wbuf, (size_t)(4 * std::max<int64_t>(S->np, 1))));
-    HCHK(dalloc(&S->cbuf, (size_t)(4 * std::max<int64_t>(N, 1))));
+    HCHK(dalloc(&S->cbuf, (size_t)(4 * std::max<int64_t>(std::max<int64_t>(N, h->nslots), 1))));
     HCHK(dalloc(&S->obsX, (size_t)(4 * std::max<int64_t>(h->nslots, 1))));
     HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
     HCHK(dalloc(&S->dcbuf, (size_t)(4 * std::max<int64_t>(h->ndep, 1))));
@@ -413,6 +413,17 @@ class Solver {
 
   static mvba::DirPair plain_dir(const double* dir) { return mvba::DirPair{dir, nullptr, nullptr, nullptr}; }
 
+  // Where pass A leaves c_o: slot order (coalesced stores, k_point_w gathers)
+  // once the point-order table outgrows the caches. Same-box kernel traces
+  // (profiles/r03/ab_co_order/): c2 (1M observations, 32 MB) pass A + k_point_w
+  // 29.8 us point order vs 36.0 slot order; c3 (10M, 320 MB) 395 vs 327 us.
+  // MVBA_CO_ORDER=point|slot forces one.
+  bool co_slot_order(const char* env) const {
+    if (env && !std::strcmp(env, "slot")) return true;
+    if (env && !std::strcmp(env, "point")) return false;
+    return h_->nslots * (int64_t)sizeof(double4) > (int64_t)128 << 20;
+  }
+
   // w_p = (V + D)^-1 (tinit + sum J_pt^T J_cam x) into wbuf (dr: frame
   // directions of x, dr.dz null for x = 0). Depth blocks need the point-lane kernel
   // (it also forms their u_d); otherwise the frame-order sweep + point solve.
@@ -428,20 +439,27 @@ class Solver {
     }
     // one segment per wave (MVBA_PASS_A_CHUNKS=1: the 4-segment solver chunks, for A/B timing)
     static const bool chunked = std::getenv("MVBA_PASS_A_CHUNKS") && std::getenv("MVBA_PASS_A_CHUNKS")[0] == '1';
+    // where pass A leaves c_o = J_pt^T z_o: at the observation's point-order
+    // position (scattered 32-B stores, k_point_w reads its run) or in slot order
+    // (coalesced stores, k_point_w gathers through po_slot). MVBA_CO_ORDER=
+    // point|slot forces one, for A/B timing.
+    static const char* co_env = std::getenv("MVBA_CO_ORDER");
+    const bool co_slot = co_slot_order(co_env);
     if (dir)
       for (const Group& G : h_->groups)
         HCHK(mvba_launch_pass_a_frame(G.model, G.deg,
                                       chunked ? h_->d_chunks + G.chunk_begin : h_->d_segchunks + G.seg_begin,
                                       chunked ? G.chunk_count : G.seg_count, h_->d_segs,
-                                      h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, h_->d_slot_po, dr, (double4*)S_->cbuf,
-                                      flags_, cauchy_c_, gate, S_->prec, obsx(), s_));
+                                      h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, co_slot ? nullptr : h_->d_slot_po, dr,
+                                      (double4*)S_->cbuf, flags_, cauchy_c_, gate, S_->prec, obsx(), s_));
     // depth blocks in frame order (z_d into du, P z_d per block for the point solve)
     const bool dep = dir && h_->ndep > 0;
     if (dep)
       HCHK(mvba_launch_depth_pa(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_pid, h_->d_dep_meas,
                                 h_->d_frec, h_->d_params, h_->d_pts, dir, xv, S_->du, h_->d_dslot_po,
                                 (double4*)S_->dcbuf, flags_, cauchy_c_, gate, s_));
-    HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, h_->d_po_slot, dir ? (const double4*)S_->cbuf : nullptr,
+    HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
+                             dir ? (const double4*)S_->cbuf : nullptr,
                              tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate,
                              dep ? h_->d_dpt_begin : nullptr, dep ? (const double4*)S_->dcbuf : nullptr, s_));
   }
@@ -563,6 +581,8 @@ class Solver {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
                                nullptr, nullptr, s_));
     // |J delta|^2 over the local reprojection and depth blocks -> scal[0]
+    // (point order; a frame-order pass A + k_point_w + |u|^2 sweep measured no
+    // gain at c2 and 17 us per CG iteration slower at c3: profiles/r03/ab_backsub/)
     HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
                             h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
                             S_->dmp + S_->ng, S_->zbuf, S_->delta + S_->ng, 3, S_->partial, S_->cnt + 5,

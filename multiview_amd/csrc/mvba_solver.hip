@@ -481,8 +481,9 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
       else
         pass_a_obs<MODEL, DEG>(rec, d, pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
       // plain store: a nontemporal store of these scattered 32-B records
-      // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM)
-      cbuf[slot_po[i]] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
+      // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM);
+      // slot_po null: stored in slot order (coalesced), k_point_w gathers
+      cbuf[slot_po ? (int64_t)slot_po[i] : i] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
                                       P0[2] * z[0] + P1[2] * z[1], 0.0);
     }
   }
@@ -558,7 +559,8 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
   double t[3] = {0.0, 0.0, 0.0};
   if (valid && cbuf)
     for (int64_t j = pt_begin[p] + sub; j < pt_begin[p + 1]; j += kLanesW) {
-      const double4 cv = cbuf[j];
+      // po_slot set: pass A stored c_o in slot order; gather it
+      const double4 cv = po_slot ? cbuf[po_slot[j]] : cbuf[j];
       t[0] += cv.x;
       t[1] += cv.y;
       t[2] += cv.z;
@@ -1096,7 +1098,12 @@ __global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict
 // are inverted in place in the output by Gauss-Jordan elimination (symmetric
 // positive definite: no pivoting; a vanishing pivot = a direction the block
 // does not see, inverted as identity like the Cholesky path).
-constexpr int kPrecLds = 88;  // 88^2 doubles = 62 KB: within the 64 KB of dynamic LDS a plain launch gets
+constexpr int kPrecLds = 88;  // 88^2 + 2 * 88 doubles = 62 KB: within the 64 KB of dynamic LDS a plain launch gets
+// Blocks wider than this (RPC distortion blocks: 22..88 entries) take the
+// Gauss-Jordan path in LDS: its n steps are 64-lane rank-1 updates, where the
+// Cholesky path's column steps and per-lane triangular solves are serial
+// chains (c3, 44-wide blocks: 262 us per preconditioner build).
+constexpr int kPrecChol = 16;
 
 __device__ void block_inverse_gj(int n, const double* __restrict__ H, const double* __restrict__ db,
                                  double* __restrict__ A, double* colk, double* rowk) {
@@ -1146,6 +1153,13 @@ __global__ void __launch_bounds__(64) k_block_prec(int32_t nblocks, const int64_
   const double* db = d + goff[b];
   if (n > kPrecLds) {
     block_inverse_gj(n, H, db, minv + hoff[b], Ls, Ls + n);
+    return;
+  }
+  if (n > kPrecChol) {
+    block_inverse_gj(n, H, db, Ls, Ls + n * n, Ls + n * n + n);
+    __syncthreads();
+    double* M = minv + hoff[b];
+    for (int e = lane; e < n * n; e += 64) M[e] = Ls[e];
     return;
   }
   for (int e = lane; e < n * n; e += 64) {
@@ -1554,7 +1568,7 @@ hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int6
                                   hipStream_t s) {
   if (nblocks <= 0) return hipSuccess;
   const int m = max_bsize < mvba::kPrecLds ? max_bsize : mvba::kPrecLds;
-  const size_t lds = sizeof(double) * (size_t)(m * m > 2 * max_bsize ? m * m : 2 * max_bsize);
+  const size_t lds = sizeof(double) * (size_t)(m * m + 2 * m > 2 * max_bsize ? m * m + 2 * m : 2 * max_bsize);
   hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(64), lds, s, nblocks, goff, hoff, bsize, hess,
                      d, minv);
   return hipGetLastError();

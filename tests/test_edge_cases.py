@@ -154,22 +154,24 @@ def test_single_observation_points_and_frames():
     rounding, i.e. by the build (the CG passes' FMA contraction and summation
     order).
 
-    Pinned: (1) with max_num_iterations = 120 (before the noise regime) every
-    run, deterministic or atomic, ends with exactly NO_CONVERGENCE ("Maximum
-    number of iterations") at the CPU LM's cost within 1e-6 -- the LM control
-    flow up to there does not depend on arrival order; (2) run into the noise
-    regime (200 iterations), two deterministic solves are bit-identical
-    (termination, iteration counts, cost, parameters) and still at that cost.
-    MVBA_SOLVER_TRACE=1 prints the steps."""
+    Pinned: (1) with function_tolerance = 1e-9 every run, deterministic or
+    atomic, ends with exactly CONVERGENCE ("Function tolerance reached") at the
+    CPU LM's cost within 1e-6: the small successful steps reach a relative cost
+    change below 1e-9 at iteration ~160-180, before the radius has grown into
+    the noise regime (profiles/r03/edge_trace_r03b.log: relative changes
+    2e-10 .. 6e-10 there, 2e-7 .. 1e-7 from the CPU cost); (2) run into the
+    noise regime at the CLI's tolerances (200 iterations), two deterministic
+    solves are bit-identical (termination, iteration counts, cost, parameters)
+    and still at that cost. MVBA_SOLVER_TRACE=1 prints the steps."""
     from oracle import lm_reference
 
     P = _single_observation_problem()
     TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
     x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
     for det in (1, 0):
-        s, _ = _solve(P, det, 120, **TOL)
-        assert s["termination_type"] == _lib.NO_CONVERGENCE, (det, s["message"])
-        assert "Maximum number of iterations" in s["message"]
+        s, _ = _solve(P, det, 400, **dict(TOL, function_tolerance=1e-9))
+        assert s["termination_type"] == _lib.CONVERGENCE, (det, s["message"])
+        assert "Function tolerance reached" in s["message"]
         assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
     runs = [_solve(P, 1, 200, **TOL) for _ in range(2)]
     for s, _ in runs:
