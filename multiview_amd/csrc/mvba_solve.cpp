@@ -69,10 +69,10 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
 hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
                                        const double* val, const double* diag, const double* x, double* y,
                                        double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                       mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s);
+                                       mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s);
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s);
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
                                 unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
                                 const mvba::LazyDir* lz, hipStream_t s);
@@ -80,7 +80,7 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
-                                 int32_t iter, const mvba::FrameDirZ* fz, hipStream_t s);
+                                 int32_t iter, const mvba::FrameDirZ* fz, const double* pq_in, hipStream_t s);
 hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
                              hipStream_t s);
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, unsigned* counter, double* out,
@@ -203,7 +203,9 @@ SolverState* alloc_state(mvba_handle* h) {
     for (double** v : {&S->G, &S->cdiag, &S->sc, &S->dmp, &S->x, &S->xn, &S->delta, &S->scr})
       HCHK(dalloc(v, (size_t)S->nc));
     HCHK(dalloc(&S->fac, (size_t)S->nh));
-    for (double** v : {&S->b, &S->r, &S->r2, &S->z, &S->p, &S->p2, &S->q, &S->tmp}) HCHK(dalloc(v, (size_t)ng1));
+    // q and tmp: one more entry for the exchanged x.y of a sharded solve
+    for (double** v : {&S->b, &S->r, &S->r2, &S->z, &S->p, &S->p2}) HCHK(dalloc(v, (size_t)ng1));
+    for (double** v : {&S->q, &S->tmp}) HCHK(dalloc(v, (size_t)ng1 + 1));
     const size_t nrep = (size_t)mvba_solver_vec_replicas() * (size_t)ng1;
     HCHK(dalloc(&S->yrep, nrep));
     HCHK(hipMemset(S->yrep, 0, nrep * sizeof(double)));
@@ -260,6 +262,12 @@ class Solver {
     flags_ = o.use_loss ? MVBA_EVAL_APPLY_LOSS : 0;
     cauchy_c_ = o.use_loss ? 1.0 / (o.robust_threshold * o.robust_threshold) : 0.0;
     single_model_ = h->groups.size() == 1;
+    // the library's own communicators know this rank (fold mode in
+    // reduce_frames); a caller's callback does not. MVBA_CG_FOLD=0 keeps the
+    // k_add_diag step after the exchange, for A/B timing.
+    static const bool no_fold = std::getenv("MVBA_CG_FOLD") && std::getenv("MVBA_CG_FOLD")[0] == '0';
+    if (o.allreduce == &mvba_comm_allreduce && !no_fold)
+      exch_rank_ = mvba_comm_rank((const mvba_comm*)o.allreduce_user);
   }
 
   void run(mvba_solver_summary* sum);
@@ -276,6 +284,7 @@ class Solver {
   bool single_model_;
   bool bounded_ = false;
   int last_cg_iters_ = 0;  // CG iterations of the previous linear solve (batch sizing only)
+  int32_t exch_rank_ = -1;  // this rank, when the exchange is a library communicator
 
   int pa_model() const { return single_model_ ? h_->groups[0].model : -1; }
   // per-slot landmark copy for the frame-order passes (MVBA_NO_OBSX=1: gather
@@ -395,21 +404,31 @@ class Solver {
                                 gate, det ? D.slab(h_->nchunks) : no_slab(),
                                 dir ? (const double4*)S_->wbuf : nullptr, s_));  // dir: du holds z_d (k_depth_pa)
     if (det && !D.ready) HCHK(det_plan_finish(D, s_));
+    // fuse (single rank): damping, x.y and the step length in the reduction.
+    // fold (sharded, library communicator: the rank is known): rank 0 adds the
+    // damping D x to its share, every rank appends its share of x.y to y, the
+    // exchange sums both, and the update kernel takes the step length from the
+    // summed dot (pq_of). Otherwise (a caller's own all-reduce) the damping and
+    // the dot follow the exchange in k_add_diag.
     const bool fuse = xv && !o_.allreduce;
+    const bool fold = xv && o_.allreduce && exch_rank_ >= 0;
+    const bool any = fuse || fold;
+    const double* dg = (fuse || (fold && exch_rank_ == 0)) ? S_->dmp : nullptr;
+    double* dot_out = fuse ? S_->scal + dot_slot : fold ? y + S_->ng : nullptr;
     if (det)
-      HCHK(mvba_launch_slab_reduce_vec(D.tier_view(), D.grid(), D.begin, D.pos, D.val,
-                                       fuse ? S_->dmp : nullptr, fuse ? xv : nullptr,
-                                       y, S_->partial, S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate,
-                                       fuse ? ctl : nullptr, fuse ? lz : nullptr, s_));
+      HCHK(mvba_launch_slab_reduce_vec(D.tier_view(), D.grid(), D.begin, D.pos, D.val, dg, any ? xv : nullptr, y,
+                                       S_->partial, S_->cnt + 4, dot_out, gate, any ? ctl : nullptr,
+                                       any ? lz : nullptr, fold ? 1 : 0, s_));
     else
-      HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, fuse ? S_->dmp : nullptr, fuse ? xv : nullptr, y,
-                                      S_->partial, S_->cnt + 4, fuse ? S_->scal + dot_slot : nullptr, gate,
-                                      fuse ? ctl : nullptr, fuse ? lz : nullptr, s_));
-    exchange(y, S_->ng, MVBA_REDUCE_SUM);
-    if (xv && !fuse)
+      HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, dg, any ? xv : nullptr, y, S_->partial, S_->cnt + 4, dot_out,
+                                      gate, any ? ctl : nullptr, any ? lz : nullptr, fold ? 1 : 0, s_));
+    exchange(y, S_->ng + (fold ? 1 : 0), MVBA_REDUCE_SUM);
+    if (xv && !any)
       HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, gate, ctl,
                                 lz, s_));
   }
+  // the exchanged p.q behind a product vector q (fold mode), else null
+  const double* pq_of(const double* q) const { return (o_.allreduce && exch_rank_ >= 0) ? q + S_->ng : nullptr; }
 
   static mvba::DirPair plain_dir(const double* dir) { return mvba::DirPair{dir, nullptr, nullptr, nullptr}; }
 
@@ -536,7 +555,8 @@ class Solver {
     auto upd = [&](int32_t mode, const double* q, int32_t iter, bool end_logic) {
       HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, 0.0, S_->p, q, S_->b, xv,
                                  S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl,
-                                 end_logic ? iter : -1, fused_dir ? &fz : nullptr, s_));
+                                 end_logic ? iter : -1, fused_dir ? &fz : nullptr,
+                                 (mode & 1) && q ? pq_of(q) : nullptr, s_));
       std::swap(S_->r, S_->r2);
     };
     upd(4 | 8, nullptr, 0, true);  // r = b, z = M^-1 r, rho

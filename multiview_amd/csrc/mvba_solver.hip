@@ -846,6 +846,17 @@ __device__ __forceinline__ void cg_step_length(CgCtl* ctl, double pq) {
   }
 }
 
+// The finalising block of the x.y reduction. local_dot (sharded solves with a
+// library communicator): the dot is this rank's share, summed by the exchange
+// that follows; the step length is taken by the update kernel from the summed
+// dot and rho_step, the rho snapshot taken here (the update kernel's own
+// finalisation overwrites rho for the next iteration while its frame blocks
+// may still be reading it).
+__device__ __forceinline__ void cg_step_finish(CgCtl* ctl, double pq, int32_t local_dot) {
+  if (local_dot) ctl->rho_step = ctl->rho;
+  else cg_step_length(ctl, pq);
+}
+
 // With lz.z set, x is the CG direction p_new = z (+ beta p_old): formed here
 // (first / beta from lz.ctl) and stored to lz.p_new for the update kernel.
 __device__ __forceinline__ double x_entry(const double* __restrict__ x, const LazyDir& lz, int64_t e) {
@@ -860,7 +871,7 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
                                                         const double* __restrict__ x, double* __restrict__ y,
                                                         double* __restrict__ partial, unsigned* __restrict__ counter,
                                                         double* __restrict__ dot_out, const int32_t* __restrict__ gate,
-                                                        CgCtl* __restrict__ ctl, LazyDir lz) {
+                                                        CgCtl* __restrict__ ctl, LazyDir lz, int32_t local_dot) {
   if (gate && *gate) return;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double d = 0.0;
@@ -881,7 +892,7 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
     d = xe * acc;
   }
   if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
-    cg_step_length(ctl, dot_out[0]);
+    cg_step_finish(ctl, dot_out[0], local_dot);
 }
 
 // Deterministic mode: y[e] = sum of entry e's slab positions in slab order (CSR
@@ -895,7 +906,7 @@ __global__ void __launch_bounds__(256) k_vec_slab_reduce(SlabTiers tiers, const 
                                                          double* __restrict__ partial, unsigned* __restrict__ counter,
                                                          double* __restrict__ dot_out,
                                                          const int32_t* __restrict__ gate, CgCtl* __restrict__ ctl,
-                                                         LazyDir lz) {
+                                                         LazyDir lz, int32_t local_dot) {
   if (gate && *gate) return;
   int64_t e;
   double acc;
@@ -907,7 +918,7 @@ __global__ void __launch_bounds__(256) k_vec_slab_reduce(SlabTiers tiers, const 
     d = xe * acc;
   }
   if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
-    cg_step_length(ctl, dot_out[0]);
+    cg_step_finish(ctl, dot_out[0], local_dot);
 }
 
 // y += diag .* x; dot_out = x.y (after a cross-rank sum of y); with ctl the
@@ -964,10 +975,30 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
                                                    double* __restrict__ r_out, double* __restrict__ z,
                                                    double* __restrict__ partial, unsigned* __restrict__ counters,
                                                    double* __restrict__ out, CgCtl* __restrict__ ctl, int32_t iter,
-                                                   FrameDirZ fz) {
+                                                   FrameDirZ fz, const double* __restrict__ pq_in) {
   if (ctl) {
     if (ctl->done) return;
-    alpha = ctl->alpha;
+    if (pq_in) {
+      // sharded solve: the step length from the exchanged p.q (every block
+      // computes the same value from the same inputs; block 0 records it)
+      const double pq = *pq_in;
+      const double a = ctl->rho_step / pq;
+      const bool indefinite = pq <= 0.0 || isinf(pq) || isnan(pq);
+      const bool bad = indefinite || isinf(a);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->first = 0;
+        if (bad) {
+          ctl->status = indefinite ? 1 : 2;
+          ctl->done = 1;
+        } else {
+          ctl->alpha = a;
+        }
+      }
+      if (bad) return;
+      alpha = a;
+    } else {
+      alpha = ctl->alpha;
+    }
   }
   if (fz.dz && (int32_t)blockIdx.x >= fz.owner_blocks) {
     const int f = ((int32_t)blockIdx.x - fz.owner_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
@@ -1495,21 +1526,21 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
 hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
                                        const double* val, const double* diag, const double* x, double* y,
                                        double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                       mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s) {
+                                       mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
   const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
   hipLaunchKernelGGL(mvba::k_vec_slab_reduce, dim3((unsigned)grid), dim3(256), 0, s, t, begin, pos, val, diag, x, y,
-                     partial, counter, dot_out, gate, ctl, l);
+                     partial, counter, dot_out, gate, ctl, l, local_dot);
   return hipGetLastError();
 }
 
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, hipStream_t s) {
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s) {
   if (ng <= 0) return hipSuccess;
   const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
   hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, diag, x,
-                     y, partial, counter, dot_out, gate, ctl, l);
+                     y, partial, counter, dot_out, gate, ctl, l, local_dot);
   return hipGetLastError();
 }
 
@@ -1528,7 +1559,7 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
-                                 int32_t iter, const mvba::FrameDirZ* fz, hipStream_t s) {
+                                 int32_t iter, const mvba::FrameDirZ* fz, const double* pq_in, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   mvba::FrameDirZ f{};
@@ -1539,7 +1570,7 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
     fblocks = (unsigned)((fz->nframes + 3) / 4);  // 4 frame waves per 256-thread block
   }
   hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks + fblocks), dim3(256), 0, s, n, ent, minv, mode, alpha,
-                     p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter, f);
+                     p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter, f, pq_in);
   return hipGetLastError();
 }
 

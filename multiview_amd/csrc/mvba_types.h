@@ -156,6 +156,7 @@ struct CgCtl {
   double eta;
   int32_t min_iter;
   int32_t max_iter;
+  double rho_step;  // sharded solves: rho of the current step, snapshot by the replica reduction
 };
 
 // Camera-side entry of the reduced system as the CG update reads it: its
