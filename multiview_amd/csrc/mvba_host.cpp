@@ -33,7 +33,7 @@ static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
-                  h->d_row_written, h->d_err, h->d_ready, h->d_lone_frames, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
+                  h->d_row_written, h->d_err, h->d_ready, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
                   h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
@@ -734,17 +734,6 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     if (e == hipSuccess) chk(hipMemset(h->d_ready, 0, (size_t)nw * sizeof(unsigned)));
   }
   {
-    // frames without a reprojection segment: k_eval_local's K0 blocks store
-    // their records (the K1 waves store the others)
-    std::vector<uint8_t> has_seg(h->nframes, 0);
-    for (const Segment& sg : segs) has_seg[sg.frame] = 1;
-    std::vector<int32_t> lone;
-    for (int64_t f = 0; f < h->nframes; f++)
-      if (!has_seg[f]) lone.push_back((int32_t)f);
-    h->nlone = (int32_t)lone.size();
-    chk(upload(&h->d_lone_frames, lone));
-  }
-  {
     // The CG passes' chunk records carry the slot range directly: (first slot,
     // observations, frame, first chunk of the frame). A chunk's segments are
     // consecutive 64-slot runs of one frame, so the passes load no Segment.
@@ -934,10 +923,9 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
                                  h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen,
                                  h->d_err, h->d_ready, s);
     else
-      e = mvba_launch_eval_local(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_lone_frames, h->nlone,
-                                 h->d_fd, h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,
-                                 h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen,
-                                 h->d_err, s);
+      e = mvba_launch_eval_local(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->d_frec,
+                                 h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts, h->d_obs_pid,
+                                 h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen, h->d_err, s);
     h->prep_done = true;
     if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
     return MVBA_OK;

@@ -60,11 +60,11 @@ hipError_t mvba_launch_eval_fused(int model, int deg, const Segment* segs, int32
                                   const double2* obs_meas, void* res, void* J, int64_t ld, int32_t flags,
                                   double cauchy_c, int32_t out_f32, int gen, int* err, unsigned* ready,
                                   hipStream_t s);
-hipError_t mvba_launch_eval_local(int model, int deg, const Segment* segs, int32_t nseg, const int32_t* lone_frames,
-                                  int32_t nlone, const FrameDesc* fd, double* frec, const double* params,
-                                  const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts,
-                                  const int32_t* obs_pid, const double2* obs_meas, void* res, void* J, int64_t ld,
-                                  int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err, hipStream_t s);
+hipError_t mvba_launch_eval_local(int model, int deg, const Segment* segs, int32_t nseg, const FrameDesc* fd,
+                                  double* frec, const double* params, const int64_t* pt_off, const uint8_t* pt_free,
+                                  int64_t npts, double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                                  void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
+                                  int gen, int* err, hipStream_t s);
 }
 
 extern "C" {
@@ -289,8 +289,6 @@ struct mvba_handle {
   uint8_t* d_row_written = nullptr;
   int* d_err = nullptr;
   unsigned* d_ready = nullptr;  // fused evaluation: per-K0-block ready words (zeroed at creation)
-  int32_t* d_lone_frames = nullptr;  // frames without a reprojection segment (k_eval_local's K0 blocks)
-  int32_t nlone = 0;
   double* d_res = nullptr;  // library-owned outputs, allocated lazily
   double* d_J = nullptr;
   int64_t ld = 0;

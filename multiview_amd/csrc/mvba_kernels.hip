@@ -342,6 +342,8 @@ __device__ __forceinline__ void obs_body(
     // into the wave's LDS area; then the landmark straight from the parameter
     // vector (no prep launch; loaded after K0 so the two register sets are
     // never live together: 3 waves per SIMD without spills)
+    // (loading the landmark's offset and free flag before K0 measured no gain:
+    // 20.0 vs 18.4-20.6 us on the 8-way shard, profiles/r03/ab_eval_local/)
     __shared__ double srec[4][kFrameRecDoubles];
     double* sr = srec[threadIdx.x >> 6];
     if (lane < kThreadsPerFrame) frame_columns<false>(F, params, sr, lane, (int)fu.epoch, fu.err);
@@ -353,8 +355,8 @@ __device__ __forceinline__ void obs_body(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     rec = sr;
     // the wave of the frame's first segment stores the record for later
-    // launches (solver, SKIP_PREP evaluations); frames without a segment get
-    // theirs from the K0 blocks of the launch
+    // launches (solver, SKIP_PREP evaluations): in a one-group problem every
+    // frame has a segment (frames are the reprojection residuals' images)
     if (wave == 0 || segs[wave - 1].frame != frame) {
       double* g = const_cast<double*>(frec) + (int64_t)frame * kFrameRecDoubles;  // k_eval_local owns frec
       for (int m = lane; m < kFrameRecDoubles; m += 64) g[m] = sr[m];
@@ -508,40 +510,28 @@ __global__ void __launch_bounds__(256) k_eval(
 }
 
 // Thin-shard evaluation in one launch (k_eval_local): landmark-gather blocks
-// (for later launches: the solver, SKIP_PREP evaluations) and K0 blocks for the
-// frames without a segment (their records, for the same later launches) come
-// first, rounded up to a multiple of 8 blocks; then the K1 blocks, whose waves
-// run K0 for their own frame into LDS (no hand-off, no wait) and store the
-// record from the frame's first segment. Used when a frame has about one
-// segment, so the per-wave K0 is not repeated: the prep launch and its
-// boundary disappear. 3 waves per SIMD (the K0 arithmetic's register file).
+// (for later launches: the solver, SKIP_PREP evaluations) come first, rounded
+// up to a multiple of 8 blocks; then the K1 blocks, whose waves run K0 for
+// their own frame into LDS (no hand-off, no wait) and store the record from the
+// frame's first segment. Used when a frame has about one segment, so the
+// per-wave K0 is not repeated: the prep launch and its boundary disappear.
+// 3 waves per SIMD (the K0 arithmetic's register file).
 template <int MODEL, int DEG, class OT, bool JAC>
 __global__ void __launch_bounds__(256, 3) k_eval_local(
-    const Segment* __restrict__ segs, int32_t nseg, const int32_t* __restrict__ lone_frames, int32_t nlone,
-    int32_t fb, int32_t pb, const FrameDesc* __restrict__ fd, double* __restrict__ frec,
-    const double* __restrict__ params, int64_t npts, double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
-    const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J, int64_t ld, int32_t flags,
-    double cauchy_c, FusedIn fu) {
+    const Segment* __restrict__ segs, int32_t nseg, int32_t pb, const FrameDesc* __restrict__ fd,
+    double* __restrict__ frec, const double* __restrict__ params, int64_t npts, double4* __restrict__ pts,
+    const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas, OT* __restrict__ res,
+    OT* __restrict__ J, int64_t ld, int32_t flags, double cauchy_c, FusedIn fu) {
   const int bid = (int)blockIdx.x;
   if ((int64_t)bid >= fu.k1_block0) {
     obs_body<MODEL, DEG, OT, JAC, kRecLocal>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld,
                                              flags, cauchy_c, fu);
     return;
   }
-  if (bid < pb) {
-    const int64_t p = (int64_t)bid * kPrepBlock + threadIdx.x;
-    if (p < npts) {
-      const int64_t o = fu.pt_off[p];
-      pts[p] = make_double4(params[o], params[o + 1], params[o + 2], fu.pt_free[p] ? 1.0 : 0.0);
-    }
-    return;
-  }
-  const int64_t t = (int64_t)(bid - pb) * kPrepBlock + threadIdx.x;
-  const int64_t k = t / kThreadsPerFrame;
-  if (bid - pb < fb && k < nlone) {
-    const int32_t f = lone_frames[k];
-    frame_columns<false>(fd[f], params, frec + (int64_t)f * kFrameRecDoubles, (int)(t % kThreadsPerFrame),
-                         (int)fu.epoch, fu.err);
+  const int64_t p = (int64_t)bid * kPrepBlock + threadIdx.x;
+  if (bid < pb && p < npts) {
+    const int64_t o = fu.pt_off[p];
+    pts[p] = make_double4(params[o], params[o + 1], params[o + 2], fu.pt_free[p] ? 1.0 : 0.0);
   }
 }
 
@@ -1122,24 +1112,22 @@ hipError_t mvba_launch_eval_fused(int model, int deg, const mvba::Segment* segs,
 }
 
 // Thin-shard evaluation in one launch (k_eval_local): landmark-gather blocks,
-// K0 blocks for the nlone frames without a segment (lone_frames), then the K1
-// blocks from a multiple of 8 on, whose waves run K0 for their own frame.
+// then the K1 blocks from a multiple of 8 on, whose waves run K0 for their own
+// frame. One model group only (every frame has a segment).
 hipError_t mvba_launch_eval_local(int model, int deg, const mvba::Segment* segs, int32_t nseg,
-                                  const int32_t* lone_frames, int32_t nlone, const mvba::FrameDesc* fd,
-                                  double* frec, const double* params, const int64_t* pt_off, const uint8_t* pt_free,
-                                  int64_t npts, double4* pts, const int32_t* obs_pid, const double2* obs_meas,
-                                  void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
-                                  int gen, int* err, hipStream_t s) {
+                                  const mvba::FrameDesc* fd, double* frec, const double* params,
+                                  const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts,
+                                  const int32_t* obs_pid, const double2* obs_meas, void* res, void* J, int64_t ld,
+                                  int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err,
+                                  hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
-  const int64_t fb = ((int64_t)nlone * mvba::kThreadsPerFrame + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
-  const int64_t k1 = (pb + fb + mvba::kXcds - 1) / mvba::kXcds * mvba::kXcds;
+  const int64_t k1 = (pb + mvba::kXcds - 1) / mvba::kXcds * mvba::kXcds;
   const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((nseg + 3) / 4));
   const mvba::FusedIn fu{pt_off, pt_free, nullptr, (unsigned)gen, k1, err};
-#define MVBA_EVL_K(M, D, OT, JC)                                                                              \
-  hipLaunchKernelGGL((mvba::k_eval_local<M, D, OT, JC>), dim3(blocks), dim3(256), 0, s, segs, nseg, lone_frames, \
-                     nlone, (int32_t)fb, (int32_t)pb, fd, frec, params, npts, pts, obs_pid, obs_meas, (OT*)res,   \
-                     (OT*)J, ld, flags, cauchy_c, fu)
+#define MVBA_EVL_K(M, D, OT, JC)                                                                               \
+  hipLaunchKernelGGL((mvba::k_eval_local<M, D, OT, JC>), dim3(blocks), dim3(256), 0, s, segs, nseg, (int32_t)pb, \
+                     fd, frec, params, npts, pts, obs_pid, obs_meas, (OT*)res, (OT*)J, ld, flags, cauchy_c, fu)
 #define MVBA_EVL(M, D)                                                                                   \
   if (flags & MVBA_EVAL_JACOBIAN) {                                                                      \
     if (out_f32) MVBA_EVL_K(M, D, float, true);                                                          \

@@ -1,0 +1,51 @@
+"""The one-launch forms of mvba_evaluate_device against the two-launch form.
+
+mvba_evaluate_device runs one launch for a one-group problem: k_eval_local
+below four segments per frame (each K1 wave computes its own frame's K0 record
+in LDS) and k_eval otherwise (K0 blocks hand the records to the K1 waves of the
+same grid). Both must write bit-identical planes to the two-launch form (the
+prep kernel, MVBA_EVAL_PREP_ONLY, then K1 with MVBA_EVAL_SKIP_PREP: the same
+arithmetic), and the frame records and landmark records they leave behind must
+serve a later SKIP_PREP evaluation (what the solver and the bench's instrumented
+steps rely on)."""
+import numpy as np
+import pytest
+
+from multiview_amd import _lib, rig
+from multiview_amd.evaluator import Evaluator
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npts,form", [(120, "k_eval_local"), (2500, "k_eval")])
+@pytest.mark.parametrize("jacobian", [True, False])
+def test_one_launch_evaluation_matches_two_launches(npts, form, jacobian):
+    import torch
+
+    R = rig.make_rig(num_sensors=3, num_ref=10, num_points=npts, obs_per_point=4, seed=5)
+    P = rig.build_problem(R)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        # the form the library picks: segments (64 observations of one image)
+        # per frame
+        obs = np.bincount(R.obs_cid)
+        segs = np.ceil(obs[obs > 0] / 64.0).sum()
+        assert ev.num_frames == (obs > 0).sum()
+        assert (segs < 4 * ev.num_frames) == (form == "k_eval_local"), (segs, ev.num_frames)
+        ld = ev.ld
+        outs = []
+        for phases in ([0], [_lib.EVAL_PREP_ONLY, _lib.EVAL_SKIP_PREP], [0, _lib.EVAL_SKIP_PREP]):
+            res = torch.full((2, ld), float("nan"), dtype=torch.float64, device="cuda")
+            jac = torch.full((ev.stride, ld), float("nan"), dtype=torch.float64, device="cuda") if jacobian else None
+            for ph in phases:
+                ev.evaluate_device(jacobian, residuals=res, jac=jac, ld=ld, phase=ph)
+            torch.cuda.synchronize()
+            ev.sync()
+            outs.append((res.cpu().numpy(), jac.cpu().numpy() if jacobian else None))
+    for r, J in outs[1:]:
+        np.testing.assert_array_equal(r, outs[0][0])
+        if jacobian:
+            np.testing.assert_array_equal(J, outs[0][1])
+    # every observation's residual slot was written
+    with Evaluator(P) as ev:
+        order = ev.order()
+    assert np.isfinite(outs[0][0][:, : order.size][:, order >= 0]).all()
