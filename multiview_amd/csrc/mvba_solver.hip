@@ -1122,31 +1122,48 @@ __global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict
 }
 
 // Block-Jacobi preconditioner (Ceres' JACOBI for ITERATIVE_SCHUR [ext]:
-// blocks of F'F + D^2): one workgroup (one wave) per camera block factors
-// H_bb + diag(d) in LDS (column-parallel Cholesky) and writes the explicit
-// inverse (lane j solves for column j), so applying it is a block mat-vec.
-// Blocks wider than kPrecLds (RPC distortion of degree >= 4: 116..220 entries)
-// are inverted in place in the output by Gauss-Jordan elimination (symmetric
-// positive definite: no pivoting; a vanishing pivot = a direction the block
-// does not see, inverted as identity like the Cholesky path).
+// blocks of F'F + D^2): one workgroup (one wave) per camera block inverts
+// H_bb + diag(d) explicitly by Gauss-Jordan elimination (symmetric positive
+// definite: no pivoting; a vanishing pivot = a direction the block does not
+// see, inverted as identity), in LDS up to kPrecLds wide, in place in the
+// output beyond (RPC distortion of degree >= 4: 116..220 entries); applying it
+// is then a block mat-vec. Lane j owns column j: n rank-1 steps with no
+// per-lane serial chain. (A column-serial Cholesky with per-lane triangular
+// solves kept its solve vector in scratch memory: 282 us per build at c3,
+// 3,000 pose blocks; profiles/r03/ab_block_prec/.)
 constexpr int kPrecLds = 88;  // 88^2 + 2 * 88 doubles = 62 KB: within the 64 KB of dynamic LDS a plain launch gets
-// Blocks wider than this (RPC distortion blocks: 22..88 entries) take the
-// Gauss-Jordan path in LDS: its n steps are 64-lane rank-1 updates, where the
-// Cholesky path's column steps and per-lane triangular solves are serial
-// chains (c3, 44-wide blocks: 262 us per preconditioner build).
-constexpr int kPrecChol = 16;
+constexpr int kPrecThreads = 256;  // 4 waves per block share the elimination steps
 
-__device__ void block_inverse_gj(int n, const double* __restrict__ H, const double* __restrict__ db,
-                                 double* __restrict__ A, double* colk, double* rowk) {
-  const int lane = threadIdx.x;
-  for (int e = lane; e < n * n; e += 64) {
-    const int i = e / n, j = e % n;
-    const double h = (j <= i) ? H[e] : H[j * n + i];  // full symmetric matrix from the lower triangle
-    A[e] = h + (i == j ? db[i] : 0.0);
+__device__ __forceinline__ void block_inverse_gj(int n, const double* __restrict__ H, const double* __restrict__ db,
+                                                 double* __restrict__ A, double* colk, double* rowk) {
+  // thread t owns column (t mod 64) (+ 64 past 64 columns) and one of the
+  // block's row ranges (one per wave): no integer division in the loops, and
+  // the n elimination steps spread over every wave of the workgroup
+  const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
+  const int rq = (n + nw - 1) / nw, r0 = (tid >> 6) * rq, r1 = min(n, r0 + rq);
+  // the lower triangle as stored (coalesced), diagonal damped
+  for (int e0 = tid; e0 < n * n; e0 += 8 * (int)blockDim.x) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int e = e0 + u * (int)blockDim.x;
+      v[u] = e < n * n ? H[e] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int e = e0 + u * (int)blockDim.x;
+      if (e < n * n) A[e] = v[u];
+    }
   }
   __syncthreads();
+  for (int j = lane; j < n; j += 64)
+    for (int i = r0; i < r1; i++) {
+      if (i < j) A[i * n + j] = A[j * n + i];  // upper triangle from the lower
+      else if (i == j) A[i * n + j] += db[i];
+    }
+  __syncthreads();
   for (int k = 0; k < n; k++) {
-    for (int i = lane; i < n; i += 64) {
+    for (int i = tid; i < n; i += blockDim.x) {
       colk[i] = A[i * n + k];
       rowk[i] = A[k * n + i];
     }
@@ -1154,28 +1171,43 @@ __device__ void block_inverse_gj(int n, const double* __restrict__ H, const doub
     const double piv = colk[k];
     const bool ok = piv > 1e-300;
     const double ip = ok ? 1.0 / piv : 0.0;
-    for (int e = lane; e < n * n; e += 64) {
-      const int i = e / n, j = e % n;
-      double v;
+    for (int j = lane; j < n; j += 64) {
+      const double rj = rowk[j] * ip;
       if (!ok) {
-        v = (i == k || j == k) ? (i == j ? 1.0 : 0.0) : A[e];
-      } else if (i == k) {
-        v = (j == k) ? ip : rowk[j] * ip;
+        for (int i = r0; i < r1; i++)
+          if (i == k || j == k) A[i * n + j] = (i == j) ? 1.0 : 0.0;
+      } else if (j == k) {
+        for (int i = r0; i < r1; i++) A[i * n + j] = (i == k) ? ip : -colk[i] * ip;
       } else {
-        v = (j == k) ? -colk[i] * ip : A[e] - colk[i] * rowk[j] * ip;
+        // 8 rows at a time: every load of the group issued before its stores
+        // (A and colk share one LDS array, so the compiler cannot move a load
+        // above an earlier store itself)
+        for (int i0 = r0; i0 < r1; i0 += 8) {
+          double a[8], c[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int i = min(i0 + u, r1 - 1);
+            a[u] = A[i * n + j];
+            c[u] = colk[i];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int i = i0 + u;
+            if (i < r1) A[i * n + j] = (i == k) ? rj : a[u] - c[u] * rj;
+          }
+        }
       }
-      A[e] = v;
     }
     __syncthreads();
   }
 }
 
-__global__ void __launch_bounds__(64) k_block_prec(int32_t nblocks, const int64_t* __restrict__ goff,
+__global__ void __launch_bounds__(kPrecThreads) k_block_prec(int32_t nblocks, const int64_t* __restrict__ goff,
                                                    const int64_t* __restrict__ hoff,
                                                    const int32_t* __restrict__ bsize,
                                                    const double* __restrict__ hess, const double* __restrict__ d,
                                                    double* __restrict__ minv) {
-  extern __shared__ double Ls[];  // [n * n], or the pivot column and row of the wide path
+  extern __shared__ double Ls[];  // [n * n | pivot column | pivot row], or the pivot column and row of the wide path
   const int b = blockIdx.x;
   if (b >= nblocks) return;
   const int n = bsize[b];
@@ -1186,54 +1218,9 @@ __global__ void __launch_bounds__(64) k_block_prec(int32_t nblocks, const int64_
     block_inverse_gj(n, H, db, minv + hoff[b], Ls, Ls + n);
     return;
   }
-  if (n > kPrecChol) {
-    block_inverse_gj(n, H, db, Ls, Ls + n * n, Ls + n * n + n);
-    __syncthreads();
-    double* M = minv + hoff[b];
-    for (int e = lane; e < n * n; e += 64) M[e] = Ls[e];
-    return;
-  }
-  for (int e = lane; e < n * n; e += 64) {
-    const int i = e / n, j = e % n;
-    Ls[e] = (j <= i) ? H[e] + (i == j ? db[i] : 0.0) : 0.0;
-  }
-  __syncthreads();
-  __shared__ double djs;
-  __shared__ int ok;
-  for (int j = 0; j < n; j++) {
-    if (lane == 0) {
-      double sj = Ls[j * n + j];
-      for (int k = 0; k < j; k++) sj -= Ls[j * n + k] * Ls[j * n + k];
-      // singular directions (e.g. all-zero columns) fall back to identity
-      ok = sj > 1e-300;
-      djs = ok ? sqrt(sj) : 1.0;
-      Ls[j * n + j] = djs;
-    }
-    __syncthreads();
-    for (int i = j + 1 + lane; i < n; i += 64) {
-      double v = Ls[i * n + j];
-      for (int k = 0; k < j; k++) v -= Ls[i * n + k] * Ls[j * n + k];
-      Ls[i * n + j] = ok ? v / djs : 0.0;
-    }
-    __syncthreads();
-  }
+  block_inverse_gj(n, H, db, Ls, Ls + n * n, Ls + n * n + n);
   double* M = minv + hoff[b];
-  double y[kPrecLds];
-  for (int j = lane; j < n; j += 64) {
-    // L y = e_j
-    for (int i = 0; i < n; i++) {
-      double v = (i == j) ? 1.0 : 0.0;
-      for (int k = j; k < i; k++) v -= Ls[i * n + k] * y[k];
-      y[i] = (i < j) ? 0.0 : v / Ls[i * n + i];
-    }
-    // L^T x = y
-    for (int i = n - 1; i >= 0; i--) {
-      double v = y[i];
-      for (int k = i + 1; k < n; k++) v -= Ls[k * n + i] * y[k];
-      y[i] = v / Ls[i * n + i];
-    }
-    for (int i = 0; i < n; i++) M[i * n + j] = y[i];
-  }
+  for (int e = lane; e < n * n; e += blockDim.x) M[e] = Ls[e];
 }
 
 // ---- compact free-parameter vectors: [camera-side entries (layout order) | 3 per point]
@@ -1600,7 +1587,8 @@ hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int6
   if (nblocks <= 0) return hipSuccess;
   const int m = max_bsize < mvba::kPrecLds ? max_bsize : mvba::kPrecLds;
   const size_t lds = sizeof(double) * (size_t)(m * m + 2 * m > 2 * max_bsize ? m * m + 2 * m : 2 * max_bsize);
-  hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(64), lds, s, nblocks, goff, hoff, bsize, hess,
+  hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(mvba::kPrecThreads), lds, s, nblocks, goff,
+                     hoff, bsize, hess,
                      d, minv);
   return hipGetLastError();
 }
