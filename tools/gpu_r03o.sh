@@ -2,7 +2,8 @@
 # Full GPU suite; fused/split/local evaluation A/B on rank 0's shard of 2-, 4-,
 # 8-way c2 splits (MVBA_EVAL_MODE), twice; then the CG passes with direct chunk
 # records against the previous build (tools/ab/base through MVBA_LIB): kernel
-# traces at c2 (twice) and c3, per-kernel medians (tools/ktrace_med.py).
+# traces at c2 (twice) and c3, per-kernel medians (tools/ktrace_med.py);
+# 'slot': pass A stores c_o in slot order and k_point_w gathers (MVBA_CO_ORDER).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -29,8 +30,10 @@ for k in 1 2; do
   done
 done
 for cfg in c2 c2 c3; do
-  for v in base cur; do
+  for v in base cur slot; do
+    unset MVBA_CO_ORDER
     if [ $v = base ]; then export MVBA_LIB=$PWD/tools/ab/base/libmvba.so; else unset MVBA_LIB; fi
+    if [ $v = slot ]; then export MVBA_CO_ORDER=slot; fi
     if [ $cfg = c3 ]; then A="--config c3 --steps 3 --ba-iters 3"; else A="--steps 5 --ba-iters 5"; fi
     d=$OUT/kt_${cfg}_${v}_$RANDOM
     timeout -s KILL 300 rocprofv3 --kernel-trace -d $d -o run --output-format csv -- python3 bench.py --no-cpu-baseline --mesh-subdiv 0 $A > $d.log 2>&1 || { tail -3 $d.log; exit 1; }
