@@ -44,6 +44,10 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                                     const double2* obs_meas, const int32_t* slot_po, mvba::DirPair dir,
                                     double4* cbuf, int32_t flags, double cauchy_c, const int32_t* gate,
                                     const double* prec, const double4* obsX, hipStream_t s);
+hipError_t mvba_launch_pass_sq(int model, int deg, const int4* chunks, int32_t nchunks, const int32_t* obs_pid,
+                               mvba::DirPair dir, const double* wbuf, int32_t wstride, const double* prec,
+                               const double4* obsX, double* partial, unsigned* counter, double* sq_out,
+                               hipStream_t s);
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
                                const double* tinit, const double* V, const double* dp, const double4* pts,
                                double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
@@ -225,6 +229,7 @@ SolverState* alloc_state(mvba_handle* h) {
     for (const Group& G : h->groups) ncost = std::max<int64_t>(ncost, (G.seg_count + 3) / 4);
     // k_cg_update: 3 partials per 256-entry block; k_vec_rep_reduce / k_add_diag one
     S->npartial = std::max<int64_t>({3072, 3 * ((S->ng + 255) / 256), S->ng + 1, mvba_pass_a_blocks(S->np), ncost,
+                                    (h->nsegs + 3) / 4,
                                     (int64_t)h->ndep_segs, (h->ndep_slots + 255) / 256});
     HCHK(dalloc(&S->partial, (size_t)S->npartial));
     HCHK(dalloc(&S->scal, 32));
@@ -600,13 +605,37 @@ class Solver {
   double back_substitute() {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
                                nullptr, nullptr, s_));
-    // |J delta|^2 over the local reprojection and depth blocks -> scal[0]
-    // (point order; a frame-order pass A + k_point_w + |u|^2 sweep measured no
-    // gain at c2 and 17 us per CG iteration slower at c3: profiles/r03/ab_backsub/)
-    HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas, h_->d_fd,
-                            h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
-                            S_->dmp + S_->ng, S_->zbuf, S_->delta + S_->ng, 3, S_->partial, S_->cnt + 5,
-                            S_->scal + 0, flags_, cauchy_c_, h_->point_extra(), S_->delta, S_->du, nullptr, S_->prec, s_));
+    // |J delta|^2 over the local reprojection and depth blocks -> scal[0].
+    // Reprojection-only problems with one model group: frame-order pass A +
+    // k_point_w (w_p into delta_p) + the |u_o|^2 sweep k_pass_sq; otherwise
+    // (depth blocks, XYZ priors, several models) the point-order pass, whose
+    // per-observation gathers of frame records outgrow the L2 at c3. Kernel
+    // traces (profiles/r03/ab_backsub/): c3 514 vs 760 us, c2 57 vs 59 us per
+    // solve. MVBA_BACKSUB=point forces the point-order pass, for A/B timing.
+    static const char* bs_env = std::getenv("MVBA_BACKSUB");
+    const bool frame_order = !(bs_env && !std::strcmp(bs_env, "point")) && h_->ndep == 0 && h_->nxyz == 0 &&
+                             h_->groups.size() == 1 && h_->groups[0].seg_count > 0 && obsx();
+    if (frame_order) {
+      const Group& G = h_->groups[0];
+      static const char* co_env = std::getenv("MVBA_CO_ORDER");
+      const bool co_slot = co_slot_order(co_env);
+      HCHK(mvba_launch_pass_a_frame(G.model, G.deg, h_->d_segchunks + G.seg_begin, G.seg_count, h_->d_segs,
+                                    h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, co_slot ? nullptr : h_->d_slot_po,
+                                    plain_dir(S_->dir), (double4*)S_->cbuf, flags_, cauchy_c_, nullptr, S_->prec,
+                                    obsx(), s_));
+      HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
+                               (const double4*)S_->cbuf, S_->G + S_->ng, S_->phess, S_->dmp + S_->ng, h_->d_pts,
+                               S_->delta + S_->ng, 3, nullptr, nullptr, nullptr, s_));
+      HCHK(mvba_launch_pass_sq(G.model, G.deg, h_->d_segchunks + G.seg_begin, G.seg_count, h_->d_obs_pid,
+                               plain_dir(S_->dir), S_->delta + S_->ng, 3, S_->prec, obsx(), S_->partial,
+                               S_->cnt + 5, S_->scal + 0, s_));
+    } else {
+      HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas,
+                              h_->d_fd, h_->d_frec, h_->d_params, h_->d_pts, S_->dir, S_->G + S_->ng, S_->phess,
+                              S_->dmp + S_->ng, S_->zbuf, S_->delta + S_->ng, 3, S_->partial, S_->cnt + 5,
+                              S_->scal + 0, flags_, cauchy_c_, h_->point_extra(), S_->delta, S_->du, nullptr,
+                              S_->prec, s_));
+    }
     HCHK(mvba_launch_axpby(3 * S_->np, -1.0, S_->delta + S_->ng, 0.0, nullptr, S_->delta + S_->ng, s_));
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);

@@ -489,6 +489,51 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
   }
 }
 
+// |J delta|^2 of the back-substitution in frame order (reprojection-only,
+// one model group): per observation u_o = z_o - J_pt w_p with z_o = J_cam,o
+// delta_c from the frame direction (dr.dz) and w_p from k_point_w (wbuf,
+// wstride doubles per point), summed over the grid into sq_out. Replaces the
+// point-order k_pass_a<..., ROWS> (4 lanes per point gathering per-frame data)
+// after the frame-order pass A + k_point_w.
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(64 * kPassAWaves) k_pass_sq(
+    const int4* __restrict__ chunks, int32_t nchunks, const int32_t* __restrict__ obs_pid, DirPair dr,
+    const double* __restrict__ wbuf, int32_t wstride, const double* __restrict__ prec,
+    const double4* __restrict__ obsX, double* __restrict__ partial, unsigned* __restrict__ counter,
+    double* __restrict__ sq_out) {
+  constexpr int ND = 6 + RowShape<MODEL, DEG>::kIntr;
+  __shared__ double sdir[kPassAWaves][ND];
+  const int lane = threadIdx.x & 63;
+  double sq = 0.0;
+  // a bounded grid (1,024 blocks), each wave striding over the chunks: the
+  // grid sum's arrival counter takes one atomic per block (39k blocks at c3
+  // serialised on it: 534 us; 256 / 512 / 1024 / 2048 blocks: 373 / 225 / 191 /
+  // 200 us at c3, 36.8 / 26.2 / 26.7 / 37.2 us at c2)
+  for (int ch = blockIdx.x * kPassAWaves + (threadIdx.x >> 6); ch < nchunks; ch += gridDim.x * kPassAWaves) {
+    const int4 c = chunks[ch];
+    const int frame = __builtin_amdgcn_readfirstlane(c.z);
+    const int nobs = __builtin_amdgcn_readfirstlane(c.y);
+    const double* __restrict__ rec = prec + (int64_t)frame * kProjDoubles;
+    double* d = sdir[threadIdx.x >> 6];
+    stage_dir<ND>(dr, frame, d, false);
+    for (int s0 = 0; s0 < nobs; s0 += 64) {
+      if (lane < nobs - s0) {
+        const int64_t i = (int64_t)c.x + s0 + lane;
+        const double* w = wbuf + (int64_t)wstride * obs_pid[i];
+        const double w0 = w[0], w1 = w[1], w2 = w[2];
+        const double4 X = obsX[i];
+        double z[2], P0[3], P1[3];
+        pass_a_obs<MODEL, DEG>(rec, d, X, double2{0.0, 0.0}, 0, 0.0, z, P0, P1, X.w);
+        const double u0 = z[0] - (P0[0] * w0 + P0[1] * w1 + P0[2] * w2);
+        const double u1 = z[1] - (P1[0] * w0 + P1[1] * w1 + P1[2] * w2);
+        sq += u0 * u0 + u1 * u1;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // sdir is rewritten by the next chunk of this wave
+  }
+  grid_sum_finalize(sq, partial, counter, sq_out);
+}
+
 // BracketedDepthError / BracketedDepthMeshError blocks in the frame-order CG
 // product: one wave per depth segment (one image: the descriptor is read once,
 // the point per lane), z_d = J_cam,d x into du (slot order; k_depth_sb forms
@@ -1456,6 +1501,22 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                      segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec, obsX)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PAF)
 #undef MVBA_PAF
+  return hipGetLastError();
+}
+
+hipError_t mvba_launch_pass_sq(int model, int deg, const int4* chunks, int32_t nchunks, const int32_t* obs_pid,
+                               mvba::DirPair dir, const double* wbuf, int32_t wstride, const double* prec,
+                               const double4* obsX, double* partial, unsigned* counter, double* sq_out,
+                               hipStream_t s) {
+  if (nchunks <= 0) return hipErrorInvalidValue;  // the grid sum needs a block
+  // MVBA_SQ_GRID: the block cap (A/B timing)
+  static const int64_t cap = std::getenv("MVBA_SQ_GRID") ? std::atoll(std::getenv("MVBA_SQ_GRID")) : 1024;
+  const unsigned grid = (unsigned)std::min<int64_t>((nchunks + mvba::kPassAWaves - 1) / mvba::kPassAWaves, cap);
+#define MVBA_PSQ(M, D)                                                                                      \
+  hipLaunchKernelGGL((mvba::k_pass_sq<M, D>), dim3(grid), dim3(64 * mvba::kPassAWaves), 0, s, chunks, nchunks,    \
+                     obs_pid, dir, wbuf, wstride, prec, obsX, partial, counter, sq_out)
+  MVBA_SOLVER_SWITCH(model, deg, MVBA_PSQ)
+#undef MVBA_PSQ
   return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ for r in csv.DictReader(open(path)):
     k = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").replace("mvba::", "")
     d[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 for k in ("k_pass_a_frame", "k_point_w", "k_pass_b", "k_vec_rep_reduce", "k_cg_update", "k_frame_lin", "k_eval", "k_obs<",
-          "k_block_prec", "k_pass_a<"):
+          "k_block_prec", "k_pass_a<", "k_pass_sq"):
     for name, v in d.items():
         if name.startswith(k):
             w = [x for x in v if x >= lo]
