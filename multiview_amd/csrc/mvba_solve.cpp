@@ -334,8 +334,10 @@ class Solver {
   }
 
   // Jacobian at the handle's parameters -> lin (all-reduced), G, phess, cdiag. Returns cost.
-  double linearize() {
-    const int32_t lf = flags_ | (o_.deterministic ? MVBA_LIN_DETERMINISTIC : 0);
+  // skip_prep: the frame and landmark records are current (the candidate's
+  // cost evaluation just ran the prep kernel at these parameters)
+  double linearize(bool skip_prep = false) {
+    const int32_t lf = flags_ | (o_.deterministic ? MVBA_LIN_DETERMINISTIC : 0) | (skip_prep ? MVBA_EVAL_SKIP_PREP : 0);
     mvba_status st = mvba_linearize_device(h_, lf, o_.robust_threshold, S_->lin, S_->lin + S_->ng,
                                            S_->G + S_->ng, S_->phess, S_->lin + S_->ng + S_->nh, (void*)s_);
     if (st != MVBA_OK) throw StatusErr{st, h_->err};
@@ -1049,11 +1051,12 @@ void Solver::run(mvba_solver_summary* sum) {
     }
     const double ratio = change / mcc;
     if (ratio > o_.min_relative_decrease) {
-      // HandleSuccessfulStep: x = candidate, re-linearize there
+      // HandleSuccessfulStep: x = candidate, re-linearize there (cost() ran the
+      // prep kernel at the candidate: its records are current)
       std::swap(S_->x, S_->xn);
       x_norm = std::sqrt(norm2_compact(S_->x));
       tl = now_s();
-      x_cost = linearize();
+      x_cost = linearize(true);
       sum->linearize_time_s += now_s() - tl;
       gmax = grad_max_norm();
       radius = std::min(o_.max_trust_region_radius,
