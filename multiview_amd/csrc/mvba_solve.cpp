@@ -469,7 +469,7 @@ class Solver {
     // position (scattered 32-B stores, k_point_w reads its run) or in slot order
     // (coalesced stores, k_point_w gathers through po_slot). MVBA_CO_ORDER=
     // point|slot forces one, for A/B timing.
-    static const char* co_env = std::getenv("MVBA_CO_ORDER");
+    const char* co_env = std::getenv("MVBA_CO_ORDER");  // read per call: tests switch it
     const bool co_slot = co_slot_order(co_env);
     if (dir)
       for (const Group& G : h_->groups)
@@ -614,12 +614,12 @@ class Solver {
     // per-observation gathers of frame records outgrow the L2 at c3. Kernel
     // traces (profiles/r03/ab_backsub/): c3 514 vs 760 us, c2 57 vs 59 us per
     // solve. MVBA_BACKSUB=point forces the point-order pass, for A/B timing.
-    static const char* bs_env = std::getenv("MVBA_BACKSUB");
+    const char* bs_env = std::getenv("MVBA_BACKSUB");  // read per call: tests switch it
     const bool frame_order = !(bs_env && !std::strcmp(bs_env, "point")) && h_->ndep == 0 && h_->nxyz == 0 &&
                              h_->groups.size() == 1 && h_->groups[0].seg_count > 0 && obsx();
     if (frame_order) {
       const Group& G = h_->groups[0];
-      static const char* co_env = std::getenv("MVBA_CO_ORDER");
+      const char* co_env = std::getenv("MVBA_CO_ORDER");  // read per call: tests switch it
       const bool co_slot = co_slot_order(co_env);
       HCHK(mvba_launch_pass_a_frame(G.model, G.deg, h_->d_segchunks + G.seg_begin, G.seg_count, h_->d_segs,
                                     h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, co_slot ? nullptr : h_->d_slot_po,
