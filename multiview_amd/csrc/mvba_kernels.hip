@@ -296,7 +296,8 @@ __device__ __forceinline__ void obs_body(
   // No reader looks at padding slots.
   constexpr int kLine = 128 / (int)sizeof(OT);
   const bool active = lane < ((count + kLine - 1) & ~(kLine - 1));
-  if (!FUSED && !active) return;
+  // (local records: every lane takes part in storing the record first)
+  if (RECM == kRecGlobal && !active) return;
   const int64_t i = (int64_t)begin + lane;
   const int64_t isrc = (int64_t)begin + min(lane, count - 1);
 
@@ -359,8 +360,9 @@ __device__ __forceinline__ void obs_body(
     // frame has a segment (frames are the reprojection residuals' images)
     if (wave == 0 || segs[wave - 1].frame != frame) {
       double* g = const_cast<double*>(frec) + (int64_t)frame * kFrameRecDoubles;  // k_eval_local owns frec
-      for (int m = lane; m < kFrameRecDoubles; m += 64) g[m] = sr[m];
+      for (int m = lane; m < kFrameRecDoubles; m += 64) g[m] = sr[m];  // all 64 lanes: the whole record
     }
+    if (!active) return;
   } else {
     P = pts[obs_pid[isrc]];
     rec = frec + (int64_t)frame * kFrameRecDoubles;

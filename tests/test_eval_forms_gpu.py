@@ -33,7 +33,14 @@ def test_one_launch_evaluation_matches_two_launches(npts, form, jacobian):
         assert (segs < 4 * ev.num_frames) == (form == "k_eval_local"), (segs, ev.num_frames)
         ld = ev.ld
         outs = []
+        # before every form the frame and landmark records are made stale: a
+        # full prep at slightly different parameters, then the real ones set,
+        # so a record entry the form under test does not rewrite shows up
+        stale = P.params * (1.0 + 1e-6) + 1e-9
         for phases in ([0], [_lib.EVAL_PREP_ONLY, _lib.EVAL_SKIP_PREP], [0, _lib.EVAL_SKIP_PREP]):
+            ev.set_params(stale)
+            ev.evaluate_device(jacobian, phase=_lib.EVAL_PREP_ONLY)
+            ev.set_params()
             res = torch.full((2, ld), float("nan"), dtype=torch.float64, device="cuda")
             jac = torch.full((ev.stride, ld), float("nan"), dtype=torch.float64, device="cuda") if jacobian else None
             for ph in phases:
