@@ -34,6 +34,24 @@ __device__ __forceinline__ int64_t xcd_block_of(int64_t b, int64_t nb) {
   return l < nb ? l : -1;
 }
 __device__ __forceinline__ int64_t xcd_block(int64_t nb) { return xcd_block_of(blockIdx.x, nb); }
+// The CG passes over frame-ordered chunks (pass A, pass B, the |u|^2 sweep)
+// and over landmarks (k_point_w: landmarks are numbered by first use in frame
+// order) take the same order, so the landmark-side data of a window of frames
+// (w_p gathers, c_o records) is fetched into one XCD's L2. MVBA_XCD_SOLVER=0
+// keeps the plain order (A/B builds).
+#ifndef MVBA_XCD_SOLVER
+#define MVBA_XCD_SOLVER 1
+#endif
+__host__ __device__ __forceinline__ unsigned xcd_grid_solver(int64_t nb) {
+  return MVBA_XCD_SOLVER ? (unsigned)(((nb + kXcds - 1) / kXcds) * kXcds) : (unsigned)nb;
+}
+__device__ __forceinline__ int64_t xcd_block_solver(int64_t nb) {
+  const int64_t b = blockIdx.x;
+  if (!MVBA_XCD_SOLVER) return b < nb ? b : -1;
+  const int64_t per = (nb + kXcds - 1) / kXcds;
+  const int64_t l = (b % kXcds) * per + b / kXcds;
+  return l < nb ? l : -1;
+}
 
 // ------------------------------------------------------------ small helpers
 __device__ __forceinline__ void quat_to_rot(double x, double y, double z, double w, double* R) {

@@ -631,6 +631,9 @@ __global__ void __launch_bounds__((64 * GramShape<MODEL, DEG>::kWaves)) k_frame_
   constexpr int W16 = T * 16;
   extern __shared__ double lds[];  // [WAVES][kStage] | w [6 x 22] | Tm [6 x 22] | cost [WAVES]
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // frame parts in the plain block order: the XCD-contiguous order of the CG
+  // passes measured slower here (c2 51.0 -> 59.3 us without the point blocks,
+  // c3 +25 us: profiles/r03/ab_xcd_solver/), then the point blocks
   if ((int)blockIdx.x >= nparts) {
     if constexpr (POINTS)
       points_lin_body<MODEL, DEG>((int64_t)(blockIdx.x - nparts) * blockDim.x + tid, pa.pt_begin, pa.npts,

@@ -458,8 +458,9 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
   constexpr int ND = 6 + RowShape<MODEL, DEG>::kIntr;  // direction entries the rows read
   __shared__ double sdir[kPassAWaves][ND];
   const int lane = threadIdx.x & 63;
-  const int ch = blockIdx.x * kPassAWaves + (threadIdx.x >> 6);
-  if (ch >= nchunks || (gate && *gate)) return;
+  const int64_t blk = xcd_block_solver((nchunks + kPassAWaves - 1) / kPassAWaves);
+  const int ch = (int)blk * kPassAWaves + (threadIdx.x >> 6);
+  if (blk < 0 || ch >= nchunks || (gate && *gate)) return;
   // (first slot, observations, frame, first chunk of the frame): the chunk's
   // segments are consecutive 64-slot runs of one frame, so no segment loads
   const int4 c = chunks[ch];
@@ -508,8 +509,17 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_sq(
   // a bounded grid (1,024 blocks), each wave striding over the chunks: the
   // grid sum's arrival counter takes one atomic per block (39k blocks at c3
   // serialised on it: 534 us; 256 / 512 / 1024 / 2048 blocks: 373 / 225 / 191 /
-  // 200 us at c3, 36.8 / 26.2 / 26.7 / 37.2 us at c2)
-  for (int ch = blockIdx.x * kPassAWaves + (threadIdx.x >> 6); ch < nchunks; ch += gridDim.x * kPassAWaves) {
+  // 200 us at c3, 36.8 / 26.2 / 26.7 / 37.2 us at c2). With MVBA_XCD_SOLVER
+  // (the grid a multiple of 8) the blocks of XCD x stride over the x-th eighth
+  // of the chunks.
+  int ch0 = blockIdx.x * kPassAWaves + (threadIdx.x >> 6), cend = nchunks, cstep = gridDim.x * kPassAWaves;
+  if (MVBA_XCD_SOLVER) {
+    const int per = (nchunks + kXcds - 1) / kXcds, x = (int)(blockIdx.x % kXcds);
+    ch0 = x * per + (int)(blockIdx.x / kXcds) * kPassAWaves + (threadIdx.x >> 6);
+    cend = min(nchunks, (x + 1) * per);
+    cstep = (int)(gridDim.x / kXcds) * kPassAWaves;
+  }
+  for (int ch = ch0; ch < cend; ch += cstep) {
     const int4 c = chunks[ch];
     const int frame = __builtin_amdgcn_readfirstlane(c.z);
     const int nobs = __builtin_amdgcn_readfirstlane(c.y);
@@ -581,7 +591,9 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
                                                  const int32_t* __restrict__ gate, const int64_t* __restrict__ dbegin,
                                                  const double4* __restrict__ dcbuf) {
   if (gate && *gate) return;
-  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t blk = xcd_block_solver((npts * kLanesW + 255) / 256);
+  if (blk < 0) return;
+  const int64_t t0 = blk * 256 + threadIdx.x;
   const int64_t p = t0 / kLanesW;
   const int sub = (int)(t0 % kLanesW);
   const bool valid = p < npts;
@@ -786,8 +798,8 @@ __global__ void __launch_bounds__(64) k_pass_b(
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   const int lane = threadIdx.x;
-  const int ch = blockIdx.x;
-  if (ch >= nchunks || (gate && *gate)) return;
+  const int ch = (int)xcd_block_solver(nchunks);
+  if (ch < 0 || (gate && *gate)) return;
   if constexpr (NA > kPassBRegCols) {
     pass_b_wide<MODEL, DEG>(chunks[ch], chunk_base + ch, segs, fd, fl, frec, params, pts, obs_pid, obs_meas, dir,
                             wbuf, yrep, ng, flags, cauchy_c, sl, obsX);
@@ -1496,7 +1508,7 @@ hipError_t mvba_launch_pass_a_frame(int model, int deg, const int4* chunks, int3
                                     const double* prec, const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PAF(M, D)                                                                                      \
-  hipLaunchKernelGGL((mvba::k_pass_a_frame<M, D>), dim3((unsigned)((nchunks + mvba::kPassAWaves - 1) /        \
+  hipLaunchKernelGGL((mvba::k_pass_a_frame<M, D>), dim3(mvba::xcd_grid_solver((nchunks + mvba::kPassAWaves - 1) / \
                      mvba::kPassAWaves)), dim3(64 * mvba::kPassAWaves), 0, s, chunks, nchunks,                 \
                      segs, pts, obs_pid, obs_meas, slot_po, dir, cbuf, flags, cauchy_c, gate, prec, obsX)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PAF)
@@ -1511,7 +1523,8 @@ hipError_t mvba_launch_pass_sq(int model, int deg, const int4* chunks, int32_t n
   if (nchunks <= 0) return hipErrorInvalidValue;  // the grid sum needs a block
   // MVBA_SQ_GRID: the block cap (A/B timing)
   static const int64_t cap = std::getenv("MVBA_SQ_GRID") ? std::atoll(std::getenv("MVBA_SQ_GRID")) : 1024;
-  const unsigned grid = (unsigned)std::min<int64_t>((nchunks + mvba::kPassAWaves - 1) / mvba::kPassAWaves, cap);
+  const unsigned grid =
+      mvba::xcd_grid_solver(std::min<int64_t>((nchunks + mvba::kPassAWaves - 1) / mvba::kPassAWaves, cap));
 #define MVBA_PSQ(M, D)                                                                                      \
   hipLaunchKernelGGL((mvba::k_pass_sq<M, D>), dim3(grid), dim3(64 * mvba::kPassAWaves), 0, s, chunks, nchunks,    \
                      obs_pid, dir, wbuf, wstride, prec, obsX, partial, counter, sq_out)
@@ -1525,7 +1538,8 @@ hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int3
                                double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
                                const double4* dcbuf, hipStream_t s) {
   if (npts <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_point_w, dim3((unsigned)((npts * mvba::kLanesW + 255) / 256)), dim3(256), 0, s, npts,
+  hipLaunchKernelGGL(mvba::k_point_w, dim3(mvba::xcd_grid_solver((npts * mvba::kLanesW + 255) / 256)), dim3(256), 0, s,
+                     npts,
                      pt_begin, po_slot,
                      cbuf, tinit, V, dp, pts, wout, wstride, gate, dbegin, dcbuf);
   return hipGetLastError();
@@ -1561,7 +1575,8 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
 #define MVBA_PB(M, D)                                                                                       \
-  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3((unsigned)nchunks), dim3(64), (mvba::pass_b_lds<M, D>()), s,\
+  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3(mvba::xcd_grid_solver(nchunks)), dim3(64),                    \
+                     (mvba::pass_b_lds<M, D>()), s,                                                           \
                      chunks, nchunks,                                                                         \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
                      dir, wbuf, yrep, ng, flags, cauchy_c, gate, sl, obsX)
