@@ -393,6 +393,27 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     h->pt_free_h = pt_free;
   }
 
+  // Within a frame, slots in landmark order (stable): the landmarks first used
+  // by one earlier frame then sit in one contiguous run of every later frame
+  // that sees them, so k_point_w's c_o gathers (points in id order) and the
+  // landmark / w_p gathers of K1 and pass B (slots in order) share lines. The
+  // numbering above is unchanged by it (a frame's new landmarks keep their
+  // relative order and follow the ones numbered before). MVBA_SLOT_ORDER=
+  // insertion keeps AddResidualBlock order within frames (A/B timing).
+  {
+    const char* so = std::getenv("MVBA_SLOT_ORDER");
+    if (!(so && !std::strcmp(so, "insertion")))
+      for (int64_t a = 0; a < N;) {
+        const int64_t ia = idx[a];
+        const int ga = grank[d->residual_camera[ia]];
+        int64_t b = a + 1;
+        while (b < N && res_frame[idx[b]] == res_frame[ia] && grank[d->residual_camera[idx[b]]] == ga) b++;
+        std::stable_sort(idx.begin() + a, idx.begin() + b,
+                         [&](int64_t x, int64_t y) { return res_pt[x] < res_pt[y]; });
+        a = b;
+      }
+  }
+
   // Device slots: every frame's residuals start on a 128-byte line (16 doubles,
   // 32 floats), so each wavefront's 64-element store chunk per Jacobian plane is
   // line-aligned (misaligned chunks write at ~60% of the aligned rate:
