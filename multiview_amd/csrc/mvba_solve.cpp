@@ -573,8 +573,12 @@ class Solver {
     // iterations past the stop are no-ops): the first batch runs to just short
     // of the previous solve's iteration count, later ones are short, so most
     // solves need one or two host reads and few gated iterations.
+    // The second batch is 2 (the previous count is the usual ending), then 4;
+    // MVBA_CG_BATCH2 sets the second (A/B timing). A gated iteration costs
+    // ≈ 20 us at c2 and ≈ 36 us at c3 (a gated pass B alone is 10 us there).
+    static const int second = std::getenv("MVBA_CG_BATCH2") ? std::max(1, std::atoi(std::getenv("MVBA_CG_BATCH2"))) : 2;
     const int first = std::max(4, last_cg_iters_ - 2);
-    for (int batch = first;; batch = 4) {
+    for (int batch = first, nb = 0;; batch = (++nb == 1) ? second : 4) {
       for (int k = 0; k < batch && i <= std::max(o_.max_linear_solver_iterations, 1); k++, i++) {
         const mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, S_->ctl, 0, 0.0};
         std::swap(S_->p, S_->p2);
