@@ -440,6 +440,10 @@ def main():
     npts = cfg["num_points"]
     flags = rig.FloatFlags(**rig.CONFIG_FLAGS.get(args.config, {}))
     strong = args.scaling == "strong"
+    # the committed per-launch PMC summaries (K1 traffic, fp64 counts, the CG
+    # iteration's kernels) were measured on the whole config on one GPU: they
+    # apply to this line only when it runs exactly that workload
+    whole_cfg = world == 1 and args.shard_of <= 1
 
     def shard_cfg(strong_split):
         c = dict(cfg)
@@ -566,7 +570,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": _pmc_traffic(args.config),
+            "traffic": _pmc_traffic(args.config) if whole_cfg else None,
+            **({} if whole_cfg else {"traffic_note": "null: the committed PMC summaries (profiles/) are per "
+                                     "launch of the whole single-GPU config, not of this rank's shard"}),
             "bytes_per_launch": bytes_eval,
             "kernel_ms": obs_ms,
             "prep_ms": prep_ms,
@@ -589,7 +595,7 @@ def main():
     line["roofline"]["stream_note"] = "1 GiB device-to-device tensor copy (read + write bytes), same stream"
     # fp64 arithmetic of the same launch (PMC instruction counts): the second
     # roofline, to name the binding resource
-    flops_tab = _pmc_flops(args.config)
+    flops_tab = _pmc_flops(args.config) if whole_cfg else {}
     k1_flops = next((v["fp64_flops"] for k, v in flops_tab.items()
                      if k.startswith("mvba::k_obs<") and k.endswith("double>")), None)
     if k1_flops is not None:
@@ -851,7 +857,7 @@ def main():
                     "wall_note": "algorithmic bytes / (linear-solver wall time / CG iterations): includes the "
                                  "residual-reset products (every 10th), the per-solve setup and host reads"}
             summ = _ba_summary(args.config)
-            if summ and world == 1:
+            if summ and whole_cfg:
                 kus = summ["kernel_us_per_cg_iteration"]
                 roof.update({
                     "kernel_us": kus,
