@@ -46,7 +46,7 @@ CPU_THREADS = 16       # reference default --num_opt_threads (rig_calibrator.cc:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
