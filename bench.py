@@ -762,6 +762,13 @@ def main():
             return e0.elapsed_time(e1) / args.steps
 
         cam_ms, pts_ms = side_ms("camera"), side_ms("points")
+        # what an LM iteration pays: after a successful step the solver
+        # linearizes at the candidate whose frame records its evaluation
+        # already stored (SKIP_PREP: both sides, no prep launch)
+        lin["kernel_ms_records_current"] = side_ms("both")
+        lin["records_current_note"] = ("K2 + replica reduce with the frame records current (SKIP_PREP), as "
+                                       "mvba_solve linearizes after a successful LM step; kernel_ms includes "
+                                       "the prep launch (first linearization at a new point)")
         mfma = float(ev.lib.mvba_lin_mfma_flops(ev.h))
         lin["camera_side_ms"] = cam_ms
         lin["point_side_ms"] = pts_ms
