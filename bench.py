@@ -88,6 +88,13 @@ def launch_plan(gpus, environ, device_count, backend, script, argv, port):
             "--master-addr", "127.0.0.1", "--master-port", str(port), script] + list(argv)
 
 
+def summaries_apply(world, shard_of):
+    """The committed per-launch PMC summaries (profiles/: K1 traffic, fp64
+    counts, the CG iteration's kernels) were measured on the whole config on
+    one GPU; a line uses them only when it runs exactly that workload."""
+    return world == 1 and shard_of <= 1
+
+
 def _free_port():
     import socket
 
@@ -443,7 +450,7 @@ def main():
     # the committed per-launch PMC summaries (K1 traffic, fp64 counts, the CG
     # iteration's kernels) were measured on the whole config on one GPU: they
     # apply to this line only when it runs exactly that workload
-    whole_cfg = world == 1 and args.shard_of <= 1
+    whole_cfg = summaries_apply(world, args.shard_of)
 
     def shard_cfg(strong_split):
         c = dict(cfg)

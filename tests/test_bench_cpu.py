@@ -38,3 +38,11 @@ def test_cg_bytes_model():
 @pytest.mark.parametrize("n", [0, 1])
 def test_cg_bytes_small(n):
     assert bench.cg_bytes(n, n, n, n, []) == (136 + 152 + 8 * (276 + 18 + 36) + 704) * n
+
+
+def test_committed_summaries_apply_to_whole_config_only():
+    # profiles/ PMC summaries are per launch of the whole config on one GPU
+    assert bench.summaries_apply(1, 1)
+    assert not bench.summaries_apply(1, 8)   # --shard-of rehearsal
+    assert not bench.summaries_apply(2, 1)   # an N > 1 rank
+    assert not bench.summaries_apply(8, 1)
