@@ -58,6 +58,12 @@ def parse():
                     help="nccl (= RCCL, default) or gloo (rehearsal of the multi-rank path on one GPU)")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="single-process rehearsal: run rank 0's shard of an N-way strong split (timing only)")
+    ap.add_argument("--ba-deadline", type=float, default=120.0,
+                    help="N > 1: seconds the LM phase may take before its RCCL communicator is aborted (the "
+                         "failure is recorded in the line, which still prints); also the communicator's "
+                         "init / enqueue deadline")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="N > 1: torch.distributed collective timeout (s)")
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
                     help="strong (default): the config is the whole job, split over the ranks; "
                          "weak: every rank owns a config-sized shard")
@@ -93,6 +99,69 @@ def summaries_apply(world, shard_of):
     counts, the CG iteration's kernels) were measured on the whole config on
     one GPU; a line uses them only when it runs exactly that workload."""
     return world == 1 and shard_of <= 1
+
+
+class PhaseGuard:
+    """Runs the bench's later phases (K2 + exchange, the LM solve, the weak-
+    scaling line) so that a failure cannot cost the evaluation headline: an
+    exception on any rank is recorded in the line under the phase's key
+    ({"error": "rank r: ..."}) and in line["errors"], every rank then skips the
+    phases that would need the others, and the caller exits non-zero after the
+    line is printed. With world > 1 the ranks agree over `ctrl`, a gloo group on
+    the CPU (independent of the RCCL communicators' state)."""
+
+    def __init__(self, line, world, rank, ctrl=None):
+        self.line, self.world, self.rank, self.ctrl = line, world, rank, ctrl
+        self.errors = {}
+        self.failed = False
+
+    def run(self, name, fn):
+        import torch.distributed as dist
+
+        if self.failed:
+            if not isinstance(self.line.get(name), dict):
+                self.line[name] = {}
+            self.line[name]["skipped"] = "an earlier phase failed on some rank"
+            return False
+        err = None
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 - recorded in the line
+            err = f"rank {self.rank}: {type(e).__name__}: {e}"
+        if self.world > 1:
+            errs = [None] * self.world
+            dist.all_gather_object(errs, err, group=self.ctrl)
+            errs = [e for e in errs if e]
+        else:
+            errs = [err] if err else []
+        if errs:
+            self.failed = True
+            self.errors[name] = errs
+            if not isinstance(self.line.get(name), dict):
+                self.line[name] = {}
+            self.line[name]["error"] = "; ".join(errs)
+            self.line["errors"] = self.errors
+        return not errs
+
+
+def injected_failure(spec, rank):
+    """Test hook (MVBA_BENCH_INJECT="exchange@R"): rank R's LM-phase exchange
+    fails, to rehearse the failure path of an N > 1 run."""
+    if not spec:
+        return False
+    what, _, who = spec.partition("@")
+    return what == "exchange" and who.isdigit() and int(who) == rank
+
+
+class FailingExchange:
+    """An exchange callback that fails at its first call (injected failure)."""
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.calls = 0
+
+    def __call__(self, ptr, count, op, stream=0):
+        raise RuntimeError("injected exchange failure (MVBA_BENCH_INJECT)")
 
 
 def _free_port():
@@ -214,7 +283,7 @@ def _stream_copy_gbs(torch, stream, nbytes=1 << 30, reps=10):
     return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
-PROFILE_ROUNDS = ("r03", "r02", "r01")  # newest first: committed PMC summaries are read from here
+PROFILE_ROUNDS = ("r04", "r03", "r02", "r01")  # newest first: committed PMC summaries are read from here
 
 
 def _profile_path(name):
@@ -226,11 +295,13 @@ def _profile_path(name):
     return os.path.join(here, "profiles", PROFILE_ROUNDS[-1], name)
 
 
-def _pmc_traffic(config):
-    """HBM bytes per K1 launch from the committed PMC summary of this config
+def _pmc_traffic(config, kind="eval"):
+    """HBM bytes per launch from the committed PMC summary of this config
     (tools/pmc_summary.py over separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-    passes of this same command; profiles/), or None."""
-    path = _profile_path(f"pmc_k1_{config}.json")
+    passes of this same command; profiles/), or None. kind "eval": the
+    one-launch evaluation (k_eval, pmc_eval_<cfg>.json); "k1": the split form's
+    K1 (k_obs, pmc_k1_<cfg>.json)."""
+    path = _profile_path(f"pmc_{'eval' if kind == 'eval' else 'k1'}_{config}.json")
     try:
         with open(path) as f:
             return float(json.load(f)["traffic_bytes_per_launch"])
@@ -435,12 +506,19 @@ def main():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
+        from datetime import timedelta
+
+        tmo = timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=tmo)
+        # control group on the CPU: ranks agree on phase failures over it,
+        # whatever state the RCCL communicators are in
+        ctrl = dist.new_group(backend="gloo", timeout=tmo)
     else:
         torch.cuda.set_device(0)
+        ctrl = None
     dev = torch.cuda.current_device()
 
     cfg = dict(rig.CONFIGS[args.config])
@@ -505,11 +583,21 @@ def main():
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        ev.sync(sh)  # raises on device-side errors (alpha out of range)
-        # Per-kernel times: the same K steps again, each split into its prep and
-        # K1 launches with HIP events on the launch stream between them. Events
-        # between kernels cost the step ~10 us (c2: 114 vs 104 us per step;
-        # tools/step_overhead.py), so the timed loop above carries none.
+        ev.sync(sh)  # raises on device-side errors (alpha out of range, fused wait given up)
+        # Per-launch times, from the same K steps run again with HIP events on
+        # the launch stream (events between kernels cost the step ~10 us, c2 114
+        # vs 104 us, tools/step_overhead.py, so the timed loop above has none):
+        # (1) the launch the timed loop runs (one k_eval / k_eval_local launch
+        # for a one-model problem, mvba_eval_form), events around each step;
+        # (2) the split form beside it: the prep launch, then K1 (k_obs) alone.
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+        for k in range(args.steps):
+            evs[k][0].record(stream)
+            step()
+            evs[k][1].record(stream)
+        torch.cuda.synchronize()
+        ev.sync(sh)
+        launch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         for k in range(args.steps):
             step(evs[k])
@@ -523,27 +611,39 @@ def main():
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-            mine = torch.tensor([1e3 * dt / args.steps, prep_ms, obs_ms, float(n), 1e3 * t_issue / args.steps],
-                                dtype=torch.float64, device="cuda")
+            mine = torch.tensor([1e3 * dt / args.steps, prep_ms, obs_ms, float(n), 1e3 * t_issue / args.steps,
+                                 launch_ms], dtype=torch.float64, device="cuda")
             allr = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(allr, mine)
             rows = [r.cpu().tolist() for r in allr]
-            per_rank = {"ms_per_step": [r[0] for r in rows], "prep_ms": [r[1] for r in rows],
-                        "kernel_ms": [r[2] for r in rows], "num_residuals": [int(r[3]) for r in rows],
+            per_rank = {"ms_per_step": [r[0] for r in rows], "launch_ms": [r[5] for r in rows],
+                        "split_prep_ms": [r[1] for r in rows], "split_k1_ms": [r[2] for r in rows],
+                        "num_residuals": [int(r[3]) for r in rows],
                         "host_issue_ms_per_step": [r[4] for r in rows]}
         del res, jac
         time_eval.host_issue_ms = 1e3 * t_issue / args.steps
-        return float(t.item()), float(tot.item()) * args.steps, prep_ms, obs_ms, per_rank
+        return float(t.item()), float(tot.item()) * args.steps, prep_ms, obs_ms, launch_ms, per_rank
 
     ev = Evaluator(P, device=dev)
     ev.set_params()
     n = ev.num_residuals
-    dt_max, total_evals, prep_ms, obs_ms, per_rank = time_eval(ev)
+    dt_max, total_evals, prep_ms, obs_ms, launch_ms, per_rank = time_eval(ev)
 
     if world == 1 and args.shard_of > 1:  # timing rehearsal, not a bench line
         cfg["shard_rehearsal"] = f"rank 0's shard of a {args.shard_of}-way landmark split, one process"
+    form = ev.eval_form()
+    model = cfg["models"][0]
     bytes_eval = ev.eval_bytes(True)                 # algorithmic bytes of K1 per launch set
-    achieved = bytes_eval / (obs_ms * 1e-3) / 1e9    # GB/s
+    bytes_prep = ev.eval_bytes_prep()                # the prep's (landmark gather + K0 frame records)
+    k1_achieved = bytes_eval / (obs_ms * 1e-3) / 1e9
+    if form == _lib.FORM_SPLIT:
+        # several camera models: the timed step is the prep launch + one K1 launch
+        # per model group; the roofline is K1's
+        kname, kernel_ms, bytes_launch, traffic_kind = f"k_obs<{model}> (K1)", obs_ms, bytes_eval, "k1"
+    else:
+        kname = f"{_lib.FORM_NAMES[form]}<{model}>"
+        kernel_ms, bytes_launch, traffic_kind = launch_ms, bytes_eval + bytes_prep, "eval"
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9    # GB/s
     line = {
         "metric": "residual+Jacobian evals/sec (3-cam rig, 1M obs)",
         "value": total_evals / dt_max,
@@ -572,20 +672,33 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_obs<radtan> (K1)",
+            "kernel": kname,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": _pmc_traffic(args.config) if whole_cfg else None,
+            "traffic": _pmc_traffic(args.config, traffic_kind) if whole_cfg else None,
             **({} if whole_cfg else {"traffic_note": "null: the committed PMC summaries (profiles/) are per "
                                      "launch of the whole single-GPU config, not of this rank's shard"}),
-            "bytes_per_launch": bytes_eval,
-            "kernel_ms": obs_ms,
-            "prep_ms": prep_ms,
-            "kernel_timing": "HIP events on the launch stream around the prep and K1 launches of K "
-                             "instrumented steps run right after the timed loop (the timed loop has no "
-                             "events: they add ~10 us per step)",
+            "bytes_per_launch": bytes_launch,
+            "bytes_note": "K1's algorithmic bytes (per observation 16 meas + 4 point index + 24 landmark + 16 "
+                          "residual + 16 per written Jacobian column)"
+                          + ("" if form == _lib.FORM_SPLIT else
+                             " + the prep's in the same launch (per landmark 65, per frame 1,456)"),
+            "kernel_ms": kernel_ms,
+            "kernel_timing": "HIP events on the launch stream around each launch of K instrumented steps run "
+                             "right after the timed loop (the timed loop has no events: they add ~10 us per "
+                             "step); the launch is the one the timed loop runs (mvba_eval_form)",
+            "split_form": {
+                "what": "the same evaluation as two launches (prep, then K1 = k_obs), event-timed",
+                "kernel": f"k_obs<{model}> (K1)",
+                "kernel_ms": obs_ms,
+                "prep_ms": prep_ms,
+                "bytes_per_launch": bytes_eval,
+                "achieved": k1_achieved,
+                "frac": k1_achieved / HBM_PEAK_GBS,
+                "traffic": _pmc_traffic(args.config, "k1") if whole_cfg else None,
+            },
         },
         "gen_s": t_gen,
         # host time to enqueue one step (Python + ctypes + the launches): when it
@@ -603,10 +716,15 @@ def main():
     # fp64 arithmetic of the same launch (PMC instruction counts): the second
     # roofline, to name the binding resource
     flops_tab = _pmc_flops(args.config) if whole_cfg else {}
-    k1_flops = next((v["fp64_flops"] for k, v in flops_tab.items()
-                     if k.startswith("mvba::k_obs<") and k.endswith("double>")), None)
+    if form == _lib.FORM_SPLIT:
+        k1_flops = next((v["fp64_flops"] for k, v in flops_tab.items()
+                         if k.startswith("mvba::k_obs<") and k.endswith("double>")), None)
+    else:
+        pre = "mvba::k_eval<" if form == _lib.FORM_FUSED else "mvba::k_eval_local<"
+        k1_flops = next((v["fp64_flops"] for k, v in flops_tab.items()
+                         if k.startswith(pre) and k.endswith("double, true>")), None)
     if k1_flops is not None:
-        tf = k1_flops / (obs_ms * 1e-3) / 1e12
+        tf = k1_flops / (kernel_ms * 1e-3) / 1e12
         line["roofline"]["fp64_flops_per_launch"] = k1_flops
         line["roofline"]["fp64_tflops"] = tf
         line["roofline"]["fp64_peak_tflops"] = FP64_PEAK_TFLOPS
@@ -702,257 +820,317 @@ def main():
     from multiview_amd.dist import NormalEquationBuffer, check_layouts_agree
 
     L = ev.lin_layout()
-    lin = None
-    if L["supported"]:
-        if world > 1:
-            check_layouts_agree(L, P.block_size, device="cuda")
-        buf = NormalEquationBuffer(L, device="cuda")
-        pg = torch.empty(3 * L["num_points"], dtype=torch.float64, device="cuda")
-        ph = torch.empty(6 * L["num_points"], dtype=torch.float64, device="cuda")
 
-        def lin_step(events=None):
-            if events is not None:
-                events[0].record(stream)
-            ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, apply_loss=True,
-                                robust_threshold=3.0, stream=sh)
-            if events is not None:
-                events[1].record(stream)
+    def phase_lin():
+        lin = None
+        if L["supported"]:
             if world > 1:
-                buf.allreduce()
-            if events is not None:
-                events[2].record(stream)
+                check_layouts_agree(L, P.block_size, device="cuda")
+            buf = NormalEquationBuffer(L, device="cuda")
+            pg = torch.empty(3 * L["num_points"], dtype=torch.float64, device="cuda")
+            ph = torch.empty(6 * L["num_points"], dtype=torch.float64, device="cuda")
 
-        for _ in range(args.warmup):
-            lin_step()
-        torch.cuda.synchronize()
-        levs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(args.steps):
-            lin_step(levs[k])
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        ldt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(ldt, op=dist.ReduceOp.MAX)
-        ev.sync(sh)
-        lin_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in levs]))
-        ar_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in levs]))
-        lin = {
-            "what": "K2 linearization (Cauchy-corrected J^T r, block-diagonal J^T J: camera side "
-                    "via fp64 MFMA Gram + in-block expansion, point side on a second stream) + RCCL "
-                    "all-reduce of the camera blocks",
-            "evals_per_s": total_evals / float(ldt.item()),
-            "ms_per_step": 1e3 * float(ldt.item()) / args.steps,
-            "kernel_ms": lin_ms,
-            "allreduce_ms": ar_ms if world > 1 else 0.0,
-            "allreduce_bytes": buf.payload_bytes if world > 1 else 0,
-            "cam_params": L["cam_grad_size"],
-        }
+            def lin_step(events=None):
+                if events is not None:
+                    events[0].record(stream)
+                ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, apply_loss=True,
+                                    robust_threshold=3.0, stream=sh)
+                if events is not None:
+                    events[1].record(stream)
+                if world > 1:
+                    buf.allreduce()
+                if events is not None:
+                    events[2].record(stream)
 
-        # the two sides timed alone (same stream, HIP events, parameters and K0
-        # records unchanged): camera side = k_frame_lin + replica reduce,
-        # point side = k_points_lin on the library's second stream
-        def side_ms(side):
-            kw = dict(apply_loss=True, robust_threshold=3.0, stream=sh, skip_prep=True, side=side)
             for _ in range(args.warmup):
-                ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, **kw)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for _ in range(args.steps):
-                ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, **kw)
-            e1.record(stream)
-            e1.synchronize()
-            return e0.elapsed_time(e1) / args.steps
+                lin_step()
+            torch.cuda.synchronize()
+            levs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k in range(args.steps):
+                lin_step(levs[k])
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            ldt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+            if world > 1:
+                dist.all_reduce(ldt, op=dist.ReduceOp.MAX)
+            ev.sync(sh)
+            lin_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in levs]))
+            ar_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in levs]))
+            lin = {
+                "what": "K2 linearization (Cauchy-corrected J^T r, block-diagonal J^T J: camera side "
+                        "via fp64 MFMA Gram + in-block expansion, point side on a second stream) + RCCL "
+                        "all-reduce of the camera blocks",
+                "evals_per_s": total_evals / float(ldt.item()),
+                "ms_per_step": 1e3 * float(ldt.item()) / args.steps,
+                "kernel_ms": lin_ms,
+                "allreduce_ms": ar_ms if world > 1 else 0.0,
+                "allreduce_bytes": buf.payload_bytes if world > 1 else 0,
+                "cam_params": L["cam_grad_size"],
+            }
 
-        cam_ms, pts_ms = side_ms("camera"), side_ms("points")
-        # what an LM iteration pays: after a successful step the solver
-        # linearizes at the candidate whose frame records its evaluation
-        # already stored (SKIP_PREP: both sides, no prep launch)
-        lin["kernel_ms_records_current"] = side_ms("both")
-        lin["records_current_note"] = ("K2 + replica reduce with the frame records current (SKIP_PREP), as "
-                                       "mvba_solve linearizes after a successful LM step; kernel_ms includes "
-                                       "the prep launch (first linearization at a new point)")
-        mfma = float(ev.lib.mvba_lin_mfma_flops(ev.h))
-        lin["camera_side_ms"] = cam_ms
-        lin["point_side_ms"] = pts_ms
-        # X1 evidence (north_star: MFMA for the dense normal-equation blocks):
-        # fp64 MFMA work issued by the camera-side Gram kernel against the
-        # MI355X fp64 matrix peak, over the camera side's time
-        lin["mfma"] = {
-            "kernel": "k_frame_lin (v_mfma_f64_16x16x4f64)",
-            "flops_per_launch": mfma,
-            "achieved_tflops": mfma / (cam_ms * 1e-3) / 1e12,
-            "peak_tflops": FP64_PEAK_TFLOPS,
-            "util": mfma / (cam_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-            "note": "issued MFMA flops (zero-padded tile columns included) / camera-side time "
-                    "(Gram + expansion + replica reduce)",
-        }
-        # fused mode: 48 B per evaluation (observation record +
-        # landmark) against the fp64 work of the linearization kernels
-        # the fused launch is k_frame_lin<model, deg, POINTS = true> (point side as
-        # extra blocks of the same launch); the POINTS = false variant and
-        # k_points_lin belong to the camera-only / point-only phases timed above
-        fused = {k: v for k, v in flops_tab.items()
-                 if k.startswith(("mvba::k_prep", "mvba::k_rep_reduce"))
-                 or (k.startswith("mvba::k_frame_lin<") and k.endswith("true>"))}
-        lin_flops = _flops_of(fused, [""]) if fused else None
-        lin_bytes = 48.0 * n
-        lin["hbm_bytes"] = lin_bytes
-        lin["hbm_frac"] = lin_bytes / (lin_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-        if lin_flops is not None:
-            tf = lin_flops / (lin_ms * 1e-3) / 1e12
-            lin["fp64_flops"] = lin_flops
-            lin["fp64_mfma_flops"] = sum(v["fp64_mfma_flops"] for v in fused.values())
-            lin["fp64_tflops"] = tf
-            lin["fp64_frac"] = tf / FP64_PEAK_TFLOPS
-            lin["bound_us"] = 1e6 * max(lin_bytes / (HBM_PEAK_GBS * 1e9), lin_flops / (FP64_PEAK_TFLOPS * 1e12))
-            lin["binding"] = "fp64" if lin_flops / FP64_PEAK_TFLOPS / 1e12 > lin_bytes / HBM_PEAK_GBS / 1e9 else "hbm"
-    line["linearize"] = lin
+            # the two sides timed alone (same stream, HIP events, parameters and K0
+            # records unchanged): camera side = k_frame_lin + replica reduce,
+            # point side = k_points_lin on the library's second stream
+            def side_ms(side):
+                kw = dict(apply_loss=True, robust_threshold=3.0, stream=sh, skip_prep=True, side=side)
+                for _ in range(args.warmup):
+                    ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, **kw)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(args.steps):
+                    ev.linearize_device(buf.grad, buf.hess, pg, ph, buf.cost, **kw)
+                e1.record(stream)
+                e1.synchronize()
+                return e0.elapsed_time(e1) / args.steps
+
+            cam_ms, pts_ms = side_ms("camera"), side_ms("points")
+            # what an LM iteration pays: after a successful step the solver
+            # linearizes at the candidate whose frame records its evaluation
+            # already stored (SKIP_PREP: both sides, no prep launch)
+            lin["kernel_ms_records_current"] = side_ms("both")
+            lin["records_current_note"] = ("K2 + replica reduce with the frame records current (SKIP_PREP), as "
+                                           "mvba_solve linearizes after a successful LM step; kernel_ms includes "
+                                           "the prep launch (first linearization at a new point)")
+            mfma = float(ev.lib.mvba_lin_mfma_flops(ev.h))
+            lin["camera_side_ms"] = cam_ms
+            lin["point_side_ms"] = pts_ms
+            # X1 evidence (north_star: MFMA for the dense normal-equation blocks):
+            # fp64 MFMA work issued by the camera-side Gram kernel against the
+            # MI355X fp64 matrix peak, over the camera side's time
+            lin["mfma"] = {
+                "kernel": "k_frame_lin (v_mfma_f64_16x16x4f64)",
+                "flops_per_launch": mfma,
+                "achieved_tflops": mfma / (cam_ms * 1e-3) / 1e12,
+                "peak_tflops": FP64_PEAK_TFLOPS,
+                "util": mfma / (cam_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                "note": "issued MFMA flops (zero-padded tile columns included) / camera-side time "
+                        "(Gram + expansion + replica reduce)",
+            }
+            # fused mode: 48 B per evaluation (observation record +
+            # landmark) against the fp64 work of the linearization kernels
+            # the fused launch is k_frame_lin<model, deg, POINTS = true> (point side as
+            # extra blocks of the same launch); the POINTS = false variant and
+            # k_points_lin belong to the camera-only / point-only phases timed above
+            fused = {k: v for k, v in flops_tab.items()
+                     if k.startswith(("mvba::k_prep", "mvba::k_rep_reduce"))
+                     or (k.startswith("mvba::k_frame_lin<") and k.endswith("true>"))}
+            lin_flops = _flops_of(fused, [""]) if fused else None
+            lin_bytes = 48.0 * n
+            lin["hbm_bytes"] = lin_bytes
+            lin["hbm_frac"] = lin_bytes / (lin_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+            if lin_flops is not None:
+                tf = lin_flops / (lin_ms * 1e-3) / 1e12
+                lin["fp64_flops"] = lin_flops
+                lin["fp64_mfma_flops"] = sum(v["fp64_mfma_flops"] for v in fused.values())
+                lin["fp64_tflops"] = tf
+                lin["fp64_frac"] = tf / FP64_PEAK_TFLOPS
+                lin["bound_us"] = 1e6 * max(lin_bytes / (HBM_PEAK_GBS * 1e9), lin_flops / (FP64_PEAK_TFLOPS * 1e12))
+                lin["binding"] = "fp64" if lin_flops / FP64_PEAK_TFLOPS / 1e12 > lin_bytes / HBM_PEAK_GBS / 1e9 else "hbm"
+        line["linearize"] = lin
+
 
     # ---- phase C: Levenberg-Marquardt (mvba_solve: ITERATIVE_SCHUR replacement)
-    if L["supported"] and args.ba_iters > 0:
-        from multiview_amd.dist import Comm, SolverExchange
+    def phase_ba():
+        if L["supported"] and args.ba_iters > 0:
+            from multiview_amd.dist import Comm, SolverExchange
 
-        comm = ex = None
-        if world > 1:
-            if args.dist_backend == "nccl":
-                comm = Comm.rccl(dev)       # library-native RCCL, stream-ordered exchange
-            else:
-                ex = SolverExchange(device=dev)  # gloo rehearsal: host-staged exchange
-        solve_kw = dict(max_num_iterations=args.ba_iters, function_tolerance=0.0, gradient_tolerance=0.0,
-                        parameter_tolerance=0.0, use_loss=1, robust_threshold=3.0, allreduce=ex, comm=comm)
-        ev.set_params()
-        ev.solve(**dict(solve_kw, max_num_iterations=1), stream=sh)  # allocation + warm-up
-        ev.set_params()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        s = ev.solve(**solve_kw, stream=sh)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        bdt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-        if world > 1:
-            dist.all_reduce(bdt, op=dist.ReduceOp.MAX)
-        iters = max(s["num_iterations"], 1)
-        line["ba"] = {
-            "what": "LM iterations (Ceres-1.14 trust region, Jacobi scaling, implicit-Schur PCG with "
-                    "block-Jacobi preconditioner, Cauchy loss 3.0), all blocks floating",
-            "iters_per_s": iters / float(bdt.item()),
-            "ms_per_iter": 1e3 * float(bdt.item()) / iters,
-            "lm_iterations": s["num_iterations"],
-            "successful_steps": s["num_successful_steps"],
-            "cg_iterations": s["num_linear_iterations"],
-            # pass B / K2 accumulate shared camera entries with fp64 atomics, so
-            # the CG count (and LM it/s) varies run to run; this one does not
-            "ms_per_cg_iteration": 1e3 * s["linear_solver_time_s"] / max(s["num_linear_iterations"], 1),
-            "linearize_s": s["linearize_time_s"],
-            "linear_solver_s": s["linear_solver_time_s"],
-            "eval_s": s["eval_time_s"],
-            "initial_cost": s["initial_cost"],
-            "final_cost": s["final_cost"],
-            "exchange": ("rccl (mvba_comm_allreduce, stream-ordered)" if comm else
-                         "gloo (host-staged callback)" if ex else "none (single rank)"),
-            "exchange_calls": ex.calls if ex else None,
-        }
-        if ev.num_depth == 0:
-            cgb = cg_bytes(ev.num_residuals, int(L["num_points"]), ev.num_frames, int(L["cam_grad_size"]),
-                           P.camera_dist_size)
-            wall_ms = line["ba"]["ms_per_cg_iteration"]
-            roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                    "bytes_per_cg_iteration": cgb,
-                    "achieved_wall": cgb / (wall_ms * 1e-3) / 1e9,
-                    "frac_wall": cgb / (wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "wall_note": "algorithmic bytes / (linear-solver wall time / CG iterations): includes the "
-                                 "residual-reset products (every 10th), the per-solve setup and host reads"}
-            summ = _ba_summary(args.config)
-            if summ and whole_cfg:
-                kus = summ["kernel_us_per_cg_iteration"]
-                roof.update({
-                    "kernel_us": kus,
-                    "achieved": cgb / (kus * 1e-6) / 1e9,
-                    "frac": cgb / (kus * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                    "traffic": summ["traffic_bytes_per_cg_iteration"],
-                    "traffic_ratio": summ["traffic_bytes_per_cg_iteration"] / cgb,
-                    "valu_floor_us": summ["valu_floor_us"],
-                    "valu_frac": summ["valu_floor_us"] / kus,
-                    "source": summ["path"] + " (rocprofv3 kernel trace: median span of non-gated iterations "
-                              "pass A -> update, boundaries included; FETCH_SIZE x2 + WRITE_SIZE and "
-                              "SQ_INSTS_VALU per kernel, median of non-gated launches)",
-                })
-            line["ba"]["roofline"] = roof
-        if world > 1:
-            # the per-CG-iteration exchange alone: one all-reduce of the
-            # camera-side product vector (cam_grad_size doubles), on the solver's
-            # stream, HIP events around K of them
-            ng = int(L["cam_grad_size"])
-            vbuf = torch.ones(ng, dtype=torch.float64, device="cuda")
-
-            def xchg():
-                if comm is not None:
-                    comm.allreduce(vbuf.data_ptr(), ng, 0, sh)
+            comm = ex = None
+            if world > 1:
+                if args.dist_backend == "nccl":
+                    # library-native RCCL, stream-ordered exchange; non-blocking
+                    # communicator whose init and enqueues fail past the deadline
+                    comm = Comm.rccl(dev, timeout_s=args.ba_deadline)
                 else:
-                    ex(vbuf.data_ptr(), ng, 0, sh)
-
-            for _ in range(args.warmup):
-                xchg()
-            torch.cuda.synchronize()
-            dist.barrier()
-            xe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            t0 = time.perf_counter()
-            xe[0].record(stream)
-            for _ in range(args.steps):
-                xchg()
-            xe[1].record(stream)
-            xe[1].synchronize()
-            host_us = 1e6 * (time.perf_counter() - t0) / args.steps
-            line["ba"]["exchange_us_per_cg_iteration"] = 1e3 * xe[0].elapsed_time(xe[1]) / args.steps
-            line["ba"]["exchange_host_us_per_call"] = host_us
-            line["ba"]["exchange_bytes_per_cg_iteration"] = 8 * ng
-            del vbuf
-        if world == 1:
-            # deterministic mode (fixed-order slab gathers instead of fp64 atomics):
-            # same LM iterations, reproducible CG count; its cost per CG iteration
+                    ex = SolverExchange(device=dev)  # gloo rehearsal: host-staged exchange
+            inject = injected_failure(os.environ.get("MVBA_BENCH_INJECT", ""), rank)
+            if inject and ex is not None:
+                ex = FailingExchange(ex)
+            elif inject and comm is not None:
+                comm.abort()  # this rank's exchanges fail; its peers meet the deadline
+            resources["comm"] = comm
+            solve_kw = dict(max_num_iterations=args.ba_iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                            parameter_tolerance=0.0, use_loss=1, robust_threshold=3.0, allreduce=ex, comm=comm)
             ev.set_params()
-            ev.solve(**dict(solve_kw, max_num_iterations=1, deterministic=1), stream=sh)
+            ev.solve(**dict(solve_kw, max_num_iterations=1), stream=sh)  # allocation + warm-up
             ev.set_params()
+            if world > 1:
+                dist.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            sd = ev.solve(**dict(solve_kw, deterministic=1), stream=sh)
+            s = ev.solve(**solve_kw, stream=sh)
             torch.cuda.synchronize()
-            ddt = time.perf_counter() - t0
-            line["ba_deterministic"] = {
-                "what": "the same LM run with mvba_solver_options.deterministic = 1",
-                "iters_per_s": max(sd["num_iterations"], 1) / ddt,
-                "cg_iterations": sd["num_linear_iterations"],
-                "ms_per_cg_iteration": 1e3 * sd["linear_solver_time_s"] / max(sd["num_linear_iterations"], 1),
-                "linearize_s": sd["linearize_time_s"],
-                "final_cost": sd["final_cost"],
+            if world > 1:
+                dist.barrier()
+            bdt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+            if world > 1:
+                dist.all_reduce(bdt, op=dist.ReduceOp.MAX)
+            iters = max(s["num_iterations"], 1)
+            line["ba"] = {
+                "what": "LM iterations (Ceres-1.14 trust region, Jacobi scaling, implicit-Schur PCG with "
+                        "block-Jacobi preconditioner, Cauchy loss 3.0), all blocks floating",
+                "iters_per_s": iters / float(bdt.item()),
+                "ms_per_iter": 1e3 * float(bdt.item()) / iters,
+                "lm_iterations": s["num_iterations"],
+                "successful_steps": s["num_successful_steps"],
+                "cg_iterations": s["num_linear_iterations"],
+                # pass B / K2 accumulate shared camera entries with fp64 atomics, so
+                # the CG count (and LM it/s) varies run to run; this one does not
+                "ms_per_cg_iteration": 1e3 * s["linear_solver_time_s"] / max(s["num_linear_iterations"], 1),
+                "linearize_s": s["linearize_time_s"],
+                "linear_solver_s": s["linear_solver_time_s"],
+                "eval_s": s["eval_time_s"],
+                "initial_cost": s["initial_cost"],
+                "final_cost": s["final_cost"],
+                "exchange": ("rccl (mvba_comm_allreduce, stream-ordered)" if comm else
+                             "gloo (host-staged callback)" if ex else "none (single rank)"),
+                "exchange_calls": ex.calls if ex else None,
             }
-        if comm is not None:
-            comm.close()
+            if ev.num_depth == 0:
+                cgb = cg_bytes(ev.num_residuals, int(L["num_points"]), ev.num_frames, int(L["cam_grad_size"]),
+                               P.camera_dist_size)
+                wall_ms = line["ba"]["ms_per_cg_iteration"]
+                roof = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                        "bytes_per_cg_iteration": cgb,
+                        "achieved_wall": cgb / (wall_ms * 1e-3) / 1e9,
+                        "frac_wall": cgb / (wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "wall_note": "algorithmic bytes / (linear-solver wall time / CG iterations): includes the "
+                                     "residual-reset products (every 10th), the per-solve setup and host reads"}
+                summ = _ba_summary(args.config)
+                if summ and whole_cfg:
+                    kus = summ["kernel_us_per_cg_iteration"]
+                    roof.update({
+                        "kernel_us": kus,
+                        "achieved": cgb / (kus * 1e-6) / 1e9,
+                        "frac": cgb / (kus * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                        "traffic": summ["traffic_bytes_per_cg_iteration"],
+                        "traffic_ratio": summ["traffic_bytes_per_cg_iteration"] / cgb,
+                        "valu_floor_us": summ["valu_floor_us"],
+                        "valu_frac": summ["valu_floor_us"] / kus,
+                        "source": summ["path"] + " (rocprofv3 kernel trace: median span of non-gated iterations "
+                                  "pass A -> update, boundaries included; FETCH_SIZE x2 + WRITE_SIZE and "
+                                  "SQ_INSTS_VALU per kernel, median of non-gated launches)",
+                    })
+                line["ba"]["roofline"] = roof
+            if world > 1:
+                # the per-CG-iteration exchange alone: one all-reduce of the
+                # camera-side product vector (cam_grad_size doubles), on the solver's
+                # stream, HIP events around K of them
+                ng = int(L["cam_grad_size"])
+                vbuf = torch.ones(ng, dtype=torch.float64, device="cuda")
+
+                def xchg():
+                    if comm is not None:
+                        comm.allreduce(vbuf.data_ptr(), ng, 0, sh)
+                    else:
+                        ex(vbuf.data_ptr(), ng, 0, sh)
+
+                for _ in range(args.warmup):
+                    xchg()
+                torch.cuda.synchronize()
+                dist.barrier()
+                xe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                t0 = time.perf_counter()
+                xe[0].record(stream)
+                for _ in range(args.steps):
+                    xchg()
+                xe[1].record(stream)
+                xe[1].synchronize()
+                host_us = 1e6 * (time.perf_counter() - t0) / args.steps
+                line["ba"]["exchange_us_per_cg_iteration"] = 1e3 * xe[0].elapsed_time(xe[1]) / args.steps
+                line["ba"]["exchange_host_us_per_call"] = host_us
+                line["ba"]["exchange_bytes_per_cg_iteration"] = 8 * ng
+                del vbuf
+            if world == 1:
+                # deterministic mode (fixed-order slab gathers instead of fp64 atomics):
+                # same LM iterations, reproducible CG count; its cost per CG iteration
+                ev.set_params()
+                ev.solve(**dict(solve_kw, max_num_iterations=1, deterministic=1), stream=sh)
+                ev.set_params()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                sd = ev.solve(**dict(solve_kw, deterministic=1), stream=sh)
+                torch.cuda.synchronize()
+                ddt = time.perf_counter() - t0
+                line["ba_deterministic"] = {
+                    "what": "the same LM run with mvba_solver_options.deterministic = 1",
+                    "iters_per_s": max(sd["num_iterations"], 1) / ddt,
+                    "cg_iterations": sd["num_linear_iterations"],
+                    "ms_per_cg_iteration": 1e3 * sd["linear_solver_time_s"] / max(sd["num_linear_iterations"], 1),
+                    "linearize_s": sd["linearize_time_s"],
+                    "final_cost": sd["final_cost"],
+                }
+            if comm is not None:
+                resources["comm"] = None
+                comm.close()
 
     # ---- N > 1: the weak-scaling line as well (config-sized shard per rank)
+    def phase_weak():
+        nonlocal ev
+        if world > 1 and strong:
+            ev.close()
+            Rw = rig.make_rig(**shard_cfg(False))
+            Pw = rig.build_problem(Rw, flags)
+            ev = Evaluator(Pw, device=dev)
+            ev.set_params()
+            wdt, wtot, _, _, w_launch_ms, w_per_rank = time_eval(ev)
+            line["weak"] = {
+                "what": f"weak scaling: every rank owns a {args.config}-sized shard of a {world} x larger problem",
+                "value": wtot / wdt,
+                "ms_per_step": 1e3 * wdt / args.steps,
+                "num_residuals_per_gpu": ev.num_residuals,
+                "kernel_ms": w_launch_ms,
+                "per_rank": w_per_rank,
+            }
+
+    # Phases B and C (and the weak-scaling line) run guarded: an exception on
+    # any rank, or an exchange that passes its deadline (the RCCL communicator is
+    # non-blocking with a deadline, and a watchdog aborts it if the solve
+    # overruns --ba-deadline), is recorded in the line under the phase's key and
+    # the line still prints with the evaluation headline; every rank then skips
+    # the phases that would need the others, and the process exits non-zero.
+    # Ranks agree on failures over a gloo control group (CPU, independent of
+    # RCCL state).
+    guard = PhaseGuard(line, world, rank, ctrl)
+
+    resources = {"comm": None}
+
+    def phase_ba_watched():
+        # watchdog: a solve that overruns the deadline (a peer that never joins
+        # an exchange) has its communicator aborted from this thread, so the
+        # pending collective returns and the solve raises instead of hanging
+        import threading
+
+        def fire():
+            c = resources.get("comm")
+            if c is not None:
+                print(f"bench.py: rank {rank}: LM phase past --ba-deadline {args.ba_deadline} s, aborting the "
+                      "RCCL communicator", file=sys.stderr, flush=True)
+                c.abort()
+
+        wd = threading.Timer(args.ba_deadline, fire) if world > 1 else None
+        if wd is not None:
+            wd.daemon = True
+            wd.start()
+        try:
+            phase_ba()
+        finally:
+            if wd is not None:
+                wd.cancel()
+            c = resources.get("comm")
+            if c is not None:
+                resources["comm"] = None
+                c.close()
+
+    guard.run("linearize", phase_lin)
+    if L["supported"] and args.ba_iters > 0:
+        guard.run("ba", phase_ba_watched)
     if world > 1 and strong:
-        ev.close()
-        Rw = rig.make_rig(**shard_cfg(False))
-        Pw = rig.build_problem(Rw, flags)
-        ev = Evaluator(Pw, device=dev)
-        ev.set_params()
-        wdt, wtot, _, w_obs_ms, w_per_rank = time_eval(ev)
-        line["weak"] = {
-            "what": f"weak scaling: every rank owns a {args.config}-sized shard of a {world} x larger problem",
-            "value": wtot / wdt,
-            "ms_per_step": 1e3 * wdt / args.steps,
-            "num_residuals_per_gpu": ev.num_residuals,
-            "kernel_ms": w_obs_ms,
-            "per_rank": w_per_rank,
-        }
+        guard.run("weak", phase_weak)
 
     if rank == 0 and world == 1 and args.mesh_subdiv > 0:
         line["mesh"] = mesh_bench(torch, stream, ev.num_residuals, args)
@@ -960,9 +1138,15 @@ def main():
         line["cpu_baseline"] = cpu_baseline(P, args.cpu_sample)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if world > 1:
+        # no rank exits (and has the launcher tear the others down) before rank 0
+        # has printed
+        dist.barrier(group=ctrl)
     ev.close()
     if world > 1:
         dist.destroy_process_group()
+    if guard.errors:
+        raise SystemExit(1)
 
 
 if __name__ == "__main__":

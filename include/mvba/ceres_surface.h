@@ -124,7 +124,7 @@ class BracketedCamBatch {
   }
   ~BracketedCamBatch() {
     if (h_) mvba_destroy(h_);
-    if (current_slot() == this) current_slot() = prev_;
+    unlink_current();
   }
 
   // The batch the static factories feed (throws if none is in scope).
@@ -332,6 +332,15 @@ class BracketedCamBatch {
   static BracketedCamBatch*& current_slot() {
     static thread_local BracketedCamBatch* cur = nullptr;
     return cur;
+  }
+  // Batches need not be destroyed in construction order: a batch leaves the
+  // chain from wherever it sits, so no later batch's prev_ points at freed
+  // memory (the top of the chain falls back to the next older live batch).
+  void unlink_current() {
+    BracketedCamBatch** link = &current_slot();
+    while (*link && *link != this) link = &(*link)->prev_;
+    if (*link == this) *link = prev_;
+    prev_ = nullptr;
   }
   void push_current() {
     prev_ = current_slot();

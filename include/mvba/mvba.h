@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MVBA_ABI_VERSION 5
+#define MVBA_ABI_VERSION 6
 
 /* Status codes. Non-zero codes mirror the reference's fatal checks. */
 typedef enum mvba_status {
@@ -67,7 +67,11 @@ typedef enum mvba_status {
    * (or "BracketedDepthMeshError: ..." rig_calibrator.cc:630-638 for a mesh block) */
   MVBA_E_DEPTH_BLOCK_SIZES = 7,
   /* "XYZError: The block sizes were not set up properly." rig_calibrator.cc:714-715 */
-  MVBA_E_XYZ_BLOCK_SIZES = 8
+  MVBA_E_XYZ_BLOCK_SIZES = 8,
+  /* Device-side bounded wait given up (the one-launch evaluation's frame-record
+   * hand-off, k_eval): the evaluation's outputs are not valid. No reference
+   * counterpart (the reference has no device). */
+  MVBA_E_DEVICE_WAIT = 9
 } mvba_status;
 
 /* Parameter-block order of one BracketedCamError residual block, exactly the
@@ -477,8 +481,19 @@ int64_t mvba_num_frames(const struct mvba_handle* h);
 int64_t mvba_num_points(const struct mvba_handle* h);
 /* Algorithmic HBM bytes of one materialised evaluation (residual+Jacobian),
  * per DESIGN.md: per residual 16 (meas) + 4 (point index) + 24 (point) +
- * 16 (residual) + 16 * (written Jacobian columns). */
+ * 16 (residual) + 16 * (written Jacobian columns). With MVBA_EVAL_PREP_ONLY:
+ * the prep's bytes (per landmark 65: parameters, offset, free flag, record
+ * store; per frame 1,456: descriptor, pose parameters, 144-double record). */
 double mvba_eval_bytes(const struct mvba_handle* h, int32_t flags);
+
+/* The launch form a full mvba_evaluate_device takes on this handle (ABI 6):
+ * MVBA_FORM_SPLIT = prep launch + one K1 launch per model group (several
+ * camera models); MVBA_FORM_FUSED = one k_eval launch (K0 blocks hand the
+ * frame records to the K1 waves of the same grid; >= 4 segments per frame);
+ * MVBA_FORM_LOCAL = one k_eval_local launch (each K1 wave computes its frame's
+ * record; thin landmark shards). */
+enum { MVBA_FORM_SPLIT = 0, MVBA_FORM_FUSED = 1, MVBA_FORM_LOCAL = 2 };
+int32_t mvba_eval_form(const struct mvba_handle* h);
 
 /* ---- Solver: GPU-resident Levenberg-Marquardt ----------------------------
  * Replaces ceres::Solve(options, &problem, &summary) of rig_calibrator.cc:1910-1919
@@ -514,17 +529,25 @@ typedef int32_t (*mvba_allreduce_fn)(double* device_buf, int64_t count, int32_t 
  * options.
  *   RCCL, one process per GPU: rank 0 calls mvba_comm_unique_id and the caller
  *   broadcasts the MVBA_COMM_ID_BYTES bytes (e.g. torch.distributed); every
- *   rank then calls mvba_comm_init_rccl (collective: blocks until all joined).
+ *   rank then calls mvba_comm_init_rccl (collective: returns once all joined).
+ *   The RCCL communicator is non-blocking (ncclConfig_t.blocking = 0): its init
+ *   and every collective enqueue are polled against a deadline
+ *   (mvba_comm_init_rccl_deadline; mvba_comm_init_rccl uses MVBA_COMM_TIMEOUT_S,
+ *   else 300 s), and past it the communicator is aborted and the call fails
+ *   (mvba_comm_error says why) instead of hanging the rank.
  *   Local, several shards in one process (one host thread and one HIP stream
  *   per shard; shards may share a device): mvba_comm_init_local fills
  *   comms[nranks]; the all-reduce meets the other shards' threads at enqueue
  *   time only and sums the shards' buffers on the device in rank order.
  * mvba_comm_abort releases every rank of a failed solve (RCCL: ncclCommAbort;
- * local: the waiting threads return failure). */
+ * local: the waiting threads return failure); it may be called from another
+ * thread while the owner waits on the solver's stream (a watchdog). */
 #define MVBA_COMM_ID_BYTES 128
 typedef struct mvba_comm mvba_comm;
 mvba_status mvba_comm_unique_id(uint8_t* id /* [MVBA_COMM_ID_BYTES] */);
 mvba_status mvba_comm_init_rccl(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, mvba_comm** out);
+mvba_status mvba_comm_init_rccl_deadline(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device,
+                                         double timeout_s /* <= 0: the default */, mvba_comm** out);
 mvba_status mvba_comm_init_local(int32_t nranks, const int32_t* devices, mvba_comm** comms /* [nranks] */);
 mvba_status mvba_comm_abort(mvba_comm* comm);
 void mvba_comm_destroy(mvba_comm* comm);

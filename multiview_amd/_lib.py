@@ -23,11 +23,13 @@ MVBA_E_INVALID = 5
 MVBA_E_NO_DEVICE = 6
 MVBA_E_DEPTH_BLOCK_SIZES = 7
 MVBA_E_XYZ_BLOCK_SIZES = 8
+MVBA_E_DEVICE_WAIT = 9
 
 STATUS_NAMES = {
     0: "MVBA_OK", 1: "MVBA_E_ALPHA_RANGE", 2: "MVBA_E_BLOCK_SIZES",
     3: "MVBA_E_BAD_DISTORTION", 4: "MVBA_E_HIP", 5: "MVBA_E_INVALID",
     6: "MVBA_E_NO_DEVICE", 7: "MVBA_E_DEPTH_BLOCK_SIZES", 8: "MVBA_E_XYZ_BLOCK_SIZES",
+    9: "MVBA_E_DEVICE_WAIT",
 }
 
 EVAL_RESIDUALS = 0x1
@@ -36,6 +38,10 @@ EVAL_APPLY_LOSS = 0x4
 EVAL_PREP_ONLY = 0x8
 EVAL_SKIP_PREP = 0x10
 EVAL_DEPTH = 0x100
+
+# mvba_eval_form: the launch form of a full evaluation
+FORM_SPLIT, FORM_FUSED, FORM_LOCAL = 0, 1, 2
+FORM_NAMES = {FORM_SPLIT: "split", FORM_FUSED: "k_eval", FORM_LOCAL: "k_eval_local"}
 
 # Jacobian row bases (MVBA_JAC_BASE_*), block order of rig_calibrator.cc:1695-1699.
 JAC_BASE = (0, 14, 28, 42, 48, 50, 52, 56)
@@ -253,6 +259,7 @@ SIGNATURES = {
     "mvba_num_frames": (C.c_int64, [C.c_void_p]),
     "mvba_num_points": (C.c_int64, [C.c_void_p]),
     "mvba_eval_bytes": (C.c_double, [C.c_void_p, C.c_int32]),
+    "mvba_eval_form": (C.c_int32, [C.c_void_p]),
     "mvba_lin_layout_info": (C.c_int, [C.c_void_p, C.POINTER(LinLayout)]),
     "mvba_cam_block_map": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mvba_point_block_map": (C.c_int, [C.c_void_p, C.c_void_p]),
@@ -291,6 +298,8 @@ SIGNATURES = {
     "mvba_lin_mfma_flops": (C.c_double, [C.c_void_p]),
     "mvba_comm_unique_id": (C.c_int, [C.c_void_p]),
     "mvba_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "mvba_comm_init_rccl_deadline": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_double,
+                                               C.POINTER(C.c_void_p)]),
     "mvba_comm_init_local": (C.c_int, [C.c_int32, C.c_void_p, C.c_void_p]),
     "mvba_comm_abort": (C.c_int, [C.c_void_p]),
     "mvba_comm_destroy": (None, [C.c_void_p]),

@@ -26,7 +26,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
+#include <thread>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -100,7 +104,9 @@ struct LocalGroup {
 struct mvba_comm {
   int kind = 0;  // 0 RCCL, 1 local
   int rank = 0, nranks = 1, device = 0;
-  ncclComm_t nccl = nullptr;
+  ncclComm_t nccl = nullptr;   // non-blocking RCCL communicator (config.blocking = 0)
+  std::atomic<bool> aborted{false};
+  double timeout_s = 0.0;      // deadline of every host-side RCCL wait
   std::shared_ptr<LocalGroup> grp;
   uint64_t calls = 0;
   std::string err;
@@ -113,6 +119,35 @@ thread_local std::string g_comm_err;
 mvba_status comm_fail(const std::string& msg) {
   g_comm_err = msg;
   return MVBA_E_INVALID;
+}
+
+// Default deadline of the RCCL waits (communicator init, collective enqueue):
+// MVBA_COMM_TIMEOUT_S, else 300 s.
+double default_timeout_s() {
+  const char* v = std::getenv("MVBA_COMM_TIMEOUT_S");
+  const double t = v ? std::atof(v) : 0.0;
+  return t > 0.0 ? t : 300.0;
+}
+
+// A non-blocking communicator's calls may return ncclInProgress: poll its
+// asynchronous state until it settles, an abort is requested, or the deadline
+// passes (then the communicator is aborted, so no rank stays stuck in it).
+ncclResult_t settle(mvba_comm* c, ncclResult_t r, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r == ncclInProgress) {
+    if (c->aborted.load()) return ncclInvalidUsage;
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+      g_comm_err = std::string(what) + ": no progress within " + std::to_string(c->timeout_s) +
+                   " s (MVBA_COMM_TIMEOUT_S); communicator aborted";
+      c->aborted.store(true);
+      (void)ncclCommAbort(c->nccl);
+      return ncclSystemError;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+    if (ncclCommGetAsyncError(c->nccl, &r) != ncclSuccess) return ncclSystemError;
+  }
+  if (r != ncclSuccess && g_comm_err.empty()) g_comm_err = std::string(what) + ": " + ncclGetErrorString(r);
+  return r;
 }
 
 int32_t local_allreduce(mvba_comm* c, double* buf, int64_t n, int32_t op, hipStream_t s) {
@@ -187,7 +222,8 @@ mvba_status mvba_comm_unique_id(uint8_t* id) {
   return MVBA_OK;
 }
 
-mvba_status mvba_comm_init_rccl(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, mvba_comm** out) {
+mvba_status mvba_comm_init_rccl_deadline(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device,
+                                         double timeout_s, mvba_comm** out) {
   if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks) return comm_fail("invalid communicator arguments");
   *out = nullptr;
   if (hipSetDevice(device) != hipSuccess) return comm_fail("hipSetDevice failed");
@@ -198,13 +234,30 @@ mvba_status mvba_comm_init_rccl(const uint8_t* id, int32_t nranks, int32_t rank,
   c->rank = rank;
   c->nranks = nranks;
   c->device = device;
-  const ncclResult_t r = ncclCommInitRank(&c->nccl, nranks, u, rank);
+  c->timeout_s = timeout_s > 0.0 ? timeout_s : default_timeout_s();
+  g_comm_err.clear();
+  // non-blocking: the init returns at once and is polled against the deadline,
+  // so a rank whose peers never join gets an error instead of a hang
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&c->nccl, nranks, u, rank, &cfg);
+  if (r == ncclSuccess || r == ncclInProgress) {
+    if (r == ncclSuccess && ncclCommGetAsyncError(c->nccl, &r) != ncclSuccess) r = ncclSystemError;
+    r = settle(c, r, "ncclCommInitRankConfig");
+  } else {
+    g_comm_err = std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r);
+  }
   if (r != ncclSuccess) {
+    if (c->nccl && !c->aborted.load()) (void)ncclCommAbort(c->nccl);
     delete c;
-    return comm_fail(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    return MVBA_E_INVALID;
   }
   *out = c;
   return MVBA_OK;
+}
+
+mvba_status mvba_comm_init_rccl(const uint8_t* id, int32_t nranks, int32_t rank, int32_t device, mvba_comm** out) {
+  return mvba_comm_init_rccl_deadline(id, nranks, rank, device, 0.0, out);
 }
 
 mvba_status mvba_comm_init_local(int32_t nranks, const int32_t* devices, mvba_comm** out) {
@@ -248,8 +301,9 @@ mvba_status mvba_comm_init_local(int32_t nranks, const int32_t* devices, mvba_co
 mvba_status mvba_comm_abort(mvba_comm* c) {
   if (!c) return MVBA_E_INVALID;
   if (c->kind == 0) {
-    if (c->nccl) (void)ncclCommAbort(c->nccl);
-    c->nccl = nullptr;
+    // callable from another thread while the owner waits on a collective
+    // (a watchdog): RCCL's abort makes the pending kernels return
+    if (c->nccl && !c->aborted.exchange(true)) (void)ncclCommAbort(c->nccl);
   } else {
     c->grp->abort();
   }
@@ -259,7 +313,7 @@ mvba_status mvba_comm_abort(mvba_comm* c) {
 void mvba_comm_destroy(mvba_comm* c) {
   if (!c) return;
   if (c->kind == 0) {
-    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->nccl && !c->aborted.load()) (void)ncclCommDestroy(c->nccl);
   } else {
     std::shared_ptr<LocalGroup> G = c->grp;
     c->grp.reset();
@@ -291,11 +345,14 @@ int32_t mvba_comm_allreduce(double* device_buf, int64_t count, int32_t op, void*
   if (!c || count < 0 || (op != MVBA_REDUCE_SUM && op != MVBA_REDUCE_MAX)) return 1;
   const hipStream_t s = static_cast<hipStream_t>(hip_stream);
   if (c->kind == 1) return local_allreduce(c, device_buf, count, op, s);
-  if (!c->nccl) return 1;
+  if (!c->nccl || c->aborted.load()) return 1;
   c->calls++;
   if (count == 0) return 0;
-  const ncclResult_t r = ncclAllReduce(device_buf, device_buf, (size_t)count, ncclDouble,
-                                       op == MVBA_REDUCE_MAX ? ncclMax : ncclSum, c->nccl, s);
+  ncclResult_t r = ncclAllReduce(device_buf, device_buf, (size_t)count, ncclDouble,
+                                 op == MVBA_REDUCE_MAX ? ncclMax : ncclSum, c->nccl, s);
+  if (r == ncclInProgress) r = settle(c, r, "ncclAllReduce");
+  if (r == ncclSuccess && ncclCommGetAsyncError(c->nccl, &r) == ncclSuccess && r == ncclInProgress)
+    r = settle(c, r, "ncclAllReduce");
   return r == ncclSuccess ? 0 : 1;
 }
 

@@ -747,8 +747,8 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_order, h->order));
   chk(upload(&h->d_row_written, h->row_written));
   chk(upload(&h->d_varsize, h->pos_K));
-  chk(dalloc(&h->d_err, 1));
-  if (e == hipSuccess) chk(hipMemset(h->d_err, 0, sizeof(int)));
+  chk(dalloc(&h->d_err, 2));  // [0] alpha range (K0), [1] fused-evaluation wait given up
+  if (e == hipSuccess) chk(hipMemset(h->d_err, 0, 2 * sizeof(int)));
   {
     const int64_t nw = std::max<int64_t>(mvba_eval_ready_words(h->nframes), 1);
     chk(dalloc(&h->d_ready, (size_t)nw));
@@ -864,8 +864,25 @@ int64_t mvba_num_points(const mvba_handle* h) { return h ? h->npts : 0; }
 double mvba_eval_bytes(const mvba_handle* h, int32_t flags) {
   if (!h) return 0.0;
   if (flags & MVBA_EVAL_DEPTH) return h->bytes_dep;
+  // the prep's algorithmic bytes: per landmark the parameter
+  // read 24 + offset 8 + free flag 1 + record store 32; per frame its
+  // descriptor 128 + the 22 pose parameters 176 + the record store 1,152
+  if (flags & MVBA_EVAL_PREP_ONLY) return 65.0 * (double)h->npts + 1456.0 * (double)h->nframes;
   return h->bytes_res + ((flags & MVBA_EVAL_JACOBIAN) ? h->bytes_jac : 0.0);
 }
+
+// Which launch form a full evaluation takes (MVBA_FORM_*); MVBA_SPLIT_PREP=1 /
+// MVBA_EVAL_MODE=split|fused|local force one, for A/B timing (read per call).
+static int eval_form(const mvba_handle* h) {
+  const char* sp = std::getenv("MVBA_SPLIT_PREP");
+  const char* m = std::getenv("MVBA_EVAL_MODE");
+  const int forced = !m ? -1 : !std::strcmp(m, "split") ? 0 : !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "local") ? 2 : -1;
+  if ((sp && sp[0] == '1') || forced == 0 || h->groups.size() != 1) return MVBA_FORM_SPLIT;
+  if (forced > 0) return forced == 1 ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
+  return h->groups[0].seg_count >= 4 * h->nframes ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
+}
+
+int32_t mvba_eval_form(const mvba_handle* h) { return h ? eval_form(h) : -1; }
 
 static mvba_status ensure_outputs(mvba_handle* h) {
   if (h->d_res) return MVBA_OK;
@@ -879,6 +896,14 @@ static mvba_status ensure_outputs(mvba_handle* h) {
 
 static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double cauchy_threshold, void* d_res,
                                         void* d_J, int64_t ld, int32_t out_f32, void* stream);
+
+// Polls of a K0 ready word before a fused-evaluation wave gives up (~0.5 s at
+// the default). MVBA_EVAL_POLL_LIMIT (read per call: tests switch it) lowers it;
+// 0 makes every wave give up at once, which tests the error path.
+static unsigned eval_poll_limit() {
+  const char* v = std::getenv("MVBA_EVAL_POLL_LIMIT");
+  return v ? (unsigned)std::strtoul(v, nullptr, 10) : (1u << 24);
+}
 
 mvba_status mvba_evaluate_device(mvba_handle* h, int32_t flags, double cauchy_threshold,
                                  double* d_res, double* d_J, int64_t ld, void* stream) {
@@ -916,7 +941,7 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
     cauchy_c = 1.0 / (cauchy_threshold * cauchy_threshold);
   }
   hipError_t e = hipSuccess;
-  // One model group with at least two segments per frame: prep and K1 in one
+  // One model group with at least four segments per frame: prep and K1 in one
   // launch (K0 blocks hand their frame records to the K1 waves of the same grid;
   // c2 101.8 vs 104.5 us, c3 2.16 vs 2.24 ms per step, same box). For thin
   // shards (about one segment per frame: c2 split 8 ways) the hand-off measured
@@ -928,21 +953,16 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
   // neither a prep launch nor a hand-off sits in front of K1 (same box, rank 0's
   // shard of c2: 2-way 56.1-56.5 vs fused 61.2-61.8 us, 8-way 19.1-20.6 vs
   // split 22.1-23.6 us; whole c2 98.4-101.1 vs fused 100.3-102.0 us;
-  // profiles/r03/ab_eval_local/). MVBA_EVAL_MODE=split|fused|local forces one
-  // form, for A/B timing.
-  static const bool split = std::getenv("MVBA_SPLIT_PREP") && std::getenv("MVBA_SPLIT_PREP")[0] == '1';
-  static const char* mode_env = std::getenv("MVBA_EVAL_MODE");
-  static const int forced = !mode_env ? -1 : !std::strcmp(mode_env, "split") ? 0
-                            : !std::strcmp(mode_env, "fused") ? 1 : !std::strcmp(mode_env, "local") ? 2 : -1;
-  if (!split && forced != 0 && h->groups.size() == 1 && !(flags & (MVBA_EVAL_SKIP_PREP | MVBA_EVAL_PREP_ONLY))) {
+  // profiles/r03/ab_eval_local/). eval_form() picks; mvba_eval_form reports it.
+  const int form = (flags & (MVBA_EVAL_SKIP_PREP | MVBA_EVAL_PREP_ONLY)) ? MVBA_FORM_SPLIT : eval_form(h);
+  if (form != MVBA_FORM_SPLIT) {
     h->gen++;
     const Group& G = h->groups[0];
-    const bool fused = forced == 1 || (forced < 0 && G.seg_count >= 4 * h->nframes);
-    if (fused)
+    if (form == MVBA_FORM_FUSED)
       e = mvba_launch_eval_fused(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->nframes,
                                  h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,
                                  h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen,
-                                 h->d_err, h->d_ready, s);
+                                 h->d_err, h->d_ready, eval_poll_limit(), s);
     else
       e = mvba_launch_eval_local(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->d_frec,
                                  h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts, h->d_obs_pid,
@@ -980,10 +1000,11 @@ mvba_status mvba_sync_status(mvba_handle* h, void* stream) {
   if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
   hipError_t e = hipStreamSynchronize((hipStream_t)stream);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_sync_status");
-  int err = 0;
-  e = hipMemcpy(&err, h->d_err, sizeof(int), hipMemcpyDeviceToHost);
+  int err[2] = {0, 0};
+  e = hipMemcpy(err, h->d_err, sizeof(err), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return h->hip_fail(e, "mvba_sync_status copy");
-  if (err >= h->gen && h->gen > 0) return h->fail(MVBA_E_ALPHA_RANGE, "Out of bounds in interpolation.");
+  const mvba_status st = device_error(err, h->gen);
+  if (st != MVBA_OK) return h->fail(st, device_error_text(st));
   return MVBA_OK;
 }
 

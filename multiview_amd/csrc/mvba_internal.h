@@ -59,7 +59,7 @@ hipError_t mvba_launch_eval_fused(int model, int deg, const Segment* segs, int32
                                   const uint8_t* pt_free, int64_t npts, double4* pts, const int32_t* obs_pid,
                                   const double2* obs_meas, void* res, void* J, int64_t ld, int32_t flags,
                                   double cauchy_c, int32_t out_f32, int gen, int* err, unsigned* ready,
-                                  hipStream_t s);
+                                  unsigned poll_limit, hipStream_t s);
 hipError_t mvba_launch_eval_local(int model, int deg, const Segment* segs, int32_t nseg, const FrameDesc* fd,
                                   double* frec, const double* params, const int64_t* pt_off, const uint8_t* pt_free,
                                   int64_t npts, double4* pts, const int32_t* obs_pid, const double2* obs_meas,
@@ -132,7 +132,21 @@ struct PoseKeyHash {
 
 constexpr int kFixedSize[7] = {7, 7, 7, 3, 1, 1, 2};
 
-
+// The device error words (handle::d_err), each raised by atomicMax to the
+// generation of the evaluation that failed, so stale words are ignored:
+// [0] K0's interpolation check (rig_calibrator.cc:346), [1] a fused-evaluation
+// wave that gave up waiting for its frame record (k_eval).
+inline mvba_status device_error(const int err[2], int gen) {
+  if (gen <= 0) return MVBA_OK;
+  if (err[0] >= gen) return MVBA_E_ALPHA_RANGE;
+  if (err[1] >= gen) return MVBA_E_DEVICE_WAIT;
+  return MVBA_OK;
+}
+inline const char* device_error_text(mvba_status st) {
+  return st == MVBA_E_ALPHA_RANGE ? "Out of bounds in interpolation."
+                                  : "fused evaluation: a wave gave up waiting for its frame record (K0 block not "
+                                    "run ahead of it); outputs of this evaluation are not valid";
+}
 
 inline int rpc_degree(int n) { return static_cast<int>(std::round(std::sqrt(2.0 * n + 5.0) / 2.0 - 1.5)); }
 inline int rpc_num_dist_params(int d) { return 2 * (d + 1) * (d + 2) - 2; }

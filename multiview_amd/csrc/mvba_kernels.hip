@@ -261,7 +261,8 @@ struct FusedIn {
   const unsigned* ready;   // one word per K0 block: = epoch once its 16 frame records are stored
   unsigned epoch;
   int64_t k1_block0;       // first K1 block of the grid (a multiple of 8: XCD order kept)
-  int* err;                // error word (LOCAL: the waves run K0 themselves)
+  int* err;                // error words: [0] alpha range (K0), [1] ready-word wait given up (k_eval)
+  unsigned poll_limit;     // k_eval: polls of the ready word before a wave gives up (0: none, tests)
 };
 
 // How a K1 wave gets its frame record: kRecGlobal reads the prep kernel's
@@ -323,10 +324,19 @@ __device__ __forceinline__ void obs_body(
     // LDS area (MI355X_MICROARCH.md, visibility: valid forms, first row).
     __shared__ double srec[4][kFrameRecDoubles];
     double* sr = srec[threadIdx.x >> 6];
+    // HIP promises no dispatch order: the launch puts every K0 block in front of
+    // the K1 blocks, and on gfx950 blocks start in index order, so the wait
+    // ends within the K0 work. The wait is bounded all the same; a wave that
+    // gives up raises error word [1] to this launch's epoch, so
+    // mvba_sync_status fails (MVBA_E_DEVICE_WAIT) instead of returning
+    // residuals built from a record that may be stale.
     if (lane == 0) {
       const unsigned* w = fu.ready + (frame >> 4);  // 16 frames per K0 block
       for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != fu.epoch; n++) {
-        if (n > (1u << 24)) break;  // bounded (~0.5 s): never reached with K0 blocks dispatched first
+        if (n >= fu.poll_limit) {
+          atomicMax(fu.err + 1, (int)fu.epoch);
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
     }
@@ -1091,13 +1101,13 @@ hipError_t mvba_launch_eval_fused(int model, int deg, const mvba::Segment* segs,
                                   const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts,
                                   const int32_t* obs_pid, const double2* obs_meas, void* res, void* J, int64_t ld,
                                   int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err,
-                                  unsigned* ready, hipStream_t s) {
+                                  unsigned* ready, unsigned poll_limit, hipStream_t s) {
   if (nseg <= 0) return hipSuccess;
   const int64_t fb = mvba_eval_ready_words(nframes);
   const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
   const int64_t k1 = (fb + pb + mvba::kXcds - 1) / mvba::kXcds * mvba::kXcds;
   const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((nseg + 3) / 4));
-  const mvba::FusedIn fu{pt_off, pt_free, ready, (unsigned)gen, k1, err};
+  const mvba::FusedIn fu{pt_off, pt_free, ready, (unsigned)gen, k1, err, poll_limit};
 #define MVBA_EVF_K(M, D, OT, JC)                                                                              \
   hipLaunchKernelGGL((mvba::k_eval<M, D, OT, JC>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, nframes,      \
                      (int32_t)fb, (int32_t)pb, frec, params, npts, pts, obs_pid, obs_meas, (OT*)res, (OT*)J, ld, \
@@ -1129,7 +1139,7 @@ hipError_t mvba_launch_eval_local(int model, int deg, const mvba::Segment* segs,
   const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
   const int64_t k1 = (pb + mvba::kXcds - 1) / mvba::kXcds * mvba::kXcds;
   const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((nseg + 3) / 4));
-  const mvba::FusedIn fu{pt_off, pt_free, nullptr, (unsigned)gen, k1, err};
+  const mvba::FusedIn fu{pt_off, pt_free, nullptr, (unsigned)gen, k1, err, 0u};
 #define MVBA_EVL_K(M, D, OT, JC)                                                                               \
   hipLaunchKernelGGL((mvba::k_eval_local<M, D, OT, JC>), dim3(blocks), dim3(256), 0, s, segs, nseg, (int32_t)pb, \
                      fd, frec, params, npts, pts, obs_pid, obs_meas, (OT*)res, (OT*)J, ld, flags, cauchy_c, fu)

@@ -328,9 +328,10 @@ class Solver {
 
   void check_alpha() {
     HCHK(hipStreamSynchronize(s_));
-    int err = 0;
-    HCHK(hipMemcpy(&err, h_->d_err, sizeof(int), hipMemcpyDeviceToHost));
-    if (err >= h_->gen && h_->gen > 0) throw StatusErr{MVBA_E_ALPHA_RANGE, "Out of bounds in interpolation."};
+    int err[2] = {0, 0};
+    HCHK(hipMemcpy(err, h_->d_err, sizeof(err), hipMemcpyDeviceToHost));
+    const mvba_status st = device_error(err, h_->gen);
+    if (st != MVBA_OK) throw StatusErr{st, device_error_text(st)};
   }
 
   // Jacobian at the handle's parameters -> lin (all-reduced), G, phess, cdiag. Returns cost.
@@ -556,7 +557,8 @@ class Solver {
     // products combine it with the previous product's records (no direction
     // kernel per iteration). Depth blocks read the direction in more kernels:
     // they keep the direction kernel (MVBA_CG_DIR_KERNEL=1 forces it, for A/B).
-    static const bool dir_kernel = std::getenv("MVBA_CG_DIR_KERNEL") && std::getenv("MVBA_CG_DIR_KERNEL")[0] == '1';
+    const char* dk_env = std::getenv("MVBA_CG_DIR_KERNEL");  // read per call: tests switch it
+    const bool dir_kernel = dk_env && dk_env[0] == '1';
     const bool fused_dir = h_->ndep == 0 && !dir_kernel;
     const mvba::FrameDirZ fz{h_->d_frame_lin, h_->d_fd, h_->d_frec, S_->dirz, (int32_t)h_->nframes, 0};
     auto upd = [&](int32_t mode, const double* q, int32_t iter, bool end_logic) {

@@ -170,7 +170,10 @@ class Comm:
         self.h = handle
 
     @classmethod
-    def rccl(cls, device: int):
+    def rccl(cls, device: int, timeout_s: float = 0.0):
+        """timeout_s: deadline of the communicator's init and of every
+        collective enqueue (<= 0: MVBA_COMM_TIMEOUT_S, else 300 s); past it the
+        communicator is aborted and the call raises instead of hanging."""
         import ctypes as C
 
         import numpy as np
@@ -189,7 +192,8 @@ class Comm:
         dist.broadcast(t, 0)
         ident = np.ascontiguousarray(t.cpu().numpy())
         h = C.c_void_p()
-        st = lib.mvba_comm_init_rccl(ident.ctypes.data, dist.get_world_size(), dist.get_rank(), device, C.byref(h))
+        st = lib.mvba_comm_init_rccl_deadline(ident.ctypes.data, dist.get_world_size(), dist.get_rank(), device,
+                                              float(timeout_s), C.byref(h))
         if st != 0:
             raise _lib.MvbaError(st, lib.mvba_comm_error().decode())
         return cls(h)

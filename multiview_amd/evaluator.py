@@ -208,6 +208,14 @@ class Evaluator:
         flags = _lib.EVAL_RESIDUALS | (_lib.EVAL_JACOBIAN if jacobian else 0)
         return float(self.lib.mvba_eval_bytes(self.h, flags))
 
+    def eval_bytes_prep(self) -> float:
+        """Algorithmic bytes of the prep (landmark gather + K0 frame records)."""
+        return float(self.lib.mvba_eval_bytes(self.h, _lib.EVAL_PREP_ONLY))
+
+    def eval_form(self) -> int:
+        """Launch form of a full evaluation (_lib.FORM_SPLIT / FORM_FUSED / FORM_LOCAL)."""
+        return int(self.lib.mvba_eval_form(self.h))
+
     # ------------------------------------------------------- normal equations
     def lin_layout(self) -> dict:
         L = _lib.LinLayout()

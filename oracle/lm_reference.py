@@ -2,7 +2,8 @@
 
 Levenberg-Marquardt with the control flow of Ceres 1.14's TrustRegionMinimizer +
 LevenbergMarquardtStrategy [ext, not vendored] (the solver rig_calibrator.cc:1910-1919
-configures), with EXACT linear solves (dense Cholesky of J'J + D) in place of
+configures), with EXACT linear solves (dense LU of J'J + D; sparse LU above
+SPARSE_COLUMNS free columns) in place of
 ITERATIVE_SCHUR's truncated CG, on the Jacobian of oracle.cpp (the restatement of
 BracketedCamError, rig_calibrator.cc:419-514). Used by tests to check that
 mvba_solve converges to the same parameters. Parity unpinned (Ceres is absent from
@@ -44,7 +45,87 @@ def _columns(P):
     return col, np.array(idx, dtype=np.int64)
 
 
+# Above this many free columns the Jacobian is kept sparse (CSR) and the damped
+# normal equations are solved by sparse LU (scipy.sparse.linalg.splu): the same
+# exact step, without a dense 2N x n matrix (BASELINE c1: 10k rows x 3.4k
+# columns). Smaller problems keep the dense path.
+SPARSE_COLUMNS = 2000
+
+
+class _Triplets:
+    """COO accumulation with np.add.at's semantics (duplicates summed)."""
+
+    def __init__(self, nrows, ncols):
+        self.shape = (nrows, ncols)
+        self.r, self.c, self.v = [], [], []
+
+    def add(self, rows, cols, vals):
+        self.r.append(np.asarray(rows, dtype=np.int64).reshape(-1))
+        self.c.append(np.broadcast_to(np.asarray(cols, dtype=np.int64), np.shape(rows)).reshape(-1))
+        self.v.append(np.asarray(vals, dtype=np.float64).reshape(-1))
+
+    def csr(self):
+        import scipy.sparse as sp
+
+        cat = (lambda a, t: np.concatenate(a) if a else np.zeros(0, t))
+        return sp.coo_matrix((cat(self.v, np.float64), (cat(self.r, np.int64), cat(self.c, np.int64))),
+                             shape=self.shape).tocsr()
+
+
+def _jacobian_sparse(P, params, col, ncols, use_loss, thr):
+    """_jacobian as a CSR matrix (same entries; reprojection, depth and XYZ rows)."""
+    from multiview_amd._lib import JAC_BASE
+    Q = dataclasses.replace(P, params=params)
+    cost, r, J = oracle_py.evaluate(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
+    N = P.num_residuals
+    nrows = 2 * N + 3 * P.num_depth_residuals + 3 * P.num_xyz_residuals
+    T = _Triplets(nrows, ncols)
+    K_of = P.camera_dist_size[P.residual_camera]
+    rows = np.arange(N)
+    for b in range(8):
+        for K in (np.unique(K_of) if b == 7 else [None]):
+            sel = rows if b < 7 else rows[K_of == K]
+            n = FIXED[b] if b < 7 else int(K)
+            if n == 0 or sel.size == 0:
+                continue
+            c0 = col[P.residual_blocks[sel, b]]
+            ok = c0 >= 0
+            Jb = J[sel, JAC_BASE[b]:JAC_BASE[b] + 2 * n].reshape(-1, 2, n)
+            for k in range(n):
+                for comp in range(2):
+                    T.add(2 * sel[ok] + comp, c0[ok] + k, Jb[ok, comp, k])
+    r = r.reshape(-1)
+    row0 = 2 * N
+    if P.num_depth_residuals:
+        cd, rd, Jd = oracle_py.evaluate_depth(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
+        for j in range(P.num_depth_residuals):
+            for b in range(7):
+                bid = int(P.depth_blocks[j, b])
+                if bid < 0 or col[bid] < 0:
+                    continue
+                size = int(P.block_size[bid])
+                base = oracle_py.DJAC_BASE[b]
+                blk = Jd[j, base:base + 3 * size].reshape(3, size)
+                rr, cc = np.meshgrid(np.arange(3), np.arange(size), indexing="ij")
+                T.add(row0 + 3 * j + rr, col[bid] + cc, blk)
+        cost += cd
+        r = np.concatenate([r, rd.reshape(-1)])
+        row0 += 3 * P.num_depth_residuals
+    if P.num_xyz_residuals:
+        cx, rx, Jx = oracle_py.evaluate_xyz(Q, apply_loss=use_loss)
+        for j in range(P.num_xyz_residuals):
+            c0 = col[int(P.xyz_block[j])]
+            if c0 >= 0:
+                rr, cc = np.meshgrid(np.arange(3), np.arange(3), indexing="ij")
+                T.add(row0 + 3 * j + rr, c0 + cc, Jx[j].reshape(3, 3))
+        cost += cx
+        r = np.concatenate([r, rx.reshape(-1)])
+    return cost, r, T.csr()
+
+
 def _jacobian(P, params, col, ncols, use_loss, thr):
+    if ncols > SPARSE_COLUMNS:
+        return _jacobian_sparse(P, params, col, ncols, use_loss, thr)
     from multiview_amd._lib import JAC_BASE
     Q = dataclasses.replace(P, params=params)
     cost, r, J = oracle_py.evaluate(Q, oracle_py.ANALYTIC, apply_loss=use_loss, robust_threshold=thr)
@@ -133,10 +214,27 @@ def solve(P, max_num_iterations=50, function_tolerance=1e-6, gradient_tolerance=
         p[idx] = x
         return p
 
+    sparse = n > SPARSE_COLUMNS
+
+    def colsq(J):
+        return np.asarray(J.multiply(J).sum(axis=0)).reshape(-1) if sparse else np.einsum("ij,ij->j", J, J)
+
+    def damped_step(J, s, c, g, radius):
+        if not sparse:
+            Js = J * s
+            As = Js.T @ Js + np.diag(np.clip(s * s * c, 1e-6, 1e32) / radius)
+            return -s * np.linalg.solve(As, s * g)
+        import scipy.sparse as sp
+        from scipy.sparse.linalg import splu
+
+        Js = J @ sp.diags(s)
+        As = (Js.T @ Js + sp.diags(np.clip(s * s * c, 1e-6, 1e32) / radius)).tocsc()
+        return -s * splu(As).solve(s * g)
+
     x = params[idx].copy()
     cost, r, J = _jacobian(P, with_x(x), col, n, use_loss, robust_threshold)
     g = J.T @ r
-    c = np.einsum("ij,ij->j", J, J)
+    c = colsq(J)
     s = 1.0 / (1.0 + np.sqrt(c)) if jacobi_scaling else np.ones(n)
     gmax = np.abs(x - plus(x, -g)).max() if n else 0.0
     radius, decrease = initial_trust_region_radius, 2.0
@@ -157,9 +255,7 @@ def solve(P, max_num_iterations=50, function_tolerance=1e-6, gradient_tolerance=
         # (TrustRegionMinimizer + LevenbergMarquardtStrategy [ext]); the same step
         # as (J'J + D)^-1 g in exact arithmetic, but far better conditioned when
         # column norms span many decades (RPC degree >= 5: cond 1e46 unscaled).
-        Js = J * s
-        As = Js.T @ Js + np.diag(np.clip(s * s * c, 1e-6, 1e32) / radius)
-        delta = -s * np.linalg.solve(As, s * g)
+        delta = damped_step(J, s, c, g, radius)
         Jd = J @ delta
         mcc = -(g @ delta + 0.5 * Jd @ Jd)
         if not (mcc > 0):
@@ -183,7 +279,7 @@ def solve(P, max_num_iterations=50, function_tolerance=1e-6, gradient_tolerance=
             x = xn
             cost, r, J = _jacobian(P, with_x(x), col, n, use_loss, robust_threshold)
             g = J.T @ r
-            c = np.einsum("ij,ij->j", J, J)
+            c = colsq(J)
             gmax = np.abs(x - plus(x, -g)).max()
             radius = min(1e16, radius / max(1.0 / 3.0, 1.0 - (2.0 * ratio - 1.0) ** 3))
             decrease = 2.0

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <fstream>
 #include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -59,7 +60,35 @@ static void write_vec(std::ofstream& f, const std::vector<T>& v) {
   f.write(reinterpret_cast<const char*>(v.data()), n * (int64_t)sizeof(T));
 }
 
+// The thread's batch chain when batches are destroyed out of construction
+// order (no GPU work: batches create their handle at the first evaluation).
+// Under the ASan build a dangling prev_ shows up as a use after free.
+static int chain_test() {
+  auto* a = new mvba::BracketedCamBatch(0);
+  auto* b = new mvba::BracketedCamBatch(0);
+  auto* c = new mvba::BracketedCamBatch(0);
+  int bad = 0;
+  auto expect = [&](mvba::BracketedCamBatch* want, const char* what) {
+    mvba::BracketedCamBatch* got = nullptr;
+    try { got = &mvba::BracketedCamBatch::Current(); } catch (const std::exception&) {}
+    if (got != want) { std::fprintf(stderr, "chain: %s\n", what); bad++; }
+  };
+  expect(c, "newest batch is current");
+  delete b;  // middle first
+  expect(c, "current unchanged after deleting the middle batch");
+  delete c;
+  expect(a, "falls back past the deleted middle batch");
+  auto* d = new mvba::BracketedCamBatch(0);
+  delete a;  // oldest while a newer one lives
+  expect(d, "current unchanged after deleting the oldest batch");
+  delete d;
+  expect(nullptr, "empty chain");
+  std::printf("chain %s\n", bad ? "FAILED" : "ok");
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc == 2 && std::string(argv[1]) == "--chain") return chain_test();
   if (argc < 3) return 2;
   std::ifstream in(argv[1], std::ios::binary);
   auto block_size = read_vec<int32_t>(in);

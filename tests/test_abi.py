@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     lib = _lib.load()
-    assert lib.mvba_abi_version() == 5
+    assert lib.mvba_abi_version() == 6
 
 
 @pytest.mark.skipif(have_gpu(), reason="checks the no-GPU behaviour")

@@ -258,6 +258,11 @@ CASES = {
     "mesh": dict(rig=dict(depth_sensors=(2,), surface="sphere", num_ref=30, num_points=300),
                  flags=dict(rig_transforms_to_float="cam1 cam2", depth_tri_weight=10.0, depth_mesh_weight=5.0,
                             mesh_tri_weight=2.0, depth_to_image_transforms_to_float="cam2", float_scale=True)),
+    # BASELINE config c1 (configs[0]): 3-sensor rig, 1k landmarks / ~5k
+    # observations, pinhole without distortion, the whole rig generator config
+    "c1": dict(config="c1",
+               flags=dict(rig_transforms_to_float="cam1 cam2",
+                          intrinsics_to_float="ref_cam:focal_length cam1:focal_length cam2:focal_length")),
 }
 
 
@@ -281,7 +286,11 @@ def test_cli_matches_oracle_pipeline(cli, tmp_path, name):
     shards = 2 if name.endswith("_2shards") else 1
     name = name.replace("_2shards", "")
     flags = dict(CASES[name]["flags"])
-    R, info = _dataset(tmp_path, seed=11 + len(name), **CASES[name].get("rig", {}))
+    if "config" in CASES[name]:
+        R = rig.make_rig(**rig.CONFIGS[CASES[name]["config"]])
+        info = rig_files.write_dataset(R, str(tmp_path / "data"))
+    else:
+        R, info = _dataset(tmp_path, seed=11 + len(name), **CASES[name].get("rig", {}))
     if "mesh_tri_weight" in flags:
         from multiview_amd import rig_files
 

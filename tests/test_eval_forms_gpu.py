@@ -56,3 +56,41 @@ def test_one_launch_evaluation_matches_two_launches(npts, form, jacobian):
     with Evaluator(P) as ev:
         order = ev.order()
     assert np.isfinite(outs[0][0][:, : order.size][:, order >= 0]).all()
+
+
+@pytest.mark.gpu
+def test_fused_wait_gives_up_with_an_error(monkeypatch):
+    """k_eval's K1 waves wait for their frame's K0 block with a bounded poll.
+    A wave that gives up raises error word [1], and mvba_sync_status reports
+    MVBA_E_DEVICE_WAIT instead of handing back residuals built from a record
+    that may be stale. MVBA_EVAL_POLL_LIMIT=0 makes every wave give up at once
+    (read per call); the next evaluation at the default limit is clean again."""
+    import torch
+
+    R = rig.make_rig(num_sensors=3, num_ref=10, num_points=2500, obs_per_point=4, seed=5)
+    P = rig.build_problem(R)
+    with Evaluator(P) as ev:
+        ev.set_params()
+        ref = None
+        for limit in ("0", None):
+            if limit is None:
+                monkeypatch.delenv("MVBA_EVAL_POLL_LIMIT", raising=False)
+            else:
+                monkeypatch.setenv("MVBA_EVAL_POLL_LIMIT", limit)
+            res = torch.full((2, ev.ld), float("nan"), dtype=torch.float64, device="cuda")
+            ev.evaluate_device(False, residuals=res, ld=ev.ld)
+            torch.cuda.synchronize()
+            if limit == "0":
+                with pytest.raises(_lib.MvbaError) as e:
+                    ev.sync()
+                assert e.value.status == _lib.MVBA_E_DEVICE_WAIT
+            else:
+                ev.sync()
+                ref = res.cpu().numpy()
+        # the clean evaluation equals the two-launch form
+        res2 = torch.full((2, ev.ld), float("nan"), dtype=torch.float64, device="cuda")
+        ev.evaluate_device(False, residuals=res2, ld=ev.ld, phase=_lib.EVAL_PREP_ONLY)
+        ev.evaluate_device(False, residuals=res2, ld=ev.ld, phase=_lib.EVAL_SKIP_PREP)
+        torch.cuda.synchronize()
+        ev.sync()
+        np.testing.assert_array_equal(res2.cpu().numpy(), ref)

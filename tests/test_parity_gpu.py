@@ -55,6 +55,20 @@ def test_parity_small_rig(oracle, name):
         _check(P, ev, oracle)
 
 
+def test_parity_c1_full(oracle):
+    """BASELINE config c1 (configs[0]) whole: 3-sensor rig, 1k landmarks /
+    ~5k observations, pinhole without distortion, every block floating;
+    residuals and Jacobian against the oracle's exact derivative, and against
+    the reference's central differences within the FD bound."""
+    R = rig.make_rig(**rig.CONFIGS["c1"])
+    P = rig.build_problem(R)
+    assert P.num_residuals > 4500 and set(P.camera_dist_size.tolist()) == {0}
+    with Evaluator(P) as ev:
+        ev.set_params()
+        _check(P, ev, oracle)
+        _check(P, ev, oracle, apply_loss=True)
+
+
 def test_parity_no_rig(oracle):
     R = rig.make_rig(num_sensors=3, num_ref=20, num_points=300, obs_per_point=5, seed=77)
     P = rig.build_problem(R, rig.FloatFlags(no_rig=True, camera_poses_to_float=("ref_cam", "cam1", "cam2"),

@@ -58,6 +58,13 @@ def test_cli_flags_under_sanitizers(tmp_path, extra, msg):
     assert p.returncode == 1 and msg in p.stderr, p.stderr
 
 
+def test_batch_chain_under_sanitizers():
+    """Ceres-adapter batches destroyed out of construction order: no dangling
+    'current batch' link (tests/cpp/test_ceres_surface.cpp --chain; no GPU)."""
+    p = _run([_bin("test_ceres_surface_san"), "--chain"])
+    assert p.returncode == 0 and "chain ok" in p.stdout, p.stdout + p.stderr
+
+
 @pytest.mark.gpu
 def test_device_paths_under_sanitizers(tmp_path, oracle):
     p = _run([_bin("san_validate"), str(tmp_path / "formats")])

@@ -57,3 +57,30 @@ def test_back_substitution_forms_agree(monkeypatch):
     assert np.isclose(sa["final_cost"], sb["final_cost"], rtol=1e-9), (sa["final_cost"], sb["final_cost"])
     scale = np.maximum(np.abs(xa), 1.0)
     assert (np.abs(xa - xb) / scale).max() < 1e-7
+
+
+@pytest.mark.gpu
+def test_cg_direction_forms_agree(monkeypatch):
+    """The CG direction records (MVBA_CG_DIR_KERNEL, read per call): the
+    default forms W p as W z + beta W p_old (the update kernel's FrameDirZ
+    blocks + pass A's DirPair writer) and the direction-kernel form computes
+    W (z + beta p_old) in k_frame_dir. Same quantities rounded in another
+    order: the solves agree to rounding. The problem is sized so linear solves
+    run past 10 CG iterations, i.e. through Ceres' residual reset
+    (i % residual_reset_period == 0), where the default form restarts from
+    the recomputed residual."""
+    R = rig.make_rig(num_sensors=3, num_ref=40, num_points=3000, obs_per_point=6, seed=13)
+    P = rig.build_problem(R)
+    runs = []
+    for form in ("0", "1"):
+        monkeypatch.setenv("MVBA_CG_DIR_KERNEL", form)
+        runs.append(_solve(P))
+    (sa, xa), (sb, xb) = runs
+    assert sa["num_linear_iterations"] > 10 * sa["num_iterations"], sa["num_linear_iterations"]
+    assert sa["num_iterations"] == sb["num_iterations"]
+    assert sa["num_successful_steps"] == sb["num_successful_steps"]
+    assert abs(sa["num_linear_iterations"] - sb["num_linear_iterations"]) <= max(2, sa["num_linear_iterations"] // 20)
+    assert sa["final_cost"] < sa["initial_cost"]
+    assert np.isclose(sa["final_cost"], sb["final_cost"], rtol=1e-9), (sa["final_cost"], sb["final_cost"])
+    scale = np.maximum(np.abs(xa), 1.0)
+    assert (np.abs(xa - xb) / scale).max() < 1e-6

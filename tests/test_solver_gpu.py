@@ -186,6 +186,28 @@ def test_converged_params_match_cpu_lm(models, use_loss, intr):
     assert _close(_others(P, x), _others(P, x_ref), 1e-6)
 
 
+def test_c1_converged_params_match_cpu_lm():
+    """BASELINE config c1 whole (3 sensors, 1k landmarks / ~5k observations,
+    pinhole): converged poses within 1e-6 of the CPU LM (north_star), other
+    free parameters within 1e-6 relative, same final cost (the CPU LM takes its
+    sparse exact-step path at this size)."""
+    from oracle import lm_reference
+
+    R = rig.make_rig(**rig.CONFIGS["c1"])
+    P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=(), intrinsics_to_float=("focal_length",)))
+    x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
+    assert s_ref["message"] in ("parameter tolerance", "function tolerance", "gradient tolerance")
+    with Evaluator(P) as ev:
+        ev.set_params()
+        s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, **TOL)
+        x = ev.get_params()
+    assert s["termination_type"] == 0, s["message"]
+    assert s["final_cost"] < s["initial_cost"]
+    assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-9)
+    assert np.abs(_poses(P, x) - _poses(P, x_ref)).max() <= 1e-6
+    assert _close(_others(P, x), _others(P, x_ref), 1e-6)
+
+
 def test_ill_conditioned_rpc_reaches_same_cost():
     """RPC distortion floated with focal and center is ill-conditioned: the RPC
     terms absorb part of that sensor's rig rotation, so two CPU runs with

@@ -11,6 +11,7 @@ import json,sys
 for ln in open(sys.argv[1]):
     if ln.startswith("{"):
         d=json.loads(ln); r=d["roofline"]; b=d.get("ba",{})
-        print("1/%s shard: %d obs, step %.1f us (prep %.1f, K1 %.1f), x%s = %.2e evals/s if ranks overlap perfectly; CG iteration %.1f us" % (sys.argv[2], d["config"]["num_residuals_per_gpu"], 1e3*d["ms_per_step"], 1e3*r["prep_ms"], 1e3*r["kernel_ms"], sys.argv[2], int(sys.argv[2])*d["value"], 1e3*b.get("ms_per_cg_iteration",0)))
+        sf=r["split_form"]
+        print("1/%s shard: %d obs, step %.1f us (%s %.1f us; split form prep %.1f + K1 %.1f), x%s = %.2e evals/s if ranks overlap perfectly; CG iteration %.1f us" % (sys.argv[2], d["config"]["num_residuals_per_gpu"], 1e3*d["ms_per_step"], r["kernel"], 1e3*r["kernel_ms"], 1e3*sf["prep_ms"], 1e3*sf["kernel_ms"], sys.argv[2], int(sys.argv[2])*d["value"], 1e3*b.get("ms_per_cg_iteration",0)))
 PY
 done
