@@ -191,8 +191,16 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   if (dev < 0 || dev >= ndev) return bad(MVBA_E_INVALID, "invalid device ordinal");
   if (hipSetDevice(dev) != hipSuccess) return bad(MVBA_E_HIP, "hipSetDevice failed");
 
+  int align = opts ? opts->slot_align : 0;
+  if (align == 0) {
+    const char* a = std::getenv("MVBA_SLOT_ALIGN");
+    align = a ? std::atoi(a) : 32;
+  }
+  if (align != 16 && align != 32) return bad(MVBA_E_INVALID, "slot_align must be 0, 16 or 32");
+
   mvba_handle* h = new mvba_handle();
   h->device = dev;
+  h->slot_align = align;
   h->nres = N;
   h->nparams = d->num_param_doubles;
   h->ncams = d->num_cameras;
@@ -414,11 +422,12 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       }
   }
 
-  // Device slots: every frame's residuals start on a 128-byte line (16 doubles,
-  // 32 floats), so each wavefront's 64-element store chunk per Jacobian plane is
-  // line-aligned (misaligned chunks write at ~60% of the aligned rate:
-  // tools/store_bench.hip), and K1 fills the frame's last line with padding.
-  constexpr int64_t kAlign = 32;  // one 128-B line of fp32 outputs (two of fp64)
+  // Device slots: every frame's residuals start on a 128-byte line (16 doubles;
+  // at the default alignment 32 also a line of 32 floats), so each wavefront's
+  // 64-element store chunk per Jacobian plane is line-aligned (misaligned
+  // chunks write at ~60% of the aligned rate: tools/store_bench.hip), and K1
+  // fills the frame's last line with padding (Segment::pad bounds it).
+  const int64_t kAlign = h->slot_align;
   int64_t nslots = 0;
   {
     int32_t prev_fr = -1;
@@ -490,6 +499,12 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     slot++;
   }
   if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
+  // Segment::pad = the slots this segment's lanes may write (K1's padding lanes
+  // fill the frame's last line but never reach the next frame's first slot)
+  for (size_t k = 0; k < segs.size(); k++) {
+    const int64_t next = k + 1 < segs.size() ? segs[k + 1].begin : nslots;
+    segs[k].pad = (int32_t)std::min<int64_t>(64, next - segs[k].begin);
+  }
   h->bytes_res = bytes_res;
   h->nsegs = (int64_t)segs.size();
   h->bytes_jac = bytes_jac;

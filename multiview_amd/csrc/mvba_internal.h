@@ -273,6 +273,7 @@ using namespace mvba_internal;
 
 struct mvba_handle {
   int device = 0;
+  int64_t slot_align = 32;  // mvba_options.slot_align: 16 or 32
   std::string err;
   int64_t nres = 0, nslots = 0, nframes = 0, npts = 0, nparams = 0;
   int64_t npts_user = 0;  // points of the caller's xyz blocks; [npts_user, npts) = mesh blocks' fixed points

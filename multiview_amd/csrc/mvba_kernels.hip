@@ -290,13 +290,15 @@ __device__ __forceinline__ void obs_body(
   const int count = __builtin_amdgcn_readfirstlane(sg.count);
   const int frame = __builtin_amdgcn_readfirstlane(sg.frame);
   // Lanes past the frame's last observation up to the next 128-B line (16
-  // fp64 / 32 fp32 slots; segments start on 32-slot boundaries) recompute the
+  // fp64 / 32 fp32 slots; segments start on 16- or 32-slot boundaries) recompute the
   // last observation and store it into their padding slots, inside the same
   // store instructions: every line of every plane is then written whole (a
   // partly written line costs HBM a read-modify-write: 110 -> 98 us at c2).
   // No reader looks at padding slots.
+  // sg.pad bounds the padding at the next frame's first slot (slot alignment 16:
+  // fp32 outputs then write the frame's last half line).
   constexpr int kLine = 128 / (int)sizeof(OT);
-  const bool active = lane < ((count + kLine - 1) & ~(kLine - 1));
+  const bool active = lane < min((count + kLine - 1) & ~(kLine - 1), __builtin_amdgcn_readfirstlane(sg.pad));
   // (local records: every lane takes part in storing the record first)
   if (RECM == kRecGlobal && !active) return;
   const int64_t i = (int64_t)begin + lane;

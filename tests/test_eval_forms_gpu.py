@@ -94,3 +94,39 @@ def test_fused_wait_gives_up_with_an_error(monkeypatch):
         torch.cuda.synchronize()
         ev.sync()
         np.testing.assert_array_equal(res2.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npts", [120, 2500])
+def test_slot_alignment_16_matches_32(npts):
+    """mvba_options.slot_align = 16 (frames start on one fp64 line) against the
+    default 32: fewer padding slots, the same residuals and Jacobians per
+    residual block (fp64 and fp32 outputs; with 16 the fp32 planes' last half
+    line of a frame is written by the padding lanes, never the next frame's)."""
+    import torch
+
+    R = rig.make_rig(num_sensors=3, num_ref=10, num_points=npts, obs_per_point=4, seed=6)
+    P = rig.build_problem(R)
+    outs = {}
+    for align in (32, 16):
+        with Evaluator(P, slot_align=align) as ev:
+            ev.set_params()
+            order = ev.order()
+            valid = order >= 0
+            got = []
+            for dt in (torch.float64, torch.float32):
+                res = torch.full((2, ev.ld), float("nan"), dtype=dt, device="cuda")
+                jac = torch.full((ev.stride, ev.ld), float("nan"), dtype=dt, device="cuda")
+                ev.evaluate_device(True, residuals=res, jac=jac, ld=ev.ld)
+                torch.cuda.synchronize()
+                ev.sync()
+                r = res.cpu().numpy()[:, : ev.num_slots][:, valid]
+                J = jac.cpu().numpy()[:, : ev.num_slots][:, valid]
+                inv = np.argsort(order[valid])
+                got.append((r[:, inv], J[:, inv]))
+            outs[align] = (ev.num_slots, got)
+    assert outs[16][0] <= outs[32][0]
+    for (r32, J32), (r16, J16) in zip(outs[32][1], outs[16][1]):
+        np.testing.assert_array_equal(r16, r32)
+        # Jacobian planes: entries of unwritten (constant-block) rows stay NaN in both
+        np.testing.assert_array_equal(J16, J32)

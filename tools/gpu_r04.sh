@@ -32,4 +32,15 @@ if [ "$STEPS" = all ] || [ "$STEPS" = bench ]; then
   run prof_c2_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2_$TAG -o run --output-format csv -- python3 bench.py --steps 200 --no-cpu-baseline --mesh-subdiv 0
   python3 tools/bench_summary.py $OUT/bench_$TAG.log $OUT/bench_c1_$TAG.log $OUT/bench_c3_$TAG.log || true
 fi
+if [ "$STEPS" = all ] || [ "$STEPS" = shard ]; then
+  # slot alignment 32 (default) vs 16 on the whole c2 and on rank 0's 1/8 shard, alternated
+  for k in 1 2; do
+    for a in 32 16; do
+      for n in 1 8; do
+        run shard${n}_a${a}_${k}_$TAG 300 env MVBA_SLOT_ALIGN=$a python3 bench.py --shard-of $n --steps 500 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0
+      done
+    done
+  done
+  python3 tools/bench_summary.py $OUT/shard*_$TAG.log || true
+fi
 exit 0
