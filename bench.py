@@ -144,6 +144,14 @@ class PhaseGuard:
         return not errs
 
 
+def kernel_degree(model):
+    """The '<MODEL, DEG' template prefix of the kernels instantiated for a
+    rig.py model name (mvba_types.h ModelKind): radtan -> '2, 0', rpc2 -> '3, 2'."""
+    if model.startswith("rpc"):
+        return f"3, {int(model[3:])}"
+    return {"none": "0, 0", "fov": "1, 0", "radtan": "2, 0", "radtan4": "2, 0"}[model]
+
+
 def injected_failure(spec, rank):
     """Test hook (MVBA_BENCH_INJECT="exchange@R"): rank R's LM-phase exchange
     fails, to rehearse the failure path of an N > 1 run."""
@@ -575,9 +583,12 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        le = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
+        le[0].record(stream)
         for k in range(args.steps):
             step()
+        le[1].record(stream)
         t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
         torch.cuda.synchronize()
         if world > 1:
@@ -597,7 +608,12 @@ def main():
             evs[k][1].record(stream)
         torch.cuda.synchronize()
         ev.sync(sh)
-        launch_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        launch_event_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        # GPU time per step of the timed loop itself: two events bracketing its K
+        # back-to-back steps (for a one-launch form: the launch's average duration
+        # with the boundary to the next launch)
+        launch_ms = le[0].elapsed_time(le[1]) / args.steps
+        time_eval.launch_event_ms = launch_event_ms
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         for k in range(args.steps):
             step(evs[k])
@@ -686,9 +702,14 @@ def main():
                           + ("" if form == _lib.FORM_SPLIT else
                              " + the prep's in the same launch (per landmark 65, per frame 1,456)"),
             "kernel_ms": kernel_ms,
-            "kernel_timing": "HIP events on the launch stream around each launch of K instrumented steps run "
-                             "right after the timed loop (the timed loop has no events: they add ~10 us per "
-                             "step); the launch is the one the timed loop runs (mvba_eval_form)",
+            "kernel_timing": ("two HIP events on the launch stream bracketing the timed loop's K back-to-back "
+                              "launches (the launch the loop runs, mvba_eval_form; per launch, boundary included)"
+                              if form != _lib.FORM_SPLIT else
+                              "HIP events on the launch stream around the K1 launch of K instrumented steps run "
+                              "right after the timed loop"),
+            "kernel_ms_event_per_launch": time_eval.launch_event_ms,
+            "event_per_launch_note": "the same launch timed with events around each of K instrumented steps after "
+                                     "the timed loop (each event pair adds ~2-4 us)",
             "split_form": {
                 "what": "the same evaluation as two launches (prep, then K1 = k_obs), event-timed",
                 "kernel": f"k_obs<{model}> (K1)",

@@ -66,3 +66,9 @@ def test_cli_exits_nonzero_without_gpus():
                        capture_output=True, text=True, env=env, timeout=300)
     assert p.returncode != 0
     assert "no GPU visible" in p.stderr
+
+
+def test_kernel_degree_names():
+    assert bench.kernel_degree("radtan") == "2, 0"
+    assert bench.kernel_degree("rpc2") == "3, 2"
+    assert bench.kernel_degree("none") == "0, 0"

@@ -292,8 +292,6 @@ def test_cli_matches_oracle_pipeline(cli, tmp_path, name):
     else:
         R, info = _dataset(tmp_path, seed=11 + len(name), **CASES[name].get("rig", {}))
     if "mesh_tri_weight" in flags:
-        from multiview_amd import rig_files
-
         flags["mesh"] = str(tmp_path / "data" / "mesh.ply")
         rig_files.write_ply(flags["mesh"], *rig.sphere_mesh(5))
     out_dir = tmp_path / "out"

@@ -22,7 +22,7 @@ run() {  # name seconds cmd...
   return $rc
 }
 if [ "$STEPS" = all ] || [ "$STEPS" = tests ]; then
-  run pytest_gpu_$TAG 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 400 --timeout-method thread
+  run pytest_gpu_$TAG 900 python -u -m pytest ${TESTS:-tests} -m gpu -q -p no:cacheprovider --timeout 400 --timeout-method thread
   run smoke_$TAG 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$STEPS" = all ] || [ "$STEPS" = bench ]; then
@@ -43,4 +43,21 @@ if [ "$STEPS" = all ] || [ "$STEPS" = shard ]; then
   done
   python3 tools/bench_summary.py $OUT/shard*_$TAG.log || true
 fi
+if [ "$STEPS" = chol ]; then
+  # X1 pricing: hand-written fp64-MFMA blocked Cholesky vs rocSOLVER dpotrf (tools/chol_bench.hip)
+  run chol512_$TAG 120 tools/chol_bench 512
+  run chol_$TAG 400 tools/chol_bench 21248
+fi
+if [ "$STEPS" = pmc ]; then
+  # per-launch HBM traffic of the evaluation launch (k_eval) and of K1 (k_obs), separate FETCH / WRITE passes
+  for CFG in ${PMC_CFGS:-c2 c3}; do
+    B="python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --ba-iters 0 --mesh-subdiv 0"
+    run fetch_${CFG}_$TAG 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_${CFG}_$TAG -o run --output-format csv -- $B
+    run write_${CFG}_$TAG 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write_${CFG}_$TAG -o run --output-format csv -- $B
+    D=$(python3 -c "import sys; sys.path.insert(0, '.'); from multiview_amd import rig; from bench import kernel_degree; m = rig.CONFIGS['$CFG']['models'][0]; print(kernel_degree(m))")
+    python3 tools/pmc_summary.py $OUT/fetch_${CFG}_$TAG/run_counter_collection.csv $OUT/write_${CFG}_$TAG/run_counter_collection.csv "k_eval<$D, double, true>" $OUT/pmc_eval_${CFG}.json $CFG
+    python3 tools/pmc_summary.py $OUT/fetch_${CFG}_$TAG/run_counter_collection.csv $OUT/write_${CFG}_$TAG/run_counter_collection.csv "k_obs<$D, double>" $OUT/pmc_k1_${CFG}.json $CFG
+  done
+fi
+if [ "$STEPS" = tests ] && [ -n "${TESTS:-}" ]; then :; fi
 exit 0
