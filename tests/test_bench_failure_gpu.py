@@ -20,9 +20,13 @@ def test_injected_exchange_failure_keeps_the_headline():
            "--mesh-subdiv", "0"]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out_dir):  # the whole run for inspection (pytest truncates messages)
+        with open(os.path.join(out_dir, "bench_failure_test.log"), "w") as f:
+            f.write(p.stdout + "\n---- stderr\n" + p.stderr)
     assert p.returncode != 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert len(lines) == 1, p.stdout[-2000:] + p.stderr[-4000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["value"] > 0
-    assert "injected exchange failure" in line["ba"].get("error", ""), (json.dumps(line)[-3000:], p.stderr[-6000:])
+    assert "injected exchange failure" in line["ba"].get("error", ""), line.get("errors")
     assert line["weak"]["skipped"]
