@@ -186,12 +186,7 @@ enum {
 
 typedef struct mvba_options {
   int32_t device;        /* HIP device ordinal */
-  /* Slot alignment of every frame's residual range in the output planes (ABI
-   * 6): 16 = one 128-B line of fp64 outputs, 32 = also one line of fp32
-   * outputs (fp32 evaluations at 16 write the frame's last half line);
-   * 0 = the default (MVBA_SLOT_ALIGN, else 32). Fewer padding slots per frame
-   * matter for thin landmark shards (~40 observations per frame). */
-  int32_t slot_align;
+  int32_t reserved0;
   double reserved1;
 } mvba_options;
 

@@ -86,7 +86,7 @@ class ProblemDesc(C.Structure):
 
 
 class Options(C.Structure):
-    _fields_ = [("device", C.c_int32), ("slot_align", C.c_int32), ("reserved1", C.c_double)]
+    _fields_ = [("device", C.c_int32), ("reserved0", C.c_int32), ("reserved1", C.c_double)]
 
 
 class DeviceView(C.Structure):

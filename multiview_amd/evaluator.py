@@ -42,11 +42,11 @@ class PinnedBuffer:
 class Evaluator:
     """GPU evaluator for a CamProblem (BracketedCamError residual blocks)."""
 
-    def __init__(self, problem: CamProblem, device: int = 0, slot_align: int = 0):
+    def __init__(self, problem: CamProblem, device: int = 0):
         self.lib = _lib.load()
         self.problem = problem
         self._desc = problem.desc()
-        opts = _lib.Options(device=device, slot_align=int(slot_align), reserved1=0.0)
+        opts = _lib.Options(device=device, reserved0=0, reserved1=0.0)
         h = C.c_void_p()
         st = self.lib.mvba_create(C.byref(self._desc), C.byref(opts), C.byref(h))
         _lib.check(st, create=True)

@@ -33,15 +33,24 @@ if [ "$STEPS" = all ] || [ "$STEPS" = bench ]; then
   python3 tools/bench_summary.py $OUT/bench_$TAG.log $OUT/bench_c1_$TAG.log $OUT/bench_c3_$TAG.log || true
 fi
 if [ "$STEPS" = all ] || [ "$STEPS" = shard ]; then
-  # slot alignment 32 (default) vs 16 on the whole c2 and on rank 0's 1/8 shard, alternated
-  for k in 1 2; do
-    for a in 32 16; do
-      for n in 1 8; do
-        run shard${n}_a${a}_${k}_$TAG 300 env MVBA_SLOT_ALIGN=$a python3 bench.py --shard-of $n --steps 500 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0
-      done
-    done
+  # rank 0's shard of an N-way landmark split of c2 (per-rank step of the strong-scaling headline)
+  for n in 1 2 4 8; do
+    run shard${n}_$TAG 300 python3 bench.py --shard-of $n --steps 500 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0
   done
   python3 tools/bench_summary.py $OUT/shard*_$TAG.log || true
+fi
+if [ "$STEPS" = ab ]; then
+  # same-box A/B against another build of the ABI (BASE=path/libmvba.so through MVBA_LIB), alternated twice
+  for k in 1 2; do
+    for v in base cur; do
+      if [ $v = base ]; then export MVBA_LIB=$PWD/$BASE; else unset MVBA_LIB; fi
+      run ab_c2_${v}_${k}_$TAG 300 python3 bench.py --steps 2000 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0
+      run ab_s8_${v}_${k}_$TAG 300 python3 bench.py --shard-of 8 --steps 500 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0
+      run ab_c3_${v}_${k}_$TAG 400 python3 bench.py --config c3 --steps 30 --ba-iters 2 --no-cpu-baseline --mesh-subdiv 0
+    done
+  done
+  unset MVBA_LIB
+  python3 tools/bench_summary.py $OUT/ab_*_$TAG.log || true
 fi
 if [ "$STEPS" = chol ]; then
   # X1 pricing: hand-written fp64-MFMA blocked Cholesky vs rocSOLVER dpotrf (tools/chol_bench.hip)
