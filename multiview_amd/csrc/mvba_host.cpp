@@ -32,7 +32,7 @@ thread_local std::string g_create_error;
 static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
-                  h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_wins, h->d_win_frames, h->d_obs_frame, h->d_order,
+                  h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
                   h->d_row_written, h->d_err, h->d_ready, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
                   h->d_po_slot,
@@ -414,52 +414,31 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       }
   }
 
-  // Device slots: K1 windows of 64 slots (mvba_types.h K1Win). Every model
-  // group starts on a window; inside a group the frames' residuals are packed
-  // densely (no per-frame alignment: a frame of 42 observations no longer takes
-  // a whole 64-lane wave), except that a window holds at most kMaxWinFrames
-  // frames: a frame that would be the (kMaxWinFrames + 1)-th to start in a
-  // window starts on the next one. Each window's 64-slot stores are whole
-  // 128-B lines (512 B per plane for fp64, 256 B for fp32); lanes past a
-  // window's valid prefix recompute its last observation into their padding
-  // slots. K1 time is set by its wave count (one wave per 64 slots):
-  // DESIGN.md §5 "Packed windows".
-  constexpr int64_t kWin = 64;
-  std::vector<int64_t> slot_of_pos(N);
+  // Device slots: every frame's residuals start on a 128-byte line of fp32
+  // outputs (32 slots; two lines of fp64), so each wavefront's 64-element store
+  // chunk per Jacobian plane is line-aligned (misaligned chunks write at ~60% of
+  // the aligned rate: tools/store_bench.hip), and K1 fills the frame's last line
+  // with padding (Segment::pad bounds it). Measured and not kept:
+  // 16-slot alignment (fewer padding slots on thin shards) and frames packed
+  // densely into 64-slot windows of several frames.
+  constexpr int64_t kAlign = 32;
   int64_t nslots = 0;
   {
-    int64_t slot = 0;
-    int cur_g = -1;
-    int32_t cur_f = -1;
-    int nf_win = 0;
+    int32_t prev_fr = -1;
+    int prev_g = -1;
     for (int64_t p = 0; p < N; p++) {
       const int64_t i = idx[p];
       const int g = grank[d->residual_camera[i]];
-      const int32_t fr = res_frame[i];
-      if (g != cur_g) {
-        slot = (slot + kWin - 1) / kWin * kWin;
-        cur_g = g;
-        cur_f = -1;
-      }
-      if (slot % kWin == 0) nf_win = 0;
-      if (fr != cur_f) {
-        if (nf_win == mvba::kMaxWinFrames) {
-          slot = (slot + kWin - 1) / kWin * kWin;
-          nf_win = 0;
-        }
-        nf_win++;
-        cur_f = fr;
-      } else if (nf_win == 0) {
-        nf_win = 1;  // the frame continues into a new window
-      }
-      slot_of_pos[p] = slot++;
+      if (res_frame[i] != prev_fr || g != prev_g) nslots = (nslots + kAlign - 1) / kAlign * kAlign;
+      prev_fr = res_frame[i];
+      prev_g = g;
+      nslots++;
     }
-    nslots = (slot + kWin - 1) / kWin * kWin;
+    nslots = (nslots + kAlign - 1) / kAlign * kAlign;
   }
   h->nslots = nslots;
   std::vector<int32_t> obs_pid(nslots, 0);
   std::vector<double2> obs_meas(nslots, make_double2(0.0, 0.0));
-  std::vector<int32_t> slot_frame(nslots, -1);
   h->order.assign(nslots, -1);
   h->row_written.assign(nslots, 0);
   h->pos_K.assign(nslots, 0);
@@ -472,24 +451,25 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     h->groups[g].deg = keys[g] % 16;
   }
   int cur_group = -1;
-  std::vector<int64_t> group_slot_end(keys.size(), 0);
+  int32_t cur_frame = -1;
+  int64_t slot = 0;
   for (int64_t p = 0; p < N; p++) {
     const int64_t i = idx[p];
     const int g = grank[d->residual_camera[i]];
     const int32_t fr = res_frame[i];
-    const int64_t slot = slot_of_pos[p];
     const bool new_group = (g != cur_group);
     if (new_group) {
       if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
       cur_group = g;
       h->groups[g].seg_begin = (int32_t)segs.size();
-      h->groups[g].res_begin = slot;
     }
+    if (new_group || fr != cur_frame) {
+      slot = (slot + kAlign - 1) / kAlign * kAlign;
+      cur_frame = fr;
+    }
+    if (new_group) h->groups[g].res_begin = slot;
     h->groups[g].res_count++;
-    group_slot_end[g] = (slot + 1 + kWin - 1) / kWin * kWin;
-    // segments (K2 and the solver passes): <= 64 consecutive slots of one frame
-    if (new_group || segs.back().frame != fr || segs.back().count == 64 ||
-        segs.back().begin + segs.back().count != slot) {
+    if (new_group || segs.back().frame != fr || segs.back().count == 64) {
       Segment sg;
       sg.begin = (int32_t)slot;
       sg.count = 0;
@@ -500,7 +480,6 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     segs.back().count++;
     obs_pid[slot] = res_pt[i];
     obs_meas[slot] = make_double2(d->residual_meas[2 * i], d->residual_meas[2 * i + 1]);
-    slot_frame[slot] = fr;
     h->order[slot] = i;
     const int mask = frames[fr].free_mask | (pt_free[res_pt[i]] ? (1 << MVBA_BLK_XYZ) : 0);
     h->row_written[slot] = (uint8_t)mask;
@@ -511,38 +490,15 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     for (int b = 0; b < 8; b++)
       if (mask & (1 << b)) cols += (b == 7) ? frames[fr].K : kFixedSize[b];
     bytes_jac += 16.0 * cols;
+    slot++;
   }
   if (cur_group >= 0) h->groups[cur_group].seg_count = (int32_t)segs.size() - h->groups[cur_group].seg_begin;
-  // K1 windows per group: valid prefix, frames in slot order
-  std::vector<mvba::K1Win> wins;
-  std::vector<int32_t> win_frames;
-  h->win_maxf = 1;
-  for (size_t g = 0; g < h->groups.size(); g++) {
-    Group& G = h->groups[g];
-    G.win_begin = (int32_t)wins.size();
-    if (G.res_count == 0) continue;
-    for (int64_t s0 = G.res_begin; s0 < group_slot_end[g]; s0 += kWin) {
-      mvba::K1Win W;
-      W.slot0 = (int32_t)s0;
-      W.fbeg = (int32_t)win_frames.size();
-      int32_t count = 0, nf = 0;
-      for (int64_t q = s0; q < s0 + kWin && slot_frame[q] >= 0; q++) {
-        if (count == 0 || slot_frame[q] != slot_frame[q - 1]) {
-          win_frames.push_back(slot_frame[q]);
-          nf++;
-        }
-        count++;
-      }
-      if (count == 0) continue;  // (cannot happen: padding only ends a window)
-      const bool first_here = s0 == G.res_begin || slot_frame[s0 - 1] != slot_frame[s0];
-      W.count = count;
-      W.nf = nf | (first_here ? (1 << 16) : 0);
-      h->win_maxf = std::max(h->win_maxf, (int)nf);
-      wins.push_back(W);
-    }
-    G.win_count = (int32_t)wins.size() - G.win_begin;
+  // Segment::pad = the slots this segment's lanes may write (K1's padding lanes
+  // fill the frame's last line but never reach the next frame's first slot)
+  for (size_t k = 0; k < segs.size(); k++) {
+    const int64_t next = k + 1 < segs.size() ? segs[k + 1].begin : nslots;
+    segs[k].pad = (int32_t)std::min<int64_t>(64, next - segs[k].begin);
   }
-  h->nwins = (int64_t)wins.size();
   h->bytes_res = bytes_res;
   h->nsegs = (int64_t)segs.size();
   h->bytes_jac = bytes_jac;
@@ -797,9 +753,6 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_obs_pid, obs_pid));
   chk(upload(&h->d_obs_meas, obs_meas));
   chk(upload(&h->d_segs, segs));
-  chk(upload(&h->d_wins, wins));
-  chk(upload(&h->d_win_frames, win_frames));
-  chk(upload(&h->d_obs_frame, slot_frame));
   chk(upload(&h->d_order, h->order));
   chk(upload(&h->d_row_written, h->row_written));
   chk(upload(&h->d_varsize, h->pos_K));
@@ -935,7 +888,7 @@ static int eval_form(const mvba_handle* h) {
   const int forced = !m ? -1 : !std::strcmp(m, "split") ? 0 : !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "local") ? 2 : -1;
   if ((sp && sp[0] == '1') || forced == 0 || h->groups.size() != 1) return MVBA_FORM_SPLIT;
   if (forced > 0) return forced == 1 ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
-  return h->groups[0].win_count >= 4 * h->nframes ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
+  return h->groups[0].seg_count >= 4 * h->nframes ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
 }
 
 int32_t mvba_eval_form(const mvba_handle* h) { return h ? eval_form(h) : -1; }
@@ -952,12 +905,6 @@ static mvba_status ensure_outputs(mvba_handle* h) {
 
 static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double cauchy_threshold, void* d_res,
                                         void* d_J, int64_t ld, int32_t out_f32, void* stream);
-
-// K1's inputs for one model group: its windows and the tables they index.
-static mvba::K1In k1_in(const mvba_handle* h, const Group& G) {
-  return mvba::K1In{h->d_wins + G.win_begin, G.win_count, h->win_maxf, h->d_win_frames, h->d_obs_frame, h->d_fd,
-                    h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas};
-}
 
 // Polls of a K0 ready word before a fused-evaluation wave gives up (~0.5 s at
 // the default). MVBA_EVAL_POLL_LIMIT (read per call: tests switch it) lowers it;
@@ -1021,12 +968,14 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
     h->gen++;
     const Group& G = h->groups[0];
     if (form == MVBA_FORM_FUSED)
-      e = mvba_launch_eval_fused(G.model, G.deg, k1_in(h, G), h->nframes, h->d_frec, h->d_pt_off, h->d_pt_free,
-                                 h->npts, h->d_pts, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen, h->d_err,
-                                 h->d_ready, eval_poll_limit(), s);
+      e = mvba_launch_eval_fused(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->nframes,
+                                 h->d_frec, h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts,
+                                 h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen,
+                                 h->d_err, h->d_ready, eval_poll_limit(), s);
     else
-      e = mvba_launch_eval_local(G.model, G.deg, k1_in(h, G), h->d_frec, h->d_pt_off, h->d_pt_free, h->npts,
-                                 h->d_pts, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen, h->d_err, s);
+      e = mvba_launch_eval_local(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->d_frec,
+                                 h->d_params, h->d_pt_off, h->d_pt_free, h->npts, h->d_pts, h->d_obs_pid,
+                                 h->d_obs_meas, d_res, d_J, ld, flags, cauchy_c, out_f32, h->gen, h->d_err, s);
     h->prep_done = true;
     if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
     return MVBA_OK;
@@ -1047,7 +996,9 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
   }
   for (size_t g = 0; g < h->groups.size() && e == hipSuccess; g++) {
     const Group& G = h->groups[g];
-    e = mvba_launch_obs(G.model, G.deg, k1_in(h, G), h->d_frec, d_res, d_J, ld, flags, cauchy_c, out_f32, s);
+    e = mvba_launch_obs(G.model, G.deg, h->d_segs + G.seg_begin, G.seg_count, h->d_fd, h->d_frec,
+                        h->d_params, h->d_pts, h->d_obs_pid, h->d_obs_meas, d_res, d_J, ld, flags,
+                        cauchy_c, out_f32, s);
   }
   if (e != hipSuccess) return h->hip_fail(e, "mvba_evaluate_device launch");
   return MVBA_OK;

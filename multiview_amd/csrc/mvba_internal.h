@@ -48,16 +48,23 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
                                   const double* frec, const double* params, const double4* pts,
                                   double* pgrad, double* phess, int32_t flags, double cauchy_c,
                                   mvba::PointExtra dc, hipStream_t s);
-hipError_t mvba_launch_obs(int model, int deg, const mvba::K1In& in, const double* frec, void* res, void* J,
-                           int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s);
+hipError_t mvba_launch_obs(int model, int deg, const Segment* segs, int32_t nseg,
+                           const FrameDesc* fd, const double* frec, const double* params,
+                           const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                           void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
+                           hipStream_t s);
 int64_t mvba_eval_ready_words(int64_t nframes);
-hipError_t mvba_launch_eval_fused(int model, int deg, const mvba::K1In& in, int64_t nframes, double* frec,
-                                  const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts, void* res,
-                                  void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32, int gen,
-                                  int* err, unsigned* ready, unsigned poll_limit, hipStream_t s);
-hipError_t mvba_launch_eval_local(int model, int deg, const mvba::K1In& in, double* frec, const int64_t* pt_off,
-                                  const uint8_t* pt_free, int64_t npts, double4* pts, void* res, void* J, int64_t ld,
-                                  int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err, hipStream_t s);
+hipError_t mvba_launch_eval_fused(int model, int deg, const Segment* segs, int32_t nseg, const FrameDesc* fd,
+                                  int64_t nframes, double* frec, const double* params, const int64_t* pt_off,
+                                  const uint8_t* pt_free, int64_t npts, double4* pts, const int32_t* obs_pid,
+                                  const double2* obs_meas, void* res, void* J, int64_t ld, int32_t flags,
+                                  double cauchy_c, int32_t out_f32, int gen, int* err, unsigned* ready,
+                                  unsigned poll_limit, hipStream_t s);
+hipError_t mvba_launch_eval_local(int model, int deg, const Segment* segs, int32_t nseg, const FrameDesc* fd,
+                                  double* frec, const double* params, const int64_t* pt_off, const uint8_t* pt_free,
+                                  int64_t npts, double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                                  void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
+                                  int gen, int* err, hipStream_t s);
 }
 
 extern "C" {
@@ -163,8 +170,6 @@ struct Group {
   int model = 0, deg = 0;
   int32_t seg_begin = 0, seg_count = 0;
   int64_t res_begin = 0, res_count = 0;
-  // K1 windows (64 slots each) of the group's slot range
-  int32_t win_begin = 0, win_count = 0;
   // solver passes: chunks of <= 4 segments of one frame (one wave each)
   int32_t chunk_begin = 0, chunk_count = 0;
   // linearization (K2): parts of <= kPartSegs segments of one frame (one block each)
@@ -294,11 +299,6 @@ struct mvba_handle {
   int32_t* d_obs_pid = nullptr;
   double2* d_obs_meas = nullptr;
   Segment* d_segs = nullptr;
-  mvba::K1Win* d_wins = nullptr;  // K1 windows (all groups)
-  int32_t* d_win_frames = nullptr;
-  int32_t* d_obs_frame = nullptr;  // frame of every slot (padding: -1)
-  int32_t win_maxf = 1;            // most frames in one window (K1's LDS per wave)
-  int64_t nwins = 0;
   int64_t* d_order = nullptr;
   uint8_t* d_row_written = nullptr;
   int* d_err = nullptr;

@@ -265,130 +265,76 @@ struct FusedIn {
   unsigned poll_limit;     // k_eval: polls of the ready word before a wave gives up (0: none, tests)
 };
 
-// How a K1 wave gets its frames' records: kRecGlobal copies the prep kernel's
-// records; kRecFused waits for the K0 blocks of the same launch (k_eval);
-// kRecLocal computes them itself (k_eval_local: thin shards, about one wave
-// per frame, where a hand-off costs more than the K0 work).
+// How a K1 wave gets its frame record: kRecGlobal reads the prep kernel's
+// record; kRecFused waits for the K0 blocks of the same launch (k_eval);
+// kRecLocal computes it itself into its LDS area (k_eval_local: thin shards,
+// about one segment per frame, where a hand-off costs more than the K0 work).
 enum { kRecGlobal = 0, kRecFused = 1, kRecLocal = 2 };
 
-// LDS per frame of a window, in doubles: the K0 record (kFrameRecDoubles), then
-// focal, centre (2), half size (2), K, free mask, the distortion offset (as a
-// double: exact below 2^53), then the distortion coefficients.
-template <int MODEL, int DEG>
-constexpr int k1_dist_max() {
-  return MODEL == kModelNone ? 0 : MODEL == kModelFov ? 1 : MODEL == kModelRadtan ? 5 : 4 * (DEG + 1) * (DEG + 2) - 4;
-}
-template <int MODEL, int DEG>
-constexpr int k1_frame_lds() {
-  return (kFrameRecDoubles + 8 + k1_dist_max<MODEL, DEG>() + 1) & ~1;
-}
-template <int MODEL, int DEG>
-size_t k1_lds_bytes(int32_t maxf) {
-  return (size_t)4 * (size_t)maxf * (size_t)k1_frame_lds<MODEL, DEG>() * sizeof(double);
-}
-
-__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
-
-// One wave per K1 window (64 slots, up to kMaxWinFrames frames): the wave
-// stages its frames' records, intrinsics and distortion coefficients in its LDS
-// area, then every lane evaluates its slot's residual block against its own
-// frame's entries. A Jacobian row that some lane of the window writes is
-// written by every lane (zero where the lane's block is constant: frames of
-// different sensors share a window), so each store instruction writes whole
-// lines; rows no lane writes are skipped (Ceres passes NULL jacobians for
-// constant blocks; readers go by row_written). Lanes past the window's valid
-// prefix recompute its last observation into their padding slots.
 template <int MODEL, int DEG, class OT, bool JAC, int RECM = kRecGlobal>
-__device__ __forceinline__ void obs_body(const K1In& in, double* __restrict__ frec, OT* __restrict__ res,
-                                         OT* __restrict__ J, int64_t ld, int32_t flags, double cauchy_c,
-                                         const FusedIn& fu = FusedIn{}) {
-  constexpr int KFL = k1_frame_lds<MODEL, DEG>();
-  constexpr int KD = k1_dist_max<MODEL, DEG>();
-  extern __shared__ double k1_lds[];
-  // 4 windows per block, XCD-contiguous
-  const int64_t blk = xcd_block_of((int64_t)blockIdx.x - (RECM != kRecGlobal ? fu.k1_block0 : 0), (in.nwin + 3) / 4);
+__device__ __forceinline__ void obs_body(
+    const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
+    const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
+    int64_t ld, int32_t flags, double cauchy_c, const FusedIn& fu = FusedIn{}) {
+  constexpr bool FUSED = (RECM == kRecFused);
+  // 4 segments per block, XCD-contiguous
+  const int64_t blk = xcd_block_of((int64_t)blockIdx.x - (RECM != kRecGlobal ? fu.k1_block0 : 0), (nseg + 3) / 4);
   if (blk < 0) return;
-  const int wid = threadIdx.x >> 6;
-  const int w = (int)(blk * 4 + wid);
+  const int wave = (int)((blk * blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
-  if (w >= in.nwin) return;
-  const K1Win W = in.wins[w];
-  const int64_t slot0 = __builtin_amdgcn_readfirstlane(W.slot0);
-  const int count = __builtin_amdgcn_readfirstlane(W.count);
-  const int fbeg = __builtin_amdgcn_readfirstlane(W.fbeg);
-  const int nfw = __builtin_amdgcn_readfirstlane(W.nf);
-  const int nf = nfw & 0xffff;
-  const bool first_here = (nfw >> 16) & 1;
-  double* fl = k1_lds + (size_t)wid * (size_t)in.maxf * KFL;
-  const int64_t i = slot0 + lane;
-  const int64_t isrc = slot0 + min(lane, count - 1);
-  const double* __restrict__ params = in.params;
+  if (wave >= nseg) return;
+  const Segment sg = segs[wave];
+  const int begin = __builtin_amdgcn_readfirstlane(sg.begin);
+  const int count = __builtin_amdgcn_readfirstlane(sg.count);
+  const int frame = __builtin_amdgcn_readfirstlane(sg.frame);
+  // Lanes past the frame's last observation up to the next 128-B line (16
+  // fp64 / 32 fp32 slots; segments start on 16- or 32-slot boundaries) recompute the
+  // last observation and store it into their padding slots, inside the same
+  // store instructions: every line of every plane is then written whole (a
+  // partly written line costs HBM a read-modify-write: 110 -> 98 us at c2).
+  // No reader looks at padding slots.
+  // sg.pad bounds the padding at the next frame's first slot (slot alignment 16:
+  // fp32 outputs then write the frame's last half line).
+  constexpr int kLine = 128 / (int)sizeof(OT);
+  const bool active = lane < min((count + kLine - 1) & ~(kLine - 1), __builtin_amdgcn_readfirstlane(sg.pad));
+  // (local records: every lane takes part in storing the record first)
+  if (RECM == kRecGlobal && !active) return;
+  const int64_t i = (int64_t)begin + lane;
+  const int64_t isrc = (int64_t)begin + min(lane, count - 1);
 
-  // this lane's landmark and measurement: issued before the frame staging,
-  // except in the local form, where they load after K0 (the two register sets
-  // are then never live together: 3 waves per SIMD without spills)
-  auto landmark = [&]() {
-    if constexpr (RECM == kRecGlobal) {
-      return in.pts[in.obs_pid[isrc]];
-    } else {
-      // straight from the parameter vector (this launch's gather blocks fill
-      // pts for later launches only)
-      const int32_t pid = in.obs_pid[isrc];
-      const int64_t po = fu.pt_off[pid];
-      return make_double4(params[po], params[po + 1], params[po + 2], fu.pt_free[pid] ? 1.0 : 0.0);
-    }
-  };
-  double4 P = make_double4(0.0, 0.0, 0.0, 0.0);
-  double2 meas = make_double2(0.0, 0.0);
-  if constexpr (RECM != kRecLocal) {
-    P = landmark();
-    meas = in.obs_meas[isrc];
-  }
+  const FrameDesc& F = fd[frame];
+  const double f = params[F.off[MVBA_BLK_FOCAL]];
+  const double c0 = params[F.off[MVBA_BLK_CENTER]];
+  const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
+  const double* __restrict__ kd = params + F.off[MVBA_BLK_DIST];
+  const int free_mask = F.free_mask;
+  const int K = F.K;
 
-  // frame scalars (lane q < nf: frame q), then the distortion coefficients
-  if (lane < nf) {
-    const FrameDesc& F = in.fd[in.win_frames[fbeg + lane]];
-    double* o = fl + lane * KFL + kFrameRecDoubles;
-    o[0] = params[F.off[MVBA_BLK_FOCAL]];
-    o[1] = params[F.off[MVBA_BLK_CENTER]];
-    o[2] = params[F.off[MVBA_BLK_CENTER] + 1];
-    o[3] = F.h0;
-    o[4] = F.h1;
-    o[5] = (double)F.K;
-    o[6] = (double)F.free_mask;
-    o[7] = (double)F.off[MVBA_BLK_DIST];
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if constexpr (KD > 0) {
-    for (int t = lane; t < nf * KD; t += 64) {
-      const int q = t / KD, c = t - q * KD;
-      const double* o = fl + q * KFL + kFrameRecDoubles;
-      if (c < (int)o[5]) fl[q * KFL + kFrameRecDoubles + 8 + c] = params[(int64_t)o[7] + c];
-    }
-  }
-  // the frames' K0 records
-  if constexpr (RECM == kRecLocal) {
-    // lanes 16 q' .. 16 q' + 15 run K0 for frame k0 + q' (the prep kernel's
-    // frame_columns, into LDS)
-    for (int k0 = 0; k0 < nf; k0 += 4) {
-      const int q = k0 + (lane >> 4);
-      if (q < nf) frame_columns<false>(in.fd[in.win_frames[fbeg + q]], params, fl + q * KFL, lane & 15,
-                                       (int)fu.epoch, fu.err);
-    }
-  } else if constexpr (RECM == kRecFused) {
+  double4 P;
+  const double* rec;
+  if constexpr (FUSED) {
+    // landmark straight from the parameter vector (this launch's gather blocks
+    // fill pts for later launches only), issued before the wait
+    const int32_t pid = obs_pid[isrc];
+    const int64_t po = fu.pt_off[pid];
+    P = make_double4(params[po], params[po + 1], params[po + 2], fu.pt_free[pid] ? 1.0 : 0.0);
+    // Wait for the frame's K0 block, then read its record: one lane polls the
+    // ready word (relaxed agent load, sc1), every record load is an sc1 load to
+    // registers (the record was stored write-through), staged in this wave's
+    // LDS area (MI355X_MICROARCH.md, visibility: valid forms, first row).
+    __shared__ double srec[4][kFrameRecDoubles];
+    double* sr = srec[threadIdx.x >> 6];
     // HIP promises no dispatch order: the launch puts every K0 block in front of
     // the K1 blocks, and on gfx950 blocks start in index order, so the wait
     // ends within the K0 work. The wait is bounded all the same; a wave that
     // gives up raises error word [1] to this launch's epoch, so
     // mvba_sync_status fails (MVBA_E_DEVICE_WAIT) instead of returning
-    // residuals built from a record that may be stale. Lane q polls frame q's
-    // ready word (relaxed agent load, sc1); every record load is an sc1 load to
-    // registers (the records were stored write-through), staged in this wave's
-    // LDS area (MI355X_MICROARCH.md, visibility: valid forms, first row).
-    if (lane < nf) {
-      const unsigned* wd = fu.ready + (in.win_frames[fbeg + lane] >> 4);  // 16 frames per K0 block
-      for (unsigned n = 0; __hip_atomic_load(wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != fu.epoch; n++) {
+    // residuals built from a record that may be stale.
+    if (lane == 0) {
+      const unsigned* w = fu.ready + (frame >> 4);  // 16 frames per K0 block
+      for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != fu.epoch; n++) {
         if (n >= fu.poll_limit) {
           atomicMax(fu.err + 1, (int)fu.epoch);
           break;
@@ -397,46 +343,45 @@ __device__ __forceinline__ void obs_body(const K1In& in, double* __restrict__ fr
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the record loads below the poll
+    const double* g = frec + (int64_t)frame * kFrameRecDoubles;
+    for (int m = lane; m < kFrameRecDoubles; m += 64)
+      sr[m] = __hip_atomic_load(const_cast<double*>(g + m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    for (int t = lane; t < nf * kFrameRecDoubles; t += 64) {
-      const int q = t / kFrameRecDoubles, m = t - q * kFrameRecDoubles;
-      const double* g = frec + (int64_t)in.win_frames[fbeg + q] * kFrameRecDoubles;
-      fl[q * KFL + m] = __hip_atomic_load(const_cast<double*>(g + m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!active) return;
+    rec = sr;
+  } else if constexpr (RECM == kRecLocal) {
+    // lanes 0..15 (always active: count >= 1) run K0 for this wave's frame
+    // into the wave's LDS area; then the landmark straight from the parameter
+    // vector (no prep launch; loaded after K0 so the two register sets are
+    // never live together: 3 waves per SIMD without spills)
+    // (loading the landmark's offset and free flag before K0 measured no gain:
+    // 20.0 vs 18.4-20.6 us on the 8-way shard, profiles/r03/ab_eval_local/)
+    __shared__ double srec[4][kFrameRecDoubles];
+    double* sr = srec[threadIdx.x >> 6];
+    if (lane < kThreadsPerFrame) frame_columns<false>(F, params, sr, lane, (int)fu.epoch, fu.err);
+    const int32_t pid = obs_pid[isrc];
+    const int64_t po = fu.pt_off[pid];
+    P = make_double4(params[po], params[po + 1], params[po + 2], fu.pt_free[pid] ? 1.0 : 0.0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    rec = sr;
+    // the wave of the frame's first segment stores the record for later
+    // launches (solver, SKIP_PREP evaluations): in a one-group problem every
+    // frame has a segment (frames are the reprojection residuals' images)
+    if (wave == 0 || segs[wave - 1].frame != frame) {
+      double* g = const_cast<double*>(frec) + (int64_t)frame * kFrameRecDoubles;  // k_eval_local owns frec
+      for (int m = lane; m < kFrameRecDoubles; m += 64) g[m] = sr[m];  // all 64 lanes: the whole record
     }
+    if (!active) return;
   } else {
-    for (int t = lane; t < nf * kFrameRecDoubles; t += 64) {
-      const int q = t / kFrameRecDoubles, m = t - q * kFrameRecDoubles;
-      fl[q * KFL + m] = frec[(int64_t)in.win_frames[fbeg + q] * kFrameRecDoubles + m];
-    }
+    P = pts[obs_pid[isrc]];
+    rec = frec + (int64_t)frame * kFrameRecDoubles;
   }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  if constexpr (RECM == kRecLocal) {
-    // the window where a frame starts stores its record for later launches
-    // (solver, SKIP_PREP evaluations): every frame has a window (frames are
-    // the reprojection residuals' images), so every record is written
-    const int q0 = first_here ? 0 : 1;
-    for (int t = lane; t < (nf - q0) * kFrameRecDoubles; t += 64) {
-      const int q = q0 + t / kFrameRecDoubles, m = t % kFrameRecDoubles;
-      frec[(int64_t)in.win_frames[fbeg + q] * kFrameRecDoubles + m] = fl[q * KFL + m];
-    }
-  }
-
-  if constexpr (RECM == kRecLocal) {
-    P = landmark();
-    meas = in.obs_meas[isrc];
-  }
-  const int32_t frame = in.obs_frame[isrc];
-  int k = 0;
-  for (int q = 1; q < nf; q++)
-    if (in.win_frames[fbeg + q] == frame) k = q;
-  const double* rec = fl + k * KFL;
-  const double* fi = rec + kFrameRecDoubles;
-  const double f = fi[0], c0 = fi[1], c1 = fi[2];
-  const int K = (int)fi[5];
-  const int free_mask = (int)fi[6];
+  const double2 meas = obs_meas[isrc];
   Proj o;
-  project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, fi + 8, K, fi[3], fi[4], o);
+  project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, kd, K, F.h0, F.h1, o);
 
   double r0 = o.d0 - meas.x;  // rig_calibrator.cc:478-479
   double r1 = o.d1 - meas.y;
@@ -462,51 +407,44 @@ __device__ __forceinline__ void obs_body(const K1In& in, double* __restrict__ fr
 #pragma unroll
   for (int blk = 0; blk < 4; blk++) {
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
-    const bool mine = (free_mask >> b) & 1;
-    if (!wave_any(mine)) continue;
+    if (!(free_mask & (1 << b))) continue;
     const int ncol = (blk == 3) ? 1 : 7;
     const int k0 = blk * 7;
     const int base = (blk == 3) ? MVBA_JAC_BASE_OFFSET : 14 * blk;
 #pragma unroll
     for (int c = 0; c < ncol; c++) {
-      const double* wk = rec + 12 + 6 * (k0 + c);
-      double j0 = a0[0] * wk[0] + a0[1] * wk[1] + a0[2] * wk[2] + G0[0] * wk[3] + G0[1] * wk[4] + G0[2] * wk[5];
-      double j1 = a1[0] * wk[0] + a1[1] * wk[1] + a1[2] * wk[2] + G1[0] * wk[3] + G1[1] * wk[4] + G1[2] * wk[5];
-      if (!mine) j0 = j1 = 0.0;
+      const double* w = rec + 12 + 6 * (k0 + c);
+      const double j0 = a0[0] * w[0] + a0[1] * w[1] + a0[2] * w[2] + G0[0] * w[3] + G0[1] * w[4] + G0[2] * w[5];
+      const double j1 = a1[0] * w[0] + a1[1] * w[1] + a1[2] * w[2] + G1[0] * w[3] + G1[1] * w[4] + G1[2] * w[5];
       stj(J, ld, base + c, i, j0);
       stj(J, ld, base + ncol + c, i, j1);
     }
   }
   // Point columns: dXc/dX = R_wc.
-  const bool pfree = P.w != 0.0;
-  if (wave_any(pfree)) {
+  if (P.w != 0.0) {
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-      double j0 = G0[0] * rec[c] + G0[1] * rec[3 + c] + G0[2] * rec[6 + c];
-      double j1 = G1[0] * rec[c] + G1[1] * rec[3 + c] + G1[2] * rec[6 + c];
-      if (!pfree) j0 = j1 = 0.0;
+      const double j0 = G0[0] * rec[c] + G0[1] * rec[3 + c] + G0[2] * rec[6 + c];
+      const double j1 = G1[0] * rec[c] + G1[1] * rec[3 + c] + G1[2] * rec[6 + c];
       stj(J, ld, MVBA_JAC_BASE_XYZ + c, i, j0);
       stj(J, ld, MVBA_JAC_BASE_XYZ + 3 + c, i, j1);
     }
   }
-  const bool ffree = (free_mask >> MVBA_BLK_FOCAL) & 1;
-  if (wave_any(ffree)) {
-    stj(J, ld, MVBA_JAC_BASE_FOCAL, i, ffree ? o.df0 * sr : 0.0);
-    stj(J, ld, MVBA_JAC_BASE_FOCAL + 1, i, ffree ? o.df1 * sr : 0.0);
+  if (free_mask & (1 << MVBA_BLK_FOCAL)) {
+    stj(J, ld, MVBA_JAC_BASE_FOCAL, i, o.df0 * sr);
+    stj(J, ld, MVBA_JAC_BASE_FOCAL + 1, i, o.df1 * sr);
   }
-  const bool cfree = (free_mask >> MVBA_BLK_CENTER) & 1;
-  if (wave_any(cfree)) {
-    const double cc = (MODEL == kModelRpc || !cfree) ? 0.0 : sr;  // RPC ignores the optical centre
+  if (free_mask & (1 << MVBA_BLK_CENTER)) {
+    const double cc = (MODEL == kModelRpc) ? 0.0 : sr;  // RPC ignores the optical centre
     stj(J, ld, MVBA_JAC_BASE_CENTER + 0, i, cc);
     stj(J, ld, MVBA_JAC_BASE_CENTER + 1, i, 0.0);
     stj(J, ld, MVBA_JAC_BASE_CENTER + 2, i, 0.0);
     stj(J, ld, MVBA_JAC_BASE_CENTER + 3, i, cc);
   }
-  const bool dfree = (free_mask >> MVBA_BLK_DIST) & 1;
-  if (!wave_any(dfree)) return;
+  if (!(free_mask & (1 << MVBA_BLK_DIST))) return;
   dist_columns<MODEL, DEG>(o, f, K, sr, [&](int c, double v0, double v1) {
-    stj(J, ld, MVBA_JAC_BASE_DIST + c, i, dfree ? v0 : 0.0);
-    stj(J, ld, MVBA_JAC_BASE_DIST + K + c, i, dfree ? v1 : 0.0);
+    stj(J, ld, MVBA_JAC_BASE_DIST + c, i, v0);
+    stj(J, ld, MVBA_JAC_BASE_DIST + K + c, i, v1);
   });
   if constexpr (MODEL == kModelRpc) {
     // Undistortion half: structurally zero.
@@ -514,80 +452,6 @@ __device__ __forceinline__ void obs_body(const K1In& in, double* __restrict__ fr
       stj(J, ld, MVBA_JAC_BASE_DIST + c, i, 0.0);
       stj(J, ld, MVBA_JAC_BASE_DIST + K + c, i, 0.0);
     }
-  }
-}
-
-// K1 with the Jacobian planes, and the residual-only evaluation under its own
-// name (k_obs_res) so kernel statistics never mix the two.
-template <int MODEL, int DEG, class OT>
-__global__ void __launch_bounds__(256) k_obs(K1In in, const double* __restrict__ frec, OT* __restrict__ res,
-                                             OT* __restrict__ J, int64_t ld, int32_t flags, double cauchy_c) {
-  obs_body<MODEL, DEG, OT, true>(in, const_cast<double*>(frec), res, J, ld, flags, cauchy_c);
-}
-template <int MODEL, int DEG, class OT>
-__global__ void __launch_bounds__(256) k_obs_res(K1In in, const double* __restrict__ frec, OT* __restrict__ res,
-                                                 OT* __restrict__ J, int64_t ld, int32_t flags, double cauchy_c) {
-  obs_body<MODEL, DEG, OT, false>(in, const_cast<double*>(frec), res, J, ld, flags, cauchy_c);
-}
-
-// Fused evaluation (one model group): prep and K1 in one launch. Blocks
-// [0, fb) run K0 for 16 frames each, storing the records write-through, and
-// publish ready[block] = epoch behind every storing wave's vmcnt(0) wait and a
-// block barrier; blocks [fb, fb + pb) gather the landmarks into pts (for later
-// launches: the solver, SKIP_PREP evaluations); blocks from fu.k1_block0 run K1,
-// whose waves issue their landmark loads, then wait for their frames' ready
-// words. K0 blocks never wait and precede every K1 block in dispatch order, so
-// every wait ends; the frame arithmetic overlaps the K1 waves' loads instead of
-// a kernel boundary.
-template <int MODEL, int DEG, class OT, bool JAC>
-__global__ void __launch_bounds__(256) k_eval(K1In in, int64_t nframes, int32_t fb, int32_t pb,
-                                              double* __restrict__ frec, int64_t npts, double4* __restrict__ pts,
-                                              OT* __restrict__ res, OT* __restrict__ J, int64_t ld, int32_t flags,
-                                              double cauchy_c, int gen, int* __restrict__ err,
-                                              unsigned* __restrict__ ready, FusedIn fu) {
-  const int bid = (int)blockIdx.x;
-  if (bid < fb) {
-    const int64_t t = (int64_t)bid * kPrepBlock + threadIdx.x;
-    const int64_t f = t / kThreadsPerFrame;
-    if (f < nframes) frame_columns<true>(in.fd[f], in.params, frec + f * kFrameRecDoubles,
-                                         (int)(t % kThreadsPerFrame), gen, err);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores have completed
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(ready + bid, fu.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  if ((int64_t)bid < fu.k1_block0) {
-    const int64_t p = (int64_t)(bid - fb) * kPrepBlock + threadIdx.x;
-    if (bid - fb < pb && p < npts) {
-      const int64_t o = fu.pt_off[p];
-      pts[p] = make_double4(in.params[o], in.params[o + 1], in.params[o + 2], fu.pt_free[p] ? 1.0 : 0.0);
-    }
-    return;
-  }
-  obs_body<MODEL, DEG, OT, JAC, kRecFused>(in, frec, res, J, ld, flags, cauchy_c, fu);
-}
-
-// Thin-shard evaluation in one launch (k_eval_local): landmark-gather blocks
-// (for later launches: the solver, SKIP_PREP evaluations) come first, rounded
-// up to a multiple of 8 blocks; then the K1 blocks, whose waves run K0 for
-// their own frames into LDS (no hand-off, no wait) and store the records of
-// the frames that start in their window. Used when a frame has about one
-// window, so the per-wave K0 is not repeated: the prep launch and its boundary
-// disappear. 3 waves per SIMD (the K0 arithmetic's register file).
-template <int MODEL, int DEG, class OT, bool JAC>
-__global__ void __launch_bounds__(256, 3) k_eval_local(K1In in, int32_t pb, double* __restrict__ frec, int64_t npts,
-                                                       double4* __restrict__ pts, OT* __restrict__ res,
-                                                       OT* __restrict__ J, int64_t ld, int32_t flags,
-                                                       double cauchy_c, FusedIn fu) {
-  const int bid = (int)blockIdx.x;
-  if ((int64_t)bid >= fu.k1_block0) {
-    obs_body<MODEL, DEG, OT, JAC, kRecLocal>(in, frec, res, J, ld, flags, cauchy_c, fu);
-    return;
-  }
-  const int64_t p = (int64_t)bid * kPrepBlock + threadIdx.x;
-  if (bid < pb && p < npts) {
-    const int64_t o = fu.pt_off[p];
-    pts[p] = make_double4(in.params[o], in.params[o + 1], in.params[o + 2], fu.pt_free[p] ? 1.0 : 0.0);
   }
 }
 
@@ -599,6 +463,92 @@ __global__ void __launch_bounds__(256, 3) k_eval_local(K1In in, int32_t pb, doub
 // (2 rows per observation): B^T B holds Z^T Z, Z^T J_intr, J_intr^T J_intr and
 // the gradients Z^T r, J_intr^T r; the expansion applies w.
 //
+// K1 with the Jacobian planes, and the residual-only evaluation under its own
+// name (k_obs_res) so kernel statistics never mix the two.
+template <int MODEL, int DEG, class OT>
+__global__ void __launch_bounds__(256) k_obs(
+    const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
+    const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
+    int64_t ld, int32_t flags, double cauchy_c) {
+  obs_body<MODEL, DEG, OT, true>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld, flags, cauchy_c);
+}
+template <int MODEL, int DEG, class OT>
+__global__ void __launch_bounds__(256) k_obs_res(
+    const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ params,
+    const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
+    const double2* __restrict__ obs_meas, OT* __restrict__ res, OT* __restrict__ J,
+    int64_t ld, int32_t flags, double cauchy_c) {
+  obs_body<MODEL, DEG, OT, false>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld, flags, cauchy_c);
+}
+
+// Fused evaluation (one model group): prep and K1 in one launch. Blocks
+// [0, fb) run K0 for 16 frames each, storing the records write-through, and
+// publish ready[block] = epoch behind every storing wave's vmcnt(0) wait and a
+// block barrier; blocks [fb, fb + pb) gather the landmarks into pts (for later
+// launches: the solver, SKIP_PREP evaluations); blocks from fu.k1_block0 run K1,
+// whose waves issue their landmark loads, then wait for their frame's ready
+// word. K0 blocks never wait and precede every K1 block in dispatch order, so
+// every wait ends; the frame arithmetic overlaps the K1 waves' loads instead of
+// a kernel boundary.
+template <int MODEL, int DEG, class OT, bool JAC>
+__global__ void __launch_bounds__(256) k_eval(
+    const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd, int64_t nframes,
+    int32_t fb, int32_t pb, double* __restrict__ frec, const double* __restrict__ params, int64_t npts,
+    double4* __restrict__ pts, const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas,
+    OT* __restrict__ res, OT* __restrict__ J, int64_t ld, int32_t flags, double cauchy_c, int gen,
+    int* __restrict__ err, unsigned* __restrict__ ready, FusedIn fu) {
+  const int bid = (int)blockIdx.x;
+  if (bid < fb) {
+    const int64_t t = (int64_t)bid * kPrepBlock + threadIdx.x;
+    const int64_t f = t / kThreadsPerFrame;
+    if (f < nframes) frame_columns<true>(fd[f], params, frec + f * kFrameRecDoubles, (int)(t % kThreadsPerFrame),
+                                         gen, err);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(ready + bid, fu.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if ((int64_t)bid < fu.k1_block0) {
+    const int64_t p = (int64_t)(bid - fb) * kPrepBlock + threadIdx.x;
+    if (bid - fb < pb && p < npts) {
+      const int64_t o = fu.pt_off[p];
+      pts[p] = make_double4(params[o], params[o + 1], params[o + 2], fu.pt_free[p] ? 1.0 : 0.0);
+    }
+    return;
+  }
+  obs_body<MODEL, DEG, OT, JAC, kRecFused>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld, flags,
+                                           cauchy_c, fu);
+}
+
+// Thin-shard evaluation in one launch (k_eval_local): landmark-gather blocks
+// (for later launches: the solver, SKIP_PREP evaluations) come first, rounded
+// up to a multiple of 8 blocks; then the K1 blocks, whose waves run K0 for
+// their own frame into LDS (no hand-off, no wait) and store the record from the
+// frame's first segment. Used when a frame has about one segment, so the
+// per-wave K0 is not repeated: the prep launch and its boundary disappear.
+// 3 waves per SIMD (the K0 arithmetic's register file).
+template <int MODEL, int DEG, class OT, bool JAC>
+__global__ void __launch_bounds__(256, 3) k_eval_local(
+    const Segment* __restrict__ segs, int32_t nseg, int32_t pb, const FrameDesc* __restrict__ fd,
+    double* __restrict__ frec, const double* __restrict__ params, int64_t npts, double4* __restrict__ pts,
+    const int32_t* __restrict__ obs_pid, const double2* __restrict__ obs_meas, OT* __restrict__ res,
+    OT* __restrict__ J, int64_t ld, int32_t flags, double cauchy_c, FusedIn fu) {
+  const int bid = (int)blockIdx.x;
+  if ((int64_t)bid >= fu.k1_block0) {
+    obs_body<MODEL, DEG, OT, JAC, kRecLocal>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld,
+                                             flags, cauchy_c, fu);
+    return;
+  }
+  const int64_t p = (int64_t)bid * kPrepBlock + threadIdx.x;
+  if (bid < pb && p < npts) {
+    const int64_t o = fu.pt_off[p];
+    pts[p] = make_double4(params[o], params[o + 1], params[o + 2], fu.pt_free[p] ? 1.0 : 0.0);
+  }
+}
+
 // k_frame_lin: one block per frame part (<= kPartSegs segments of ONE frame),
 // WAVES waves per block. Each wave builds the Gram of its segments' rows (a
 // K = 128-deep GEMM per segment on fp64 MFMA v_mfma_f64_16x16x4, B staged in
@@ -1116,14 +1066,16 @@ hipError_t mvba_launch_prep(const mvba::FrameDesc* fd, int64_t nframes, const do
   }
 
 // model: ModelKind; deg: RPC degree (1..kMaxRpcDegree) when model == kModelRpc.
-// in: the group's K1 windows (mvba_types.h K1In); frec: the prep's records.
-hipError_t mvba_launch_obs(int model, int deg, const mvba::K1In& in, const double* frec, void* res, void* J,
-                           int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32, hipStream_t s) {
-  if (in.nwin <= 0) return hipSuccess;
-  const unsigned blocks = mvba::xcd_grid((in.nwin + 3) / 4);
-#define MVBA_OBS_K(KER, M, D, OT)                                                                          \
-  hipLaunchKernelGGL((mvba::KER<M, D, OT>), dim3(blocks), dim3(256), (mvba::k1_lds_bytes<M, D>(in.maxf)), s, in, \
-                     frec, (OT*)res, (OT*)J, ld, flags, cauchy_c)
+hipError_t mvba_launch_obs(int model, int deg, const mvba::Segment* segs, int32_t nseg,
+                           const mvba::FrameDesc* fd, const double* frec, const double* params,
+                           const double4* pts, const int32_t* obs_pid, const double2* obs_meas,
+                           void* res, void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32,
+                           hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
+  const unsigned blocks = mvba::xcd_grid((nseg + 3) / 4);
+#define MVBA_OBS_K(KER, M, D, OT)                                                                            \
+  hipLaunchKernelGGL((mvba::KER<M, D, OT>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, frec, params, pts, \
+                     obs_pid, obs_meas, (OT*)res, (OT*)J, ld, flags, cauchy_c)
 #define MVBA_OBS(M, D)                                                                                   \
   if (flags & MVBA_EVAL_JACOBIAN) {                                                                      \
     if (out_f32) MVBA_OBS_K(k_obs, M, D, float);                                                         \
@@ -1146,20 +1098,22 @@ int64_t mvba_eval_ready_words(int64_t nframes) {
   return (nframes * mvba::kThreadsPerFrame + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
 }
 
-hipError_t mvba_launch_eval_fused(int model, int deg, const mvba::K1In& in, int64_t nframes, double* frec,
-                                  const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts, void* res,
-                                  void* J, int64_t ld, int32_t flags, double cauchy_c, int32_t out_f32, int gen,
-                                  int* err, unsigned* ready, unsigned poll_limit, hipStream_t s) {
-  if (in.nwin <= 0) return hipSuccess;
+hipError_t mvba_launch_eval_fused(int model, int deg, const mvba::Segment* segs, int32_t nseg,
+                                  const mvba::FrameDesc* fd, int64_t nframes, double* frec, const double* params,
+                                  const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts,
+                                  const int32_t* obs_pid, const double2* obs_meas, void* res, void* J, int64_t ld,
+                                  int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err,
+                                  unsigned* ready, unsigned poll_limit, hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
   const int64_t fb = mvba_eval_ready_words(nframes);
   const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
   const int64_t k1 = (fb + pb + mvba::kXcds - 1) / mvba::kXcds * mvba::kXcds;
-  const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((in.nwin + 3) / 4));
+  const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((nseg + 3) / 4));
   const mvba::FusedIn fu{pt_off, pt_free, ready, (unsigned)gen, k1, err, poll_limit};
 #define MVBA_EVF_K(M, D, OT, JC)                                                                              \
-  hipLaunchKernelGGL((mvba::k_eval<M, D, OT, JC>), dim3(blocks), dim3(256), (mvba::k1_lds_bytes<M, D>(in.maxf)), s, \
-                     in, nframes, (int32_t)fb, (int32_t)pb, frec, npts, pts, (OT*)res, (OT*)J, ld, flags, cauchy_c,  \
-                     gen, err, ready, fu)
+  hipLaunchKernelGGL((mvba::k_eval<M, D, OT, JC>), dim3(blocks), dim3(256), 0, s, segs, nseg, fd, nframes,      \
+                     (int32_t)fb, (int32_t)pb, frec, params, npts, pts, obs_pid, obs_meas, (OT*)res, (OT*)J, ld, \
+                     flags, cauchy_c, gen, err, ready, fu)
 #define MVBA_EVF(M, D)                                                                                   \
   if (flags & MVBA_EVAL_JACOBIAN) {                                                                      \
     if (out_f32) MVBA_EVF_K(M, D, float, true);                                                          \
@@ -1176,18 +1130,21 @@ hipError_t mvba_launch_eval_fused(int model, int deg, const mvba::K1In& in, int6
 
 // Thin-shard evaluation in one launch (k_eval_local): landmark-gather blocks,
 // then the K1 blocks from a multiple of 8 on, whose waves run K0 for their own
-// frames. One model group only (every frame has a window).
-hipError_t mvba_launch_eval_local(int model, int deg, const mvba::K1In& in, double* frec, const int64_t* pt_off,
-                                  const uint8_t* pt_free, int64_t npts, double4* pts, void* res, void* J, int64_t ld,
-                                  int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err, hipStream_t s) {
-  if (in.nwin <= 0) return hipSuccess;
+// frame. One model group only (every frame has a segment).
+hipError_t mvba_launch_eval_local(int model, int deg, const mvba::Segment* segs, int32_t nseg,
+                                  const mvba::FrameDesc* fd, double* frec, const double* params,
+                                  const int64_t* pt_off, const uint8_t* pt_free, int64_t npts, double4* pts,
+                                  const int32_t* obs_pid, const double2* obs_meas, void* res, void* J, int64_t ld,
+                                  int32_t flags, double cauchy_c, int32_t out_f32, int gen, int* err,
+                                  hipStream_t s) {
+  if (nseg <= 0) return hipSuccess;
   const int64_t pb = (npts + mvba::kPrepBlock - 1) / mvba::kPrepBlock;
   const int64_t k1 = (pb + mvba::kXcds - 1) / mvba::kXcds * mvba::kXcds;
-  const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((in.nwin + 3) / 4));
+  const unsigned blocks = (unsigned)(k1 + mvba::xcd_grid((nseg + 3) / 4));
   const mvba::FusedIn fu{pt_off, pt_free, nullptr, (unsigned)gen, k1, err, 0u};
 #define MVBA_EVL_K(M, D, OT, JC)                                                                               \
-  hipLaunchKernelGGL((mvba::k_eval_local<M, D, OT, JC>), dim3(blocks), dim3(256), (mvba::k1_lds_bytes<M, D>(in.maxf)), \
-                     s, in, (int32_t)pb, frec, npts, pts, (OT*)res, (OT*)J, ld, flags, cauchy_c, fu)
+  hipLaunchKernelGGL((mvba::k_eval_local<M, D, OT, JC>), dim3(blocks), dim3(256), 0, s, segs, nseg, (int32_t)pb, \
+                     fd, frec, params, npts, pts, obs_pid, obs_meas, (OT*)res, (OT*)J, ld, flags, cauchy_c, fu)
 #define MVBA_EVL(M, D)                                                                                   \
   if (flags & MVBA_EVAL_JACOBIAN) {                                                                      \
     if (out_f32) MVBA_EVL_K(M, D, float, true);                                                          \

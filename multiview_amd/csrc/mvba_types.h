@@ -3,7 +3,6 @@
 #ifndef MVBA_TYPES_H_
 #define MVBA_TYPES_H_
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace mvba {
@@ -45,35 +44,6 @@ struct Segment {
   int32_t count;
   int32_t frame;
   int32_t pad;
-};
-
-// K1 window (the evaluation's unit of work, one wavefront): 64 consecutive
-// slots of one model group, 64-slot aligned, so every store instruction of a
-// Jacobian plane writes 512 whole bytes. Frames are packed densely in the
-// slots (no per-frame alignment), so a window holds the observations of up to
-// kMaxWinFrames frames; the wave stages every frame's record, intrinsics and
-// distortion coefficients in LDS and each lane reads its own frame's.
-constexpr int kMaxWinFrames = 8;
-struct K1Win {
-  int32_t slot0;  // first slot
-  int32_t count;  // valid slots: a prefix of the window (the rest is padding)
-  int32_t fbeg;   // the window's frames in slot order: win_frames[fbeg, fbeg + nf)
-  int32_t nf;     // bits 0..15 frame count; bit 16: frame 0 starts in this window
-};
-
-// K1's inputs (every launch form): the windows of one model group and the
-// per-slot / per-frame tables they index.
-struct K1In {
-  const K1Win* wins;
-  int32_t nwin;
-  int32_t maxf;               // most frames in one window (LDS per wave)
-  const int32_t* win_frames;
-  const int32_t* obs_frame;   // frame of each slot
-  const struct FrameDesc* fd;
-  const double* params;
-  const double4* pts;         // landmark records (split form)
-  const int32_t* obs_pid;
-  const double2* obs_meas;
 };
 
 // Distortion model kinds (camera_params.cc:181-207 dispatch by size).

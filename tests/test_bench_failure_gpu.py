@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.gpu
 def test_injected_exchange_failure_keeps_the_headline():
     env = dict(os.environ, MVBA_BENCH_INJECT="exchange@1", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--config", "c1",
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--config", "c2",
            "--steps", "20", "--warmup", "2", "--ba-iters", "2", "--dist-timeout", "20", "--no-cpu-baseline",
            "--mesh-subdiv", "0"]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=240, cwd=ROOT)
