@@ -522,8 +522,12 @@ def main():
         else:
             dist.init_process_group(args.dist_backend, timeout=tmo)
         # control group on the CPU: ranks agree on phase failures over it,
-        # whatever state the RCCL communicators are in
-        ctrl = dist.new_group(backend="gloo", timeout=tmo)
+        # whatever state the RCCL communicators are in. A failing rank may wait
+        # there while a peer is still inside a collective that only its own
+        # timeout (--dist-timeout) or the LM watchdog (--ba-deadline) ends, so
+        # its timeout covers both.
+        ctrl = dist.new_group(backend="gloo", timeout=timedelta(
+            seconds=2 * args.dist_timeout + args.ba_deadline + 60))
     else:
         torch.cuda.set_device(0)
         ctrl = None

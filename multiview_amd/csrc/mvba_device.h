@@ -53,28 +53,6 @@ __device__ __forceinline__ int64_t xcd_block_solver(int64_t nb) {
   return l < nb ? l : -1;
 }
 
-// Streaming loads of the CG passes' once-read per-observation inputs (slot
-// records, point indices, slot maps): nontemporal, so they do not push the
-// gathered tables (w_p, c_o) out of the XCD's L2. MVBA_NT_STREAM=0 builds
-// plain loads (A/B).
-#ifndef MVBA_NT_STREAM
-#define MVBA_NT_STREAM 1
-#endif
-template <class T>
-__device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (MVBA_NT_STREAM) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-__device__ __forceinline__ double4 ld_stream(const double4* p) {
-  if constexpr (MVBA_NT_STREAM) {
-    typedef double d4v __attribute__((ext_vector_type(4)));
-    const d4v v = __builtin_nontemporal_load(reinterpret_cast<const d4v*>(p));
-    return make_double4(v.x, v.y, v.z, v.w);
-  } else {
-    return *p;
-  }
-}
-
 // ------------------------------------------------------------ small helpers
 __device__ __forceinline__ void quat_to_rot(double x, double y, double z, double w, double* R) {
   // Eigen QuaternionBase::toRotationMatrix [ext], no normalisation.

@@ -69,15 +69,14 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
-                              const double4* obsX, int32_t nrep, hipStream_t s);
+                              const double4* obsX, hipStream_t s);
 hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const int64_t* begin, const int64_t* pos,
                                        const double* val, const double* diag, const double* x, double* y,
                                        double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
                                        mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, int32_t nrep,
-                                      hipStream_t s);
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s);
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
                                 unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
                                 const mvba::LazyDir* lz, hipStream_t s);
@@ -406,7 +405,7 @@ class Solver {
       HCHK(mvba_launch_pass_b(G.model, G.deg, h_->d_chunks + G.chunk_begin, G.chunk_count, G.chunk_begin,
                               h_->d_segs, h_->d_fd, h_->d_frame_lin, h_->d_frec, h_->d_params, h_->d_pts,
                               h_->d_obs_pid, h_->d_obs_meas, dir, (const double4*)S_->wbuf, S_->yrep, S_->ng, flags_,
-                              cauchy_c_, gate, det ? D.slab(0) : no_slab(), obsx(), vec_replicas(), s_));
+                              cauchy_c_, gate, det ? D.slab(0) : no_slab(), obsx(), s_));
     if (h_->ndep > 0)
       HCHK(mvba_launch_depth_sb(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_pid, h_->d_dep_meas, h_->d_frec,
                                 h_->d_params, h_->d_pts, h_->d_frame_lin, S_->du, S_->yrep, S_->ng, flags_, cauchy_c_,
@@ -430,29 +429,11 @@ class Solver {
                                        any ? lz : nullptr, fold ? 1 : 0, s_));
     else
       HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, dg, any ? xv : nullptr, y, S_->partial, S_->cnt + 4, dot_out,
-                                      gate, any ? ctl : nullptr, any ? lz : nullptr, fold ? 1 : 0, vec_replicas(),
-                                      s_));
+                                      gate, any ? ctl : nullptr, any ? lz : nullptr, fold ? 1 : 0, s_));
     exchange(y, S_->ng + (fold ? 1 : 0), MVBA_REDUCE_SUM);
     if (xv && !any)
       HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, gate, ctl,
                                 lz, s_));
-  }
-  // Replicas pass B adds into (default mode): enough that each replica of a
-  // shared entry (a sensor's extrinsics / intrinsics, added by every chunk of
-  // the sensor's frames) takes about as many adds as at c2 with 32, and fewer
-  // for the few chunks of a thin shard, whose replica sum then reads less (the
-  // 1/8 shard of c2: 16). Depth segments add into kDepthReplicas of the same
-  // buffer: all 32. MVBA_VEC_NREP=8|16|32 forces one (read per call, A/B).
-  int32_t vec_replicas() const {
-    const int32_t nmax = mvba_solver_vec_replicas();
-    if (h_->ndep > 0) return nmax;
-    if (const char* v = std::getenv("MVBA_VEC_NREP")) {
-      const int r = std::atoi(v);
-      if (r == 8 || r == 16 || r == nmax) return r;
-    }
-    int32_t r = 8;
-    while (r < nmax && (int64_t)r * 192 < (int64_t)h_->nchunks) r *= 2;
-    return r;
   }
   // the exchanged p.q behind a product vector q (fold mode), else null
   const double* pq_of(const double* q) const { return (o_.allreduce && exch_rank_ >= 0) ? q + S_->ng : nullptr; }

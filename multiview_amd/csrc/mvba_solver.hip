@@ -477,16 +477,14 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
       const int64_t i = (int64_t)c.x + s0 + lane;
       double z[2], P0[3], P1[3];
       // obsX (K2's per-slot record): landmark + Cauchy weight, no measurement read
-      if (obsX) {
-        const double4 X = ld_stream(obsX + i);
-        pass_a_obs<MODEL, DEG>(rec, d, X, double2{0.0, 0.0}, flags, cauchy_c, z, P0, P1, X.w);
-      }
+      if (obsX)
+        pass_a_obs<MODEL, DEG>(rec, d, obsX[i], double2{0.0, 0.0}, flags, cauchy_c, z, P0, P1, obsX[i].w);
       else
         pass_a_obs<MODEL, DEG>(rec, d, pts[obs_pid[i]], obs_meas[i], flags, cauchy_c, z, P0, P1);
       // plain store: a nontemporal store of these scattered 32-B records
       // doubles the kernel (49 vs 24 us at c2, partial lines go to HBM);
       // slot_po null: stored in slot order (coalesced), k_point_w gathers
-      cbuf[slot_po ? (int64_t)ld_stream(slot_po + i) : i] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
+      cbuf[slot_po ? (int64_t)slot_po[i] : i] = make_double4(P0[0] * z[0] + P1[0] * z[1], P0[1] * z[0] + P1[1] * z[1],
                                       P0[2] * z[0] + P1[2] * z[1], 0.0);
     }
   }
@@ -619,7 +617,7 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
   if (valid && cbuf)
     for (int64_t j = pt_begin[p] + sub; j < pt_begin[p + 1]; j += kLanesW) {
       // po_slot set: pass A stored c_o in slot order; gather it
-      const double4 cv = po_slot ? cbuf[ld_stream(po_slot + j)] : cbuf[j];
+      const double4 cv = po_slot ? cbuf[po_slot[j]] : cbuf[j];
       t[0] += cv.x;
       t[1] += cv.y;
       t[2] += cv.z;
@@ -669,7 +667,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
                                             const double2* __restrict__ obs_meas, const double* __restrict__ dir,
                                             const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng,
                                             int32_t flags, double cauchy_c, const Slab& sl,
-                                            const double4* __restrict__ obsX, int32_t rmask) {
+                                            const double4* __restrict__ obsX) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   extern __shared__ double st[];  // [NA + 1][kWideLd]: columns, then u
@@ -690,9 +688,9 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
         const int slot = 2 * (lane & 31);
         if (lane < count) {
           const int64_t i = (int64_t)c.x + s0 + lane;
-          const int32_t pid = ld_stream(obs_pid + i);
+          const int32_t pid = obs_pid[i];
           const double4 w = wbuf[pid];
-          const double4 X = obsX ? ld_stream(obsX + i) : pts[pid];
+          const double4 X = obsX ? obsX[i] : pts[pid];
           Proj o;
           project<MODEL, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
           double hr;
@@ -755,7 +753,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
 #pragma unroll
   for (int a = 0; a < 6; a++) zs[a] = __shfl(acc0, a, 64);
   const FrameLin& L = fl[frame];
-  double* y = yrep + (int64_t)(chunk_id & rmask) * ng;
+  double* y = yrep + (int64_t)(chunk_id & (kVecReplicas - 1)) * ng;
   if (lane < kPoseCols) {
     const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
     const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
@@ -787,8 +785,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
 // (wbuf, double4 per point); then the sums of Z^T u_o and J_I^T u_o,
 // wave-reduced; the lanes map the 6 frame-local sums through the generators
 // w_k to the pose columns (y_k = w_k . (Z^T u)) and add pose + intrinsic columns
-// into replica (chunk mod the solve's replica count, rmask + 1 <= kVecReplicas)
-// of the camera-side vector.
+// into replica (chunk mod kVecReplicas) of the camera-side vector.
 template <int MODEL, int DEG>
 __global__ void __launch_bounds__(64) k_pass_b(
     const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
@@ -797,7 +794,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     const double4* __restrict__ pts, const int32_t* __restrict__ obs_pid,
     const double2* __restrict__ obs_meas, const double* __restrict__ dir,
     const double4* __restrict__ wbuf, double* __restrict__ yrep, int64_t ng, int32_t flags, double cauchy_c,
-    const int32_t* __restrict__ gate, Slab sl, const double4* __restrict__ obsX, int32_t rmask) {
+    const int32_t* __restrict__ gate, Slab sl, const double4* __restrict__ obsX) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
   const int lane = threadIdx.x;
@@ -805,7 +802,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
   if (ch < 0 || (gate && *gate)) return;
   if constexpr (NA > kPassBRegCols) {
     pass_b_wide<MODEL, DEG>(chunks[ch], chunk_base + ch, segs, fd, fl, frec, params, pts, obs_pid, obs_meas, dir,
-                            wbuf, yrep, ng, flags, cauchy_c, sl, obsX, rmask);
+                            wbuf, yrep, ng, flags, cauchy_c, sl, obsX);
     return;
   } else {
   const int4 c = chunks[ch];
@@ -820,9 +817,9 @@ __global__ void __launch_bounds__(64) k_pass_b(
   for (int s0 = 0; s0 < nobs; s0 += 64) {
     if (lane < nobs - s0) {
       const int64_t i = (int64_t)c.x + s0 + lane;
-      const int32_t pid = ld_stream(obs_pid + i);
+      const int32_t pid = obs_pid[i];
       const double4 w = wbuf[pid];
-      const double4 X = obsX ? ld_stream(obsX + i) : pts[pid];
+      const double4 X = obsX ? obsX[i] : pts[pid];
       double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], P0[3], P1[3], r[2], hr;
 #pragma unroll
       for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;
@@ -860,7 +857,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
   }
   // every lane holds the totals; lane k < 22 -> pose column k, 22.. -> intrinsics
   const FrameLin& L = fl[frame];
-  double* y = yrep + (int64_t)((chunk_base + ch) & rmask) * ng;
+  double* y = yrep + (int64_t)((chunk_base + ch) & (kVecReplicas - 1)) * ng;
   int64_t dst = -1;
   double v = 0.0;
   if (lane < kPoseCols) {
@@ -926,7 +923,6 @@ __device__ __forceinline__ double x_entry(const double* __restrict__ x, const La
   return v;
 }
 
-template <int NR>
 __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yrep, int64_t n,
                                                         const double* __restrict__ diag,
                                                         const double* __restrict__ x, double* __restrict__ y,
@@ -940,14 +936,14 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
     const double xe = (x || lz.z) ? x_entry(x, lz, e) : 0.0;
     // all replica loads in flight before the first add / zeroing store (the
     // stores go through the same pointer, so a fused loop serialises them)
-    double v[NR];
+    double v[kVecReplicas];
 #pragma unroll
-    for (int r = 0; r < NR; r++) v[r] = yrep[r * n + e];
+    for (int r = 0; r < kVecReplicas; r++) v[r] = yrep[r * n + e];
     double acc = 0.0;
 #pragma unroll
-    for (int r = 0; r < NR; r++) acc += v[r];
+    for (int r = 0; r < kVecReplicas; r++) acc += v[r];
 #pragma unroll
-    for (int r = 0; r < NR; r++) yrep[r * n + e] = 0.0;
+    for (int r = 0; r < kVecReplicas; r++) yrep[r * n + e] = 0.0;
     if (diag) acc += diag[e] * xe;
     y[e] = acc;
     d = xe * acc;
@@ -1576,16 +1572,14 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               const double* frec, const double* params, const double4* pts, const int32_t* obs_pid,
                               const double2* obs_meas, const double* dir, const double4* wbuf, double* yrep,
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
-                              const double4* obsX, int32_t nrep, hipStream_t s) {
+                              const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
-  if (nrep < 1 || nrep > mvba::kVecReplicas || (nrep & (nrep - 1))) return hipErrorInvalidValue;
-  const int32_t rmask = nrep - 1;
 #define MVBA_PB(M, D)                                                                                       \
   hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3(mvba::xcd_grid_solver(nchunks)), dim3(64),                    \
                      (mvba::pass_b_lds<M, D>()), s,                                                           \
                      chunks, nchunks,                                                                         \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
-                     dir, wbuf, yrep, ng, flags, cauchy_c, gate, sl, obsX, rmask)
+                     dir, wbuf, yrep, ng, flags, cauchy_c, gate, sl, obsX)
   MVBA_SOLVER_SWITCH(model, deg, MVBA_PB)
 #undef MVBA_PB
   return hipGetLastError();
@@ -1605,22 +1599,11 @@ hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const in
 
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, int32_t nrep,
-                                      hipStream_t s) {
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s) {
   if (ng <= 0) return hipSuccess;
   const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
-  const dim3 grid((unsigned)((ng + 255) / 256));
-  if (nrep == 8)
-    hipLaunchKernelGGL(mvba::k_vec_rep_reduce<8>, grid, dim3(256), 0, s, yrep, ng, diag, x, y, partial, counter,
-                       dot_out, gate, ctl, l, local_dot);
-  else if (nrep == 16)
-    hipLaunchKernelGGL(mvba::k_vec_rep_reduce<16>, grid, dim3(256), 0, s, yrep, ng, diag, x, y, partial, counter,
-                       dot_out, gate, ctl, l, local_dot);
-  else if (nrep == mvba::kVecReplicas)
-    hipLaunchKernelGGL(mvba::k_vec_rep_reduce<mvba::kVecReplicas>, grid, dim3(256), 0, s, yrep, ng, diag, x, y,
-                       partial, counter, dot_out, gate, ctl, l, local_dot);
-  else
-    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, diag, x,
+                     y, partial, counter, dot_out, gate, ctl, l, local_dot);
   return hipGetLastError();
 }
 

@@ -100,5 +100,8 @@ def test_cg_direction_forms_agree(monkeypatch):
     assert (np.abs(xa - xb) / scale).max() < 1e-7
     (sa, xa), (sb, xb) = conv
     assert sa["termination_type"] == 0 and sb["termination_type"] == 0, (sa["message"], sb["message"])
+    # the same minimum: the cost to rounding (some intrinsics / rig directions of
+    # this rig are nearly flat, so converged parameters differ there by up to
+    # 2e-3 at costs equal to 1e-9, as two CPU runs with different radii do:
+    # tests/test_solver_gpu.py::test_ill_conditioned_rpc_reaches_same_cost)
     assert np.isclose(sa["final_cost"], sb["final_cost"], rtol=1e-9), (sa["final_cost"], sb["final_cost"])
-    assert (np.abs(xa - xb) / np.maximum(np.abs(xa), 1.0)).max() < 1e-6
