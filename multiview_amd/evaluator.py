@@ -293,6 +293,13 @@ class Evaluator:
         o = options or default_solver_options(**kw)
         s = _lib.SolverSummary()
         st = self.lib.mvba_solve(self.h, C.byref(o), C.byref(s), C.c_void_p(stream or 0))
+        cb_errors = getattr(o, "_callback_errors", None)
+        if st != _lib.MVBA_OK and cb_errors:
+            # the library only sees a non-zero return from the all-reduce
+            # callback: name the Python exception that caused it
+            msg = self.lib.mvba_last_error(self.h).decode()
+            first = cb_errors[0]
+            raise _lib.MvbaError(st, f"{msg} ({type(first).__name__}: {first})") from first
         _lib.check(st, self.h)
         return summary_dict(s)
 
@@ -337,6 +344,7 @@ def default_solver_options(**kw) -> _lib.SolverOptions:
     o = _lib.SolverOptions()
     lib.mvba_solver_default_options(C.byref(o))
     keep = []
+    cb_errors = []
     for k, v in kw.items():
         if k in ("lower_bounds", "upper_bounds"):
             if v is None:
@@ -359,7 +367,7 @@ def default_solver_options(**kw) -> _lib.SolverOptions:
 
             nargs = len(inspect.signature(v).parameters)
 
-            def _cb(ptr, count, op, stream, user, _f=v, _n=nargs):
+            def _cb(ptr, count, op, stream, user, _f=v, _n=nargs, _errs=cb_errors):
                 try:
                     if _n >= 4:
                         _f(ptr, count, op, stream or 0)
@@ -373,6 +381,7 @@ def default_solver_options(**kw) -> _lib.SolverOptions:
                     return 0
                 except Exception as e:  # noqa: BLE001 - reported as a failed status
                     print(f"allreduce callback failed: {e!r}")
+                    _errs.append(e)
                     return 1
             fn = _lib.AllreduceFn(_cb)
             keep.append(fn)
@@ -382,6 +391,7 @@ def default_solver_options(**kw) -> _lib.SolverOptions:
                 raise AttributeError(f"unknown solver option {k}")
             setattr(o, k, v)
     o._keep = keep  # keep arrays / callback alive for the call
+    o._callback_errors = cb_errors  # exceptions the all-reduce callback swallowed
     return o
 
 
