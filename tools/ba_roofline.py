@@ -2,7 +2,7 @@
 """Committed summary of one CG iteration (the BA half of the metric) from a
 rocprofv3 kernel trace and the separate --pmc passes of the same bench command.
 
-usage: ba_roofline.py OUT.json CONFIG kernel_trace.csv fetch.csv write.csv sq.csv
+usage: ba_roofline.py OUT.json CONFIG kernel_trace.csv fetch.csv write.csv sq.csv [l2.csv]
 
 A CG iteration of a reprojection-only problem is the launch sequence
     k_pass_a_frame -> k_point_w -> k_pass_b -> k_vec_rep_reduce -> k_cg_update
@@ -15,7 +15,8 @@ from the PMC passes, per kernel, the median over its launches in the upper
 half (the non-gated ones):
   FETCH_SIZE x 2 (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md
   HBM section) + WRITE_SIZE -> traffic bytes, SQ_INSTS_VALU -> issue floor
-  (4 cycles per fp64 wave instruction on one of 1,024 SIMDs at 2.4 GHz).
+  (4 cycles per fp64 wave instruction on one of 1,024 SIMDs at 2.4 GHz);
+  with l2.csv (TCC_HIT_sum, TCC_MISS_sum) the L2 hit rate per kernel.
 bench.py reads OUT.json for ba.roofline's kernel time, traffic and VALU floor.
 """
 import csv
@@ -69,10 +70,11 @@ def pmc(paths):
 
 def main():
     out, cfg, trace, fetch, write, sq = sys.argv[1:7]
+    extra = [a for a in sys.argv[7:8] if a]
     its = trace_iterations(trace)
     if not its:
         raise SystemExit("no non-gated CG iterations in the trace")
-    counters = pmc([fetch, write, sq])
+    counters = pmc([fetch, write, sq] + extra)
     per_k = {}
     traffic = valu = 0.0
     for k in SEQ:
@@ -84,6 +86,9 @@ def main():
         for name, key in (("wait_frac", "SQ_WAIT_ANY"), ("active_frac", "SQ_ACTIVE_INST_ANY")):
             if c.get("SQ_WAVE_CYCLES"):
                 per_k[k][name] = c.get(key, 0.0) / c["SQ_WAVE_CYCLES"]
+        if c.get("TCC_HIT_sum") is not None and c.get("TCC_MISS_sum") is not None:
+            tot = c["TCC_HIT_sum"] + c["TCC_MISS_sum"]
+            per_k[k]["l2_hit"] = c["TCC_HIT_sum"] / tot if tot else None
         traffic += fb + wb
         valu += c.get("SQ_INSTS_VALU", 0.0)
     res = {
@@ -100,7 +105,7 @@ def main():
     print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
     for k, v in per_k.items():
         print(f"{k:18s} {v['us']:7.2f} us  fetch {v['fetch_bytes'] / 1e6:7.2f} MB  write {v['write_bytes'] / 1e6:7.2f} MB"
-              f"  valu {v['valu_insts'] or 0:10.0f}  wait {v.get('wait_frac', 0):.2f}")
+              f"  valu {v['valu_insts'] or 0:10.0f}  wait {v.get('wait_frac', 0):.2f}  l2hit {v.get('l2_hit') or 0:.2f}")
 
 
 if __name__ == "__main__":

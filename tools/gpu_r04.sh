@@ -52,6 +52,12 @@ if [ "$STEPS" = ab ]; then
   unset MVBA_LIB
   python3 tools/bench_summary.py $OUT/ab_*_$TAG.log || true
 fi
+if [ "$STEPS" = configs ]; then
+  # the BASELINE.md table's other rows: c4 whole on one GPU, c5 (depth, fp32 eval line)
+  run bench_c5_$TAG 600 python3 bench.py --config c5 --steps 200 --no-cpu-baseline --mesh-subdiv 0
+  run bench_c4_$TAG 900 python3 bench.py --config c4 --steps 20 --ba-iters 2 --no-cpu-baseline --mesh-subdiv 0
+  python3 tools/bench_summary.py $OUT/bench_c5_$TAG.log $OUT/bench_c4_$TAG.log || true
+fi
 if [ "$STEPS" = chol ]; then
   # X1 pricing: hand-written fp64-MFMA blocked Cholesky vs rocSOLVER dpotrf (tools/chol_bench.hip)
   run chol512_$TAG 120 tools/chol_bench 512
