@@ -316,12 +316,7 @@ __global__ void __launch_bounds__(64) k_depth_sb(const Segment* __restrict__ seg
   }
   {
 #pragma unroll
-    for (int q = 0; q < NA; q++) {
-      double v = acc[q];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      acc[q] = v;
-    }
+    for (int q = 0; q < NA; q++) acc[q] = wave_sum_f64(acc[q]);
     const FrameLin& L = fl[frame];
     double* y = yrep + (int64_t)(seg & (kDReplicas - 1)) * ng;
     int64_t dst = -1;

@@ -155,6 +155,59 @@ __device__ __forceinline__ void cross(const double* a, const double* b, double* 
   c[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+// Sum of v over the 64 lanes of a wave, returned to every lane (all lanes
+// active) as a wave-uniform value. DPP moves only (VALU, no LDS round trip):
+// xor 1 and xor 2 by quad_perm, row_half_mirror and row_mirror give every lane
+// its 16-lane row's sum, row_bcast:15 / row_bcast:31 carry the row sums up to
+// lane 63, whose total v_readlane returns. The __shfl_xor butterfly it replaces
+// costs 12 ds_bpermute_b32 and six dependent LDS round trips per value.
+#ifndef MVBA_DPP_REDUCE
+#define MVBA_DPP_REDUCE 1
+#endif
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#if MVBA_DPP_REDUCE
+  v += dpp_f64<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_f64<0x140, 0xf>(v);  // row_mirror: every lane holds its row's sum
+  v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3: lane 63 holds the total
+  return readlane_f64(v, 63);
+#else
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+#endif
+}
+
+// Sum of v over aligned groups of N lanes (N = 4, 8 or 16), returned to every
+// lane of the group (all lanes active): the first steps of wave_sum_f64.
+template <int N>
+__device__ __forceinline__ double group_sum_f64(double v) {
+  static_assert(N == 4 || N == 8 || N == 16, "group of 4, 8 or 16 lanes");
+#if MVBA_DPP_REDUCE
+  v += dpp_f64<0xB1, 0xf>(v);
+  v += dpp_f64<0x4E, 0xf>(v);
+  if constexpr (N >= 8) v += dpp_f64<0x141, 0xf>(v);
+  if constexpr (N >= 16) v += dpp_f64<0x140, 0xf>(v);
+#else
+  for (int off = 1; off < N; off <<= 1) v += __shfl_xor(v, off, 64);
+#endif
+  return v;
+}
+
 // Write one pose column record: omega, v = dt - omega x t.
 __device__ __forceinline__ void put_col(double* rec, int k, const double* om, const double* dt,
                                         const double* t) {
@@ -410,9 +463,7 @@ template <int K>
 __device__ __forceinline__ void block_sum(double* v) {
   __shared__ double wsum[K][16];
 #pragma unroll
-  for (int k = 0; k < K; k++)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+  for (int k = 0; k < K; k++) v[k] = wave_sum_f64(v[k]);
   const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();  // wsum may still be read by a previous call
   if ((threadIdx.x & 63) == 0)

@@ -1005,12 +1005,9 @@ __device__ __forceinline__ void points_lin_body(
     }
   }
 #pragma unroll
-  for (int off = 1; off < kLanesPerPoint; off <<= 1) {
+  for (int c = 0; c < 6; c++) V[c] = group_sum_f64<kLanesPerPoint>(V[c]);
 #pragma unroll
-    for (int c = 0; c < 6; c++) V[c] += __shfl_xor(V[c], off, 64);
-#pragma unroll
-    for (int c = 0; c < 3; c++) g[c] += __shfl_xor(g[c], off, 64);
-  }
+  for (int c = 0; c < 3; c++) g[c] = group_sum_f64<kLanesPerPoint>(g[c]);
   if (!valid) return;
   // lane `sub` writes entries sub, sub + 4, ... of the 9 outputs
   for (int c = sub; c < 9; c += kLanesPerPoint) {

@@ -585,7 +585,9 @@ class Solver {
         const mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, S_->ctl, 0, 0.0};
         std::swap(S_->p, S_->p2);
         if (fused_dir) {
-          apply_schur_cg(S_->q, gate, S_->ctl, lz, mvba::DirPair{S_->dirz, S_->dirp[pp], S_->dirp[pp ^ 1], S_->ctl});
+          apply_schur_cg(S_->q, gate, S_->ctl, lz,
+                         mvba::DirPair{S_->dirz, S_->dirp[pp], S_->dirp[pp ^ 1], S_->ctl, lz.z, lz.p_old,
+                                       h_->d_frame_lin});
           pp ^= 1;
         } else {
           apply_schur(S_->p, S_->q, 0, gate, S_->ctl, &lz);

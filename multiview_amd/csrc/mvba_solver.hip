@@ -96,11 +96,28 @@ __device__ __forceinline__ void stage_dir(const DirPair& D, int frame, double* s
     first = D.ctl->first;
     beta = D.ctl->beta;
   }
-  for (int m = lane; m < N; m += 64) {
+  const int nrec = D.z ? 6 : N;  // entries taken from the frame records
+  for (int m = lane; m < nrec; m += 64) {
     double v = D.dz[base + m];
     if (!first) v = __fma_rn(beta, D.dp[base + m], v);
     sd[m] = v;
     if (writer) D.dp_out[base + m] = v;
+  }
+  if (D.z) {
+    // intrinsic entries 0 focal, 1..2 centre, 3.. distortion: p_new's own
+    // entries, lazy_p's arithmetic (zero for constant blocks and past K)
+    const FrameLin& L = ((const FrameLin*)D.fl)[frame];
+    const int nd = L.width - 10;  // live distortion entries
+    for (int m = 6 + lane; m < N; m += 64) {
+      const int q = m - 6;
+      int64_t e = -1;
+      if (q == 0) e = L.goff[MVBA_BLK_FOCAL];
+      else if (q < 3) e = L.goff[MVBA_BLK_CENTER] >= 0 ? L.goff[MVBA_BLK_CENTER] + (q - 1) : -1;
+      else if (q - 3 < nd) e = L.goff[MVBA_BLK_DIST] >= 0 ? L.goff[MVBA_BLK_DIST] + (q - 3) : -1;
+      const double v = e < 0 ? 0.0 : first ? D.z[e] : __fma_rn(beta, D.p_old[e], D.z[e]);
+      sd[m] = v;
+      if (writer) D.dp_out[base + m] = v;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -109,7 +126,7 @@ __device__ __forceinline__ void stage_dir(const DirPair& D, int frame, double* s
 // One wave per frame: lane k < 22 takes pose column k (w_k x_k, butterfly-summed
 // over the wave), lanes 22.. copy the intrinsic entries. X(b, j): entry j of the
 // frame's camera block b (MVBA_BLK_*) of x; called only for floating blocks.
-template <class XF>
+template <bool POSE_ONLY = false, class XF>
 __device__ __forceinline__ void frame_dir_body(const FrameLin& L, int32_t K, const double* __restrict__ frec_f,
                                                int lane, XF X, double* __restrict__ d) {
   double u[6] = {0, 0, 0, 0, 0, 0};
@@ -134,6 +151,7 @@ __device__ __forceinline__ void frame_dir_body(const FrameLin& L, int32_t K, con
       if (lane == a) v = u[a];
     d[lane] = v;
   }
+  if constexpr (POSE_ONLY) return;
   // lanes 22.. copy the intrinsic entries: 0 focal, 1..2 centre, 3.. distortion
   const int nd = L.width - 10;
   for (int m = lane - kPoseCols; m >= 0 && m < 3 + nd; m += 64 - kPoseCols) {
@@ -371,9 +389,7 @@ __global__ void __launch_bounds__(256) k_pass_a(
     }
   }
 #pragma unroll
-  for (int off = 1; off < kLanesA; off <<= 1)
-#pragma unroll
-    for (int q = 0; q < 3; q++) tv[q] += __shfl_xor(tv[q], off, 64);
+  for (int q = 0; q < 3; q++) tv[q] = group_sum_f64<kLanesA>(tv[q]);
   double w[3] = {0.0, 0.0, 0.0};
   double sq = 0.0;
   if (valid && X.w != 0.0) {
@@ -630,9 +646,7 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
       t[2] += cv.z;
     }
 #pragma unroll
-  for (int off = 1; off < kLanesW; off <<= 1)
-#pragma unroll
-    for (int q = 0; q < 3; q++) t[q] += __shfl_xor(t[q], off, 64);
+  for (int q = 0; q < 3; q++) t[q] = group_sum_f64<kLanesW>(t[q]);
   if (!solver) return;
   double w[3] = {0.0, 0.0, 0.0};
   if (freep != 0.0) {
@@ -849,12 +863,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     }
   }
 #pragma unroll
-  for (int q = 0; q < NA; q++) {
-    double v = acc[q];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    acc[q] = v;
-  }
+  for (int q = 0; q < NA; q++) acc[q] = wave_sum_f64(acc[q]);
   // every lane holds the totals; lane k < 22 -> pose column k, 22.. -> intrinsics
   const FrameLin& L = fl[frame];
   double* y = yrep + (int64_t)((chunk_base + ch) & (kVecReplicas - 1)) * ng;
@@ -1070,8 +1079,8 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
       return cg_zentry(CgEntry{(int32_t)L.goff[blk], nb, L.hoff[blk] + (int64_t)j * nb}, minv, mode, alpha, q, b,
                        r_in);
     };
-    frame_dir_body(L, K, fz.frec + (int64_t)f * kFrameRecDoubles, (int)(threadIdx.x & 63), Z,
-                   fz.dz + (int64_t)f * kDirStride);
+    frame_dir_body<true>(L, K, fz.frec + (int64_t)f * kFrameRecDoubles, (int)(threadIdx.x & 63), Z,
+                         fz.dz + (int64_t)f * kDirStride);
     return;
   }
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -186,15 +186,24 @@ struct LazyDir {
 // d = dz + beta dp from dz = W z (the CG update kernel's frame blocks) and
 // dp = W p_old (the previous product's records, stored by pass A into dp_out),
 // so no separate direction kernel runs between the update and pass A.
+// With z set, only the 6 pose sums come from dz / dp: the intrinsic entries of
+// d are the camera-side entries of p_new themselves, formed from the global
+// vectors z and p_old (fl: the frame's block offsets), as the reduction that
+// stores p_new forms them (the update's frame blocks then skip them: at RPC
+// degree 2 they were 47 block-row products per frame, most of the update).
 struct DirPair {
   const double* dz;
   const double* dp;  // null: d = dz
   double* dp_out;    // pass A: d stored here by one wave per frame (null: not stored)
   const CgCtl* ctl;  // first / beta
+  const double* z = nullptr;      // intrinsic entries from z / p_old (null: from dz / dp)
+  const double* p_old = nullptr;
+  const void* fl = nullptr;       // FrameLin
 };
 
 // Frame blocks of the CG update kernel: dz = W z for every frame, z = M^-1 r_new
-// recomputed from the same inputs as the entry blocks (owner_blocks of them).
+// recomputed from the same inputs as the entry blocks (owner_blocks of them);
+// the 6 pose sums only (pass A forms the intrinsic entries, DirPair::z).
 struct FrameDirZ {
   const void* fl;  // FrameLin
   const FrameDesc* fd;

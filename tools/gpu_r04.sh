@@ -40,17 +40,42 @@ if [ "$STEPS" = all ] || [ "$STEPS" = shard ]; then
   python3 tools/bench_summary.py $OUT/shard*_$TAG.log || true
 fi
 if [ "$STEPS" = ab ]; then
-  # same-box A/B against another build of the ABI (BASE=path/libmvba.so through MVBA_LIB), alternated twice
+  # same-box A/B against other builds of the ABI (BASE="path/libmvba.so ..." through
+  # MVBA_LIB; "cur" = the in-tree library), alternated twice
   for k in 1 2; do
-    for v in base cur; do
-      if [ $v = base ]; then export MVBA_LIB=$PWD/$BASE; else unset MVBA_LIB; fi
-      run ab_c2_${v}_${k}_$TAG 300 python3 bench.py --steps 2000 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0
-      run ab_s8_${v}_${k}_$TAG 300 python3 bench.py --shard-of 8 --steps 500 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0
-      run ab_c3_${v}_${k}_$TAG 400 python3 bench.py --config c3 --steps 30 --ba-iters 2 --no-cpu-baseline --mesh-subdiv 0
+    for v in $BASE cur; do
+      if [ $v = cur ]; then unset MVBA_LIB; t=cur; else export MVBA_LIB=$PWD/$v; t=$(basename $(dirname $v)); fi
+      for c in ${AB_CFGS:-c2 s8 c3}; do
+        case $c in
+          c2) run ab_c2_${t}_${k}_$TAG 300 python3 bench.py --steps 2000 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0 ;;
+          s8) run ab_s8_${t}_${k}_$TAG 300 python3 bench.py --shard-of 8 --steps 500 --ba-iters 3 --no-cpu-baseline --mesh-subdiv 0 ;;
+          c3) run ab_c3_${t}_${k}_$TAG 400 python3 bench.py --config c3 --steps 30 --ba-iters 2 --no-cpu-baseline --mesh-subdiv 0 ;;
+        esac
+      done
     done
   done
   unset MVBA_LIB
   python3 tools/bench_summary.py $OUT/ab_*_$TAG.log || true
+fi
+if [ "$STEPS" = abk ]; then
+  # same-box kernel-trace A/B of the CG iteration (BASE as for ab): per-kernel
+  # medians over the non-gated iterations (tools/cg_iter_med.py)
+  for k in 1 2; do
+    for v in $BASE cur; do
+      if [ $v = cur ]; then unset MVBA_LIB; t=cur; else export MVBA_LIB=$PWD/$v; t=$(basename $(dirname $v)); fi
+      for c in ${AB_CFGS:-c2 s8 c3}; do
+        case $c in
+          c2) A="--ba-iters 5" ;;
+          s8) A="--shard-of 8 --ba-iters 5" ;;
+          c3) A="--config c3 --ba-iters 2" ;;
+        esac
+        run kt_${c}_${t}_${k}_$TAG 400 rocprofv3 --kernel-trace -d $OUT/kt_${c}_${t}_${k}_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --mesh-subdiv 0 $A
+        python3 tools/cg_iter_med.py ${c}_${t}_${k} $(find $OUT/kt_${c}_${t}_${k}_$TAG -name '*kernel_trace.csv' | head -1) | tee -a $OUT/cg_iter_$TAG.txt
+        find $OUT/kt_${c}_${t}_${k}_$TAG -name '*kernel_trace.csv' -exec gzip {} \;
+      done
+    done
+  done
+  unset MVBA_LIB
 fi
 if [ "$STEPS" = configs ]; then
   # the BASELINE.md table's other rows: c4 whole on one GPU, c5 (depth, fp32 eval line)
