@@ -326,6 +326,39 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     frame_index.emplace(k, id);
     res_frame[i] = id;
   }
+  // Frame numbering in capture order (image timestamp, then camera, then order
+  // of first use), not in order of first use: AddResidualBlock order is
+  // landmark-major (rig_calibrator.cc:1614-1752), so first use scatters the
+  // images of one stretch of the trajectory over the whole frame range. In
+  // capture order, frames next to each other see the same landmarks: the
+  // landmark numbering below (first use in frame order) becomes a band, the
+  // frame-order CG passes of one XCD gather landmark-side vectors (w_p) from an
+  // L2-sized window, and the point-order pass gathers each landmark's c_o from
+  // a few neighbouring frame ranges. MVBA_FRAME_ORDER=first_use keeps the old
+  // numbering (A/B timing).
+  {
+    const char* fo = std::getenv("MVBA_FRAME_ORDER");
+    if (!(fo && !std::strcmp(fo, "first_use")) && frames.size() > 1) {
+      const size_t nf = frames.size();
+      std::vector<int32_t> ord(nf);
+      for (size_t f = 0; f < nf; f++) ord[f] = (int32_t)f;
+      std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) {
+        if (frames[a].sc != frames[b].sc) return frames[a].sc < frames[b].sc;
+        return frames[a].cam < frames[b].cam;
+      });
+      std::vector<int32_t> rank(nf);
+      for (size_t q = 0; q < nf; q++) rank[ord[q]] = (int32_t)q;
+      std::vector<FrameDesc> frames2(nf);
+      std::vector<std::array<int32_t, 8>> blocks2(nf);
+      for (size_t f = 0; f < nf; f++) {
+        frames2[rank[f]] = frames[f];
+        blocks2[rank[f]] = frame_blocks[f];
+      }
+      frames.swap(frames2);
+      frame_blocks.swap(blocks2);
+      for (auto& v : res_frame) v = rank[v];
+    }
+  }
   h->nframes = (int64_t)frames.size();
   h->res_frame = res_frame;
   h->frame_blocks = frame_blocks;
