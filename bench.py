@@ -545,17 +545,23 @@ def main():
     def shard_cfg(strong_split):
         c = dict(cfg)
         if strong_split:
-            # the config's landmark count is the whole problem, split into
-            # contiguous landmark ranges
-            split = world if world > 1 else max(1, args.shard_of)
-            c["point_range"] = (rank * npts // split, (rank + 1) * npts // split)
+            # the config's whole problem (make_strong_shard cuts it)
+            c["point_range"] = (0, npts)
         else:
             # each rank owns a config-sized shard of an N x larger problem
             c["point_range"] = (rank * npts, (rank + 1) * npts)
         return c
 
+    def make_strong_shard():
+        # the config's landmarks split into contiguous ranges of capture order
+        # (rig.shard_points): every rank generates the whole problem and keeps
+        # its range, so the shards partition exactly the N = 1 workload
+        split = world if world > 1 else max(1, args.shard_of)
+        R = rig.make_rig(**shard_cfg(True))
+        return R if split == 1 else rig.shard_points(R, rank, split)
+
     t0 = time.perf_counter()
-    R = rig.make_rig(**shard_cfg(strong))
+    R = make_strong_shard() if strong else rig.make_rig(**shard_cfg(False))
     P = rig.build_problem(R, flags)
     t_gen = time.perf_counter() - t0
 

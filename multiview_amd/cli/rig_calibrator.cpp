@@ -611,7 +611,7 @@ struct Plan {
 // shard) plus the points of a landmark range.
 struct Shard {
   int device = 0;
-  int pid_lo = 0, pid_hi = 0;
+  int index = 0;  // position in the landmark split (shard_of)
   BlockSet blocks;
   std::vector<int32_t> res_blocks, res_cam, dep_blocks, xyz_block;
   std::vector<double> res_meas, res_stamps, dep_meas, dep_weight, dep_stamps, xyz_ref, xyz_weight, xyz_thr;
@@ -1103,22 +1103,34 @@ static int run(int argc, char** argv) {
     }
     if (plan.cam.empty()) fatal("No inlier observations are left to optimize.");
 
-    // shards: contiguous landmark ranges balanced by residual count
+    // shards: contiguous landmark ranges of capture order (the timestamp of a
+    // landmark's first observing image, then its id), balanced by residual
+    // count: each shard then holds the images of one stretch of the trajectory
+    // (plus the tracks' reach) instead of observations in every image, so its
+    // per-image work shrinks with the split too (bench.py splits the same way,
+    // rig.shard_points)
     std::vector<Shard> shards((size_t)ngpu);
-    {
-      std::vector<int64_t> per_pid((size_t)npid + 1, 0);
-      for (const auto& r : plan.cam) per_pid[(size_t)r.pid + 1]++;
-      for (int p = 0; p < npid; p++) per_pid[(size_t)p + 1] += per_pid[(size_t)p];
-      int lo = 0;
-      for (int s = 0; s < ngpu; s++) {
-        const int64_t target = per_pid[(size_t)npid] * (s + 1) / ngpu;
-        int hi = lo;
-        while (hi < npid && (per_pid[(size_t)hi + 1] <= target || s == ngpu - 1)) hi++;
-        shards[(size_t)s].pid_lo = lo;
-        shards[(size_t)s].pid_hi = hi;
-        shards[(size_t)s].device = (device0 + s) % ndev;  // shards share GPUs when there are fewer
-        lo = hi;
+    std::vector<int> shard_of((size_t)npid, 0);
+    if (ngpu > 1) {
+      std::vector<double> first((size_t)npid, std::numeric_limits<double>::infinity());
+      std::vector<int64_t> per_pid((size_t)npid, 0);
+      for (const auto& r : plan.cam) {
+        first[(size_t)r.pid] = std::min(first[(size_t)r.pid], r.stamps[2]);
+        per_pid[(size_t)r.pid]++;
       }
+      std::vector<int> ord((size_t)npid);
+      for (int p = 0; p < npid; p++) ord[(size_t)p] = p;
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return first[(size_t)a] < first[(size_t)b]; });
+      const int64_t tot = std::max<int64_t>((int64_t)plan.cam.size(), 1);
+      int64_t acc = 0;
+      for (int p : ord) {
+        shard_of[(size_t)p] = (int)std::min<int64_t>(ngpu - 1, acc * ngpu / tot);
+        acc += per_pid[(size_t)p];
+      }
+    }
+    for (int s = 0; s < ngpu; s++) {
+      shards[(size_t)s].index = s;
+      shards[(size_t)s].device = (device0 + s) % ndev;  // shards share GPUs when there are fewer
     }
     // camera-side blocks first, in the order the whole problem references them,
     // so every shard has the same camera layout; constancy and bounds are
@@ -1156,7 +1168,7 @@ static int run(int argc, char** argv) {
       S.res_meas.reserve(2 * nres_hint);
       S.res_stamps.reserve(3 * nres_hint);
       for (const auto& r : plan.cam) {
-        if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
+        if (shard_of[(size_t)r.pid] != S.index) continue;
         for (int b = 0; b < 8; b++) S.res_blocks.push_back(b == MVBA_BLK_XYZ ? point(r.pid) : r.id[b]);
         S.res_cam.push_back(r.cam_type);
         S.res_meas.insert(S.res_meas.end(), r.meas, r.meas + 2);
@@ -1164,7 +1176,7 @@ static int run(int argc, char** argv) {
         S.res_feature.push_back(r.feature);
       }
       for (const auto& r : plan.depth) {
-        if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
+        if (shard_of[(size_t)r.pid] != S.index) continue;
         for (int b = 0; b < 7; b++)
           S.dep_blocks.push_back(b == MVBA_DBLK_XYZ ? (r.mesh ? -1 : point(r.pid)) : r.id[b]);
         S.dep_meas.insert(S.dep_meas.end(), r.meas, r.meas + 3);
@@ -1175,7 +1187,7 @@ static int run(int argc, char** argv) {
         S.any_mesh = S.any_mesh || r.mesh;
       }
       for (const auto& r : plan.xyz) {
-        if (r.pid < S.pid_lo || r.pid >= S.pid_hi) continue;
+        if (shard_of[(size_t)r.pid] != S.index) continue;
         S.xyz_block.push_back(point(r.pid));
         S.xyz_ref.insert(S.xyz_ref.end(), r.ref, r.ref + 3);
         S.xyz_weight.push_back(r.weight);

@@ -440,15 +440,15 @@ class Solver {
 
   static mvba::DirPair plain_dir(const double* dir) { return mvba::DirPair{dir, nullptr, nullptr, nullptr}; }
 
-  // Where pass A leaves c_o: slot order (coalesced stores, k_point_w gathers)
-  // once the point-order table outgrows the caches. Same-box kernel traces
-  // (profiles/r03/ab_co_order/): c2 (1M observations, 32 MB) pass A + k_point_w
-  // 29.8 us point order vs 36.0 slot order; c3 (10M, 320 MB) 395 vs 327 us.
+  // Where pass A leaves c_o: slot order (coalesced stores, k_point_w gathers).
+  // With frames in first-use order the point-order scatter won below ~128 MB of
+  // table (profiles/r03/ab_co_order/: c2 pass A + k_point_w 29.8 us point order
+  // vs 36.0 slot order; c3 395 vs 327 us); with frames in capture order (the
+  // gathers of neighbouring landmarks share lines) slot order wins at both
+  // sizes (profiles/r04/r04m/: c2 27.9 vs 29.0 us, c3 303 vs 361 us).
   // MVBA_CO_ORDER=point|slot forces one.
   bool co_slot_order(const char* env) const {
-    if (env && !std::strcmp(env, "slot")) return true;
-    if (env && !std::strcmp(env, "point")) return false;
-    return h_->nslots * (int64_t)sizeof(double4) > (int64_t)128 << 20;
+    return !(env && !std::strcmp(env, "point"));
   }
 
   // w_p = (V + D)^-1 (tinit + sum J_pt^T J_cam x) into wbuf (dr: frame

@@ -469,6 +469,39 @@ def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, mode
 SPHERE_RADIUS = 4.0
 
 
+def shard_points(R: Rig, rank: int, world: int) -> Rig:
+    """Rank's landmark-range shard of ``R`` in capture order:
+    landmarks ordered by the capture time of their first observation (then by
+    id), cut into ``world`` contiguous ranges of equal observation count. A
+    shard keeps every camera and the observations of its landmarks, relabelled
+    0..k-1 in id order (pid-major order is kept). Contiguous ranges of the
+    user's ids would give every shard observations in every image; ranges in
+    capture order give each shard the images of one stretch of the trajectory
+    (plus the tracks' reach), so its per-image work shrinks with the split too."""
+    import dataclasses
+
+    npts = len(R.xyz)
+    first = np.full(npts, np.inf)
+    np.minimum.at(first, R.obs_pid, R.cam_stamp[R.obs_cid])
+    order = np.lexsort((np.arange(npts), first))
+    cum = np.cumsum(np.bincount(R.obs_pid, minlength=npts)[order])
+    tot = int(cum[-1]) if npts else 0
+    cuts = [0] + [int(np.searchsorted(cum, tot * r // world, side="right")) for r in range(1, world)] + [npts]
+    sel = np.sort(order[cuts[rank]:cuts[rank + 1]])
+    newid = -np.ones(npts, dtype=np.int64)
+    newid[sel] = np.arange(sel.size)
+    keep = newid[R.obs_pid] >= 0
+    init = dict(R.init)
+    init["xyz"] = R.init["xyz"][sel]
+    depth_obs, depth_meas = R.depth_obs, R.depth_meas
+    if depth_obs is not None:
+        obs_new = np.cumsum(keep) - 1
+        dk = keep[depth_obs]
+        depth_obs, depth_meas = obs_new[depth_obs[dk]], depth_meas[dk]
+    return dataclasses.replace(R, xyz=R.xyz[sel], obs_pid=newid[R.obs_pid[keep]], obs_cid=R.obs_cid[keep],
+                               obs_pix=R.obs_pix[keep], init=init, depth_obs=depth_obs, depth_meas=depth_meas)
+
+
 def sphere_mesh(subdiv: int = 5, radius: float = SPHERE_RADIUS):
     """Icosphere (float32 vertices on the sphere, uint32 faces, outward winding):
     the synthetic stand-in for the --mesh PLY of a scene with surface="sphere"."""

@@ -136,8 +136,10 @@ def _c4_shard(rank):
 
 
 def test_full_size_c4_shards(oracle):
-    """c4: 8-sensor rig, 5M landmarks, 50M observations, as the 8 landmark-range
-    shards of the 8-GPU run (bench.py --config c4), each evaluated on this GPU.
+    """c4: 8-sensor rig, 5M landmarks, 50M observations, as 8 landmark-range
+    shards (make_rig point ranges: each shard's landmarks from its own stream;
+    bench.py cuts the whole problem in capture order instead, rig.shard_points),
+    each evaluated on this GPU.
     Shards are generated by 8 worker processes (CPU only) while the GPU checks
     the previous ones."""
     total = 0

@@ -70,3 +70,32 @@ def test_shards_partition_points():
     assert np.array_equal(a.init["world_to_ref"], b.init["world_to_ref"])
     assert np.array_equal(full.init["world_to_ref"], a.init["world_to_ref"])
     assert a.xyz.shape[0] == 50 and b.xyz.shape[0] == 50
+
+
+def test_capture_order_shards_partition_the_problem():
+    """rig.shard_points (bench.py's strong split): the shards partition the
+    landmarks and observations of the whole problem exactly (same pixels, same
+    images, pid-major order), balance the observation count, keep depth
+    observations attached to theirs, and each shard sees a stretch of the
+    trajectory: far fewer images than the whole problem."""
+    R = rig.make_rig(num_sensors=4, num_ref=200, num_points=4000, obs_per_point=6.0, seed=5,
+                     models=["radtan"] * 4, depth_sensors=(3,))
+    world = 4
+    shards = [rig.shard_points(R, r, world) for r in range(world)]
+    assert sum(len(S.xyz) for S in shards) == len(R.xyz)
+    assert sum(len(S.obs_pid) for S in shards) == len(R.obs_pid)
+    assert sum(len(S.depth_obs) for S in shards) == len(R.depth_obs)
+    whole = {(tuple(R.xyz[p]), c, tuple(x)) for p, c, x in zip(R.obs_pid, R.obs_cid, R.obs_pix)}
+    got = set()
+    for S in shards:
+        assert np.all(np.diff(S.obs_pid) >= 0)
+        assert np.array_equal(S.init["world_to_ref"], R.init["world_to_ref"])
+        assert abs(len(S.obs_pid) - len(R.obs_pid) / world) < 0.02 * len(R.obs_pid)
+        assert len(np.unique(S.obs_cid)) < 0.5 * len(R.cam_type)
+        got |= {(tuple(S.xyz[p]), c, tuple(x)) for p, c, x in zip(S.obs_pid, S.obs_cid, S.obs_pix)}
+        # the depth point travels with its observation
+        src = {(tuple(R.xyz[R.obs_pid[o]]), R.obs_cid[o]): tuple(m) for o, m in zip(R.depth_obs, R.depth_meas)}
+        for o, m in zip(S.depth_obs, S.depth_meas):
+            assert src[(tuple(S.xyz[S.obs_pid[o]]), S.obs_cid[o])] == tuple(m)
+        rig.build_problem(S)
+    assert got == whole

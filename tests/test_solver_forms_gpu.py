@@ -95,9 +95,10 @@ def test_cg_direction_forms_agree(monkeypatch):
     (sa, xa), (sb, xb) = exact
     assert sa["num_linear_iterations"] > 10 and sb["num_linear_iterations"] > 10
     # CG to eta = 1e-14 on this 3,000-landmark problem: the two roundings
-    # agree to the system's conditioning (measured 3e-8)
+    # agree to the system's conditioning (measured 3e-8 with frames in first-use
+    # order, 1.2e-7 in capture order: profiles/r04/r04m/pytest_gpu_r04m.log)
     scale = np.maximum(np.abs(xa), 1.0)
-    assert (np.abs(xa - xb) / scale).max() < 1e-7
+    assert (np.abs(xa - xb) / scale).max() < 5e-7
     (sa, xa), (sb, xb) = conv
     assert sa["termination_type"] == 0 and sb["termination_type"] == 0, (sa["message"], sb["message"])
     # the same minimum: the cost to rounding (some intrinsics / rig directions of
