@@ -573,10 +573,17 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       G.part_begin = (int32_t)parts.size();
       G.gram_width = h->lin_ok ? mvba_gram_width(G.model, G.deg) : 0;
       G.w16 = (G.gram_width + 15) / 16 * 16;
+      // segments per pass-B chunk (one wave): mvba::kChunkSegs; MVBA_CHUNK_SEGS
+      // overrides it (A/B timing)
+      static const int chunk_segs = [] {
+        const char* e = std::getenv("MVBA_CHUNK_SEGS");
+        const int v = e ? std::atoi(e) : mvba::kChunkSegs;
+        return v >= 1 && v <= 64 ? v : mvba::kChunkSegs;
+      }();
       for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++) {
         const Segment& sg = segs[sidx];
         if (chunks.size() == (size_t)G.chunk_begin || chunks.back().z != sg.frame ||
-            chunks.back().y == mvba::kChunkSegs) {
+            chunks.back().y == chunk_segs) {
           int4 c;
           c.x = sidx;
           c.y = 0;
@@ -915,13 +922,18 @@ double mvba_eval_bytes(const mvba_handle* h, int32_t flags) {
 
 // Which launch form a full evaluation takes (MVBA_FORM_*); MVBA_SPLIT_PREP=1 /
 // MVBA_EVAL_MODE=split|fused|local force one, for A/B timing (read per call).
+// One model group: k_eval_local at every size. With frames in capture order it
+// measured faster than the fused form (K0 blocks handing records to the K1
+// waves) on the whole c2 (95.5-96.5 vs 100.9-101.5 us), equal on c3
+// (2.14-2.20 vs 2.17 ms), and faster on every shard of c2 (N = 2 / 4 / 8:
+// 53.0 / 28.0 / 17.9 vs 57.7 / 35.0 / 24.1 us), profiles/r04/r04o, r04p.
 static int eval_form(const mvba_handle* h) {
   const char* sp = std::getenv("MVBA_SPLIT_PREP");
   const char* m = std::getenv("MVBA_EVAL_MODE");
   const int forced = !m ? -1 : !std::strcmp(m, "split") ? 0 : !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "local") ? 2 : -1;
   if ((sp && sp[0] == '1') || forced == 0 || h->groups.size() != 1) return MVBA_FORM_SPLIT;
   if (forced > 0) return forced == 1 ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
-  return h->groups[0].seg_count >= 4 * h->nframes ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
+  return MVBA_FORM_LOCAL;
 }
 
 int32_t mvba_eval_form(const mvba_handle* h) { return h ? eval_form(h) : -1; }
@@ -983,19 +995,14 @@ static mvba_status evaluate_device_impl(mvba_handle* h, int32_t flags, double ca
     cauchy_c = 1.0 / (cauchy_threshold * cauchy_threshold);
   }
   hipError_t e = hipSuccess;
-  // One model group with at least four segments per frame: prep and K1 in one
-  // launch (K0 blocks hand their frame records to the K1 waves of the same grid;
-  // c2 101.8 vs 104.5 us, c3 2.16 vs 2.24 ms per step, same box). For thin
-  // shards (about one segment per frame: c2 split 8 ways) the hand-off measured
-  // slower than two launches (27.9 vs 24.1 us: the fused kernel's K0-sized
-  // register file, 156 VGPRs, 3 waves per SIMD). MVBA_SPLIT_PREP=1 forces two
-  // launches, for A/B timing.
-  // Fewer than four segments per frame (shards of a landmark split) run
-  // k_eval_local: every K1 wave computes its own frame's record in LDS, so
-  // neither a prep launch nor a hand-off sits in front of K1 (same box, rank 0's
-  // shard of c2: 2-way 56.1-56.5 vs fused 61.2-61.8 us, 8-way 19.1-20.6 vs
-  // split 22.1-23.6 us; whole c2 98.4-101.1 vs fused 100.3-102.0 us;
-  // profiles/r03/ab_eval_local/). eval_form() picks; mvba_eval_form reports it.
+  // One model group: one launch. k_eval_local (the default, eval_form): every
+  // K1 wave computes its own frame's record in LDS, so neither a prep launch
+  // nor a hand-off sits in front of K1. k_eval (MVBA_EVAL_MODE=fused): K0
+  // blocks hand their frame records to the K1 waves of the same grid (round 3's
+  // choice above four segments per frame; slower once frames are numbered in
+  // capture order, profiles/r04/r04p/). Several model groups: the prep launch,
+  // then K1 per group. MVBA_SPLIT_PREP=1 forces two launches (A/B timing);
+  // mvba_eval_form reports the form.
   const int form = (flags & (MVBA_EVAL_SKIP_PREP | MVBA_EVAL_PREP_ONLY)) ? MVBA_FORM_SPLIT : eval_form(h);
   if (form != MVBA_FORM_SPLIT) {
     h->gen++;

@@ -66,6 +66,35 @@ __device__ __forceinline__ void obs_rows(const FrameDesc& F, const double* __res
   });
 }
 
+// RPC monomials of the centred undistorted pixel in the coefficient order of
+// compute_rpc (rpc_distortion.cc:116-160: degree dg, then q): m[k] = u0^(dg-q) u1^q.
+// Every RPC distortion column is one of them times a per-row scale (the
+// coefficients of num_x / den_x / num_y / den_y: iDx m_k, -(Nx/Dx)/Dx m_k, and
+// the same for y, dist_columns), with the other row structurally zero: the CG
+// passes fold the columns into dot products with the monomials instead of
+// forming them (no multiply-adds of structural zeros).
+template <int DEG>
+struct RpcShape {
+  static constexpr int kNl = (DEG + 1) * (DEG + 2) / 2;  // coefficients of a numerator
+  // first distortion column of num_x, den_x (no constant), num_y, den_y
+  static constexpr int kNx = 0, kDx = kNl, kNy = 2 * kNl - 1, kDy = 3 * kNl - 1;
+};
+template <int DEG>
+__device__ __forceinline__ void rpc_monomials(double u0, double u1, double* m) {
+  double px[DEG + 1], py[DEG + 1];
+  double vx = 1.0, vy = 1.0;
+#pragma unroll
+  for (int k = 0; k <= DEG; k++) {
+    px[k] = vx; vx *= u0;
+    py[k] = vy; vy *= u1;
+  }
+  int k = 0;
+#pragma unroll
+  for (int dg = 0; dg <= DEG; dg++)
+#pragma unroll
+    for (int q = 0; q <= dg; q++) m[k++] = px[dg - q] * py[q];
+}
+
 template <int MODEL, int DEG>
 struct RowShape {
   static constexpr int kDist = (MODEL == kModelNone) ? 0 : (MODEL == kModelFov) ? 1
@@ -254,6 +283,9 @@ __device__ __forceinline__ void pass_a_obs(const double* __restrict__ rec, const
     z0 += sr * dirf[7];
     z1 += sr * dirf[8];
   }
+  // (the distortion columns one by one, structural zeros included: folding
+  // them through the monomials as pass B does raised pass A from 74 to 100
+  // VGPRs and its c3 time from 178 to 212 us, profiles/r04/r04o/)
   dist_columns<MODEL, DEG>(o, f, K, sr, [&](int q, double a0, double a1) {
     z0 += a0 * dirf[9 + q];
     z1 += a1 * dirf[9 + q];
@@ -793,6 +825,92 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
   }
 }
 
+// Pass B's per-observation work for RPC (degree <= 3, register accumulators):
+// obs_rows + the loop of k_pass_b with the distortion columns folded through
+// the monomials (RpcShape): z takes the four monomial dot products with the
+// direction's num / den entries, each accumulator of a distortion column gets
+// (row scale * u) * monomial, and the structurally zero rows (the other
+// coordinate's half, the centre columns) cost nothing.
+template <int DEG>
+__device__ __forceinline__ void pass_b_rpc_obs(const FrameDesc& F, const double* __restrict__ rec,
+                                               const double* __restrict__ params, double4 X, double2 m,
+                                               int32_t flags, double cauchy_c, double sr_given,
+                                               const double* __restrict__ d, double4 w, double* acc) {
+  using RS = RpcShape<DEG>;
+  const double f = params[F.off[MVBA_BLK_FOCAL]];
+  const double c0 = params[F.off[MVBA_BLK_CENTER]];
+  const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
+  Proj o;
+  project<kModelRpc, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+  double sr = sr_given;
+  if (sr < 0.0) {
+    double hr;
+    sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
+  }
+  const double fz = f / o.Xc[2] * sr;
+  const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+  const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
+  double a0[3], a1[3];
+  cross(o.Xc, G0, a0);
+  cross(o.Xc, G1, a1);
+  double mono[RS::kNl];
+  rpc_monomials<DEG>(o.u0, o.u1, mono);
+  const double iDx = o.aux0 * sr, iDy = o.aux1 * sr;
+  const double mqx = -o.aux2 * iDx, mqy = -o.aux3 * iDy;
+  const double fx = o.df0 * sr, fy = o.df1 * sr;
+  double z0 = 0.0, z1 = 0.0;
+  if (d) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      z0 += a0[a] * d[a];
+      z1 += a1[a] * d[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      z0 += G0[a] * d[3 + a];
+      z1 += G1[a] * d[3 + a];
+    }
+    z0 += fx * d[6];
+    z1 += fy * d[6];
+    const double* dd = d + 9;
+    double snx = mono[0] * dd[RS::kNx], sny = mono[0] * dd[RS::kNy], sdx = 0.0, sdy = 0.0;
+#pragma unroll
+    for (int k = 1; k < RS::kNl; k++) {
+      snx += mono[k] * dd[RS::kNx + k];
+      sdx += mono[k] * dd[RS::kDx + k - 1];
+      sny += mono[k] * dd[RS::kNy + k];
+      sdy += mono[k] * dd[RS::kDy + k - 1];
+    }
+    z0 += iDx * snx + mqx * sdx;
+    z1 += iDy * sny + mqy * sdy;
+  }
+  double P0[3], P1[3];
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    P0[q] = G0[0] * rec[q] + G0[1] * rec[3 + q] + G0[2] * rec[6 + q];
+    P1[q] = G1[0] * rec[q] + G1[1] * rec[3 + q] + G1[2] * rec[6 + q];
+  }
+  const double ux = z0 - (P0[0] * w.x + P0[1] * w.y + P0[2] * w.z);
+  const double uy = z1 - (P1[0] * w.x + P1[1] * w.y + P1[2] * w.z);
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    acc[a] += a0[a] * ux + a1[a] * uy;
+    acc[3 + a] += G0[a] * ux + G1[a] * uy;
+  }
+  acc[6] += fx * ux + fy * uy;  // focal; the centre columns (7, 8) are zero for RPC
+  const double ax = iDx * ux, bx = mqx * ux, ay = iDy * uy, by = mqy * uy;
+#pragma unroll
+  for (int k = 0; k < RS::kNl; k++) {
+    acc[9 + RS::kNx + k] += ax * mono[k];
+    acc[9 + RS::kNy + k] += ay * mono[k];
+  }
+#pragma unroll
+  for (int k = 1; k < RS::kNl; k++) {
+    acc[9 + RS::kDx + k - 1] += bx * mono[k];
+    acc[9 + RS::kDy + k - 1] += by * mono[k];
+  }
+}
+
 // ------------------------------------------------------------ pass B (frame order)
 // One wave per frame chunk: per observation u_o = z_o - J_pt w_p, with
 // z_o = J_cam,o x from the frame direction (dir; null: x = 0) and w_p from pass A
@@ -834,6 +952,11 @@ __global__ void __launch_bounds__(64) k_pass_b(
       const int32_t pid = obs_pid[i];
       const double4 w = wbuf[pid];
       const double4 X = obsX ? obsX[i] : pts[pid];
+      if constexpr (MODEL == kModelRpc) {
+        pass_b_rpc_obs<DEG>(F, rec, params, X, obsX ? double2{0.0, 0.0} : obs_meas[i], flags, cauchy_c,
+                            obsX ? X.w : -1.0, d, w, acc);
+        continue;
+      }
       double Z0[6], Z1[6], I0[RS::kIntr], I1[RS::kIntr], P0[3], P1[3], r[2], hr;
 #pragma unroll
       for (int q = 0; q < RS::kIntr; q++) I0[q] = I1[q] = 0.0;

@@ -1,8 +1,8 @@
 """The one-launch forms of mvba_evaluate_device against the two-launch form.
 
-mvba_evaluate_device runs one launch for a one-group problem: k_eval_local
-below four segments per frame (each K1 wave computes its own frame's K0 record
-in LDS) and k_eval otherwise (K0 blocks hand the records to the K1 waves of the
+mvba_evaluate_device runs one launch for a one-group problem: k_eval_local by
+default (each K1 wave computes its own frame's K0 record in LDS) or, forced by
+MVBA_EVAL_MODE=fused, k_eval (K0 blocks hand the records to the K1 waves of the
 same grid). Both must write bit-identical planes to the two-launch form (the
 prep kernel, MVBA_EVAL_PREP_ONLY, then K1 with MVBA_EVAL_SKIP_PREP: the same
 arithmetic), and the frame records and landmark records they leave behind must
@@ -16,21 +16,21 @@ from multiview_amd.evaluator import Evaluator
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("npts,form", [(120, "k_eval_local"), (2500, "k_eval")])
+@pytest.mark.parametrize("npts", [120, 2500])
+@pytest.mark.parametrize("form", ["k_eval_local", "k_eval"])
 @pytest.mark.parametrize("jacobian", [True, False])
-def test_one_launch_evaluation_matches_two_launches(npts, form, jacobian):
+def test_one_launch_evaluation_matches_two_launches(monkeypatch, npts, form, jacobian):
     import torch
 
     R = rig.make_rig(num_sensors=3, num_ref=10, num_points=npts, obs_per_point=4, seed=5)
     P = rig.build_problem(R)
+    if form == "k_eval":
+        monkeypatch.setenv("MVBA_EVAL_MODE", "fused")
     with Evaluator(P) as ev:
         ev.set_params()
-        # the form the library picks: segments (64 observations of one image)
-        # per frame
         obs = np.bincount(R.obs_cid)
-        segs = np.ceil(obs[obs > 0] / 64.0).sum()
         assert ev.num_frames == (obs > 0).sum()
-        assert (segs < 4 * ev.num_frames) == (form == "k_eval_local"), (segs, ev.num_frames)
+        assert ev.eval_form() == (_lib.FORM_FUSED if form == "k_eval" else _lib.FORM_LOCAL)
         ld = ev.ld
         outs = []
         # before every form the frame and landmark records are made stale: a
@@ -69,8 +69,10 @@ def test_fused_wait_gives_up_with_an_error(monkeypatch):
 
     R = rig.make_rig(num_sensors=3, num_ref=10, num_points=2500, obs_per_point=4, seed=5)
     P = rig.build_problem(R)
+    monkeypatch.setenv("MVBA_EVAL_MODE", "fused")  # k_local is the default form
     with Evaluator(P) as ev:
         ev.set_params()
+        assert ev.eval_form() == _lib.FORM_FUSED
         ref = None
         for limit in ("0", None):
             if limit is None:
@@ -99,9 +101,11 @@ def test_fused_wait_gives_up_with_an_error(monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("npts,models", [(120, ["radtan", "radtan4", "radtan"]), (2500, ["rpc2"] * 3),
                                           (60, ["radtan", "fov", "radtan"])])
-def test_every_form_matches_the_oracle(oracle, npts, models):
-    """The one-launch form the library picks (k_eval_local for 120 / 60
-    landmarks, k_eval for 2500) and the two-launch form agree with the oracle
+@pytest.mark.parametrize("mode", [None, "fused"])
+def test_every_form_matches_the_oracle(oracle, monkeypatch, npts, models, mode):
+    """The one-launch forms (k_eval_local, the default; k_eval with
+    MVBA_EVAL_MODE=fused; the two-group problem runs split) and the two-launch
+    form agree with the oracle
     per residual block on planes initialised to NaN: constant blocks differ
     between sensors (ref_cam poses float, cam1's rig transform floats), radtan
     K = 4 and 5 share a model group, fov and radtan are two groups."""
@@ -112,6 +116,8 @@ def test_every_form_matches_the_oracle(oracle, npts, models):
                                             intrinsics_to_float=("focal_length", "distortion")))
     _, r_o, J_o = oracle.evaluate(P, oracle.ANALYTIC)
     colmax = np.maximum(np.abs(J_o).max(axis=0), 1e-12)
+    if mode:
+        monkeypatch.setenv("MVBA_EVAL_MODE", mode)
     with Evaluator(P) as ev:
         ev.set_params()
         order = ev.order()

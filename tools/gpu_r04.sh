@@ -28,7 +28,7 @@ fi
 if [ "$STEPS" = all ] || [ "$STEPS" = bench ]; then
   run bench_$TAG 600 python bench.py
   run bench_c1_$TAG 300 python bench.py --config c1 --mesh-subdiv 0
-  run bench_c3_$TAG 600 python bench.py --config c3 --steps 50 --no-cpu-baseline --mesh-subdiv 0
+  run bench_c3_$TAG 600 python bench.py --config c3 --steps 50 --mesh-subdiv 0
   run prof_c2_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2_$TAG -o run --output-format csv -- python3 bench.py --steps 200 --no-cpu-baseline --mesh-subdiv 0
   python3 tools/bench_summary.py $OUT/bench_$TAG.log $OUT/bench_c1_$TAG.log $OUT/bench_c3_$TAG.log || true
 fi
@@ -79,8 +79,8 @@ if [ "$STEPS" = abk ]; then
 fi
 if [ "$STEPS" = configs ]; then
   # the BASELINE.md table's other rows: c4 whole on one GPU, c5 (depth, fp32 eval line)
-  run bench_c5_$TAG 600 python3 bench.py --config c5 --steps 200 --no-cpu-baseline --mesh-subdiv 0
-  run bench_c4_$TAG 900 python3 bench.py --config c4 --steps 20 --ba-iters 2 --no-cpu-baseline --mesh-subdiv 0
+  run bench_c5_$TAG 600 python3 bench.py --config c5 --steps 200 --mesh-subdiv 0
+  run bench_c4_$TAG 900 python3 bench.py --config c4 --steps 20 --ba-iters 2 --mesh-subdiv 0
   python3 tools/bench_summary.py $OUT/bench_c5_$TAG.log $OUT/bench_c4_$TAG.log || true
 fi
 if [ "$STEPS" = chol ]; then
@@ -89,13 +89,13 @@ if [ "$STEPS" = chol ]; then
   run chol_$TAG 400 tools/chol_bench 21248
 fi
 if [ "$STEPS" = pmc ]; then
-  # per-launch HBM traffic of the evaluation launch (k_eval) and of K1 (k_obs), separate FETCH / WRITE passes
+  # per-launch HBM traffic of the evaluation launch (k_eval_local, the default form) and of K1 (k_obs), separate FETCH / WRITE passes
   for CFG in ${PMC_CFGS:-c2 c3}; do
     B="python3 bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --ba-iters 0 --mesh-subdiv 0"
     run fetch_${CFG}_$TAG 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_${CFG}_$TAG -o run --output-format csv -- $B
     run write_${CFG}_$TAG 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write_${CFG}_$TAG -o run --output-format csv -- $B
     D=$(python3 -c "import sys; sys.path.insert(0, '.'); from multiview_amd import rig; from bench import kernel_degree; m = rig.CONFIGS['$CFG']['models'][0]; print(kernel_degree(m))")
-    python3 tools/pmc_summary.py $OUT/fetch_${CFG}_$TAG/run_counter_collection.csv $OUT/write_${CFG}_$TAG/run_counter_collection.csv "k_eval<$D, double, true>" $OUT/pmc_eval_${CFG}.json $CFG
+    python3 tools/pmc_summary.py $OUT/fetch_${CFG}_$TAG/run_counter_collection.csv $OUT/write_${CFG}_$TAG/run_counter_collection.csv "k_eval_local<$D, double, true>" $OUT/pmc_eval_${CFG}.json $CFG
     python3 tools/pmc_summary.py $OUT/fetch_${CFG}_$TAG/run_counter_collection.csv $OUT/write_${CFG}_$TAG/run_counter_collection.csv "k_obs<$D, double>" $OUT/pmc_k1_${CFG}.json $CFG
   done
 fi
