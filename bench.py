@@ -12,7 +12,9 @@ columns).
 Multi-GPU (one process per GPU, torchrun): observations are sharded by
 landmark range. The headline is STRONG scaling: the config's
 landmarks (c2: 100k landmarks / 1M observations) are the whole job, split into
-N contiguous landmark ranges; evaluation has no data-path collective; value =
+N contiguous landmark ranges of capture order (rig.shard_points: landmarks by
+the timestamp of their first observing image, equal observation counts);
+evaluation has no data-path collective; value =
 all ranks' evals / max time. With N > 1 a "weak" object adds the weak-scaling
 line (each rank owns a config-sized shard of an N x larger problem). The LM
 phase exchanges through the library's RCCL communicator (mvba_comm, stream-
@@ -124,6 +126,9 @@ class PhaseGuard:
             self.line[name]["skipped"] = "an earlier phase failed on some rank"
             return False
         err = None
+        # progress on stderr (long phases at c3 / c4 would otherwise be silent
+        # for minutes; stdout carries only the one JSON line)
+        print(f"[bench] rank {self.rank}: phase {name}", file=sys.stderr, flush=True)
         try:
             fn()
         except Exception as e:  # noqa: BLE001 - recorded in the line
@@ -1166,6 +1171,7 @@ def main():
     if rank == 0 and world == 1 and args.mesh_subdiv > 0:
         line["mesh"] = mesh_bench(torch, stream, ev.num_residuals, args)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        print("[bench] cpu baseline", file=sys.stderr, flush=True)
         line["cpu_baseline"] = cpu_baseline(P, args.cpu_sample)
     if rank == 0:
         print(json.dumps(line), flush=True)

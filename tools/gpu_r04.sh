@@ -28,7 +28,7 @@ fi
 if [ "$STEPS" = all ] || [ "$STEPS" = bench ]; then
   run bench_$TAG 600 python bench.py
   run bench_c1_$TAG 300 python bench.py --config c1 --mesh-subdiv 0
-  run bench_c3_$TAG 600 python bench.py --config c3 --steps 50 --mesh-subdiv 0
+  run bench_c3_$TAG 600 python bench.py --config c3 --steps 50 --mesh-subdiv 0 --cpu-sample 200000
   run prof_c2_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2_$TAG -o run --output-format csv -- python3 bench.py --steps 200 --no-cpu-baseline --mesh-subdiv 0
   python3 tools/bench_summary.py $OUT/bench_$TAG.log $OUT/bench_c1_$TAG.log $OUT/bench_c3_$TAG.log || true
 fi
@@ -79,8 +79,8 @@ if [ "$STEPS" = abk ]; then
 fi
 if [ "$STEPS" = configs ]; then
   # the BASELINE.md table's other rows: c4 whole on one GPU, c5 (depth, fp32 eval line)
-  run bench_c5_$TAG 600 python3 bench.py --config c5 --steps 200 --mesh-subdiv 0
-  run bench_c4_$TAG 900 python3 bench.py --config c4 --steps 20 --ba-iters 2 --mesh-subdiv 0
+  run bench_c5_$TAG 600 python3 bench.py --config c5 --steps 200 --mesh-subdiv 0 --cpu-sample 1000000
+  run bench_c4_$TAG 900 python3 bench.py --config c4 --steps 20 --ba-iters 2 --mesh-subdiv 0 --cpu-sample 1000000
   python3 tools/bench_summary.py $OUT/bench_c5_$TAG.log $OUT/bench_c4_$TAG.log || true
 fi
 if [ "$STEPS" = chol ]; then
