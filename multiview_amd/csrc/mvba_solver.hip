@@ -630,7 +630,10 @@ __global__ void __launch_bounds__(64) k_depth_pa(const Segment* __restrict__ seg
 
 // w_p = (V + D)^-1 (tinit + sum_o c_o), kLanesW lanes per point gathering its
 // c_o (lane-strided, then a butterfly sum); cbuf null: x = 0
-constexpr int kLanesW = 8;
+#ifndef MVBA_LANES_W
+#define MVBA_LANES_W 8
+#endif
+constexpr int kLanesW = MVBA_LANES_W;
 __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __restrict__ pt_begin,
                                                  const int32_t* __restrict__ po_slot, const double4* __restrict__ cbuf,
                                                  const double* __restrict__ tinit, const double* __restrict__ V,
