@@ -573,11 +573,17 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       G.part_begin = (int32_t)parts.size();
       G.gram_width = h->lin_ok ? mvba_gram_width(G.model, G.deg) : 0;
       G.w16 = (G.gram_width + 15) / 16 * 16;
-      // segments per pass-B chunk (one wave): mvba::kChunkSegs; MVBA_CHUNK_SEGS
-      // overrides it (A/B timing)
-      static const int chunk_segs = [] {
+      // segments per CG chunk (one wave of pass B and pass A): mvba::kChunkSegs,
+      // 2x that where images average 12+ segments (c3, 17 per image: pass B
+      // 197 -> 182 us; c2, 5 per image, measured slower with 16: 22 -> 27 us;
+      // profiles/r04/r04t/). MVBA_CHUNK_SEGS overrides it (A/B timing).
+      int32_t gframes = 0;
+      for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++)
+        if (sidx == G.seg_begin || segs[sidx].frame != segs[sidx - 1].frame) gframes++;
+      const int chunk_segs = [&] {
         const char* e = std::getenv("MVBA_CHUNK_SEGS");
-        const int v = e ? std::atoi(e) : mvba::kChunkSegs;
+        const int v = e ? std::atoi(e)
+                        : (G.seg_count >= 12 * (int64_t)std::max(gframes, 1) ? 2 * mvba::kChunkSegs : mvba::kChunkSegs);
         return v >= 1 && v <= 64 ? v : mvba::kChunkSegs;
       }();
       for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++) {

@@ -464,8 +464,17 @@ class Solver {
                               h_->point_extra(), xv, S_->du, gate, S_->prec, s_));
       return;
     }
-    // one segment per wave (MVBA_PASS_A_CHUNKS=1: the 4-segment solver chunks, for A/B timing)
-    static const bool chunked = std::getenv("MVBA_PASS_A_CHUNKS") && std::getenv("MVBA_PASS_A_CHUNKS")[0] == '1';
+    // one pass-B chunk (8 or 16 segments of one image) per wave when there are
+    // enough of them to fill the chip (4,096+, four waves per SIMD): with frames
+    // in capture order the landmark gathers are cheap and the direction staging
+    // per wave amortises over more observations (c3, 18k chunks: pass A 176 ->
+    // 132-144 us; c2, 3k chunks: equal; a 1/8 c2 shard, 470 chunks: 6.0 -> 10.3
+    // us, so it keeps one segment per wave; profiles/r04/r04t/, r04w/).
+    // MVBA_PASS_A_CHUNKS=0|1 forces one (read per call, for A/B timing)
+    const char* pa_env = std::getenv("MVBA_PASS_A_CHUNKS");
+    int32_t nchunks_all = 0;
+    for (const Group& G : h_->groups) nchunks_all += G.chunk_count;
+    const bool chunked = pa_env ? pa_env[0] == '1' : nchunks_all >= 4096;
     // where pass A leaves c_o = J_pt^T z_o: at the observation's point-order
     // position (scattered 32-B stores, k_point_w reads its run) or in slot order
     // (coalesced stores, k_point_w gathers through po_slot). MVBA_CO_ORDER=
