@@ -988,7 +988,8 @@ def main():
                 ex = FailingExchange(ex)
             elif inject and comm is not None:
                 comm.abort()  # this rank's exchanges fail; its peers meet the deadline
-            resources["comm"] = comm
+            with comm_lock:
+                resources["comm"] = comm
             solve_kw = dict(max_num_iterations=args.ba_iters, function_tolerance=0.0, gradient_tolerance=0.0,
                             parameter_tolerance=0.0, use_loss=1, robust_threshold=3.0, allreduce=ex, comm=comm)
             ev.set_params()
@@ -1100,9 +1101,7 @@ def main():
                     "linearize_s": sd["linearize_time_s"],
                     "final_cost": sd["final_cost"],
                 }
-            if comm is not None:
-                resources["comm"] = None
-                comm.close()
+            take_comm_and_close()
 
     # ---- N > 1: the weak-scaling line as well (config-sized shard per rank)
     def phase_weak():
@@ -1134,19 +1133,32 @@ def main():
     guard = PhaseGuard(line, world, rank, ctrl)
 
     resources = {"comm": None}
+    # the LM phase's watchdog (fire below) and the phase's own teardown both
+    # reach the communicator: one lock, and the teardown takes the communicator
+    # out of `resources` before closing it, so an abort never runs during or
+    # after the close (Timer.cancel() does not wait for a fire() in progress)
+    import threading
+
+    comm_lock = threading.Lock()
+
+    def take_comm_and_close():
+        with comm_lock:
+            c = resources.get("comm")
+            resources["comm"] = None
+        if c is not None:
+            c.close()
 
     def phase_ba_watched():
         # watchdog: a solve that overruns the deadline (a peer that never joins
         # an exchange) has its communicator aborted from this thread, so the
         # pending collective returns and the solve raises instead of hanging
-        import threading
-
         def fire():
-            c = resources.get("comm")
-            if c is not None:
-                print(f"bench.py: rank {rank}: LM phase past --ba-deadline {args.ba_deadline} s, aborting the "
-                      "RCCL communicator", file=sys.stderr, flush=True)
-                c.abort()
+            with comm_lock:
+                c = resources.get("comm")
+                if c is not None:
+                    print(f"bench.py: rank {rank}: LM phase past --ba-deadline {args.ba_deadline} s, aborting the "
+                          "RCCL communicator", file=sys.stderr, flush=True)
+                    c.abort()
 
         wd = threading.Timer(args.ba_deadline, fire) if world > 1 else None
         if wd is not None:
@@ -1157,10 +1169,7 @@ def main():
         finally:
             if wd is not None:
                 wd.cancel()
-            c = resources.get("comm")
-            if c is not None:
-                resources["comm"] = None
-                c.close()
+            take_comm_and_close()
 
     guard.run("linearize", phase_lin)
     if L["supported"] and args.ba_iters > 0:

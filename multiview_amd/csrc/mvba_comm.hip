@@ -105,6 +105,12 @@ struct mvba_comm {
   int kind = 0;  // 0 RCCL, 1 local
   int rank = 0, nranks = 1, device = 0;
   ncclComm_t nccl = nullptr;   // non-blocking RCCL communicator (config.blocking = 0)
+  // Every NCCL call on nccl (enqueue, async-error poll, abort, destroy) runs
+  // under nccl_m, and `aborted` is checked under it: mvba_comm_abort may come
+  // from a watchdog thread while the owner enqueues or polls, and ncclCommAbort
+  // frees the communicator. The lock is never held across a sleep or a stream
+  // wait, so an abort is never blocked behind a long wait.
+  std::mutex nccl_m;
   std::atomic<bool> aborted{false};
   double timeout_s = 0.0;      // deadline of every host-side RCCL wait
   std::shared_ptr<LocalGroup> grp;
@@ -135,6 +141,8 @@ double default_timeout_s() {
 ncclResult_t settle(mvba_comm* c, ncclResult_t r, const char* what) {
   const auto t0 = std::chrono::steady_clock::now();
   while (r == ncclInProgress) {
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+    std::lock_guard<std::mutex> lk(c->nccl_m);
     if (c->aborted.load()) return ncclInvalidUsage;
     if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
       g_comm_err = std::string(what) + ": no progress within " + std::to_string(c->timeout_s) +
@@ -143,7 +151,6 @@ ncclResult_t settle(mvba_comm* c, ncclResult_t r, const char* what) {
       (void)ncclCommAbort(c->nccl);
       return ncclSystemError;
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
     if (ncclCommGetAsyncError(c->nccl, &r) != ncclSuccess) return ncclSystemError;
   }
   if (r != ncclSuccess && g_comm_err.empty()) g_comm_err = std::string(what) + ": " + ncclGetErrorString(r);
@@ -242,6 +249,7 @@ mvba_status mvba_comm_init_rccl_deadline(const uint8_t* id, int32_t nranks, int3
   cfg.blocking = 0;
   ncclResult_t r = ncclCommInitRankConfig(&c->nccl, nranks, u, rank, &cfg);
   if (r == ncclSuccess || r == ncclInProgress) {
+    // c is not published yet (no other thread can abort it): no lock needed
     if (r == ncclSuccess && ncclCommGetAsyncError(c->nccl, &r) != ncclSuccess) r = ncclSystemError;
     r = settle(c, r, "ncclCommInitRankConfig");
   } else {
@@ -302,7 +310,10 @@ mvba_status mvba_comm_abort(mvba_comm* c) {
   if (!c) return MVBA_E_INVALID;
   if (c->kind == 0) {
     // callable from another thread while the owner waits on a collective
-    // (a watchdog): RCCL's abort makes the pending kernels return
+    // (a watchdog): RCCL's abort makes the pending kernels return. Under
+    // nccl_m: the owner is then never inside an NCCL call on the handle this
+    // frees, and its next call sees `aborted` before touching it.
+    std::lock_guard<std::mutex> lk(c->nccl_m);
     if (c->nccl && !c->aborted.exchange(true)) (void)ncclCommAbort(c->nccl);
   } else {
     c->grp->abort();
@@ -313,7 +324,8 @@ mvba_status mvba_comm_abort(mvba_comm* c) {
 void mvba_comm_destroy(mvba_comm* c) {
   if (!c) return;
   if (c->kind == 0) {
-    if (c->nccl && !c->aborted.load()) (void)ncclCommDestroy(c->nccl);
+    std::lock_guard<std::mutex> lk(c->nccl_m);
+    if (c->nccl && !c->aborted.exchange(true)) (void)ncclCommDestroy(c->nccl);
   } else {
     std::shared_ptr<LocalGroup> G = c->grp;
     c->grp.reset();
@@ -345,14 +357,18 @@ int32_t mvba_comm_allreduce(double* device_buf, int64_t count, int32_t op, void*
   if (!c || count < 0 || (op != MVBA_REDUCE_SUM && op != MVBA_REDUCE_MAX)) return 1;
   const hipStream_t s = static_cast<hipStream_t>(hip_stream);
   if (c->kind == 1) return local_allreduce(c, device_buf, count, op, s);
-  if (!c->nccl || c->aborted.load()) return 1;
+  if (!c->nccl) return 1;
   c->calls++;
-  if (count == 0) return 0;
-  ncclResult_t r = ncclAllReduce(device_buf, device_buf, (size_t)count, ncclDouble,
-                                 op == MVBA_REDUCE_MAX ? ncclMax : ncclSum, c->nccl, s);
+  if (count == 0) return c->aborted.load() ? 1 : 0;
+  ncclResult_t r;
+  {
+    std::lock_guard<std::mutex> lk(c->nccl_m);
+    if (c->aborted.load()) return 1;
+    r = ncclAllReduce(device_buf, device_buf, (size_t)count, ncclDouble, op == MVBA_REDUCE_MAX ? ncclMax : ncclSum,
+                      c->nccl, s);
+    if (r == ncclSuccess && ncclCommGetAsyncError(c->nccl, &r) != ncclSuccess) r = ncclSystemError;
+  }
   if (r == ncclInProgress) r = settle(c, r, "ncclAllReduce");
-  if (r == ncclSuccess && ncclCommGetAsyncError(c->nccl, &r) == ncclSuccess && r == ncclInProgress)
-    r = settle(c, r, "ncclAllReduce");
   return r == ncclSuccess ? 0 : 1;
 }
 

@@ -161,8 +161,22 @@ __device__ __forceinline__ void cross(const double* a, const double* b, double* 
 // its 16-lane row's sum, row_bcast:15 / row_bcast:31 carry the row sums up to
 // lane 63, whose total v_readlane returns. The __shfl_xor butterfly it replaces
 // costs 12 ds_bpermute_b32 and six dependent LDS round trips per value.
+//
+// Requirements (gfx9 wave64 only, which is the only target this library
+// builds): row_bcast:15/31 exist on GFX9 and not on GFX10+, and the lane-63
+// readlane takes the total only if every lane of the wave is active (EXEC all
+// ones) at the call. Every caller reduces with the whole wave converged (the
+// reductions sit after the per-lane branches, whose inactive lanes contribute
+// 0.0). MVBA_DPP_REDUCE=0 builds the shuffle butterfly, which needs neither.
 #ifndef MVBA_DPP_REDUCE
 #define MVBA_DPP_REDUCE 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && MVBA_DPP_REDUCE
+// GFX9 (CDNA) runs wave64 only, so __GFX9__ asserts both the DPP controls and
+// the wave size (this clang defines no wavefront-size macro)
+#if !defined(__GFX9__)
+#error "wave_sum_f64's DPP row_bcast reduction needs a GFX9 wave64 target (gfx950); or set MVBA_DPP_REDUCE=0"
+#endif
 #endif
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ double dpp_f64(double v) {

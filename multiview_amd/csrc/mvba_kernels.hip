@@ -262,7 +262,7 @@ struct FusedIn {
   unsigned epoch;
   int64_t k1_block0;       // first K1 block of the grid (a multiple of 8: XCD order kept)
   int* err;                // error words: [0] alpha range (K0), [1] ready-word wait given up (k_eval)
-  unsigned poll_limit;     // k_eval: polls of the ready word before a wave gives up (0: none, tests)
+  unsigned poll_limit;     // k_eval: polls of the ready word before a wave gives up (0: every wave fails at once, tests)
 };
 
 // How a K1 wave gets its frame record: kRecGlobal reads the prep kernel's
@@ -332,7 +332,11 @@ __device__ __forceinline__ void obs_body(
     // gives up raises error word [1] to this launch's epoch, so
     // mvba_sync_status fails (MVBA_E_DEVICE_WAIT) instead of returning
     // residuals built from a record that may be stale.
-    if (lane == 0) {
+    // poll_limit 0 (tests) fails every wave before its first poll, whatever the
+    // dispatch timing, so the error path is exercised deterministically.
+    if (lane == 0 && fu.poll_limit == 0) {
+      atomicMax(fu.err + 1, (int)fu.epoch);
+    } else if (lane == 0) {
       const unsigned* w = fu.ready + (frame >> 4);  // 16 frames per K0 block
       for (unsigned n = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != fu.epoch; n++) {
         if (n >= fu.poll_limit) {

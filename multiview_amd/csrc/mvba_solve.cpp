@@ -76,7 +76,8 @@ hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const in
                                        mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s);
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s);
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot,
+                                      double* dot_zero, hipStream_t s);
 hipError_t mvba_launch_add_diag(int64_t n, const double* diag, const double* x, double* y, double* partial,
                                 unsigned* counter, double* dot_out, const int32_t* gate, mvba::CgCtl* ctl,
                                 const mvba::LazyDir* lz, hipStream_t s);
@@ -143,7 +144,7 @@ struct SolverState {
   double* du = nullptr;       // [3 depth slots] u_d (point-order pass A) or z_d (k_depth_pa) -> k_depth_sb
   double* dcbuf = nullptr;    // [4 depth blocks] P z_d at the point-order position (k_depth_pa -> k_point_w)
   double* partial = nullptr;  // [npartial]
-  double* scal = nullptr;     // [32] device scalars
+  double* scal = nullptr;     // [32] device scalars; [24..25]: the CG's p.q accumulators (kPqSlot)
   unsigned* cnt = nullptr;    // [8] grid-reduction counters (kept zero between kernels)
   double* hscal = nullptr;    // [32] pinned host mirror
   mvba::CgCtl* ctl = nullptr; // device CG control (single-rank solves)
@@ -289,7 +290,28 @@ class Solver {
   bool single_model_;
   bool bounded_ = false;
   int last_cg_iters_ = 0;  // CG iterations of the previous linear solve (batch sizing only)
+  // MVBA_CG_TIMING=1: host-side split of the linear-solver wall time, printed
+  // at the end of the solve (where a CG iteration's wall time goes)
+  struct CgTiming {
+    double rhs = 0, start = 0, enqueue = 0, wait = 0, backsub = 0;
+    int solves = 0, batches = 0, enqueued = 0, iters = 0;
+  } tm_;
+  static bool cg_timing() {
+    static const bool on = std::getenv("MVBA_CG_TIMING") && std::getenv("MVBA_CG_TIMING")[0] == '1';
+    return on;
+  }
   int32_t exch_rank_ = -1;  // this rank, when the exchange is a library communicator
+  // Single-rank, non-deterministic CG: the replica reduction adds p.q into
+  // scal[kPqSlot + par] with one atomic per block (no finalising block) and the
+  // update kernel takes the step length from it; par = the CG iteration's
+  // parity (double buffer: each reduction zeroes the slot the previous update
+  // read). MVBA_CG_PQ=grid keeps the last-block reduction (A/B timing).
+  static constexpr int kPqSlot = 24;
+  int cg_par_ = 0;
+  bool pq_atomic() const {
+    const char* e = std::getenv("MVBA_CG_PQ");  // read per call: tests switch it
+    return !o_.allreduce && !o_.deterministic && !(e && !std::strcmp(e, "grid"));
+  }
 
   int pa_model() const { return single_model_ ? h_->groups[0].model : -1; }
   // per-slot landmark copy for the frame-order passes (MVBA_NO_OBSX=1: gather
@@ -421,22 +443,32 @@ class Solver {
     const bool fuse = xv && !o_.allreduce;
     const bool fold = xv && o_.allreduce && exch_rank_ >= 0;
     const bool any = fuse || fold;
+    const bool atomic_pq = fuse && ctl && !det && pq_atomic();
     const double* dg = (fuse || (fold && exch_rank_ == 0)) ? S_->dmp : nullptr;
-    double* dot_out = fuse ? S_->scal + dot_slot : fold ? y + S_->ng : nullptr;
+    double* dot_out = atomic_pq ? S_->scal + kPqSlot + cg_par_
+                      : fuse   ? S_->scal + dot_slot
+                      : fold   ? y + S_->ng
+                               : nullptr;
     if (det)
       HCHK(mvba_launch_slab_reduce_vec(D.tier_view(), D.grid(), D.begin, D.pos, D.val, dg, any ? xv : nullptr, y,
                                        S_->partial, S_->cnt + 4, dot_out, gate, any ? ctl : nullptr,
                                        any ? lz : nullptr, fold ? 1 : 0, s_));
     else
       HCHK(mvba_launch_rep_reduce_vec(S_->yrep, S_->ng, dg, any ? xv : nullptr, y, S_->partial, S_->cnt + 4, dot_out,
-                                      gate, any ? ctl : nullptr, any ? lz : nullptr, fold ? 1 : 0, s_));
+                                      gate, any ? ctl : nullptr, any ? lz : nullptr, atomic_pq ? 2 : fold ? 1 : 0,
+                                      S_->scal + kPqSlot + (cg_par_ ^ 1), s_));
     exchange(y, S_->ng + (fold ? 1 : 0), MVBA_REDUCE_SUM);
     if (xv && !any)
       HCHK(mvba_launch_add_diag(S_->ng, S_->dmp, xv, y, S_->partial, S_->cnt + 4, S_->scal + dot_slot, gate, ctl,
                                 lz, s_));
   }
   // the exchanged p.q behind a product vector q (fold mode), else null
-  const double* pq_of(const double* q) const { return (o_.allreduce && exch_rank_ >= 0) ? q + S_->ng : nullptr; }
+  // (fold mode), or the CG product's atomic accumulator (single rank), else null
+  const double* pq_of(const double* q) const {
+    if (o_.allreduce && exch_rank_ >= 0) return q + S_->ng;
+    if (q == S_->q && pq_atomic()) return S_->scal + kPqSlot + cg_par_;
+    return nullptr;
+  }
 
   static mvba::DirPair plain_dir(const double* dir) { return mvba::DirPair{dir, nullptr, nullptr, nullptr}; }
 
@@ -550,17 +582,21 @@ class Solver {
     CgResult R;
     const int64_t n = S_->ng;
     double* xv = S_->delta;
+    const double tc0 = now_s();
     HCHK(hipMemsetAsync(xv, 0, (size_t)std::max<int64_t>(n, 1) * sizeof(double), s_));
     if (n == 0) return R;
-    dot(n, S_->b, S_->b, 0);
-    const double norm_b = std::sqrt(fetch(1)[0]);
-    if (norm_b == 0.0) return R;
     mvba::CgCtl c{};
     c.eta = o_.eta;
     c.min_iter = o_.min_linear_solver_iterations;
     c.max_iter = o_.max_linear_solver_iterations;
     *S_->hctl = c;
     HCHK(hipMemcpyAsync(S_->ctl, S_->hctl, sizeof(mvba::CgCtl), hipMemcpyHostToDevice, s_));
+    if (pq_atomic()) HCHK(hipMemsetAsync(S_->scal + kPqSlot, 0, 2 * sizeof(double), s_));
+    // b.b straight into the control block: the first update's finalisation stops
+    // the solve at |b| = 0 (Ceres: "Convergence. |b| = 0.", x = 0), so the host
+    // does not wait for it (one stream sync per linear solve less)
+    HCHK(mvba_launch_dot(n, S_->b, S_->b, S_->partial, S_->cnt + 6, &S_->ctl->bb, s_));
+    if (cg_timing()) tm_.start += now_s() - tc0;
     const int32_t* gate = &S_->ctl->done;
     // Reprojection-only problems: the CG update's frame blocks form W z and the
     // products combine it with the previous product's records (no direction
@@ -590,9 +626,13 @@ class Solver {
     static const int second = std::getenv("MVBA_CG_BATCH2") ? std::max(1, std::atoi(std::getenv("MVBA_CG_BATCH2"))) : 2;
     const int first = std::max(4, last_cg_iters_ - 2);
     for (int batch = first, nb = 0;; batch = (++nb == 1) ? second : 4) {
+      const double tb0 = now_s();
+      if (cg_timing()) tm_.batches++;
       for (int k = 0; k < batch && i <= std::max(o_.max_linear_solver_iterations, 1); k++, i++) {
+        if (cg_timing()) tm_.enqueued++;
         const mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, S_->ctl, 0, 0.0};
         std::swap(S_->p, S_->p2);
+        cg_par_ = i & 1;
         if (fused_dir) {
           apply_schur_cg(S_->q, gate, S_->ctl, lz,
                          mvba::DirPair{S_->dirz, S_->dirp[pp], S_->dirp[pp ^ 1], S_->ctl, lz.z, lz.p_old,
@@ -609,8 +649,13 @@ class Solver {
           upd(1 | 2 | 8, S_->q, i, true);
         }
       }
+      const double tb1 = now_s();
       HCHK(hipMemcpyAsync(S_->hctl, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
       HCHK(hipStreamSynchronize(s_));
+      if (cg_timing()) {
+        tm_.enqueue += tb1 - tb0;
+        tm_.wait += now_s() - tb1;
+      }
       if (S_->hctl->done) break;
       if (i > std::max(o_.max_linear_solver_iterations, 1)) break;  // not reached: the device stops at max_iter
     }
@@ -998,12 +1043,20 @@ void Solver::run(mvba_solver_summary* sum) {
     HCHK(mvba_launch_block_prec(S_->nblocks, S_->max_bsize, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->dmp,
                                 S_->fac, s_));
     schur_rhs();
+    if (cg_timing()) {
+      HCHK(hipStreamSynchronize(s_));
+      tm_.rhs += now_s() - ts;
+      tm_.solves++;
+    }
     const CgResult cgr = cg_device();
     sum->num_linear_iterations += cgr.iters;
+    if (cg_timing()) tm_.iters += cgr.iters;
     bool valid = cgr.status != 2;
     double mcc = 0.0;
     if (valid) {
+      const double tbs = now_s();
       mcc = back_substitute();
+      if (cg_timing()) tm_.backsub += now_s() - tbs;
       valid = std::isfinite(mcc) && mcc > 0.0;
     }
     sum->linear_solver_time_s += now_s() - ts;
@@ -1097,6 +1150,15 @@ void Solver::run(mvba_solver_summary* sum) {
   sum->num_iterations = iteration;
   sum->final_cost = x_cost;
   sum->total_time_s = now_s() - t0;
+  if (cg_timing() && tm_.solves)
+    std::fprintf(stderr,
+                 "mvba cg timing: %d solves, %d CG iterations (%d enqueued, %d batches) | us per solve: rhs+prec %.1f, "
+                 "cg start (|b| read) %.1f, back-substitution %.1f | us per enqueued iteration: enqueue %.1f, "
+                 "wait %.1f | loop us per CG iteration %.1f\n",
+                 tm_.solves, tm_.iters, tm_.enqueued, tm_.batches, 1e6 * tm_.rhs / tm_.solves,
+                 1e6 * tm_.start / tm_.solves, 1e6 * tm_.backsub / tm_.solves,
+                 1e6 * tm_.enqueue / std::max(tm_.enqueued, 1), 1e6 * tm_.wait / std::max(tm_.enqueued, 1),
+                 1e6 * (tm_.enqueue + tm_.wait) / std::max(tm_.iters, 1));
 }
 
 }  // namespace

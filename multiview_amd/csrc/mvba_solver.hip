@@ -1058,13 +1058,24 @@ __device__ __forceinline__ double x_entry(const double* __restrict__ x, const La
   return v;
 }
 
+// local_dot 2 (single rank): no finalising block. Each block adds its share of
+// x.y to dot_out with one fp64 atomic, block 0 zeroes dot_zero (the other slot of
+// the double-buffered accumulator, read by the previous update kernel) and
+// snapshots rho; the update kernel takes the step length from the sum (the
+// sharded path's form), so the arrival counter and the last block's partial
+// loads leave the CG iteration's critical path.
 __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yrep, int64_t n,
                                                         const double* __restrict__ diag,
                                                         const double* __restrict__ x, double* __restrict__ y,
                                                         double* __restrict__ partial, unsigned* __restrict__ counter,
                                                         double* __restrict__ dot_out, const int32_t* __restrict__ gate,
-                                                        CgCtl* __restrict__ ctl, LazyDir lz, int32_t local_dot) {
+                                                        CgCtl* __restrict__ ctl, LazyDir lz, int32_t local_dot,
+                                                        double* __restrict__ dot_zero) {
   if (gate && *gate) return;
+  if (local_dot == 2 && blockIdx.x == 0 && threadIdx.x == 0) {
+    *dot_zero = 0.0;
+    ctl->rho_step = ctl->rho;
+  }
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double d = 0.0;
   if (e < n) {
@@ -1082,6 +1093,11 @@ __global__ void __launch_bounds__(256) k_vec_rep_reduce(double* __restrict__ yre
     if (diag) acc += diag[e] * xe;
     y[e] = acc;
     d = xe * acc;
+  }
+  if (local_dot == 2) {
+    block_sum<1>(&d);
+    if (threadIdx.x == 0) atomicAdd(dot_out, d);
+    return;
   }
   if (dot_out && grid_sum_finalize(d, partial, counter, dot_out) && ctl && threadIdx.x == 0)
     cg_step_finish(ctl, dot_out[0], local_dot);
@@ -1236,6 +1252,12 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
       const double rho_next = sums[2];
       auto bad = [](double v) { return v == 0.0 || isinf(v) || isnan(v); };
       if (iter == 0) {  // r = b, z = M^-1 r: initial rho, Q0 = 0
+        if (ctl->bb == 0.0) {  // "Convergence. |b| = 0." (x stays 0)
+          ctl->status = 0;
+          ctl->iters = 0;
+          ctl->done = 1;
+          return;
+        }
         ctl->Q0 = 0.0;
         ctl->first = 1;
         if (bad(rho_next)) {
@@ -1734,11 +1756,13 @@ hipError_t mvba_launch_slab_reduce_vec(mvba::SlabTiers t, int64_t grid, const in
 
 hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* diag, const double* x, double* y,
                                       double* partial, unsigned* counter, double* dot_out, const int32_t* gate,
-                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot, hipStream_t s) {
+                                      mvba::CgCtl* ctl, const mvba::LazyDir* lz, int32_t local_dot,
+                                      double* dot_zero, hipStream_t s) {
   if (ng <= 0) return hipSuccess;
+  if (local_dot == 2 && (!dot_out || !dot_zero || !ctl)) return hipErrorInvalidValue;
   const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
   hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, diag, x,
-                     y, partial, counter, dot_out, gate, ctl, l, local_dot);
+                     y, partial, counter, dot_out, gate, ctl, l, local_dot, dot_zero);
   return hipGetLastError();
 }
 

@@ -158,6 +158,7 @@ struct CgCtl {
   int32_t min_iter;
   int32_t max_iter;
   double rho_step;  // sharded solves: rho of the current step, snapshot by the replica reduction
+  double bb;        // b.b of the linear solve (|b| = 0: converged at iteration 0, x = 0)
 };
 
 // Camera-side entry of the reduced system as the CG update reads it: its

@@ -292,3 +292,33 @@ def solve(P, max_num_iterations=50, function_tolerance=1e-6, gradient_tolerance=
             summary["unsuccessful"] += 1
     summary.update(final_cost=cost, iterations=it)
     return with_x(x), summary
+
+
+def first_step_system(P, use_loss=False, robust_threshold=3.0, initial_trust_region_radius=1e4):
+    """The damped, Jacobi-scaled normal equations of the first LM iteration,
+    A y = b with A = (J S)'(J S) + diag(clip(S^2 c, 1e-6, 1e32) / radius),
+    b = -S g and the step delta = S y (the system damped_step solves in
+    solve()), plus the spectrum bounds that turn a residual into an error bound:
+    ||y - y*|| / ||y*|| <= kappa ||A y - b|| / ||b|| for the SPD A.
+    Returns dict(A (scipy CSC), b, s, idx (packed parameter indices of the free
+    columns), x0, lam_max, lam_min, kappa, y_exact)."""
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import eigsh, splu
+
+    col, idx = _columns(P)
+    n = idx.size
+    x0 = P.params[idx].copy()
+    _, r, J = _jacobian(P, P.params.copy(), col, n, use_loss, robust_threshold)
+    J = sp.csr_matrix(J)
+    g = J.T @ r
+    c = np.asarray(J.multiply(J).sum(axis=0)).reshape(-1)
+    s = 1.0 / (1.0 + np.sqrt(c))
+    Js = J @ sp.diags(s)
+    A = (Js.T @ Js + sp.diags(np.clip(s * s * c, 1e-6, 1e32) / initial_trust_region_radius)).tocsc()
+    b = -s * g
+    lu = splu(A)
+    y = lu.solve(b)
+    lam_max = float(eigsh(A, k=1, which="LA", return_eigenvectors=False, tol=1e-6)[0])
+    lam_min = float(eigsh(A, k=1, sigma=0.0, which="LM", return_eigenvectors=False, tol=1e-6)[0])
+    return dict(A=A, b=b, s=s, idx=idx, x0=x0, lam_max=lam_max, lam_min=lam_min, kappa=lam_max / lam_min,
+                y_exact=y)

@@ -160,25 +160,36 @@ def test_single_observation_points_and_frames():
     change below 1e-9 at iteration ~160-180, before the radius has grown into
     the noise regime (profiles/r03/edge_trace_r03b.log: relative changes
     2e-10 .. 6e-10 there, 2e-7 .. 1e-7 from the CPU cost); (2) run into the
-    noise regime at the CLI's tolerances (200 iterations), two deterministic
-    solves are bit-identical (termination, iteration counts, cost, parameters)
-    and within 1e-5 of that cost: a noise-regime FAILURE (5 invalid steps) can
-    end the solve before the slow null-direction steps reach the 1e-6 band (one
-    build stopped at 1.03e-6 above the CPU cost, profiles/r04/r04k/
-    pytest_gpu_r04k.log). MVBA_SOLVER_TRACE=1 prints the steps."""
+    noise regime at the CLI's tolerances, two deterministic solves are
+    bit-identical (termination, iteration counts, cost, parameters), and each
+    continues the path of (1)'s deterministic run: same build, same start,
+    deterministic sums, and function_tolerance only decides where a run stops,
+    so the 1e-16 run repeats the 1e-9 run's iterations and then accepts only
+    cost-decreasing steps. Its iteration count is at least (1)'s and its cost at
+    most (1)'s, hence within 1e-6 of the CPU LM too. Both runs get the same
+    iteration cap (400): round 4's part (2) stopped at 200 iterations while (1)
+    converged later than that with frames in capture order, and its cost was
+    still 1.03e-6 above the CPU's (profiles/r04/r04k/pytest_gpu_r04k.log); that
+    is a cap, not a drift. MVBA_SOLVER_TRACE=1 prints the steps."""
     from oracle import lm_reference
 
     P = _single_observation_problem()
     TOL = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
     x_ref, s_ref = lm_reference.solve(P, max_num_iterations=100, use_loss=True, **TOL)
+    conv = {}
     for det in (1, 0):
         s, _ = _solve(P, det, 400, **dict(TOL, function_tolerance=1e-9))
         assert s["termination_type"] == _lib.CONVERGENCE, (det, s["message"])
         assert "Function tolerance reached" in s["message"]
         assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
-    runs = [_solve(P, 1, 200, **TOL) for _ in range(2)]
+        conv[det] = s
+    runs = [_solve(P, 1, 400, **TOL) for _ in range(2)]
+    c1 = conv[1]
     for s, _ in runs:
-        assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-5), (s["final_cost"], s_ref["final_cost"])
+        assert s["num_iterations"] >= c1["num_iterations"], (s["num_iterations"], c1["num_iterations"])
+        assert s["num_successful_steps"] >= c1["num_successful_steps"]
+        assert s["final_cost"] <= c1["final_cost"], (s["final_cost"], c1["final_cost"])
+        assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
     _same_run(runs[0], runs[1])
 
 

@@ -63,8 +63,9 @@ def test_fused_wait_gives_up_with_an_error(monkeypatch):
     """k_eval's K1 waves wait for their frame's K0 block with a bounded poll.
     A wave that gives up raises error word [1], and mvba_sync_status reports
     MVBA_E_DEVICE_WAIT instead of handing back residuals built from a record
-    that may be stale. MVBA_EVAL_POLL_LIMIT=0 makes every wave give up at once
-    (read per call); the next evaluation at the default limit is clean again."""
+    that may be stale. MVBA_EVAL_POLL_LIMIT=0 makes every wave raise the error
+    before its first poll (read per call; deterministic, whatever the dispatch
+    timing); the next evaluation at the default limit is clean again."""
     import torch
 
     R = rig.make_rig(num_sensors=3, num_ref=10, num_points=2500, obs_per_point=4, seed=5)

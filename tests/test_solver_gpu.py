@@ -62,11 +62,13 @@ def test_one_exact_step_matches_dense_lm(use_loss):
     assert np.array_equal(x[~m], P.params[~m])
 
 
-@pytest.mark.parametrize("models", [["rpc4", "radtan"], ["rpc6", "fov"]])
+@pytest.mark.parametrize("models", [["rpc2", "radtan"], ["rpc3", "fov"], ["rpc4", "radtan"], ["rpc6", "fov"]])
 def test_one_exact_step_high_rpc_degree(models):
-    """RPC degree 4 and 6 (K = 116 / 220: the wide-row pass B and Gram paths,
-    distortion blocks of 116 / 220 entries): one exact-CG LM step equals the
-    dense step (relative 1e-8), focal + distortion floating."""
+    """RPC distortion floating, one exact-CG LM step equals the dense step
+    (relative 1e-8), focal + distortion floating. Degrees 2 and 3 take pass B's
+    register path that folds the distortion columns through the monomials
+    (pass_b_rpc_obs: the kNx/kDx/kNy/kDy index mapping of each degree); degrees
+    4 and 6 (K = 116 / 220) the wide-row pass B and Gram paths."""
     from oracle import lm_reference
 
     R = rig.make_rig(num_sensors=len(models), num_ref=10, num_points=250, obs_per_point=5, models=models, seed=97)
