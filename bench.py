@@ -296,7 +296,7 @@ def _stream_copy_gbs(torch, stream, nbytes=1 << 30, reps=10):
     return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
-PROFILE_ROUNDS = ("r04", "r03", "r02", "r01")  # newest first: committed PMC summaries are read from here
+PROFILE_ROUNDS = ("r05", "r04", "r03", "r02", "r01")  # newest first: committed PMC summaries are read from here
 
 
 def _profile_path(name):
@@ -312,9 +312,10 @@ def _pmc_traffic(config, kind="eval"):
     """HBM bytes per launch from the committed PMC summary of this config
     (tools/pmc_summary.py over separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
     passes of this same command; profiles/), or None. kind "eval": the
-    one-launch evaluation (k_eval, pmc_eval_<cfg>.json); "k1": the split form's
-    K1 (k_obs, pmc_k1_<cfg>.json)."""
-    path = _profile_path(f"pmc_{'eval' if kind == 'eval' else 'k1'}_{config}.json")
+    one-launch evaluation (k_eval_local / k_eval, pmc_eval_<cfg>.json); "k1":
+    the split form's K1 (k_obs, pmc_k1_<cfg>.json); "depth": K1-depth
+    (k_depth_obs<double>, pmc_depth_<cfg>.json)."""
+    path = _profile_path(f"pmc_{kind}_{config}.json")
     try:
         with open(path) as f:
             return float(json.load(f)["traffic_bytes_per_launch"])
@@ -790,13 +791,25 @@ def main():
         dbytes = float(ev.lib.mvba_eval_bytes(ev.h, _lib.EVAL_DEPTH))
         line["depth"] = {
             "what": "BracketedDepthError residual+Jacobian (K1-depth, materialised, column planes)",
+            "kernel": "k_depth_obs<double>",
             "num_depth_residuals": ev.num_depth,
             "evals_per_s": ev.num_depth / (d_ms * 1e-3),
             "kernel_ms": d_ms,
             "bytes_per_launch": dbytes,
             "achieved_GBps": dbytes / (d_ms * 1e-3) / 1e9,
             "frac_of_hbm_peak": dbytes / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            # HBM bytes per launch from the committed FETCH / WRITE passes of this
+            # config (pmc_depth_<cfg>.json) and its fp64 work (pmc_flops_<cfg>.json)
+            "traffic": _pmc_traffic(args.config, "depth") if whole_cfg else None,
         }
+        d_flops = next((v["fp64_flops"] for k, v in flops_tab.items() if k.startswith("mvba::k_depth_obs<double>")),
+                       None)
+        if d_flops is not None:
+            dtf = d_flops / (d_ms * 1e-3) / 1e12
+            line["depth"].update({"fp64_flops_per_launch": d_flops, "fp64_tflops": dtf,
+                                  "fp64_frac": dtf / FP64_PEAK_TFLOPS,
+                                  "binding": "hbm" if dbytes / (d_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                  >= dtf / FP64_PEAK_TFLOPS else "fp64"})
 
     # ---- fp32 evaluation (config c5 is quoted "fp32 eval / fp64 solve"): the same
     # fp64 arithmetic, outputs rounded to float at the store (half the output bytes)

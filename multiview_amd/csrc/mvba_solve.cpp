@@ -156,6 +156,23 @@ struct SolverState {
   int32_t max_bsize = 0;
   int64_t *goff = nullptr, *hoff = nullptr, *cam_poff = nullptr;
   DetPlan b_det;              // deterministic pass B (slab rows per chunk / depth segment)
+  // Captured CG iteration runs (hipGraph): iterations at offsets [o, o + L) of
+  // a 10-iteration period (Ceres' residual reset), replayed by one
+  // hipGraphLaunch. sig: every host value the captured launches depend on
+  // (device pointers, forms, solver options); a changed signature drops them.
+  struct CgGraph {
+    int o = 0, L = 0;
+    hipGraphExec_t exec = nullptr;
+  };
+  std::vector<CgGraph> graphs;
+  std::vector<uintptr_t> graph_sig;
+  bool graphs_broken = false;  // a capture failed: eager launches from then on
+  hipStream_t own_stream = nullptr;  // solves called on the null stream run here (capturable)
+  void drop_graphs() {
+    for (CgGraph& g : graphs)
+      if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    graphs.clear();
+  }
 };
 
 void solver_state_free(SolverState* S) {
@@ -168,6 +185,8 @@ void solver_state_free(SolverState* S) {
   if (S->hscal) (void)hipHostFree(S->hscal);
   if (S->hctl) (void)hipHostFree(S->hctl);
   S->b_det.release();
+  S->drop_graphs();
+  if (S->own_stream) (void)hipStreamDestroy(S->own_stream);
   delete S;
 }
 
@@ -578,6 +597,55 @@ class Solver {
   // gated by ctl->done, one host read per batch. Sharded solves run the same
   // loop: the per-iteration exchange of the product is stream-ordered and the
   // replicated camera-side state gives every rank the same stopping decisions.
+  // Host values the launches of one CG iteration depend on, beyond the
+  // iteration's offset in the reset period: a captured iteration is replayed
+  // only while all of them are unchanged.
+  std::vector<uintptr_t> cg_signature(bool fused_dir) const {
+    auto u = [](const void* p) { return (uintptr_t)p; };
+    const char* co = std::getenv("MVBA_CO_ORDER");
+    const char* pa = std::getenv("MVBA_PASS_A_CHUNKS");
+    std::vector<uintptr_t> v = {
+        (uintptr_t)fused_dir, (uintptr_t)pq_atomic(), (uintptr_t)co_slot_order(co), (uintptr_t)(pa ? pa[0] : 0),
+        (uintptr_t)flags_, (uintptr_t)std::llround(cauchy_c_ * 1e15), (uintptr_t)S_->ng, (uintptr_t)h_->nframes,
+        u(obsx()), u(h_->d_params), u(h_->d_pts), u(h_->d_frec), u(h_->d_fd), u(h_->d_frame_lin), u(h_->d_segs),
+        u(h_->d_chunks), u(h_->d_segchunks), u(h_->d_obs_pid), u(h_->d_obs_meas), u(h_->d_slot_po),
+        u(h_->d_po_slot), u(h_->d_pt_begin), u(h_->d_pt_off), u(h_->d_pt_free), u(h_->d_dep_segs),
+        u(h_->d_dep_desc), u(h_->d_dep_pid), u(h_->d_dep_meas), u(h_->d_dslot_po), u(h_->d_dpt_begin),
+        u(h_->d_po_frame), u(h_->d_po_meas), (uintptr_t)h_->npts, (uintptr_t)h_->nchunks,
+        (uintptr_t)h_->ndep_segs, (uintptr_t)o_.deterministic};
+    if (o_.deterministic) {
+      const DetPlan& D = S_->b_det;
+      for (uintptr_t x : {u(D.val), u(D.begin), u(D.pos), u(D.tiers), (uintptr_t)D.nheavy, (uintptr_t)D.nmedium,
+                          (uintptr_t)D.nlight, (uintptr_t)D.width})
+        v.push_back(x);
+    }
+    for (const Group& G : h_->groups) {
+      v.push_back((uintptr_t)G.model);
+      v.push_back((uintptr_t)G.deg);
+      v.push_back((uintptr_t)G.chunk_begin);
+      v.push_back((uintptr_t)G.chunk_count);
+      v.push_back((uintptr_t)G.seg_begin);
+      v.push_back((uintptr_t)G.seg_count);
+    }
+    return v;
+  }
+
+  // PCG on S delta_c = b (conjugate_gradients_solver.cc [ext]) with every
+  // scalar step on the device (CgCtl): iterations are enqueued in batches and
+  // gated by ctl->done, one host read per batch. Sharded solves run the same
+  // loop: the per-iteration exchange of the product is stream-ordered and the
+  // replicated camera-side state gives every rank the same stopping decisions.
+  //
+  // Every launch argument of iteration i is a function of i mod 10 (the
+  // double-buffered p, r, direction records and p.q accumulator by the parity
+  // of i, the residual reset at i % 10 == 0; the iteration number itself is
+  // counted on the device, CgCtl::it), so single-rank solves capture runs of
+  // iterations as hipGraphs once per handle and replay them: a batch of k
+  // iterations costs a few graph launches instead of 5 k kernel launches, whose
+  // host time (≈ 25 us per iteration, 5-6 us per hipLaunchKernel) bound the
+  // CG iteration of small problems (profiles/r05/r05b/s8_timing_r05b.log:
+  // enqueue 27.6 us vs 16.1 us of wait per iteration on the 1/8 c2 shard).
+  // MVBA_CG_GRAPH=0: eager launches (A/B timing).
   CgResult cg_device() {
     CgResult R;
     const int64_t n = S_->ng;
@@ -589,6 +657,7 @@ class Solver {
     c.eta = o_.eta;
     c.min_iter = o_.min_linear_solver_iterations;
     c.max_iter = o_.max_linear_solver_iterations;
+    c.it = 0;
     *S_->hctl = c;
     HCHK(hipMemcpyAsync(S_->ctl, S_->hctl, sizeof(mvba::CgCtl), hipMemcpyHostToDevice, s_));
     if (pq_atomic()) HCHK(hipMemsetAsync(S_->scal + kPqSlot, 0, 2 * sizeof(double), s_));
@@ -606,16 +675,86 @@ class Solver {
     const bool dir_kernel = dk_env && dk_env[0] == '1';
     const bool fused_dir = h_->ndep == 0 && !dir_kernel;
     const mvba::FrameDirZ fz{h_->d_frame_lin, h_->d_fd, h_->d_frec, S_->dirz, (int32_t)h_->nframes, 0};
-    auto upd = [&](int32_t mode, const double* q, int32_t iter, bool end_logic) {
-      HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, 0.0, S_->p, q, S_->b, xv,
-                                 S_->r, S_->r2, S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl,
-                                 end_logic ? iter : -1, fused_dir ? &fz : nullptr,
+    // p[i & 1] = the direction of iteration i (p[(i - 1) & 1] the previous
+    // one), r[i & 1] = the residual iteration i starts from, dirp likewise
+    double* const P[2] = {S_->p, S_->p2};
+    double* const Rv[2] = {S_->r, S_->r2};
+    auto upd = [&](int32_t mode, const double* q, const double* p, const double* r_in, double* r_out) {
+      HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, 0.0, p, q, S_->b, xv, r_in, r_out, S_->z, S_->partial,
+                                 S_->cnt, S_->scal + 8, S_->ctl, mvba::kIterFromCtl, fused_dir ? &fz : nullptr,
                                  (mode & 1) && q ? pq_of(q) : nullptr, s_));
-      std::swap(S_->r, S_->r2);
     };
-    upd(4 | 8, nullptr, 0, true);  // r = b, z = M^-1 r, rho
+    upd(4 | 8, nullptr, P[0], Rv[0], Rv[1]);  // r = b, z = M^-1 r, rho
+    auto body = [&](int i) {
+      const mvba::LazyDir lz{S_->z, P[(i - 1) & 1], P[i & 1], n, S_->ctl, 0, 0.0};
+      cg_par_ = i & 1;
+      if (fused_dir)
+        apply_schur_cg(S_->q, gate, S_->ctl, lz,
+                       mvba::DirPair{S_->dirz, S_->dirp[(i - 1) & 1], S_->dirp[i & 1], S_->ctl, lz.z, lz.p_old,
+                                     h_->d_frame_lin});
+      else
+        apply_schur(P[i & 1], S_->q, 0, gate, S_->ctl, &lz);
+      double* r_in = Rv[i & 1];
+      double* r_out = Rv[(i + 1) & 1];
+      if (i % 10 == 0) {  // residual reset: r = b - A x
+        upd(1, S_->q, P[i & 1], r_in, nullptr);
+        apply_schur(xv, S_->tmp, 1, gate, nullptr);
+        upd(4 | 8, S_->tmp, P[i & 1], r_in, r_out);
+      } else {
+        upd(1 | 2 | 8, S_->q, P[i & 1], r_in, r_out);
+      }
+    };
+    // graphs: single rank (a library exchange or a callback inside the iteration
+    // is not captured), a capturable (non-null) stream; deterministic mode once
+    // its slab plan is recorded (schur_rhs's product records it, so always here)
+    const char* g_env = std::getenv("MVBA_CG_GRAPH");  // read per call: tests switch it
+    const bool use_graphs = !(g_env && g_env[0] == '0') && !o_.allreduce && s_ != nullptr &&
+                            (!o_.deterministic || S_->b_det.ready) && !S_->graphs_broken;
+    if (use_graphs) {
+      std::vector<uintptr_t> sig = cg_signature(fused_dir);
+      if (sig != S_->graph_sig) {
+        S_->drop_graphs();
+        S_->graph_sig = std::move(sig);
+      }
+    }
+    // iterations [i, i + L) with i's offset o = (i - 1) % 10 and L <= 10 - o:
+    // one replay of the captured run (captured on first use)
+    auto run_chunk = [&](int i, int L) {
+      const int o = (i - 1) % 10;
+      for (const SolverState::CgGraph& g : S_->graphs)
+        if (g.o == o && g.L == L) {
+          HCHK(hipGraphLaunch(g.exec, s_));
+          return;
+        }
+      hipGraph_t graph = nullptr;
+      hipGraphExec_t exec = nullptr;
+      if (hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        S_->graphs_broken = true;
+        for (int k = 0; k < L; k++) body(i + k);
+        return;
+      }
+      bool ok = true;
+      try {
+        for (int k = 0; k < L; k++) body(i + k);
+      } catch (...) {
+        ok = false;
+      }
+      const hipError_t ec = hipStreamEndCapture(s_, &graph);
+      ok = ok && ec == hipSuccess && graph;
+      if (ok && hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) ok = false;
+      if (graph) (void)hipGraphDestroy(graph);
+      if (!ok) {
+        (void)hipGetLastError();
+        if (exec) (void)hipGraphExecDestroy(exec);
+        S_->graphs_broken = true;
+        for (int k = 0; k < L; k++) body(i + k);  // this run eagerly; later ones too
+        return;
+      }
+      S_->graphs.push_back(SolverState::CgGraph{o, L, exec});
+      HCHK(hipGraphLaunch(exec, s_));
+    };
     int i = 1;
-    int pp = 0;  // dirp[pp] holds W p_old
     // Batch sizes only decide where the host looks at the control block (gated
     // iterations past the stop are no-ops): the first batch runs to just short
     // of the previous solve's iteration count, later ones are short, so most
@@ -624,30 +763,32 @@ class Solver {
     // MVBA_CG_BATCH2 sets the second (A/B timing). A gated iteration costs
     // ≈ 20 us at c2 and ≈ 36 us at c3 (a gated pass B alone is 10 us there).
     static const int second = std::getenv("MVBA_CG_BATCH2") ? std::max(1, std::atoi(std::getenv("MVBA_CG_BATCH2"))) : 2;
-    const int first = std::max(4, last_cg_iters_ - 2);
+    int first = std::max(4, last_cg_iters_ - 2);
+    const int imax = std::max(o_.max_linear_solver_iterations, 1);
+    static const int kGraphRun = std::getenv("MVBA_CG_GRAPH_RUN") ? std::max(1, std::min(10, std::atoi(std::getenv("MVBA_CG_GRAPH_RUN")))) : 10;
+    if (use_graphs) first = (first + kGraphRun - 1) / kGraphRun * kGraphRun;
     for (int batch = first, nb = 0;; batch = (++nb == 1) ? second : 4) {
+      if (use_graphs) batch = (batch + kGraphRun - 1) / kGraphRun * kGraphRun;
       const double tb0 = now_s();
       if (cg_timing()) tm_.batches++;
-      for (int k = 0; k < batch && i <= std::max(o_.max_linear_solver_iterations, 1); k++, i++) {
-        if (cg_timing()) tm_.enqueued++;
-        const mvba::LazyDir lz{S_->z, S_->p, S_->p2, n, S_->ctl, 0, 0.0};
-        std::swap(S_->p, S_->p2);
-        cg_par_ = i & 1;
-        if (fused_dir) {
-          apply_schur_cg(S_->q, gate, S_->ctl, lz,
-                         mvba::DirPair{S_->dirz, S_->dirp[pp], S_->dirp[pp ^ 1], S_->ctl, lz.z, lz.p_old,
-                                       h_->d_frame_lin});
-          pp ^= 1;
-        } else {
-          apply_schur(S_->p, S_->q, 0, gate, S_->ctl, &lz);
+      const int iend = std::min(i + batch, imax + 1);  // iterations [i, iend)
+      if (cg_timing()) tm_.enqueued += iend - i;
+      if (use_graphs && !S_->graphs_broken) {
+        // runs of kGraphRun iterations aligned to the reset period (10: one run
+        // per period, captured by the first solve that reaches iteration 10;
+        // batches round up to whole runs); a shorter tail only at
+        // max_linear_solver_iterations. Same-box A/B (profiles/r05/r05d/): the
+        // 1/8 c2 shard's CG loop 43.5-44.0 us per iteration eager, 42.7 with
+        // runs of 2, 40.8-41.1 with runs of 10; c2 76.7-77.1 / 79.6 / 76.6-76.9
+        // (GPU-bound there: the graph removes host time, not GPU-side gaps)
+        while (i < iend) {
+          const int o = (i - 1) % 10;
+          const int L = std::min({kGraphRun - o % kGraphRun, 10 - o, imax + 1 - i});
+          run_chunk(i, L);
+          i += L;
         }
-        if (i % 10 == 0) {  // residual reset: r = b - A x
-          upd(1, S_->q, i, false);
-          apply_schur(xv, S_->tmp, 1, gate, nullptr);
-          upd(4 | 8, S_->tmp, i, true);
-        } else {
-          upd(1 | 2 | 8, S_->q, i, true);
-        }
+      } else {
+        for (; i < iend; i++) body(i);
       }
       const double tb1 = now_s();
       HCHK(hipMemcpyAsync(S_->hctl, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
@@ -657,7 +798,7 @@ class Solver {
         tm_.wait += now_s() - tb1;
       }
       if (S_->hctl->done) break;
-      if (i > std::max(o_.max_linear_solver_iterations, 1)) break;  // not reached: the device stops at max_iter
+      if (i > imax) break;  // not reached: the device stops at max_iter
     }
     R.iters = S_->hctl->iters;
     R.status = S_->hctl->status;
@@ -1199,7 +1340,20 @@ mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver
   if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
   try {
     if (!h->solver) h->solver = alloc_state(h);
-    Solver sv(h, *o, (hipStream_t)stream);
+    // A caller on the null stream gets the handle's own stream: the CG loop's
+    // graphs cannot be captured on the null stream. The solve is host-
+    // synchronous anyway (it ends with a stream sync); it starts after all
+    // earlier device work, so it sees the caller's null-stream writes.
+    // (single-rank solves only: sharded ones keep the caller's stream, and a
+    // device-wide sync could wait on a peer shard's pending exchange)
+    hipStream_t st = (hipStream_t)stream;
+    if (!st && !o->allreduce) {
+      if (!h->solver->own_stream)
+        HCHK(hipStreamCreateWithFlags(&h->solver->own_stream, hipStreamNonBlocking));
+      HCHK(hipDeviceSynchronize());
+      st = h->solver->own_stream;
+    }
+    Solver sv(h, *o, st);
     // K2 writes the CG passes' per-slot records for the duration of the solve
     struct ObsxScope {
       mvba_handle* h;

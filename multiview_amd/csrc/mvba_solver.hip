@@ -1235,7 +1235,7 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
       x[i] = xi;
     }
     const double ri = cg_rnew(mode, alpha, q, b, r_in, i);
-    r_out[i] = ri;
+    if (mode & 6) r_out[i] = ri;  // mode 1 alone (before a residual reset) leaves r to the reset
     if (mode & 8) {
       const double zi = cg_zentry(E, minv, mode, alpha, q, b, r_in);
       z[i] = zi;
@@ -1250,6 +1250,7 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
     if (grid_sum3_finalize(xb, xr, rz, partial, counters, out, sums, nb) && ctl && threadIdx.x == 0) {
       const double sxb = sums[0], sxr = sums[1];
       const double rho_next = sums[2];
+      if (iter == kIterFromCtl) iter = ctl->it++;
       auto bad = [](double v) { return v == 0.0 || isinf(v) || isnan(v); };
       if (iter == 0) {  // r = b, z = M^-1 r: initial rho, Q0 = 0
         if (ctl->bb == 0.0) {  // "Convergence. |b| = 0." (x stays 0)

@@ -159,7 +159,10 @@ struct CgCtl {
   int32_t max_iter;
   double rho_step;  // sharded solves: rho of the current step, snapshot by the replica reduction
   double bb;        // b.b of the linear solve (|b| = 0: converged at iteration 0, x = 0)
+  int32_t it;       // next CG iteration number (the update kernel's finalisation counts on the device,
+                    // so a captured iteration's launch arguments do not depend on its number)
 };
+constexpr int32_t kIterFromCtl = -2;  // k_cg_update iter argument: take it from CgCtl::it
 
 // Camera-side entry of the reduced system as the CG update reads it: its
 // block's first entry, the block size and the offset of the entry's row of

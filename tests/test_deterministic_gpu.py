@@ -97,3 +97,27 @@ def test_deterministic_solve_is_reproducible(depth):
     assert np.abs(_poses(P, xdet) - _poses(P, xd)).max() <= 1e-6
     o_det, o_d = _others(P, xdet), _others(P, xd)
     assert np.abs(o_det - o_d).max() <= 1e-6 * max(1.0, np.abs(o_d).max())
+
+
+@pytest.mark.parametrize("depth", [False, True])
+def test_graph_replayed_cg_equals_eager(monkeypatch, depth):
+    """Single-rank solves replay captured runs of CG iterations (hipGraph,
+    mvba_solve.cpp cg_device; MVBA_CG_GRAPH=0 launches every kernel eagerly).
+    The captured launches are the eager ones with the same arguments, so in
+    deterministic mode the two give bit-identical solves: CG counts, costs,
+    parameters. Long enough for the residual reset (every 10th iteration) and
+    both parities of the double-buffered vectors, with the captured runs
+    replayed across several linear solves of one handle."""
+    P = _rig_problem(depth)
+    runs = []
+    for g in ("0", "1"):
+        monkeypatch.setenv("MVBA_CG_GRAPH", g)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(max_num_iterations=6, use_loss=1, robust_threshold=3.0, deterministic=1, **TOL)
+            runs.append((s, ev.get_params()))
+    (sa, xa), (sb, xb) = runs
+    assert sa["num_linear_iterations"] > 20, sa["num_linear_iterations"]
+    for k in ("termination_type", "num_iterations", "num_successful_steps", "num_linear_iterations", "final_cost"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+    assert np.array_equal(xa, xb)
