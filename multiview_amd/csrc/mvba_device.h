@@ -222,6 +222,110 @@ __device__ __forceinline__ double group_sum_f64(double v) {
   return v;
 }
 
+// Sums of NV per-lane values over the wave, TRANSPOSED (all lanes active):
+// with P = the power of two >= NV (<= 64) and m = log2 P, each of the first m
+// steps pairs every lane with a partner that differs in one lane bit (5, 4, 3,
+// 2, 1, 0 in turn) and halves the values a lane holds: the lane keeps the half
+// its bit selects and adds the partner's copy of it (the partner sends that
+// half). The remaining 6 - m steps add the last value over the lower lane bits.
+// On return v[0] of lane l is the total of value l >> (6 - m). Pairings:
+// v_permlane32_swap / v_permlane16_swap (gfx950) for bits 5 and 4 (the swap
+// itself selects the halves), DPP row_mirror / row_half_mirror / quad_perm
+// for bits 3..0. About 4 instructions per value against wave_sum_f64's ~20
+// per value (pass B reduces its 14..47 accumulators once per chunk).
+__device__ __forceinline__ void swap32_f64(double& x, double& y) {
+  const long long bx = __builtin_bit_cast(long long, x), by = __builtin_bit_cast(long long, y);
+  const auto lo = __builtin_amdgcn_permlane32_swap((int)bx, (int)by, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((int)(bx >> 32), (int)(by >> 32), false, false);
+  x = __builtin_bit_cast(double, ((long long)hi[0] << 32) | (unsigned)lo[0]);
+  y = __builtin_bit_cast(double, ((long long)hi[1] << 32) | (unsigned)lo[1]);
+}
+__device__ __forceinline__ void swap16_f64(double& x, double& y) {
+  const long long bx = __builtin_bit_cast(long long, x), by = __builtin_bit_cast(long long, y);
+  const auto lo = __builtin_amdgcn_permlane16_swap((int)bx, (int)by, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((int)(bx >> 32), (int)(by >> 32), false, false);
+  x = __builtin_bit_cast(double, ((long long)hi[0] << 32) | (unsigned)lo[0]);
+  y = __builtin_bit_cast(double, ((long long)hi[1] << 32) | (unsigned)lo[1]);
+}
+// the partner's v over lane bit B (B = 3, 2, 1, 0), inside a 16-lane row
+template <int B>
+__device__ __forceinline__ double partner_f64(double v) {
+  if constexpr (B == 3) return dpp_f64<0x140, 0xf>(v);  // row_mirror: l <-> 15 - l
+  else if constexpr (B == 2) return dpp_f64<0x141, 0xf>(v);  // row_half_mirror: l <-> 7 - l
+  else if constexpr (B == 1) return dpp_f64<0x4E, 0xf>(v);  // quad_perm [2,3,0,1]
+  else return dpp_f64<0xB1, 0xf>(v);  // quad_perm [1,0,3,2]
+}
+template <int B, int L>
+__device__ __forceinline__ void tsum_step(double* v, int lane) {
+  constexpr int H = L / 2;
+  if constexpr (B == 5) {
+#pragma unroll
+    for (int j = 0; j < H; j++) {
+      double x = v[j], y = v[j + H];
+      swap32_f64(x, y);
+      v[j] = x + y;
+    }
+  } else if constexpr (B == 4) {
+#pragma unroll
+    for (int j = 0; j < H; j++) {
+      double x = v[j], y = v[j + H];
+      swap16_f64(x, y);
+      v[j] = x + y;
+    }
+  } else {
+    const bool hi = (lane >> B) & 1;
+#pragma unroll
+    for (int j = 0; j < H; j++) {
+      const double keep = hi ? v[j + H] : v[j];
+      const double send = hi ? v[j] : v[j + H];
+      v[j] = keep + partner_f64<B>(send);
+    }
+  }
+}
+template <int B>
+__device__ __forceinline__ double plain_step(double x) {
+  if constexpr (B == 5) {
+    double y = x;
+    swap32_f64(x, y);
+    return x + y;
+  } else if constexpr (B == 4) {
+    double y = x;
+    swap16_f64(x, y);
+    return x + y;
+  } else {
+    return x + partner_f64<B>(x);
+  }
+}
+template <int NV>
+struct TSum {
+  static constexpr int P = NV <= 1 ? 1 : NV <= 2 ? 2 : NV <= 4 ? 4 : NV <= 8 ? 8 : NV <= 16 ? 16 : NV <= 32 ? 32 : 64;
+  static constexpr int M = P == 1 ? 0 : P == 2 ? 1 : P == 4 ? 2 : P == 8 ? 3 : P == 16 ? 4 : P == 32 ? 5 : 6;
+  static constexpr int kShift = 6 - M;  // lane l holds value l >> kShift
+};
+// w: TSum<NV>::P values (entries NV.. zero), reduced in place
+template <int NV>
+__device__ __forceinline__ double wave_sum_transpose(double* w, int lane) {
+  static_assert(NV >= 1 && NV <= 64, "1..64 values");
+  using T = TSum<NV>;
+  constexpr int P = T::P, M = T::M;
+  // selection steps on bits 5 .. 6 - M (L values -> L / 2)
+  if constexpr (M >= 1) tsum_step<5, P>(w, lane);
+  if constexpr (M >= 2) tsum_step<4, P / 2>(w, lane);
+  if constexpr (M >= 3) tsum_step<3, P / 4>(w, lane);
+  if constexpr (M >= 4) tsum_step<2, P / 8>(w, lane);
+  if constexpr (M >= 5) tsum_step<1, P / 16>(w, lane);
+  if constexpr (M >= 6) tsum_step<0, P / 32>(w, lane);
+  // plain sums over the remaining lower bits
+  double r = w[0];
+  if constexpr (M <= 0) r = plain_step<5>(r);
+  if constexpr (M <= 1) r = plain_step<4>(r);
+  if constexpr (M <= 2) r = plain_step<3>(r);
+  if constexpr (M <= 3) r = plain_step<2>(r);
+  if constexpr (M <= 4) r = plain_step<1>(r);
+  if constexpr (M <= 5) r = plain_step<0>(r);
+  return r;
+}
+
 // Write one pose column record: omega, v = dt - omega x t.
 __device__ __forceinline__ void put_col(double* rec, int k, const double* om, const double* dt,
                                         const double* t) {

@@ -33,9 +33,9 @@ static void free_all(mvba_handle* h) {
   if (!h) return;
   void* ptrs[] = {h->d_params, h->d_fd,      h->d_frec,  h->d_pt_off, h->d_pt_free,
                   h->d_pts,    h->d_obs_pid, h->d_obs_meas, h->d_segs, h->d_order,
-                  h->d_row_written, h->d_err, h->d_ready, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_frame_lin,
+                  h->d_row_written, h->d_err, h->d_ready, h->d_res, h->d_J, h->d_chunks, h->d_segchunks, h->d_achunks, h->d_frame_lin,
                   h->d_parts, h->d_rep, h->d_pt_begin, h->d_po_frame, h->d_po_meas, h->d_slot_po,
-                  h->d_po_slot,
+                  h->d_po_slot,       h->d_wtiles,  h->d_wlane_pid, h->d_wlane_slot, h->d_wlane_pos,
                   h->d_dep_desc, h->d_dep_pid, h->d_dep_meas, h->d_dep_segs, h->d_dep_order, h->d_dres, h->d_dJ,
                   h->d_dpt_begin, h->d_dpo_slot, h->d_dslot_po, h->d_xpt_begin, h->d_xref, h->d_xcc, h->d_xkind, h->d_xpid,
                   h->d_xorder, h->d_xout, h->d_xscal, h->d_xcnt, h->d_varsize, h->d_tres, h->d_tcost,
@@ -573,18 +573,39 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
       G.part_begin = (int32_t)parts.size();
       G.gram_width = h->lin_ok ? mvba_gram_width(G.model, G.deg) : 0;
       G.w16 = (G.gram_width + 15) / 16 * 16;
-      // segments per CG chunk (one wave of pass B and pass A): mvba::kChunkSegs,
-      // 2x that where images average 12+ segments (c3, 17 per image: pass B
-      // 197 -> 182 us; c2, 5 per image, measured slower with 16: 22 -> 27 us;
-      // profiles/r04/r04t/). MVBA_CHUNK_SEGS overrides it (A/B timing).
+      // segments per pass-B chunk (one wave): mvba::kChunkSegs, 2x that where
+      // images average 12+ segments (c3, 17 per image: pass B 197 -> 182 us;
+      // profiles/r04/r04t/), and halved (8 -> 4 -> 2 -> 1) while the group
+      // would have fewer than kMinChunks chunks: thin shards have one or two
+      // 8-segment chunks per image, too few waves to cover the gathers' latency
+      // (1/8 c2 shard, 470 chunks: pass B 10.5 us with 8-segment chunks, 6.9
+      // with 2; whole c2, 3,008 chunks: 21.9 us with 8, 23.0 with 4;
+      // profiles/r05/r05g/). MVBA_CHUNK_SEGS overrides it (A/B timing).
       int32_t gframes = 0;
-      for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++)
-        if (sidx == G.seg_begin || segs[sidx].frame != segs[sidx - 1].frame) gframes++;
+      std::vector<int32_t> fsegs;  // segments per frame run of the group
+      for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++) {
+        if (sidx == G.seg_begin || segs[sidx].frame != segs[sidx - 1].frame) {
+          gframes++;
+          fsegs.push_back(0);
+        }
+        fsegs.back()++;
+      }
+      auto nchunks_of = [&](int cs) {
+        int64_t c = 0;
+        for (int32_t m : fsegs) c += (m + cs - 1) / cs;
+        return c;
+      };
+      constexpr int64_t kMinChunks = 1024;  // one wave per SIMD
       const int chunk_segs = [&] {
         const char* e = std::getenv("MVBA_CHUNK_SEGS");
-        const int v = e ? std::atoi(e)
-                        : (G.seg_count >= 12 * (int64_t)std::max(gframes, 1) ? 2 * mvba::kChunkSegs : mvba::kChunkSegs);
-        return v >= 1 && v <= 64 ? v : mvba::kChunkSegs;
+        if (e) {
+          const int v = std::atoi(e);
+          return v >= 1 && v <= 64 ? v : mvba::kChunkSegs;
+        }
+        if (G.seg_count >= 12 * (int64_t)std::max(gframes, 1)) return 2 * mvba::kChunkSegs;
+        int cs = mvba::kChunkSegs;
+        while (cs > 1 && nchunks_of(cs) < kMinChunks) cs /= 2;
+        return cs;
       }();
       for (int32_t sidx = G.seg_begin; sidx < G.seg_begin + G.seg_count; sidx++) {
         const Segment& sg = segs[sidx];
@@ -827,6 +848,27 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
     std::vector<int4> sc(segs.size());
     for (size_t k = 0; k < segs.size(); k++) sc[k] = direct((int32_t)k, 1, k == 0 || segs[k - 1].frame != segs[k].frame);
     chk(upload(&h->d_segchunks, sc));
+    // pass A's chunks: runs of at most kChunkSegs segments of one frame, also
+    // where pass B's chunks are 2x that (c3 pass A: 131 us on 8-segment chunks,
+    // 144 on 16-segment ones, profiles/r04/r04w/). MVBA_PASS_A_SEGS overrides
+    // the run length (A/B timing).
+    const int asegs = [] {
+      const char* e = std::getenv("MVBA_PASS_A_SEGS");
+      const int v = e ? std::atoi(e) : mvba::kChunkSegs;
+      return v >= 1 && v <= 64 ? v : mvba::kChunkSegs;
+    }();
+    std::vector<int4> ac;
+    for (Group& G : h->groups) {
+      G.achunk_begin = (int32_t)ac.size();
+      for (int32_t a = G.seg_begin; a < G.seg_begin + G.seg_count;) {
+        int32_t b = a + 1;
+        while (b < G.seg_begin + G.seg_count && b - a < asegs && segs[b].frame == segs[a].frame) b++;
+        ac.push_back(direct(a, b - a, a == G.seg_begin || segs[a - 1].frame != segs[a].frame));
+        a = b;
+      }
+      G.achunk_count = (int32_t)ac.size() - G.achunk_begin;
+    }
+    chk(upload(&h->d_achunks, ac));
   }
   {
     void* p = nullptr;
@@ -848,6 +890,45 @@ mvba_status mvba_create(const mvba_problem_desc* d, const mvba_options* opts, mv
   chk(upload(&h->d_po_meas, po_meas));
   chk(upload(&h->d_slot_po, slot_po));
   chk(upload(&h->d_po_slot, po_slot));
+  {
+    // k_point_w_seg's wave tiles: consecutive points packed whole into <= 64
+    // lanes (one lane per reprojection residual, one for a point without any);
+    // a track longer than a wave gets a tile of its own (lane-strided loop)
+    std::vector<int4> tiles;
+    std::vector<int32_t> lpid, lslot, lpos;
+    lpid.reserve((size_t)N + (size_t)h->npts / 8 + 64);
+    lslot.reserve(lpid.capacity());
+    lpos.reserve(lpid.capacity());
+    int32_t first = 0, count = 0;
+    auto flush = [&]() {
+      if (count > 0) tiles.push_back(make_int4(first, count, -1, 0));
+      first = (int32_t)lpid.size();
+      count = 0;
+    };
+    for (int64_t p = 0; p < h->npts; p++) {
+      const int64_t n = pt_begin[(size_t)p + 1] - pt_begin[(size_t)p];
+      if (n > 64) {
+        flush();
+        tiles.push_back(make_int4(first, 0, (int32_t)p, 0));
+        continue;
+      }
+      const int32_t m = (int32_t)std::max<int64_t>(n, 1);
+      if (count + m > 64) flush();
+      for (int32_t k = 0; k < m; k++) {
+        const int64_t j = n > 0 ? pt_begin[(size_t)p] + k : -1;
+        lpid.push_back((int32_t)p);
+        lpos.push_back((int32_t)j);
+        lslot.push_back(j >= 0 ? po_slot[(size_t)j] : -1);
+      }
+      count += m;
+    }
+    flush();
+    h->nwtiles = (int32_t)tiles.size();
+    chk(upload(&h->d_wtiles, tiles));
+    chk(upload(&h->d_wlane_pid, lpid));
+    chk(upload(&h->d_wlane_slot, lslot));
+    chk(upload(&h->d_wlane_pos, lpos));
+  }
   chk(upload(&h->d_dep_desc, ddesc));
   {
     std::vector<int32_t> dpid(ddesc.size());

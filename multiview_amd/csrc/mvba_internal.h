@@ -172,6 +172,7 @@ struct Group {
   int64_t res_begin = 0, res_count = 0;
   // solver passes: chunks of <= 4 segments of one frame (one wave each)
   int32_t chunk_begin = 0, chunk_count = 0;
+  int32_t achunk_begin = 0, achunk_count = 0;  // pass A's chunks (<= kChunkSegs segments; d_achunks)
   // linearization (K2): parts of <= kPartSegs segments of one frame (one block each)
   int32_t part_begin = 0, part_count = 0;
   int32_t gram_width = 0, w16 = 0;
@@ -347,6 +348,7 @@ struct mvba_handle {
   std::vector<int32_t> pt_block_ids;    // point index -> block id
   int4* d_chunks = nullptr;
   int4* d_segchunks = nullptr;          // one chunk per segment (seg, 1, frame, -)
+  int4* d_achunks = nullptr;            // pass A: runs of <= kChunkSegs segments of one frame (direct records)
   void* d_frame_lin = nullptr;
   int4* d_parts = nullptr;              // K2 frame parts (seg_begin, seg_count, frame, -)
   double* d_rep = nullptr;  // nrep copies of [cam_grad | cam_hess | cost], kept zero between calls
@@ -355,6 +357,15 @@ struct mvba_handle {
   double2* d_po_meas = nullptr;
   int32_t* d_slot_po = nullptr;          // device slot -> point-order index (-1 = padding)
   int32_t* d_po_slot = nullptr;          // point-order index -> device slot
+  // k_point_w_seg: wave tiles of whole tracks (first lane, lanes, long-track
+  // point or -1, -) and per lane its point, slot (slot-order c_o) and point-order
+  // position (point-order c_o); -1 for the one lane of a point without
+  // reprojection residuals
+  int4* d_wtiles = nullptr;
+  int32_t* d_wlane_pid = nullptr;
+  int32_t* d_wlane_slot = nullptr;
+  int32_t* d_wlane_pos = nullptr;
+  int32_t nwtiles = 0;
   std::vector<int64_t> cam_poff;         // camera-side entry -> packed parameter offset
   int32_t nchunks = 0;
   int32_t nparts = 0;                    // K2 frame parts over all model groups

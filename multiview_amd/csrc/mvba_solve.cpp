@@ -52,6 +52,11 @@ hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int3
                                const double* tinit, const double* V, const double* dp, const double4* pts,
                                double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
                                const double4* dcbuf, hipStream_t s);
+hipError_t mvba_launch_point_w_seg(int32_t ntiles, const int4* tiles, const int32_t* wlane_pid,
+                                   const int32_t* wlane_idx, const int64_t* pt_begin, const int32_t* po_idx,
+                                   const double4* cbuf, const double* tinit, const double* V, const double* dp,
+                                   const double4* pts, double* wout, int32_t wstride, const int32_t* gate,
+                                   hipStream_t s);
 hipError_t mvba_launch_depth_pa(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const int32_t* dpid, const double4* dmeas, const double* frec, const double* params,
                                 const double4* pts, const double* dir, const double* xcam, double* du,
@@ -168,6 +173,7 @@ struct SolverState {
   std::vector<uintptr_t> graph_sig;
   bool graphs_broken = false;  // a capture failed: eager launches from then on
   hipStream_t own_stream = nullptr;  // solves called on the null stream run here (capturable)
+  hipEvent_t ev[2] = {nullptr, nullptr};  // the merged LM step's candidate-evaluation span
   void drop_graphs() {
     for (CgGraph& g : graphs)
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -187,6 +193,8 @@ void solver_state_free(SolverState* S) {
   S->b_det.release();
   S->drop_graphs();
   if (S->own_stream) (void)hipStreamDestroy(S->own_stream);
+  for (hipEvent_t e : S->ev)
+    if (e) (void)hipEventDestroy(e);
   delete S;
 }
 
@@ -274,6 +282,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(upload(&S->goff, h->cam_goff));
     HCHK(upload(&S->hoff, h->cam_hoff));
     HCHK(upload(&S->cam_poff, h->cam_poff));
+    for (hipEvent_t& e : S->ev) HCHK(hipEventCreate(&e));
   } catch (...) {
     solver_state_free(S);
     throw;
@@ -327,6 +336,10 @@ class Solver {
   // read). MVBA_CG_PQ=grid keeps the last-block reduction (A/B timing).
   static constexpr int kPqSlot = 24;
   int cg_par_ = 0;
+  bool merged_reads() const {
+    const char* e = std::getenv("MVBA_LM_MERGED");  // read per call: tests switch it
+    return !(e && e[0] == '0');
+  }
   bool pq_atomic() const {
     const char* e = std::getenv("MVBA_CG_PQ");  // read per call: tests switch it
     return !o_.allreduce && !o_.deterministic && !(e && !std::strcmp(e, "grid"));
@@ -378,6 +391,26 @@ class Solver {
   // Jacobian at the handle's parameters -> lin (all-reduced), G, phess, cdiag. Returns cost.
   // skip_prep: the frame and landmark records are current (the candidate's
   // cost evaluation just ran the prep kernel at these parameters)
+  // enqueue-only form (merged LM step): the cost lands in scal[cost_slot], the
+  // device error word is read with the step's one fetch (fetch_checked)
+  void linearize_enqueue(bool skip_prep, int cost_slot) {
+    const int32_t lf = flags_ | (o_.deterministic ? MVBA_LIN_DETERMINISTIC : 0) | (skip_prep ? MVBA_EVAL_SKIP_PREP : 0);
+    mvba_status st = mvba_linearize_device(h_, lf, o_.robust_threshold, S_->lin, S_->lin + S_->ng,
+                                           S_->G + S_->ng, S_->phess, S_->lin + S_->ng + S_->nh, (void*)s_);
+    if (st != MVBA_OK) throw StatusErr{st, h_->err};
+    exchange(S_->lin, S_->ng + S_->nh + 1, MVBA_REDUCE_SUM);
+    if (S_->ng)
+      HCHK(hipMemcpyAsync(S_->G, S_->lin, (size_t)S_->ng * sizeof(double), hipMemcpyDeviceToDevice, s_));
+    HCHK(mvba_launch_extract_diag(S_->nblocks, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->np, S_->phess,
+                                  S_->ng, S_->cdiag, s_));
+    HCHK(hipMemcpyAsync(S_->scal + cost_slot, S_->lin + S_->ng + S_->nh, sizeof(double), hipMemcpyDeviceToDevice,
+                        s_));
+  }
+  void grad_max_enqueue(int slot) {
+    HCHK(mvba_launch_proj_grad_max(S_->nc, S_->x, S_->G, S_->lo, S_->hi, S_->partial, S_->scal + slot, s_));
+    exchange(S_->scal + slot, 1, MVBA_REDUCE_MAX);
+  }
+
   double linearize(bool skip_prep = false) {
     const int32_t lf = flags_ | (o_.deterministic ? MVBA_LIN_DETERMINISTIC : 0) | (skip_prep ? MVBA_EVAL_SKIP_PREP : 0);
     mvba_status st = mvba_linearize_device(h_, lf, o_.robust_threshold, S_->lin, S_->lin + S_->ng,
@@ -393,6 +426,58 @@ class Solver {
     HCHK(hipMemcpyAsync(&c, S_->lin + S_->ng + S_->nh, sizeof(double), hipMemcpyDeviceToHost, s_));
     HCHK(hipStreamSynchronize(s_));
     return c;
+  }
+
+  // One host read of scal[0..n) and the device error word (K0's alpha range
+  // check); throws on a device error. The merged LM step below reads every
+  // scalar a decision needs with one of these instead of one sync per quantity.
+  const double* fetch_checked(int n) {
+    HCHK(hipMemcpyAsync(S_->hscal, S_->scal, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s_));
+    HCHK(hipMemcpyAsync(S_->hscal + kErrSlot, h_->d_err, 2 * sizeof(int), hipMemcpyDeviceToHost, s_));
+    HCHK(hipStreamSynchronize(s_));
+    int err[2];
+    std::memcpy(err, S_->hscal + kErrSlot, sizeof(err));
+    const mvba_status st = device_error(err, h_->gen);
+    if (st != MVBA_OK) throw StatusErr{st, device_error_text(st)};
+    return S_->hscal;
+  }
+  static constexpr int kErrSlot = 30;  // hscal[30]: the device error word (2 ints)
+
+  // cost() without its host reads: the candidate's cost into scal[16], summed
+  // over ranks (stream-ordered)
+  void cost_enqueue() {
+    prep();
+    double* acc = S_->scal + 16;
+    HCHK(hipMemsetAsync(acc, 0, sizeof(double), s_));
+    for (const Group& G : h_->groups) {
+      int64_t nb = 0;
+      HCHK(mvba_launch_cost(G.model, G.deg, h_->d_segs + G.seg_begin, G.seg_count, h_->d_fd, h_->d_frec,
+                            h_->d_params, h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, flags_, cauchy_c_,
+                            S_->partial, s_, &nb));
+      HCHK(mvba_launch_sum(nb, S_->partial, S_->scal + 17, s_));
+      HCHK(mvba_launch_axpby(1, 1.0, acc, 1.0, S_->scal + 17, acc, s_));
+    }
+    if (h_->ndep > 0) {
+      int64_t nb = 0;
+      HCHK(mvba_launch_depth_cost(h_->ndep_slots, h_->d_dep_desc, h_->d_dep_order, h_->d_dep_meas, h_->d_frec,
+                                  h_->d_params, h_->d_pts, flags_, cauchy_c_, S_->partial, s_, &nb));
+      HCHK(mvba_launch_sum(nb, S_->partial, S_->scal + 17, s_));
+      HCHK(mvba_launch_axpby(1, 1.0, acc, 1.0, S_->scal + 17, acc, s_));
+    }
+    if (h_->nxyz > 0) {
+      HCHK(mvba_launch_xyz_cost(h_->nxyz, h_->d_xpid, h_->d_xref, h_->d_xcc, h_->d_pts, flags_, h_->d_xscal + 1,
+                                h_->d_xcnt, h_->d_xscal, s_));
+      HCHK(mvba_launch_axpby(1, 1.0, acc, 1.0, h_->d_xscal, acc, s_));
+    }
+    exchange(acc, 1, MVBA_REDUCE_SUM);
+  }
+
+  // |v|^2 over the compact vector into scal[pt_slot] (points, summed over
+  // ranks) and scal[cam_slot] (camera part, replicated), no host read
+  void norm2_enqueue(const double* v, int pt_slot, int cam_slot) {
+    dot(3 * S_->np, v + S_->ng, v + S_->ng, pt_slot);
+    exchange(S_->scal + pt_slot, 1, MVBA_REDUCE_SUM);
+    dot(S_->ng, v, v, cam_slot);
   }
 
   // Cost at the handle's parameters (prep + cost kernels), summed over ranks.
@@ -515,7 +600,8 @@ class Solver {
                               h_->point_extra(), xv, S_->du, gate, S_->prec, s_));
       return;
     }
-    // one pass-B chunk (8 or 16 segments of one image) per wave when there are
+    // one chunk of up to 8 segments of one image per wave (d_achunks; pass B's
+    // chunks are 16 segments where images average 12+) when there are
     // enough of them to fill the chip (4,096+, four waves per SIMD): with frames
     // in capture order the landmark gathers are cheap and the direction staging
     // per wave amortises over more observations (c3, 18k chunks: pass A 176 ->
@@ -524,7 +610,7 @@ class Solver {
     // MVBA_PASS_A_CHUNKS=0|1 forces one (read per call, for A/B timing)
     const char* pa_env = std::getenv("MVBA_PASS_A_CHUNKS");
     int32_t nchunks_all = 0;
-    for (const Group& G : h_->groups) nchunks_all += G.chunk_count;
+    for (const Group& G : h_->groups) nchunks_all += G.achunk_count;
     const bool chunked = pa_env ? pa_env[0] == '1' : nchunks_all >= 4096;
     // where pass A leaves c_o = J_pt^T z_o: at the observation's point-order
     // position (scattered 32-B stores, k_point_w reads its run) or in slot order
@@ -535,8 +621,8 @@ class Solver {
     if (dir)
       for (const Group& G : h_->groups)
         HCHK(mvba_launch_pass_a_frame(G.model, G.deg,
-                                      chunked ? h_->d_chunks + G.chunk_begin : h_->d_segchunks + G.seg_begin,
-                                      chunked ? G.chunk_count : G.seg_count, h_->d_segs,
+                                      chunked ? h_->d_achunks + G.achunk_begin : h_->d_segchunks + G.seg_begin,
+                                      chunked ? G.achunk_count : G.seg_count, h_->d_segs,
                                       h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, co_slot ? nullptr : h_->d_slot_po, dr,
                                       (double4*)S_->cbuf, flags_, cauchy_c_, gate, S_->prec, obsx(), s_));
     // depth blocks in frame order (z_d into du, P z_d per block for the point solve)
@@ -545,10 +631,23 @@ class Solver {
       HCHK(mvba_launch_depth_pa(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_pid, h_->d_dep_meas,
                                 h_->d_frec, h_->d_params, h_->d_pts, dir, xv, S_->du, h_->d_dslot_po,
                                 (double4*)S_->dcbuf, flags_, cauchy_c_, gate, s_));
-    HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
-                             dir ? (const double4*)S_->cbuf : nullptr,
-                             tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate,
-                             dep ? h_->d_dpt_begin : nullptr, dep ? (const double4*)S_->dcbuf : nullptr, s_));
+    if (dir && !dep && point_w_tiles())
+      HCHK(mvba_launch_point_w_seg(h_->nwtiles, h_->d_wtiles, h_->d_wlane_pid,
+                                   co_slot ? h_->d_wlane_slot : h_->d_wlane_pos, h_->d_pt_begin,
+                                   co_slot ? h_->d_po_slot : nullptr, (const double4*)S_->cbuf, tinit, S_->phess,
+                                   S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate, s_));
+    else
+      HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
+                               dir ? (const double4*)S_->cbuf : nullptr,
+                               tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate,
+                               dep ? h_->d_dpt_begin : nullptr, dep ? (const double4*)S_->dcbuf : nullptr, s_));
+  }
+
+  // k_point_w_seg (wave tiles of whole tracks, one lane per residual) when
+  // MVBA_POINT_W=tiles; the default is 8 lanes per point (k_point_w)
+  bool point_w_tiles() const {
+    const char* e = std::getenv("MVBA_POINT_W");  // read per call: tests switch it
+    return h_->nwtiles > 0 && e && !std::strcmp(e, "tiles");
   }
 
   // y = S x (implicit Schur complement with damping); x.y -> scal[dot_slot].
@@ -606,9 +705,10 @@ class Solver {
     const char* pa = std::getenv("MVBA_PASS_A_CHUNKS");
     std::vector<uintptr_t> v = {
         (uintptr_t)fused_dir, (uintptr_t)pq_atomic(), (uintptr_t)co_slot_order(co), (uintptr_t)(pa ? pa[0] : 0),
+        (uintptr_t)point_w_tiles(), u(h_->d_wtiles), u(h_->d_wlane_pid), u(h_->d_wlane_slot), u(h_->d_wlane_pos),
         (uintptr_t)flags_, (uintptr_t)std::llround(cauchy_c_ * 1e15), (uintptr_t)S_->ng, (uintptr_t)h_->nframes,
         u(obsx()), u(h_->d_params), u(h_->d_pts), u(h_->d_frec), u(h_->d_fd), u(h_->d_frame_lin), u(h_->d_segs),
-        u(h_->d_chunks), u(h_->d_segchunks), u(h_->d_obs_pid), u(h_->d_obs_meas), u(h_->d_slot_po),
+        u(h_->d_chunks), u(h_->d_segchunks), u(h_->d_achunks), u(h_->d_obs_pid), u(h_->d_obs_meas), u(h_->d_slot_po),
         u(h_->d_po_slot), u(h_->d_pt_begin), u(h_->d_pt_off), u(h_->d_pt_free), u(h_->d_dep_segs),
         u(h_->d_dep_desc), u(h_->d_dep_pid), u(h_->d_dep_meas), u(h_->d_dslot_po), u(h_->d_dpt_begin),
         u(h_->d_po_frame), u(h_->d_po_meas), (uintptr_t)h_->npts, (uintptr_t)h_->nchunks,
@@ -807,7 +907,7 @@ class Solver {
   }
 
   // delta_p = -(V+D)^-1 (g_p + W' delta_c); returns model cost change -(g'delta + |J delta|^2 / 2)
-  double back_substitute() {
+  double back_substitute(bool fetch_now = true) {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
                                nullptr, nullptr, s_));
     // |J delta|^2 over the local reprojection and depth blocks -> scal[0].
@@ -828,9 +928,15 @@ class Solver {
                                     h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, co_slot ? nullptr : h_->d_slot_po,
                                     plain_dir(S_->dir), (double4*)S_->cbuf, flags_, cauchy_c_, nullptr, S_->prec,
                                     obsx(), s_));
-      HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
-                               (const double4*)S_->cbuf, S_->G + S_->ng, S_->phess, S_->dmp + S_->ng, h_->d_pts,
-                               S_->delta + S_->ng, 3, nullptr, nullptr, nullptr, s_));
+      if (point_w_tiles())
+        HCHK(mvba_launch_point_w_seg(h_->nwtiles, h_->d_wtiles, h_->d_wlane_pid,
+                                     co_slot ? h_->d_wlane_slot : h_->d_wlane_pos, h_->d_pt_begin,
+                                     co_slot ? h_->d_po_slot : nullptr, (const double4*)S_->cbuf, S_->G + S_->ng,
+                                     S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->delta + S_->ng, 3, nullptr, s_));
+      else
+        HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
+                                 (const double4*)S_->cbuf, S_->G + S_->ng, S_->phess, S_->dmp + S_->ng, h_->d_pts,
+                                 S_->delta + S_->ng, 3, nullptr, nullptr, nullptr, s_));
       HCHK(mvba_launch_pass_sq(G.model, G.deg, h_->d_segchunks + G.seg_begin, G.seg_count, h_->d_obs_pid,
                                plain_dir(S_->dir), S_->delta + S_->ng, 3, S_->prec, obsx(), S_->partial,
                                S_->cnt + 5, S_->scal + 0, s_));
@@ -845,7 +951,11 @@ class Solver {
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);
     dot(S_->ng, S_->G, S_->delta, 2);  // g_c' delta_c (global already)
-    const double* hs = fetch(3);
+    if (!fetch_now) return 0.0;
+    return model_change(fetch(3));
+  }
+  // the model cost change from the back-substitution's scal[0..2]
+  double model_change(const double* hs) {
     for (int k = 0; k < 3; k++) last_mc_[k] = hs[k];
     return -(hs[1] + hs[2] + 0.5 * hs[0]);
   }
@@ -1194,13 +1304,43 @@ void Solver::run(mvba_solver_summary* sum) {
     if (cg_timing()) tm_.iters += cgr.iters;
     bool valid = cgr.status != 2;
     double mcc = 0.0;
+    // Merged step (unbounded problems; MVBA_LM_MERGED=0: one host read per
+    // quantity, as before): the candidate x + delta, its cost and |step| are
+    // enqueued behind the back-substitution and read back together with the
+    // model cost change and the device error word, one stream sync instead of
+    // four. An invalid step then restores the parameters it moved.
+    const bool merged = !bounded_ && merged_reads();
+    double m_cand = 0.0, m_step2 = 0.0, m_eval_gpu_s = 0.0;
     if (valid) {
       const double tbs = now_s();
-      mcc = back_substitute();
-      if (cg_timing()) tm_.backsub += now_s() - tbs;
+      if (merged) {
+        back_substitute(false);
+        HCHK(hipEventRecord(S_->ev[0], s_));
+        HCHK(mvba_launch_plus(nc, S_->x, S_->delta, S_->lo, S_->hi, S_->xn, s_));
+        set_params_from(S_->xn);
+        cost_enqueue();
+        HCHK(mvba_launch_axpby(S_->nc, 1.0, S_->xn, -1.0, S_->x, S_->scr, s_));
+        norm2_enqueue(S_->scr, 3, 4);
+        HCHK(hipEventRecord(S_->ev[1], s_));
+        const double* hs = fetch_checked(17);
+        mcc = model_change(hs);
+        m_cand = hs[16];
+        m_step2 = hs[3] + hs[4];
+        float ms = 0.0f;
+        HCHK(hipEventElapsedTime(&ms, S_->ev[0], S_->ev[1]));
+        m_eval_gpu_s = 1e-3 * ms;  // the candidate's share of the wait (eval time)
+      } else {
+        mcc = back_substitute();
+      }
+      if (cg_timing()) tm_.backsub += now_s() - tbs - m_eval_gpu_s;
       valid = std::isfinite(mcc) && mcc > 0.0;
+      if (merged && !valid) {  // the speculative candidate moved the parameters
+        set_params_from(S_->x);
+        prep();
+      }
     }
-    sum->linear_solver_time_s += now_s() - ts;
+    sum->linear_solver_time_s += now_s() - ts - m_eval_gpu_s;
+    sum->eval_time_s += m_eval_gpu_s;
     static const bool trace = std::getenv("MVBA_SOLVER_TRACE") && std::getenv("MVBA_SOLVER_TRACE")[0] == '1';
     if (trace)
       std::fprintf(stderr,
@@ -1231,13 +1371,16 @@ void Solver::run(mvba_solver_summary* sum) {
       const double gtd = dot_global(S_->G, S_->delta);
       armijo(x_cost, gtd, &relinearized);
     }
-    // ComputeCandidatePointAndEvaluateCost
-    HCHK(mvba_launch_plus(nc, S_->x, S_->delta, S_->lo, S_->hi, S_->xn, s_));
-    set_params_from(S_->xn);
-    double cand = cost();
+    // ComputeCandidatePointAndEvaluateCost (merged: already read with the step)
+    double cand = m_cand;
+    if (!merged) {
+      HCHK(mvba_launch_plus(nc, S_->x, S_->delta, S_->lo, S_->hi, S_->xn, s_));
+      set_params_from(S_->xn);
+      cand = cost();
+    }
     if (!std::isfinite(cand)) cand = std::numeric_limits<double>::max();
     sum->eval_time_s += now_s() - te;
-    const double step_norm = std::sqrt(step_norm2());
+    const double step_norm = merged ? std::sqrt(m_step2) : std::sqrt(step_norm2());
     auto restore_x = [&]() {
       set_params_from(S_->x);
       prep();
@@ -1265,11 +1408,25 @@ void Solver::run(mvba_solver_summary* sum) {
       // HandleSuccessfulStep: x = candidate, re-linearize there (cost() ran the
       // prep kernel at the candidate: its records are current)
       std::swap(S_->x, S_->xn);
-      x_norm = std::sqrt(norm2_compact(S_->x));
-      tl = now_s();
-      x_cost = linearize(true);
-      sum->linearize_time_s += now_s() - tl;
-      gmax = grad_max_norm();
+      if (merged) {
+        // |x|, the linearization at x (records current: cost() ran K0 there) and
+        // the projected-gradient max norm, read back together
+        tl = now_s();
+        norm2_enqueue(S_->x, 5, 6);
+        linearize_enqueue(true, 1);
+        grad_max_enqueue(0);
+        const double* hs = fetch_checked(7);
+        x_norm = std::sqrt(hs[5] + hs[6]);
+        x_cost = hs[1];
+        gmax = hs[0];
+        sum->linearize_time_s += now_s() - tl;
+      } else {
+        x_norm = std::sqrt(norm2_compact(S_->x));
+        tl = now_s();
+        x_cost = linearize(true);
+        sum->linearize_time_s += now_s() - tl;
+        gmax = grad_max_norm();
+      }
       radius = std::min(o_.max_trust_region_radius,
                         radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * ratio - 1.0, 3)));
       decrease = 2.0;

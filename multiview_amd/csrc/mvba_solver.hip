@@ -694,12 +694,111 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
   for (int q = 0; q < 3; q++) wout[wstride * p + q] = w[q];
 }
 
+// k_point_w as wave tiles of whole tracks (reprojection-only problems): lane l
+// of a tile takes one residual of a point (wlane_pid / wlane_idx: the c_o index
+// of that residual, -1 for a point without any), so a lane's chain is one round
+// trip to its point and c_o index, one to c_o; the point's lanes are consecutive
+// and a segmented scan (shuffles, pid equality at each distance) leaves the
+// track's sum in its last lane, which loaded the point's V, damping and right-
+// hand side alongside the gather and solves. Tracks longer than a wave have a
+// tile of their own (lane-strided loop over po_idx, wave sum).
+__global__ void __launch_bounds__(256) k_point_w_seg(int32_t ntiles, const int4* __restrict__ tiles,
+                                                     const int32_t* __restrict__ wlane_pid,
+                                                     const int32_t* __restrict__ wlane_idx,
+                                                     const int64_t* __restrict__ pt_begin,
+                                                     const int32_t* __restrict__ po_idx,
+                                                     const double4* __restrict__ cbuf, const double* __restrict__ tinit,
+                                                     const double* __restrict__ V, const double* __restrict__ dp,
+                                                     const double4* __restrict__ pts, double* __restrict__ wout,
+                                                     int32_t wstride, const int32_t* __restrict__ gate) {
+  if (gate && *gate) return;
+  const int64_t blk = xcd_block_solver((ntiles + 3) / 4);
+  const int tile = (int)blk * 4 + (int)(threadIdx.x >> 6);
+  if (blk < 0 || tile >= ntiles) return;
+  const int lane = threadIdx.x & 63;
+  const int4 T = tiles[tile];
+  const int first = __builtin_amdgcn_readfirstlane(T.x);
+  const int count = __builtin_amdgcn_readfirstlane(T.y);
+  const int lp = __builtin_amdgcn_readfirstlane(T.z);
+  auto solve_store = [&](int64_t p, double t0, double t1, double t2) {
+    double t[3] = {t0, t1, t2}, w[3] = {0.0, 0.0, 0.0};
+    if (pts[p].w != 0.0) {
+      if (tinit)
+#pragma unroll
+        for (int q = 0; q < 3; q++) t[q] += tinit[3 * p + q];
+      solve3(V + 6 * p, dp + 3 * p, t, w);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) wout[wstride * p + q] = w[q];
+  };
+  if (lp >= 0) {  // one long track
+    double t[3] = {0.0, 0.0, 0.0};
+    for (int64_t j = pt_begin[lp] + lane; j < pt_begin[lp + 1]; j += 64) {
+      const double4 cv = cbuf[po_idx ? po_idx[j] : j];
+      t[0] += cv.x;
+      t[1] += cv.y;
+      t[2] += cv.z;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) t[q] = wave_sum_f64(t[q]);
+    if (lane == 0) solve_store(lp, t[0], t[1], t[2]);
+    return;
+  }
+  const bool act = lane < count;
+  const int32_t pid = act ? wlane_pid[first + lane] : -1 - lane;
+  const int32_t idx = act ? wlane_idx[first + lane] : -1;
+  const int32_t pid_next = __shfl(pid, lane + 1 < 64 ? lane + 1 : lane, 64);
+  const bool last = act && (lane == count - 1 || pid_next != pid);
+  // the solving lane's point data, issued beside the gather
+  double Vp[6] = {0, 0, 0, 0, 0, 0}, dpp[3] = {0, 0, 0}, ti[3] = {0, 0, 0};
+  double freep = 0.0;
+  if (last) {
+    freep = pts[pid].w;
+#pragma unroll
+    for (int q = 0; q < 6; q++) Vp[q] = V[6 * (int64_t)pid + q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) dpp[q] = dp[3 * (int64_t)pid + q];
+    if (tinit)
+#pragma unroll
+      for (int q = 0; q < 3; q++) ti[q] = tinit[3 * (int64_t)pid + q];
+  }
+  double4 c = make_double4(0.0, 0.0, 0.0, 0.0);
+  if (idx >= 0) c = cbuf[idx];
+  double t0 = c.x, t1 = c.y, t2 = c.z;
+  // segmented inclusive scan over the track's consecutive lanes
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int src = lane >= off ? lane - off : lane;
+    const double u0 = __shfl(t0, src, 64), u1 = __shfl(t1, src, 64), u2 = __shfl(t2, src, 64);
+    const int32_t pu = __shfl(pid, src, 64);
+    if (lane >= off && pu == pid) {
+      t0 += u0;
+      t1 += u1;
+      t2 += u2;
+    }
+  }
+  if (!last) return;
+  double t[3] = {t0, t1, t2}, w[3] = {0.0, 0.0, 0.0};
+  if (freep != 0.0) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) t[q] += ti[q];
+    solve3(Vp, dpp, t, w);
+  }
+#pragma unroll
+  for (int q = 0; q < 3; q++) wout[wstride * (int64_t)pid + q] = w[q];
+}
+
 // ------------------------------------------------------------ pass B, wide rows
 // Wide intrinsic blocks (RPC degree >= 4: up to 113 intrinsic columns) do not
 // fit per-lane accumulators: the lanes of one half-segment write their row pair
 // [Z | I] and u_o straight into LDS ([column][row], as the Gram staging of K2),
 // then every lane reduces its columns (lane, lane + 64) over the 64 rows.
 constexpr int kPassBRegCols = 48;  // register accumulators up to this many columns
+// pass B's end-of-chunk reduction: transposed wave sums (wave_sum_transpose)
+// or one full wave_sum_f64 per accumulator (MVBA_PASSB_TRED=0, A/B builds)
+#ifndef MVBA_PASSB_TRED
+#define MVBA_PASSB_TRED 1
+#endif
 constexpr int kWideLd = 66;
 
 template <int MODEL, int DEG>
@@ -945,9 +1044,15 @@ __global__ void __launch_bounds__(64) k_pass_b(
   const FrameDesc& F = fd[frame];
   const double* __restrict__ rec = frec + (int64_t)frame * kFrameRecDoubles;
   const double* __restrict__ d = dir ? dir + (int64_t)frame * kDirStride : nullptr;
-  double acc[NA];
+  // RPC (VALU-bound pass B, c3): the transposed reduction, accumulators padded
+  // to its power of two (entries NA.. stay 0); the other models keep one
+  // wave_sum_f64 per accumulator (the transposed form raises their VGPRs:
+  // radtan 112 -> 138, and their pass B is latency-bound, not VALU-bound)
+  constexpr bool kTred = MVBA_PASSB_TRED && MODEL == kModelRpc;
+  constexpr int NACC = kTred ? TSum<NA>::P : NA;
+  double acc[NACC];
 #pragma unroll
-  for (int q = 0; q < NA; q++) acc[q] = 0.0;
+  for (int q = 0; q < NACC; q++) acc[q] = 0.0;
   const int nobs = __builtin_amdgcn_readfirstlane(c.y);
   for (int s0 = 0; s0 < nobs; s0 += 64) {
     if (lane < nobs - s0) {
@@ -988,11 +1093,43 @@ __global__ void __launch_bounds__(64) k_pass_b(
       for (int q = 0; q < RS::kIntr; q++) acc[6 + q] += I0[q] * u.x + I1[q] * u.y;
     }
   }
+  const FrameLin& L = fl[frame];
+  double* y = yrep + (int64_t)((chunk_base + ch) & (kVecReplicas - 1)) * ng;
+  if constexpr (kTred) {
+  // transposed wave sums: lane l holds the total of accumulator l >> S; the six
+  // Z^T u sums go to every lane through readlane, pose column k on lane k,
+  // intrinsic column q on the first lane holding accumulator 6 + q
+  {
+    constexpr int S = TSum<NA>::kShift;
+    const double tv = wave_sum_transpose<NA>(acc, lane);
+    double zs[6];
+#pragma unroll
+    for (int a = 0; a < 6; a++) zs[a] = readlane_f64(tv, a << S);
+    if (lane < kPoseCols) {
+      const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
+      const int b = (blk == 3) ? MVBA_BLK_OFFSET : blk;
+      if (L.goff[b] >= 0) {
+        const double* wk = rec + 12 + 6 * lane;
+        double v = 0.0;
+#pragma unroll
+        for (int a = 0; a < 6; a++) v += wk[a] * zs[a];
+        accumulate(y, L.goff[b] + (lane - 7 * blk), v, sl, chunk_base + ch, lane);
+      }
+    }
+    const int idx = lane >> S;
+    const int q = idx - 6;  // 0 focal, 1..2 center, 3.. distortion
+    if ((lane & ((1 << S) - 1)) == 0 && q >= 0 && q < RS::kIntr) {
+      int64_t dst = -1;
+      if (q == 0) dst = L.goff[MVBA_BLK_FOCAL];
+      else if (q < 3) dst = L.goff[MVBA_BLK_CENTER] >= 0 ? L.goff[MVBA_BLK_CENTER] + (q - 1) : -1;
+      else if (q - 3 < F.K) dst = L.goff[MVBA_BLK_DIST] >= 0 ? L.goff[MVBA_BLK_DIST] + (q - 3) : -1;
+      if (dst >= 0) accumulate(y, dst, tv, sl, chunk_base + ch, kPoseCols + q);
+    }
+  }
+  } else {
 #pragma unroll
   for (int q = 0; q < NA; q++) acc[q] = wave_sum_f64(acc[q]);
   // every lane holds the totals; lane k < 22 -> pose column k, 22.. -> intrinsics
-  const FrameLin& L = fl[frame];
-  double* y = yrep + (int64_t)((chunk_base + ch) & (kVecReplicas - 1)) * ng;
   int64_t dst = -1;
   double v = 0.0;
   if (lane < kPoseCols) {
@@ -1016,6 +1153,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     }
   }
   if (dst >= 0) accumulate(y, dst, v, sl, chunk_base + ch, lane);
+  }
   }
 }
 
@@ -1348,6 +1486,7 @@ __global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict
 // 3,000 pose blocks; profiles/r03/ab_block_prec/.)
 constexpr int kPrecLds = 88;  // 88^2 + 2 * 88 doubles = 62 KB: within the 64 KB of dynamic LDS a plain launch gets
 constexpr int kPrecThreads = 256;  // 4 waves per block share the elimination steps
+constexpr int kPrecSmall = 8;      // blocks up to this size: k_block_prec_small (one wave each)
 
 __device__ __forceinline__ void block_inverse_gj(int n, const double* __restrict__ H, const double* __restrict__ db,
                                                  double* __restrict__ A, double* colk, double* rowk) {
@@ -1421,11 +1560,12 @@ __global__ void __launch_bounds__(kPrecThreads) k_block_prec(int32_t nblocks, co
                                                    const int64_t* __restrict__ hoff,
                                                    const int32_t* __restrict__ bsize,
                                                    const double* __restrict__ hess, const double* __restrict__ d,
-                                                   double* __restrict__ minv) {
+                                                   double* __restrict__ minv, int32_t small_done) {
   extern __shared__ double Ls[];  // [n * n | pivot column | pivot row], or the pivot column and row of the wide path
   const int b = blockIdx.x;
   if (b >= nblocks) return;
   const int n = bsize[b];
+  if (n <= kPrecSmall && small_done) return;  // k_block_prec_small's
   const int lane = threadIdx.x;
   const double* H = hess + hoff[b];
   const double* db = d + goff[b];
@@ -1436,6 +1576,48 @@ __global__ void __launch_bounds__(kPrecThreads) k_block_prec(int32_t nblocks, co
   block_inverse_gj(n, H, db, Ls, Ls + n * n, Ls + n * n + n);
   double* M = minv + hoff[b];
   for (int e = lane; e < n * n; e += blockDim.x) M[e] = Ls[e];
+}
+
+// Blocks of at most 8 entries (poses, rig, offsets, focal, centre, radtan /
+// FOV distortion: every camera block of c2): one wave per block, lane 8 i + j
+// holds A[i][j] in a register and the n Gauss-Jordan steps of
+// block_inverse_gj (same formulas, same pivot rule) take the pivot row,
+// column and element by lane shuffles: no LDS staging, no block barriers.
+// A 256-thread workgroup per 7x7 block spent most of its ~14 us build in the
+// barrier-separated steps of mostly idle waves (profiles/r05/r05e/).
+__global__ void __launch_bounds__(256) k_block_prec_small(int32_t nblocks, const int64_t* __restrict__ goff,
+                                                          const int64_t* __restrict__ hoff,
+                                                          const int32_t* __restrict__ bsize,
+                                                          const double* __restrict__ hess,
+                                                          const double* __restrict__ d, double* __restrict__ minv) {
+  const int b = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (b >= nblocks) return;
+  const int n = bsize[b];
+  if (n > kPrecSmall) return;  // k_block_prec's
+  const int lane = threadIdx.x & 63, i = lane >> 3, j = lane & 7;
+  const bool act = i < n && j < n;
+  const double* H = hess + hoff[b];
+  double a = 0.0;
+  if (act) {
+    a = i >= j ? H[i * n + j] : H[j * n + i];  // the lower triangle as stored
+    if (i == j) a += d[goff[b] + i];
+  }
+  for (int k = 0; k < n; k++) {
+    const double colk = __shfl(a, (i << 3) + k, 64);
+    const double rowk = __shfl(a, (k << 3) + j, 64);
+    const double piv = __shfl(a, (k << 3) + k, 64);
+    const bool ok = piv > 1e-300;
+    const double ip = ok ? 1.0 / piv : 0.0;
+    const double rj = rowk * ip;
+    if (!ok) {
+      if (i == k || j == k) a = (i == j) ? 1.0 : 0.0;
+    } else if (j == k) {
+      a = (i == k) ? ip : -colk * ip;
+    } else {
+      a = (i == k) ? rj : a - colk * rj;
+    }
+  }
+  if (act) minv[hoff[b] + i * n + j] = a;
 }
 
 // ---- compact free-parameter vectors: [camera-side entries (layout order) | 3 per point]
@@ -1703,6 +1885,17 @@ hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int3
   return hipGetLastError();
 }
 
+hipError_t mvba_launch_point_w_seg(int32_t ntiles, const int4* tiles, const int32_t* wlane_pid,
+                                   const int32_t* wlane_idx, const int64_t* pt_begin, const int32_t* po_idx,
+                                   const double4* cbuf, const double* tinit, const double* V, const double* dp,
+                                   const double4* pts, double* wout, int32_t wstride, const int32_t* gate,
+                                   hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_point_w_seg, dim3(mvba::xcd_grid_solver((ntiles + 3) / 4)), dim3(256), 0, s, ntiles,
+                     tiles, wlane_pid, wlane_idx, pt_begin, po_idx, cbuf, tinit, V, dp, pts, wout, wstride, gate);
+  return hipGetLastError();
+}
+
 hipError_t mvba_launch_depth_pa(const mvba::Segment* segs, int32_t nseg, const mvba::DepthDesc* dd,
                                 const int32_t* dpid, const double4* dmeas, const double* frec, const double* params,
                                 const double4* pts, const double* dir, const double* xcam, double* du,
@@ -1821,11 +2014,18 @@ hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int6
                                   const int32_t* bsize, const double* hess, const double* d, double* minv,
                                   hipStream_t s) {
   if (nblocks <= 0) return hipSuccess;
+  // MVBA_PREC_SMALL=0: every block by the workgroup form (A/B timing)
+  static const bool small = !(std::getenv("MVBA_PREC_SMALL") && std::getenv("MVBA_PREC_SMALL")[0] == '0');
+  if (small) {
+    hipLaunchKernelGGL(mvba::k_block_prec_small, dim3((unsigned)((nblocks + 3) / 4)), dim3(256), 0, s, nblocks, goff,
+                       hoff, bsize, hess, d, minv);
+    if (max_bsize <= mvba::kPrecSmall) return hipGetLastError();
+  }
   const int m = max_bsize < mvba::kPrecLds ? max_bsize : mvba::kPrecLds;
   const size_t lds = sizeof(double) * (size_t)(m * m + 2 * m > 2 * max_bsize ? m * m + 2 * m : 2 * max_bsize);
   hipLaunchKernelGGL(mvba::k_block_prec, dim3((unsigned)nblocks), dim3(mvba::kPrecThreads), lds, s, nblocks, goff,
                      hoff, bsize, hess,
-                     d, minv);
+                     d, minv, small ? 1 : 0);
   return hipGetLastError();
 }
 

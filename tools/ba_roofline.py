@@ -31,7 +31,8 @@ SEQ = ["k_pass_a_frame", "k_point_w", "k_pass_b", "k_vec_rep_reduce", "k_cg_upda
 
 def short(name):
     name = re.sub(r"\(.*", "", name).replace("void ", "").replace("mvba::", "")
-    return re.sub(r"<.*", "", name).strip()
+    name = re.sub(r"<.*", "", name).strip()
+    return {"k_point_w_seg": "k_point_w"}.get(name, name)  # the point solve's tile form
 
 
 def trace_iterations(path):
@@ -40,12 +41,19 @@ def trace_iterations(path):
         for r in csv.DictReader(f):
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     ev.sort()
-    its = []
+    groups = []
     for i in range(1, len(ev) - len(SEQ) + 1):
         if [e[2] for e in ev[i:i + len(SEQ)]] != SEQ or ev[i - 1][2] == "k_frame_dir":
             continue
-        grp = ev[i:i + len(SEQ)]
-        if (grp[2][1] - grp[2][0]) / 1e3 < 8.0:  # gated
+        groups.append(ev[i:i + len(SEQ)])
+    if not groups:
+        return []
+    # gated iterations (past the CG stop) return at once: their pass B is a
+    # small fraction of a working one's (any chunking, any problem size)
+    pb_max = max((g[2][1] - g[2][0]) for g in groups)
+    its = []
+    for grp in groups:
+        if (grp[2][1] - grp[2][0]) < 0.4 * pb_max:
             continue
         its.append({"span_us": (grp[-1][1] - grp[0][0]) / 1e3,
                     **{k: (e[1] - e[0]) / 1e3 for k, e in zip(SEQ, grp)}})
