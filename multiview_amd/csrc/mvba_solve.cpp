@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <mutex>
 
 #include "mvba_internal.h"
 
@@ -172,7 +173,6 @@ struct SolverState {
   std::vector<CgGraph> graphs;
   std::vector<uintptr_t> graph_sig;
   bool graphs_broken = false;  // a capture failed: eager launches from then on
-  hipStream_t own_stream = nullptr;  // solves called on the null stream run here (capturable)
   hipEvent_t ev[2] = {nullptr, nullptr};  // the merged LM step's candidate-evaluation span
   void drop_graphs() {
     for (CgGraph& g : graphs)
@@ -192,7 +192,6 @@ void solver_state_free(SolverState* S) {
   if (S->hctl) (void)hipHostFree(S->hctl);
   S->b_det.release();
   S->drop_graphs();
-  if (S->own_stream) (void)hipStreamDestroy(S->own_stream);
   for (hipEvent_t e : S->ev)
     if (e) (void)hipEventDestroy(e);
   delete S;
@@ -865,7 +864,17 @@ class Solver {
     static const int second = std::getenv("MVBA_CG_BATCH2") ? std::max(1, std::atoi(std::getenv("MVBA_CG_BATCH2"))) : 2;
     int first = std::max(4, last_cg_iters_ - 2);
     const int imax = std::max(o_.max_linear_solver_iterations, 1);
-    static const int kGraphRun = std::getenv("MVBA_CG_GRAPH_RUN") ? std::max(1, std::min(10, std::atoi(std::getenv("MVBA_CG_GRAPH_RUN")))) : 10;
+    // graph run length: 10 (one run per reset period) for long solves, shorter
+    // runs (aligned to the period: 5, 2, 1) when the previous solve was short,
+    // so rounding a batch up to whole runs adds few gated iterations (a gated
+    // iteration still dispatches every block of its five launches: ~36 us at
+    // c3, whose solves take 3-8 CG iterations; profiles/r05/r05h/).
+    // MVBA_CG_GRAPH_RUN fixes it (A/B timing).
+    const int kGraphRun = [&] {
+      if (const char* e = std::getenv("MVBA_CG_GRAPH_RUN")) return std::max(1, std::min(10, std::atoi(e)));
+      const int last = std::max(last_cg_iters_, 1);
+      return last >= 20 ? 10 : last >= 10 ? 5 : last >= 4 ? 2 : 1;
+    }();
     if (use_graphs) first = (first + kGraphRun - 1) / kGraphRun * kGraphRun;
     for (int batch = first, nb = 0;; batch = (++nb == 1) ? second : 4) {
       if (use_graphs) batch = (batch + kGraphRun - 1) / kGraphRun * kGraphRun;
@@ -1485,6 +1494,24 @@ void mvba_solver_default_options(mvba_solver_options* o) {
   o->robust_threshold = 0.0;
 }
 
+// One non-blocking stream per device for solves called on the null stream,
+// created on first use and kept for the process's lifetime (handles come and go
+// per pass in the CLI; a stream per handle would be created and destroyed with
+// each, and the sanitizer build's runtime teardown trips over the freed queue
+// memory it still holds: profiles/r05/r05h/san_cli_g0_r05h.log).
+hipStream_t solver_stream(int device) {
+  static std::mutex m;
+  static std::vector<hipStream_t> streams;
+  std::lock_guard<std::mutex> lk(m);
+  if ((int)streams.size() <= device) streams.resize((size_t)device + 1, nullptr);
+  if (!streams[(size_t)device] &&
+      hipStreamCreateWithFlags(&streams[(size_t)device], hipStreamNonBlocking) != hipSuccess) {
+    streams[(size_t)device] = nullptr;
+    throw HipErr{hipErrorOutOfMemory, "hipStreamCreateWithFlags"};
+  }
+  return streams[(size_t)device];
+}
+
 mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver_summary* summary,
                        void* stream) {
   if (!h || !o || !summary) return MVBA_E_INVALID;
@@ -1504,11 +1531,10 @@ mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver
     // (single-rank solves only: sharded ones keep the caller's stream, and a
     // device-wide sync could wait on a peer shard's pending exchange)
     hipStream_t st = (hipStream_t)stream;
-    if (!st && !o->allreduce) {
-      if (!h->solver->own_stream)
-        HCHK(hipStreamCreateWithFlags(&h->solver->own_stream, hipStreamNonBlocking));
+    static const bool own = !(std::getenv("MVBA_OWN_STREAM") && std::getenv("MVBA_OWN_STREAM")[0] == '0');
+    if (!st && !o->allreduce && own) {
       HCHK(hipDeviceSynchronize());
-      st = h->solver->own_stream;
+      st = solver_stream(h->device);
     }
     Solver sv(h, *o, st);
     // K2 writes the CG passes' per-slot records for the duration of the solve
