@@ -349,9 +349,23 @@ struct Proj {
   double df0, df1;         // total d(d)/d(f)
   double m0, m1, r2;       // FOV / RADTAN: u / f, |u/f|^2
   double aux0, aux1, aux2, aux3;  // FOV: f dconv/dw; RPC: 1/Dx, 1/Dy, Nx/Dx, Ny/Dy
+  double iz;               // 1 / Xc[2] (FAST projections only)
 };
 
-template <int MODEL, int DEG>
+// f / Xc[2] * s: the division as the reference writes it, or (FAST) by the
+// reciprocal the FAST projection already took
+template <bool FAST>
+__device__ __forceinline__ double fz_of(double f, const Proj& o, double s) {
+  if constexpr (FAST) return f * o.iz * s;
+  else return f / o.Xc[2] * s;
+}
+
+// FAST (the CG passes only: their rows feed inner products, never a residual
+// or Jacobian an API returns): one reciprocal instead of the reference's
+// divisions, u / f taken as X.hnormalized() itself, RPC quotients by the
+// denominators' reciprocals. Each fp64 division is a ~12-instruction sequence;
+// pass B at c2 issued 6 per observation. Results differ by rounding only.
+template <int MODEL, int DEG, bool FAST = false>
 __device__ __forceinline__ void project(const double* __restrict__ rec, double X0, double X1, double X2,
                                         double f, double c0, double c1, const double* __restrict__ kd,
                                         int K, double h0, double h1, Proj& o) {
@@ -360,8 +374,14 @@ __device__ __forceinline__ void project(const double* __restrict__ rec, double X
   o.Xc[1] = rec[3] * X0 + rec[4] * X1 + rec[5] * X2 + rec[10];
   o.Xc[2] = rec[6] * X0 + rec[7] * X1 + rec[8] * X2 + rec[11];
   // u = f .* X.hnormalized() (:473)
-  o.nx = o.Xc[0] / o.Xc[2];
-  o.ny = o.Xc[1] / o.Xc[2];
+  if constexpr (FAST) {
+    o.iz = 1.0 / o.Xc[2];
+    o.nx = o.Xc[0] * o.iz;
+    o.ny = o.Xc[1] * o.iz;
+  } else {
+    o.nx = o.Xc[0] / o.Xc[2];
+    o.ny = o.Xc[1] / o.Xc[2];
+  }
   const double u0 = f * o.nx, u1 = f * o.ny;
   o.u0 = u0;
   o.u1 = u1;
@@ -378,7 +398,7 @@ __device__ __forceinline__ void project(const double* __restrict__ rec, double X
     const double w = kd[0];
     const double tw2 = tan(0.5 * w);
     const double pc1 = 1.0 / w, pc2 = 2.0 * tw2;
-    const double m0 = u0 / f, m1 = u1 / f;
+    const double m0 = FAST ? o.nx : u0 / f, m1 = FAST ? o.ny : u1 / f;
     const double ru = sqrt(m0 * m0 + m1 * m1);
     const double a = ru * pc2;
     const double at = atan(a);
@@ -402,7 +422,7 @@ __device__ __forceinline__ void project(const double* __restrict__ rec, double X
     // camera_params.cc:282-308 (Tsai)
     const double k1 = kd[0], k2 = kd[1], p1 = kd[2], p2 = kd[3];
     const double k3 = (K == 5) ? kd[4] : 0.0;
-    const double m0 = u0 / f, m1 = u1 / f;
+    const double m0 = FAST ? o.nx : u0 / f, m1 = FAST ? o.ny : u1 / f;
     const double r2 = m0 * m0 + m1 * m1;
     const double radial = 1.0 + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2;
     double e0 = radial * m0, e1 = radial * m1;
@@ -446,9 +466,14 @@ __device__ __forceinline__ void project(const double* __restrict__ rec, double X
         }
       }
     }
-    o.d0 = N[0] / N[1] + h0;
-    o.d1 = N[2] / N[3] + h1;
     const double iDx = 1.0 / N[1], iDy = 1.0 / N[3];
+    if constexpr (FAST) {
+      o.d0 = N[0] * iDx + h0;
+      o.d1 = N[2] * iDy + h1;
+    } else {
+      o.d0 = N[0] / N[1] + h0;
+      o.d1 = N[2] / N[3] + h1;
+    }
     const double qx = N[0] * iDx, qy = N[2] * iDy;
     o.A00 = (Nx_[0] - qx * Nx_[1]) * iDx; o.A01 = (Ny_[0] - qx * Ny_[1]) * iDx;
     o.A10 = (Nx_[2] - qy * Nx_[3]) * iDy; o.A11 = (Ny_[2] - qy * Ny_[3]) * iDy;

@@ -174,6 +174,7 @@ struct SolverState {
   std::vector<uintptr_t> graph_sig;
   bool graphs_broken = false;  // a capture failed: eager launches from then on
   hipEvent_t ev[2] = {nullptr, nullptr};  // the merged LM step's candidate-evaluation span
+  hipEvent_t ev_cg[2] = {nullptr, nullptr};  // the CG's pipelined batches
   void drop_graphs() {
     for (CgGraph& g : graphs)
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
@@ -193,6 +194,8 @@ void solver_state_free(SolverState* S) {
   S->b_det.release();
   S->drop_graphs();
   for (hipEvent_t e : S->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : S->ev_cg)
     if (e) (void)hipEventDestroy(e);
   delete S;
 }
@@ -262,7 +265,9 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->scal, 32));
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hscal), 32 * sizeof(double)));
     HCHK(hipMalloc(reinterpret_cast<void**>(&S->ctl), sizeof(mvba::CgCtl)));
-    HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hctl), sizeof(mvba::CgCtl)));
+    // [0]: the solve's initial control block (H2D source); [1], [2]: the
+    // pipelined batches' read-backs
+    HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hctl), 3 * sizeof(mvba::CgCtl)));
     std::vector<int32_t> bs(S->nblocks);
     for (int32_t k = 0; k < S->nblocks; k++) {
       const int32_t bid = h->cam_block_ids[k];
@@ -282,6 +287,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(upload(&S->hoff, h->cam_hoff));
     HCHK(upload(&S->cam_poff, h->cam_poff));
     for (hipEvent_t& e : S->ev) HCHK(hipEventCreate(&e));
+    for (hipEvent_t& e : S->ev_cg) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   } catch (...) {
     solver_state_free(S);
     throw;
@@ -873,10 +879,17 @@ class Solver {
     const int kGraphRun = [&] {
       if (const char* e = std::getenv("MVBA_CG_GRAPH_RUN")) return std::max(1, std::min(10, std::atoi(e)));
       const int last = std::max(last_cg_iters_, 1);
-      return last >= 20 ? 10 : last >= 10 ? 5 : last >= 4 ? 2 : 1;
+      return last >= 40 ? 10 : last >= 10 ? 5 : last >= 4 ? 2 : 1;
     }();
     if (use_graphs) first = (first + kGraphRun - 1) / kGraphRun * kGraphRun;
-    for (int batch = first, nb = 0;; batch = (++nb == 1) ? second : 4) {
+    // Pipelined batches: the next batch is enqueued before the host waits for
+    // the previous one's control block (a pinned copy per batch, read after its
+    // event), so the GPU never idles through the host's turnaround; a stop seen
+    // in batch k leaves batch k + 1 to run as gated no-ops. MVBA_CG_PIPE=0: one
+    // batch at a time (enqueue, stream sync, read).
+    const char* pipe_env = std::getenv("MVBA_CG_PIPE");  // read per call
+    const bool pipelined = !(pipe_env && pipe_env[0] == '0');
+    auto enqueue_batch = [&](int batch, int slot) {
       if (use_graphs) batch = (batch + kGraphRun - 1) / kGraphRun * kGraphRun;
       const double tb0 = now_s();
       if (cg_timing()) tm_.batches++;
@@ -899,16 +912,36 @@ class Solver {
       } else {
         for (; i < iend; i++) body(i);
       }
-      const double tb1 = now_s();
-      HCHK(hipMemcpyAsync(S_->hctl, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
-      HCHK(hipStreamSynchronize(s_));
-      if (cg_timing()) {
-        tm_.enqueue += tb1 - tb0;
-        tm_.wait += now_s() - tb1;
+      HCHK(hipMemcpyAsync(S_->hctl + slot, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
+      HCHK(hipEventRecord(S_->ev_cg[slot - 1], s_));
+      if (cg_timing()) tm_.enqueue += now_s() - tb0;
+    };
+    auto wait_batch = [&](int slot) -> const mvba::CgCtl& {
+      const double tw = now_s();
+      HCHK(hipEventSynchronize(S_->ev_cg[slot - 1]));
+      if (cg_timing()) tm_.wait += now_s() - tw;
+      return S_->hctl[slot];
+    };
+    int slot = 1;
+    enqueue_batch(first, slot);
+    const mvba::CgCtl* last = nullptr;
+    for (int nb = 0;;) {
+      const int next = 3 - slot;
+      bool ahead = false;
+      if (pipelined && i <= imax) {
+        enqueue_batch((++nb == 1) ? second : 4, next);
+        ahead = true;
       }
-      if (S_->hctl->done) break;
-      if (i > imax) break;  // not reached: the device stops at max_iter
+      last = &wait_batch(slot);
+      if (last->done) break;
+      if (i > imax) {  // every iteration is enqueued: the newest batch's state is final (stopped at max_iter)
+        if (ahead) last = &wait_batch(next);
+        break;
+      }
+      if (!ahead) enqueue_batch((++nb == 1) ? second : 4, next);
+      slot = next;
     }
+    *S_->hctl = *last;
     R.iters = S_->hctl->iters;
     R.status = S_->hctl->status;
     last_cg_iters_ = R.iters;

@@ -14,6 +14,14 @@
 
 namespace mvba {
 
+// the CG passes' projection with reciprocals instead of the reference's
+// divisions (project<..., FAST>, mvba_device.h); MVBA_FAST_PROJ=0 builds the
+// divisions (A/B builds)
+#ifndef MVBA_FAST_PROJ
+#define MVBA_FAST_PROJ 1
+#endif
+constexpr bool kFastProj = MVBA_FAST_PROJ;
+
 constexpr int kDirStride = 128;    // per-frame direction record: u (6) | x_intr (<= 122: RPC degree 6 has 113)
 #ifndef MVBA_VEC_REPLICAS
 #define MVBA_VEC_REPLICAS 32
@@ -34,7 +42,7 @@ __device__ __forceinline__ void obs_rows(const FrameDesc& F, const double* __res
   const double c0 = params[F.off[MVBA_BLK_CENTER]];
   const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
   Proj o;
-  project<MODEL, DEG>(rec, X0, X1, X2, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+  project<MODEL, DEG, kFastProj>(rec, X0, X1, X2, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
   double sr = sr_given;
   if (sr < 0.0) {
     const double r0 = o.d0 - meas.x, r1 = o.d1 - meas.y;
@@ -42,7 +50,7 @@ __device__ __forceinline__ void obs_rows(const FrameDesc& F, const double* __res
     r[0] = r0 * sr;
     r[1] = r1 * sr;
   }
-  const double fz = f / o.Xc[2] * sr;
+  const double fz = fz_of<kFastProj>(f, o, sr);
   const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
   const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
   double a0[3], a1[3];
@@ -258,10 +266,10 @@ __device__ __forceinline__ void pass_a_obs(const double* __restrict__ rec, const
   const double f = rec[12];
   const int K = (int)rec[17];
   Proj o;
-  project<MODEL, DEG>(rec, X.x, X.y, X.z, f, rec[13], rec[14], rec + 18, K, rec[15], rec[16], o);
+  project<MODEL, DEG, kFastProj>(rec, X.x, X.y, X.z, f, rec[13], rec[14], rec + 18, K, rec[15], rec[16], o);
   double hr;
   const double sr = sr_given >= 0.0 ? sr_given : loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
-  const double fz = f / o.Xc[2] * sr;
+  const double fz = fz_of<kFastProj>(f, o, sr);
   const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
   const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
 #pragma unroll
@@ -840,7 +848,8 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
           const double4 w = wbuf[pid];
           const double4 X = obsX ? obsX[i] : pts[pid];
           Proj o;
-          project<MODEL, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+          project<MODEL, DEG, kFastProj>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1,
+                                    o);
           double hr;
           double sr;
           if (obsX) {
@@ -849,7 +858,7 @@ __device__ __forceinline__ void pass_b_wide(int4 c, int32_t chunk_id, const Segm
             const double2 m = obs_meas[i];
             sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
           }
-          const double fz = f / o.Xc[2] * sr;
+          const double fz = fz_of<kFastProj>(f, o, sr);
           const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
           const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
           double a0[3], a1[3];
@@ -943,13 +952,13 @@ __device__ __forceinline__ void pass_b_rpc_obs(const FrameDesc& F, const double*
   const double c0 = params[F.off[MVBA_BLK_CENTER]];
   const double c1 = params[F.off[MVBA_BLK_CENTER] + 1];
   Proj o;
-  project<kModelRpc, DEG>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
+  project<kModelRpc, DEG, kFastProj>(rec, X.x, X.y, X.z, f, c0, c1, params + F.off[MVBA_BLK_DIST], F.K, F.h0, F.h1, o);
   double sr = sr_given;
   if (sr < 0.0) {
     double hr;
     sr = loss_scale(o.d0 - m.x, o.d1 - m.y, flags, cauchy_c, &hr);
   }
-  const double fz = f / o.Xc[2] * sr;
+  const double fz = fz_of<kFastProj>(f, o, sr);
   const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
   const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
   double a0[3], a1[3];
@@ -1021,7 +1030,9 @@ __device__ __forceinline__ void pass_b_rpc_obs(const FrameDesc& F, const double*
 // w_k to the pose columns (y_k = w_k . (Z^T u)) and add pose + intrinsic columns
 // into replica (chunk mod kVecReplicas) of the camera-side vector.
 template <int MODEL, int DEG>
-__global__ void __launch_bounds__(64) k_pass_b(
+// (min waves per EU: keeps radtan / none within 128 VGPRs under the 128-thread
+// bound, as under the old 64-thread one; FOV needs ~155, RPC more)
+__global__ void __launch_bounds__(128, MODEL == kModelRpc ? 1 : MODEL == kModelFov ? 3 : 4) k_pass_b(
     const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
     const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
     const double* __restrict__ frec, const double* __restrict__ params,
@@ -1031,7 +1042,7 @@ __global__ void __launch_bounds__(64) k_pass_b(
     const int32_t* __restrict__ gate, Slab sl, const double4* __restrict__ obsX) {
   using RS = RowShape<MODEL, DEG>;
   constexpr int NA = 6 + RS::kIntr;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int ch = (int)xcd_block_solver(nchunks);
   if (ch < 0 || (gate && *gate)) return;
   if constexpr (NA > kPassBRegCols) {
@@ -1054,7 +1065,11 @@ __global__ void __launch_bounds__(64) k_pass_b(
 #pragma unroll
   for (int q = 0; q < NACC; q++) acc[q] = 0.0;
   const int nobs = __builtin_amdgcn_readfirstlane(c.y);
-  for (int s0 = 0; s0 < nobs; s0 += 64) {
+  // 1 or 2 waves per chunk (blockDim; the launcher's choice): with 2, wave w
+  // takes segments w, w + 2, ... and wave 1 hands its per-lane accumulators to
+  // wave 0 through LDS before the one reduction + atomics of the chunk
+  const int nw = (int)(blockDim.x >> 6), wv = (int)(threadIdx.x >> 6);
+  for (int s0 = 64 * wv; s0 < nobs; s0 += 64 * nw) {
     if (lane < nobs - s0) {
       const int64_t i = (int64_t)c.x + s0 + lane;
       const int32_t pid = obs_pid[i];
@@ -1091,6 +1106,18 @@ __global__ void __launch_bounds__(64) k_pass_b(
       for (int a = 0; a < 6; a++) acc[a] += Z0[a] * u.x + Z1[a] * u.y;
 #pragma unroll
       for (int q = 0; q < RS::kIntr; q++) acc[6 + q] += I0[q] * u.x + I1[q] * u.y;
+    }
+  }
+  if constexpr (MODEL != kModelRpc) {
+    __shared__ double comb[NA][64];
+    if (nw > 1) {
+      if (wv == 1)
+#pragma unroll
+        for (int q = 0; q < NA; q++) comb[q][lane] = acc[q];
+      __syncthreads();
+      if (wv == 1) return;
+#pragma unroll
+      for (int q = 0; q < NA; q++) acc[q] += comb[q][lane];
     }
   }
   const FrameLin& L = fl[frame];
@@ -1925,8 +1952,15 @@ hipError_t mvba_launch_pass_b(int model, int deg, const int4* chunks, int32_t nc
                               int64_t ng, int32_t flags, double cauchy_c, const int32_t* gate, mvba::Slab sl,
                               const double4* obsX, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
+  // two waves per chunk for the register-accumulator models other than RPC
+  // (latency-bound pass B: more waves to cover the gathers, one reduction);
+  // RPC (VALU-bound at c3) and the wide rows keep one. MVBA_PASSB_WAVES=1|2
+  // (read per call) forces it for the non-RPC models (A/B timing).
+  const char* pw = std::getenv("MVBA_PASSB_WAVES");
+  const unsigned pb_threads = (model != mvba::kModelRpc && !(pw && pw[0] == '1')) ? 128u : 64u;
 #define MVBA_PB(M, D)                                                                                       \
-  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3(mvba::xcd_grid_solver(nchunks)), dim3(64),                    \
+  hipLaunchKernelGGL((mvba::k_pass_b<M, D>), dim3(mvba::xcd_grid_solver(nchunks)),                            \
+                     dim3(M == mvba::kModelRpc ? 64u : pb_threads),                                           \
                      (mvba::pass_b_lds<M, D>()), s,                                                           \
                      chunks, nchunks,                                                                         \
                      chunk_base, segs, fd, (const mvba::FrameLin*)fl, frec, params, pts, obs_pid, obs_meas,     \
