@@ -882,13 +882,16 @@ class Solver {
       return last >= 40 ? 10 : last >= 10 ? 5 : last >= 4 ? 2 : 1;
     }();
     if (use_graphs) first = (first + kGraphRun - 1) / kGraphRun * kGraphRun;
-    // Pipelined batches: the next batch is enqueued before the host waits for
-    // the previous one's control block (a pinned copy per batch, read after its
-    // event), so the GPU never idles through the host's turnaround; a stop seen
-    // in batch k leaves batch k + 1 to run as gated no-ops. MVBA_CG_PIPE=0: one
-    // batch at a time (enqueue, stream sync, read).
+    // Pipelined batches (MVBA_CG_PIPE=1, read per call): the next batch is
+    // enqueued before the host waits for the previous one's control block (a
+    // pinned copy per batch, read after its event), so the GPU does not idle
+    // through the host's turnaround, but a stop seen in batch k leaves batch
+    // k + 1 to run as gated no-ops ahead of the back-substitution. Same box
+    // (profiles/r05/r05k/): CG loop 42.5 vs 42.2 us per iteration (1/8 c2
+    // shard), 73.6 vs 74.0 (c2), back-substitution +46 / +64 us per solve
+    // behind the gated batch: not the default.
     const char* pipe_env = std::getenv("MVBA_CG_PIPE");  // read per call
-    const bool pipelined = !(pipe_env && pipe_env[0] == '0');
+    const bool pipelined = pipe_env && pipe_env[0] == '1';
     auto enqueue_batch = [&](int batch, int slot) {
       if (use_graphs) batch = (batch + kGraphRun - 1) / kGraphRun * kGraphRun;
       const double tb0 = now_s();

@@ -183,9 +183,12 @@ def test_single_observation_points_and_frames():
         assert "Function tolerance reached" in s["message"]
         assert np.isclose(s["final_cost"], s_ref["final_cost"], rtol=1e-6), (s["final_cost"], s_ref["final_cost"])
         conv[det] = s
+        print(f"deterministic={det}, function_tolerance 1e-9: {s['num_iterations']} LM iterations, "
+              f"cost {s['final_cost']:.10g} (CPU LM {s_ref['final_cost']:.10g}, {s_ref['iterations']} iterations)")
     runs = [_solve(P, 1, 400, **TOL) for _ in range(2)]
     c1 = conv[1]
     for s, _ in runs:
+        print(f"tolerance 1e-16: {s['num_iterations']} LM iterations ({s['message']}), cost {s['final_cost']:.10g}")
         assert s["num_iterations"] >= c1["num_iterations"], (s["num_iterations"], c1["num_iterations"])
         assert s["num_successful_steps"] >= c1["num_successful_steps"]
         assert s["final_cost"] <= c1["final_cost"], (s["final_cost"], c1["final_cost"])

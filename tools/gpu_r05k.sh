@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
 TAG=${1:-r05k}
-timeout -k 10 500 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread tests/test_solver_gpu.py tests/test_solver_forms_gpu.py tests/test_deterministic_gpu.py tests/test_edge_cases.py > $OUT/pytest_solver_$TAG.log 2>&1
+timeout -k 10 500 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread tests/test_solver_gpu.py tests/test_solver_forms_gpu.py tests/test_deterministic_gpu.py tests/test_edge_cases.py -s > $OUT/pytest_solver_$TAG.log 2>&1
 rc=$?; echo "pytest rc $rc"; tail -3 $OUT/pytest_solver_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 bash tools/gpu_kt_r05.sh $TAG "c2 s8" "w2=MVBA_PASSB_WAVES=2 w1=MVBA_PASSB_WAVES=1" || exit 1
@@ -30,3 +30,17 @@ for cfg in s8 c2; do
   done
 done
 timeout -k 10 300 python tools/c3_alloc_probe.py 5 > $OUT/c3_alloc_$TAG.log 2>&1; tail -7 $OUT/c3_alloc_$TAG.log
+# K2 waves per frame part: same-box A/B (tools/ab/flin1, flin4 = -DMVBA_FLIN_WAVES=1 / 4; the tree: 2)
+for k in 1 2; do
+  for v in cur flin1 flin4; do
+    if [ $v = cur ]; then unset MVBA_LIB; else export MVBA_LIB=$PWD/tools/ab/$v/libmvba.so; fi
+    timeout -k 10 300 python bench.py --steps 200 --no-cpu-baseline --mesh-subdiv 0 --ba-iters 0 > $OUT/lin_${v}_${k}_$TAG.log 2>&1 || exit 1
+    echo "lin $v $k: $(python3 -c "
+import json,sys
+for l in open('$OUT/lin_${v}_${k}_$TAG.log'):
+    if l.startswith('{'):
+        d=json.loads(l); L=d.get('linearize',{}); print('kernel_ms', round(L.get('kernel_ms',0)*1e3,1), 'records_current', round(L.get('kernel_ms_records_current',0)*1e3,1), 'mfma util', round(L.get('mfma',{}).get('util',0),3))
+")"
+  done
+done
+unset MVBA_LIB
