@@ -96,7 +96,7 @@ hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, con
                              hipStream_t s);
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, unsigned* counter, double* out,
                            hipStream_t s);
-hipError_t mvba_launch_sum(int64_t n, const double* partial, double* out, hipStream_t s);
+hipError_t mvba_launch_sum(int64_t n, double* partial, double* out, hipStream_t s);
 hipError_t mvba_launch_block_prec(int32_t nblocks, int32_t max_bsize, const int64_t* goff, const int64_t* hoff,
                                   const int32_t* bsize, const double* hess, const double* d, double* minv,
                                   hipStream_t s);
@@ -260,7 +260,8 @@ SolverState* alloc_state(mvba_handle* h) {
     // k_cg_update: 3 partials per 256-entry block; k_vec_rep_reduce / k_add_diag one
     S->npartial = std::max<int64_t>({3072, 3 * ((S->ng + 255) / 256), S->ng + 1, mvba_pass_a_blocks(S->np), ncost,
                                     (h->nsegs + 3) / 4,
-                                    (int64_t)h->ndep_segs, (h->ndep_slots + 255) / 256});
+                                    (int64_t)h->ndep_segs, (h->ndep_slots + 255) / 256}) +
+                   1024;  // mvba_launch_sum's second level sits behind the first's partials
     HCHK(dalloc(&S->partial, (size_t)S->npartial));
     HCHK(dalloc(&S->scal, 32));
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hscal), 32 * sizeof(double)));

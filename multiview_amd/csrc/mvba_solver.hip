@@ -1501,6 +1501,23 @@ __global__ void __launch_bounds__(256) k_sum(int64_t n, const double* __restrict
   if (threadIdx.x == 0) out[0] = red[0];
 }
 
+// First level of a two-level deterministic sum: block b adds partial[b per ..
+// (b + 1) per) in a fixed order (thread-strided, then a fixed tree) into out[b]
+__global__ void __launch_bounds__(256) k_sum_level(int64_t n, int64_t per, const double* __restrict__ partial,
+                                                   double* __restrict__ out) {
+  __shared__ double red[256];
+  const int64_t b0 = (int64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+  double acc = 0.0;
+  for (int64_t e = b0 + threadIdx.x; e < b1; e += 256) acc += partial[e];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
 // Block-Jacobi preconditioner (Ceres' JACOBI for ITERATIVE_SCHUR [ext]:
 // blocks of F'F + D^2): one workgroup (one wave) per camera block inverts
 // H_bb + diag(d) explicitly by Gauss-Jordan elimination (symmetric positive
@@ -2031,16 +2048,31 @@ hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, con
   return hipGetLastError();
 }
 
-// dot(x, y) -> out (device scalar) via partials[256] and a counter (zero, re-armed)
+// dot(x, y) -> out (device scalar) via partials[<= 2048] and a counter (zero,
+// re-armed). Blocks: about 4 elements per thread, at most 2048 (the round-4
+// fixed 256 blocks left one wave per SIMD: c3's 3M-entry point-side dots took
+// 14.6 us each, profiles/r05/r05k/)
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, unsigned* counter,
                            double* out, hipStream_t s) {
-  const int blocks = 256;
+  const int64_t want = (n + 1023) / 1024;
+  const int blocks = (int)(want < 1 ? 1 : want > 2048 ? 2048 : want);
   hipLaunchKernelGGL(mvba::k_dot_fin, dim3(blocks), dim3(256), 0, s, n, x, y, partial, counter, out);
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_sum(int64_t n, const double* partial, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(mvba::k_sum, dim3(1), dim3(256), 0, s, n, partial, out);
+// out[0] = sum partial[0..n) in a fixed order; past 4096 partials in two levels
+// (blocks of n / 1024+ partials into partial[n ..], then one block): the
+// partial array must hold n + 1024 entries. One block over c3's 39k cost
+// partials took 40.7 us (profiles/r05/r05k/).
+hipError_t mvba_launch_sum(int64_t n, double* partial, double* out, hipStream_t s) {
+  if (n <= 4096) {
+    hipLaunchKernelGGL(mvba::k_sum, dim3(1), dim3(256), 0, s, n, partial, out);
+    return hipGetLastError();
+  }
+  const int64_t nb2 = std::min<int64_t>(1024, (n + 4095) / 4096);
+  const int64_t per = (n + nb2 - 1) / nb2;
+  hipLaunchKernelGGL(mvba::k_sum_level, dim3((unsigned)nb2), dim3(256), 0, s, n, per, partial, partial + n);
+  hipLaunchKernelGGL(mvba::k_sum, dim3(1), dim3(256), 0, s, nb2, partial + n, out);
   return hipGetLastError();
 }
 
@@ -2113,8 +2145,10 @@ hipError_t mvba_launch_plus(int64_t n, const double* x, const double* delta, con
 
 hipError_t mvba_launch_proj_grad_max(int64_t n, const double* x, const double* g, const double* lower,
                                      const double* upper, double* partial, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(mvba::k_proj_grad_max, dim3(256), dim3(256), 0, s, n, x, g, lower, upper, partial);
-  hipLaunchKernelGGL(mvba::k_max, dim3(1), dim3(256), 0, s, (int64_t)256, partial, out);
+  const int64_t want = (n + 1023) / 1024;
+  const int blocks = (int)(want < 1 ? 1 : want > 2048 ? 2048 : want);
+  hipLaunchKernelGGL(mvba::k_proj_grad_max, dim3(blocks), dim3(256), 0, s, n, x, g, lower, upper, partial);
+  hipLaunchKernelGGL(mvba::k_max, dim3(1), dim3(256), 0, s, (int64_t)blocks, partial, out);
   return hipGetLastError();
 }
 
