@@ -604,7 +604,13 @@ typedef struct mvba_solver_summary {
 } mvba_solver_summary;
 
 void mvba_solver_default_options(mvba_solver_options* o);
-/* Runs LM from the handle's current parameters (mvba_set_params first). */
+/* Runs LM from the handle's current parameters (mvba_set_params first).
+ * Host-synchronous: returns when the solve is done. hip_stream: the stream the
+ * solve runs on. NULL with a single-rank solve (allreduce NULL): the library
+ * waits for all earlier device work (hipDeviceSynchronize) and runs on its own
+ * per-device stream, whose CG iterations it can capture and replay as graphs
+ * (the null stream cannot be captured). NULL with a sharded solve: the null
+ * stream itself. */
 mvba_status mvba_solve(struct mvba_handle* h, const mvba_solver_options* o, mvba_solver_summary* summary,
                        void* hip_stream);
 /* Copy the handle's current packed parameter vector to host memory. */

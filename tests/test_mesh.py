@@ -264,24 +264,38 @@ def test_depth_mesh_linearize_parity(oracle, apply_loss):
 @pytest.mark.gpu
 def test_depth_mesh_one_exact_step_matches_dense_lm():
     """Mesh blocks (camera-side rows only, their fixed point never moves) and
-    mesh_tri priors in the implicit Schur product: one exact-CG LM step equals
-    the dense step; the mesh points are untouched."""
+    mesh_tri priors in the implicit Schur product: one CG LM step (eta =
+    1e-14) against the CPU's exact step of the same damped, Jacobi-scaled
+    normal equations (residual <= 1e-8, error <= kappa x residual, every
+    parameter within 1e-6; tests/test_solver_forms_gpu.py's check); the
+    constant parameters (mesh points among them) are untouched.
+
+    Deterministic mode: this system has kappa ~7e4 and Ceres' q-criterion
+    stops the CG at rounding stagnation (75-86 iterations here), so the
+    atomic path's stopping point moves with the order of its fp64 sums:
+    24 atomic-path runs of one binary gave relative residuals 5e-11 .. 4e-9
+    (tools/mesh_probe.py, profiles/r05/r05n/); a comparison with the dense
+    step at 1e-8 of max |x| failed on one run of r05m by that spread alone."""
     from oracle import lm_reference
-    from test_solver_gpu import TOL, _close, _free_mask
+    from test_solver_forms_gpu import _check_against_exact_step
+    from test_solver_gpu import TOL, _free_mask
 
     R = _sphere_rig(seed=21, num_ref=16, num_points=300)
     P = rig.build_problem(R, _mesh_flags(camera_poses_to_float=()), mesh_xyz=_oracle_mesh_xyz(R))
     assert (P.depth_blocks[:, 5] == -1).any() and (P.xyz_kind == 1).any()
+    m = _free_mask(P)
     for use_loss in (False, True):
-        x_ref, s_ref = lm_reference.solve(P, max_num_iterations=1, use_loss=use_loss, **TOL)
+        _, s_ref = lm_reference.solve(P, max_num_iterations=1, use_loss=use_loss, **TOL)
+        sysm = lm_reference.first_step_system(P, use_loss=use_loss, robust_threshold=3.0)
         with Evaluator(P) as ev:
             ev.set_params()
             s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=2000, use_loss=int(use_loss),
-                         robust_threshold=3.0, **TOL)
+                         robust_threshold=3.0, deterministic=1, **TOL)
             x = ev.get_params()
         assert np.isclose(s["initial_cost"], s_ref["initial_cost"], rtol=1e-11)
-        m = _free_mask(P)
-        assert _close(x[m], x_ref[m], 1e-8), (use_loss, np.abs(x[m] - x_ref[m]).max())
+        assert s["num_successful_steps"] == 1
+        _check_against_exact_step(sysm, x, f"mesh use_loss={use_loss}")
+        assert np.array_equal(x[~m], P.params[~m])
         assert x.size == P.params.size
 
 
