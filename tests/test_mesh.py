@@ -293,7 +293,7 @@ def test_depth_mesh_one_exact_step_matches_dense_lm():
                          robust_threshold=3.0, deterministic=1, **TOL)
             x = ev.get_params()
         assert np.isclose(s["initial_cost"], s_ref["initial_cost"], rtol=1e-11)
-        assert s["num_successful_steps"] == 1
+        assert s["num_successful_steps"] == 2  # iteration 0 + the accepted step (Ceres' count)
         _check_against_exact_step(sysm, x, f"mesh use_loss={use_loss}")
         assert np.array_equal(x[~m], P.params[~m])
         assert x.size == P.params.size

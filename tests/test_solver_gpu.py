@@ -537,7 +537,7 @@ def _rccl_world1_worker(port, out):
         P = rig.build_problem(rig.make_rig(**CFG), FLAGS)
         with Evaluator(P) as ev:
             ev.set_params()
-            s = ev.solve(max_num_iterations=20, comm=comm, **TOL)
+            s = ev.solve(max_num_iterations=100, comm=comm, **TOL)
             np.save(out, ev.get_params())
             np.save(out + ".cost.npy", np.array([s["final_cost"], s["termination_type"]]))
         comm.close()
@@ -550,7 +550,12 @@ def test_rccl_comm_world1_solve(tmp_path):
     child process: the communicator bench.py builds for N > 1 initialises from
     the torch.distributed-broadcast unique id, and a solve exchanging through it
     converges to the unsharded solve's point (the exchange is an identity at
-    world 1, so only the plumbing is under test)."""
+    world 1, so only the plumbing is under test). Both solves run to
+    convergence, like the sharded tests: the RCCL run takes the sharded
+    product form (p.q exchanged with the product) and the single-rank one the
+    atomic p.q, so their truncated CG steps differ by rounding, and a
+    comparison after 20 LM iterations (not yet converged) compares two points
+    of two trajectories (r05t, with a third p.q form: points > 1e-6 apart)."""
     import multiprocessing as mpc
     import socket
 
@@ -570,13 +575,13 @@ def test_rccl_comm_world1_solve(tmp_path):
     P = rig.build_problem(rig.make_rig(**CFG), FLAGS)
     with Evaluator(P) as ev:
         ev.set_params()
-        s_ref = ev.solve(max_num_iterations=20, **TOL)
+        s_ref = ev.solve(max_num_iterations=100, **TOL)
         P.params = ev.get_params()
         cam, pts = _cam_values(ev, P), _points_by_block(ev, P)
         P.params = np.load(out)
         cam_r, pts_r = _cam_values(ev, P), _points_by_block(ev, P)
     cost, term = np.load(out + ".cost.npy")
-    assert int(term) == s_ref["termination_type"]
+    assert int(term) == s_ref["termination_type"] == 0
     assert np.isclose(cost, s_ref["final_cost"], rtol=1e-9)
     # same tolerances as the sharded tests (normalised poses: |q| is a gauge direction)
     assert _close(cam_r, cam, 1e-6)
