@@ -504,6 +504,9 @@ __global__ void __launch_bounds__(256) k_pass_a(
 // segment per chunk: nothing is reduced per frame here, and 4x the waves of
 // the 4-segment chunks hide the point gathers better).
 constexpr int kPassAWaves = 4;
+#ifndef MVBA_PASSA_PIPE
+#define MVBA_PASSA_PIPE 1  // pipelined slot-record loads (-DMVBA_PASSA_PIPE=0: the plain loop, A/B)
+#endif
 template <int MODEL, int DEG>
 __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
     const int4* __restrict__ chunks, int32_t nchunks, const Segment* __restrict__ segs,
@@ -528,6 +531,26 @@ __global__ void __launch_bounds__(64 * kPassAWaves) k_pass_a_frame(
   double* d = sdir[threadIdx.x >> 6];
   const bool writer = dr.dp_out && c.w;
   stage_dir<ND>(dr, frame, d, writer);
+  if (obsX && MVBA_PASSA_PIPE && nobs > 64) {
+    // chunks of several segments (c3): the next 64 slot records loaded before
+    // this step's arithmetic (a software pipeline; c3 pass A 133 -> 127 us,
+    // profiles/r05/r05v/). One-segment chunks (c2) keep the plain loop: the
+    // pipelined form measured 1 us slower there (17.3 vs 16.3 us)
+    double4 Xn = lane < nobs ? obsX[c.x + lane] : make_double4(0.0, 0.0, 0.0, 0.0);
+    for (int s0 = 0; s0 < nobs; s0 += 64) {
+      const double4 X = Xn;
+      if (s0 + 64 < nobs && lane < nobs - s0 - 64) Xn = obsX[(int64_t)c.x + s0 + 64 + lane];
+      if (lane < nobs - s0) {
+        const int64_t i = (int64_t)c.x + s0 + lane;
+        double z[2], P0[3], P1[3];
+        pass_a_obs<MODEL, DEG>(rec, d, X, double2{0.0, 0.0}, flags, cauchy_c, z, P0, P1, X.w);
+        cbuf[slot_po ? (int64_t)slot_po[i] : i] = make_double4(P0[0] * z[0] + P1[0] * z[1],
+                                                               P0[1] * z[0] + P1[1] * z[1],
+                                                               P0[2] * z[0] + P1[2] * z[1], 0.0);
+      }
+    }
+    return;
+  }
   for (int s0 = 0; s0 < nobs; s0 += 64) {
     if (lane < nobs - s0) {
       const int64_t i = (int64_t)c.x + s0 + lane;
@@ -807,6 +830,9 @@ constexpr int kPassBRegCols = 48;  // register accumulators up to this many colu
 #ifndef MVBA_PASSB_TRED
 #define MVBA_PASSB_TRED 1
 #endif
+#ifndef MVBA_PASSB_PIPE
+#define MVBA_PASSB_PIPE 1  // RPC pass B: software-pipelined gathers (-DMVBA_PASSB_PIPE=0: the plain loop, A/B)
+#endif
 constexpr int kWideLd = 66;
 
 template <int MODEL, int DEG>
@@ -1069,6 +1095,33 @@ __global__ void __launch_bounds__(128, MODEL == kModelRpc ? 1 : MODEL == kModelF
   // takes segments w, w + 2, ... and wave 1 hands its per-lane accumulators to
   // wave 0 through LDS before the one reduction + atomics of the chunk
   const int nw = (int)(blockDim.x >> 6), wv = (int)(threadIdx.x >> 6);
+  if constexpr (MODEL == kModelRpc && MVBA_PASSB_PIPE) {
+    // RPC (VALU-heavy, 3 waves per SIMD: too few to hide the gathers, wait_frac
+    // 0.52 at c3, profiles/r04/ba_c3.json): a software pipeline over the
+    // chunk's 64-observation steps, the next step's slot record, point index
+    // and w_p loads issued before this step's arithmetic
+    int32_t pid_n = 0;
+    double4 w_n = make_double4(0.0, 0.0, 0.0, 0.0), X_n = w_n;
+    double2 m_n = make_double2(0.0, 0.0);
+    auto fetch = [&](int s) {
+      if (lane < nobs - s) {
+        const int64_t i = (int64_t)c.x + s + lane;
+        pid_n = obs_pid[i];
+        if (obsX) X_n = obsX[i];
+        else m_n = obs_meas[i];
+        w_n = wbuf[pid_n];
+        if (!obsX) X_n = pts[pid_n];
+      }
+    };
+    fetch(64 * wv);
+    for (int s0 = 64 * wv; s0 < nobs; s0 += 64 * nw) {
+      const bool act = lane < nobs - s0;
+      const double4 w = w_n, X = X_n;
+      const double2 m = m_n;
+      if (s0 + 64 * nw < nobs) fetch(s0 + 64 * nw);
+      if (act) pass_b_rpc_obs<DEG>(F, rec, params, X, m, flags, cauchy_c, obsX ? X.w : -1.0, d, w, acc);
+    }
+  } else
   for (int s0 = 64 * wv; s0 < nobs; s0 += 64 * nw) {
     if (lane < nobs - s0) {
       const int64_t i = (int64_t)c.x + s0 + lane;

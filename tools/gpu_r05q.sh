@@ -14,3 +14,5 @@ for k in 1 2; do
     echo "$v $k: $(python3 tools/bench_summary.py $OUT/c4eval_${v}_${k}_$TAG.log | tail -1 | cut -c1-160)"
   done
 done
+# c2 pass A with the pipelined loop gated to multi-segment chunks (tools/ab/pipe)
+REPS="1" bash tools/gpu_kt_r05.sh $TAG "c2" "cur=MVBA_CG_GRAPH=1 pipe=MVBA_LIB=$PWD/tools/ab/pipe/libmvba.so" || exit 1
