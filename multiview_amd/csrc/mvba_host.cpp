@@ -1009,17 +1009,25 @@ double mvba_eval_bytes(const mvba_handle* h, int32_t flags) {
 
 // Which launch form a full evaluation takes (MVBA_FORM_*); MVBA_SPLIT_PREP=1 /
 // MVBA_EVAL_MODE=split|fused|local force one, for A/B timing (read per call).
-// One model group: k_eval_local at every size. With frames in capture order it
-// measured faster than the fused form (K0 blocks handing records to the K1
-// waves) on the whole c2 (95.5-96.5 vs 100.9-101.5 us), equal on c3
-// (2.14-2.20 vs 2.17 ms), and faster on every shard of c2 (N = 2 / 4 / 8:
-// 53.0 / 28.0 / 17.9 vs 57.7 / 35.0 / 24.1 us), profiles/r04/r04o, r04p.
+// One model group: k_eval_local up to kLocalSegsPerFrame segments per frame.
+// With frames in capture order it measured faster than the fused form (K0
+// blocks handing records to the K1 waves) on the whole c2 (95.5-96.5 vs
+// 100.9-101.5 us), equal on c3 (2.14-2.20 vs 2.17 ms), and faster on every
+// shard of c2 (N = 2 / 4 / 8: 53.0 / 28.0 / 17.9 vs 57.7 / 35.0 / 24.1 us),
+// profiles/r04/r04o, r04p; and against the split form (prep launch + K1) c2
+// 95.7 vs 107.2 us, c3 2.14 vs 2.20 ms (profiles/r05/r05m/). Past that every
+// frame's K0 runs in too many waves: c4 (~39 segments per frame) split 6.66 /
+// 6.67 ms per step, local 7.58 / 7.62, fused 7.78 / 7.79 (same box,
+// profiles/r05/r05w/), so the split form takes over there (c3: ~17).
+static constexpr double kLocalSegsPerFrame = 24.0;
 static int eval_form(const mvba_handle* h) {
   const char* sp = std::getenv("MVBA_SPLIT_PREP");
   const char* m = std::getenv("MVBA_EVAL_MODE");
   const int forced = !m ? -1 : !std::strcmp(m, "split") ? 0 : !std::strcmp(m, "fused") ? 1 : !std::strcmp(m, "local") ? 2 : -1;
   if ((sp && sp[0] == '1') || forced == 0 || h->groups.size() != 1) return MVBA_FORM_SPLIT;
   if (forced > 0) return forced == 1 ? MVBA_FORM_FUSED : MVBA_FORM_LOCAL;
+  if (h->nframes > 0 && (double)h->groups[0].seg_count > kLocalSegsPerFrame * (double)h->nframes)
+    return MVBA_FORM_SPLIT;
   return MVBA_FORM_LOCAL;
 }
 

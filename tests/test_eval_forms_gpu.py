@@ -144,3 +144,31 @@ def test_every_form_matches_the_oracle(oracle, monkeypatch, npts, models, mode):
             assert np.all(np.abs(J[live] - Jo[live]) <= 1e-9 * cm[live])
             dead = ~live & np.isfinite(J)
             assert np.all(np.abs(J[dead]) <= 1e-9 * cm[dead])
+
+
+@pytest.mark.gpu
+def test_dense_frames_take_the_split_form(monkeypatch):
+    """Past 24 segments (1,536 observations) per frame the default form is the
+    split one (prep launch + K1: c4's ~39 segments per frame measured 12 %
+    faster than k_eval_local, profiles/r05/r05w/), and it writes the same
+    planes as the forced one-launch form."""
+    import torch
+
+    R = rig.make_rig(num_sensors=1, num_ref=4, num_points=3000, obs_per_point=3, seed=9)
+    P = rig.build_problem(R)
+    outs = []
+    for mode in (None, "local"):
+        if mode:
+            monkeypatch.setenv("MVBA_EVAL_MODE", mode)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            assert ev.num_residuals > 24 * 64 * ev.num_frames
+            assert ev.eval_form() == (_lib.FORM_LOCAL if mode else _lib.FORM_SPLIT)
+            res = torch.full((2, ev.ld), float("nan"), dtype=torch.float64, device="cuda")
+            jac = torch.full((ev.stride, ev.ld), float("nan"), dtype=torch.float64, device="cuda")
+            ev.evaluate_device(True, residuals=res, jac=jac, ld=ev.ld)
+            torch.cuda.synchronize()
+            ev.sync()
+            outs.append((res.cpu().numpy(), jac.cpu().numpy()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])

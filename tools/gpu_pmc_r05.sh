@@ -33,7 +33,8 @@ for CFG in ${PMC_CFGS:-c2 c3 c4 c5}; do
   WR=$(find $D/write -name '*counter_collection.csv' | head -1)
   python3 tools/pmc_flops.py $F $OUT/pmc_flops_${CFG}.json $CFG
   DEG=$(python3 -c "import sys; sys.path.insert(0, '.'); from multiview_amd import rig; from bench import kernel_degree; print(kernel_degree(rig.CONFIGS['$CFG']['models'][0]))")
-  python3 tools/pmc_summary.py $FE $WR "k_eval_local<$DEG, double, true>" $OUT/pmc_eval_${CFG}.json $CFG
+  # (c4 takes the split form: no k_eval_local launch in its timed loop)
+  python3 tools/pmc_summary.py $FE $WR "k_eval_local<$DEG, double, true>" $OUT/pmc_eval_${CFG}.json $CFG || echo "no k_eval_local summary for $CFG"
   python3 tools/pmc_summary.py $FE $WR "k_obs<$DEG, double>" $OUT/pmc_k1_${CFG}.json $CFG
   if [ $CFG = c5 ]; then
     python3 tools/pmc_summary.py $FE $WR "k_depth_obs<double>" $OUT/pmc_depth_${CFG}.json $CFG
