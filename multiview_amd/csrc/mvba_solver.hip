@@ -830,6 +830,9 @@ constexpr int kPassBRegCols = 48;  // register accumulators up to this many colu
 #ifndef MVBA_PASSB_TRED
 #define MVBA_PASSB_TRED 1
 #endif
+#ifndef MVBA_RPC_PB_WAVES
+#define MVBA_RPC_PB_WAVES 1  // min waves per EU of RPC (degree <= 2) pass B (launch bounds; A/B builds)
+#endif
 #ifndef MVBA_PASSB_PIPE
 #define MVBA_PASSB_PIPE 1  // RPC pass B: software-pipelined gathers (-DMVBA_PASSB_PIPE=0: the plain loop, A/B)
 #endif
@@ -1058,7 +1061,7 @@ __device__ __forceinline__ void pass_b_rpc_obs(const FrameDesc& F, const double*
 template <int MODEL, int DEG>
 // (min waves per EU: keeps radtan / none within 128 VGPRs under the 128-thread
 // bound, as under the old 64-thread one; FOV needs ~155, RPC more)
-__global__ void __launch_bounds__(128, MODEL == kModelRpc ? 1 : MODEL == kModelFov ? 3 : 4) k_pass_b(
+__global__ void __launch_bounds__(128, MODEL == kModelRpc ? (DEG <= 2 ? MVBA_RPC_PB_WAVES : 1) : MODEL == kModelFov ? 3 : 4) k_pass_b(
     const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
     const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
     const double* __restrict__ frec, const double* __restrict__ params,
