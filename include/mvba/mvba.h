@@ -488,10 +488,12 @@ double mvba_eval_bytes(const struct mvba_handle* h, int32_t flags);
 
 /* The launch form a full mvba_evaluate_device takes on this handle (ABI 6):
  * MVBA_FORM_SPLIT = prep launch + one K1 launch per model group (several
- * camera models); MVBA_FORM_FUSED = one k_eval launch (K0 blocks hand the
- * frame records to the K1 waves of the same grid; MVBA_EVAL_MODE=fused);
+ * camera models, or one model past 24 segments of 64 observations per image,
+ * where recomputing the frame record in every wave costs more than the prep
+ * launch); MVBA_FORM_FUSED = one k_eval launch (K0 blocks hand the frame
+ * records to the K1 waves of the same grid; MVBA_EVAL_MODE=fused);
  * MVBA_FORM_LOCAL = one k_eval_local launch (each K1 wave computes its frame's
- * record; the default for one camera model). */
+ * record; the default for one camera model up to that density). */
 enum { MVBA_FORM_SPLIT = 0, MVBA_FORM_FUSED = 1, MVBA_FORM_LOCAL = 2 };
 int32_t mvba_eval_form(const struct mvba_handle* h);
 
