@@ -23,8 +23,13 @@ namespace mvba {
 constexpr bool kFastProj = MVBA_FAST_PROJ;
 
 constexpr int kDirStride = 128;    // per-frame direction record: u (6) | x_intr (<= 122: RPC degree 6 has 113)
+// pass-B vector replicas (chunk mod R): 32 since round 2 (8 contended then);
+// with 8-segment chunks 16 measured best: c2 CG iteration 60.4 / 60.5 vs 61.3 /
+// 61.8 us of kernels (replica sum 5.0 vs 5.4), c3 452.7 / 455.8 vs 456.1 /
+// 455.9, 1/8 shard equal; 8 contends again (c2 pass B 25.3 vs 19.2 us),
+// profiles/r05/r05aa/
 #ifndef MVBA_VEC_REPLICAS
-#define MVBA_VEC_REPLICAS 32
+#define MVBA_VEC_REPLICAS 16
 #endif
 constexpr int kVecReplicas = MVBA_VEC_REPLICAS;  // power of two
 
