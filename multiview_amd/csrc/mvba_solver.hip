@@ -23,13 +23,15 @@ namespace mvba {
 constexpr bool kFastProj = MVBA_FAST_PROJ;
 
 constexpr int kDirStride = 128;    // per-frame direction record: u (6) | x_intr (<= 122: RPC degree 6 has 113)
-// pass-B vector replicas (chunk mod R): 32 since round 2 (8 contended then);
-// with 8-segment chunks 16 measured best: c2 CG iteration 60.4 / 60.5 vs 61.3 /
-// 61.8 us of kernels (replica sum 5.0 vs 5.4), c3 452.7 / 455.8 vs 456.1 /
-// 455.9, 1/8 shard equal; 8 contends again (c2 pass B 25.3 vs 19.2 us),
-// profiles/r05/r05aa/
+// pass-B vector replicas (chunk mod R): 32 since round 2 (8 contended then).
+// Round 5 re-measured 16 with 8-segment chunks: c2 CG iteration 60.4 / 60.5 vs
+// 61.3 / 61.8 us of kernels, c3 452.7 / 455.8 vs 456.1 / 455.9, 1/8 shard
+// equal (profiles/r05/r05aa/), but the full GPU suite on that build sent the
+// atomic and deterministic depth solves of test_deterministic_solve_is_
+// reproducible[True] to different Cauchy minima within 50 iterations (6896.5
+// vs 6893.7, r05zz): 32 kept (-DMVBA_VEC_REPLICAS=16 for A/B builds)
 #ifndef MVBA_VEC_REPLICAS
-#define MVBA_VEC_REPLICAS 16
+#define MVBA_VEC_REPLICAS 32
 #endif
 constexpr int kVecReplicas = MVBA_VEC_REPLICAS;  // power of two
 
