@@ -66,6 +66,10 @@ def parse():
                          "init / enqueue deadline")
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="N > 1: torch.distributed collective timeout (s)")
+    ap.add_argument("--ba-exchange", default="auto", choices=("auto", "rccl"),
+                    help="auto: the exchange N > 1 takes (RCCL), none at N = 1; rccl: at N = 1 too, through a "
+                         "one-rank RCCL communicator (rehearsal of the sharded LM path: fold-mode CG tail, the "
+                         "ncclAllReduce inside the captured CG runs), e.g. with --shard-of 8")
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"),
                     help="strong (default): the config is the whole job, split over the ranks; "
                          "weak: every rank owns a config-sized shard")
@@ -996,6 +1000,11 @@ def main():
                     comm = Comm.rccl(dev, timeout_s=args.ba_deadline)
                 else:
                     ex = SolverExchange(device=dev)  # gloo rehearsal: host-staged exchange
+            elif args.ba_exchange == "rccl":
+                # one-rank RCCL communicator: the sharded solve's code path
+                # (exchange enqueues, fold-mode CG tail, captured CG runs with
+                # the all-reduce inside), timed on one GPU
+                comm = Comm.rccl_world1(dev, timeout_s=args.ba_deadline)
             inject = injected_failure(os.environ.get("MVBA_BENCH_INJECT", ""), rank)
             if inject and ex is not None:
                 ex = FailingExchange(ex)
@@ -1036,9 +1045,12 @@ def main():
                 "eval_s": s["eval_time_s"],
                 "initial_cost": s["initial_cost"],
                 "final_cost": s["final_cost"],
-                "exchange": ("rccl (mvba_comm_allreduce, stream-ordered)" if comm else
-                             "gloo (host-staged callback)" if ex else "none (single rank)"),
+                "exchange": ("rccl (mvba_comm_allreduce, stream-ordered)" if comm and world > 1 else
+                             "rccl (one-rank communicator: the sharded path rehearsed, mvba_comm_allreduce)"
+                             if comm else "gloo (host-staged callback)" if ex else "none (single rank)"),
                 "exchange_calls": ex.calls if ex else None,
+                # captured CG runs replayed (0: every CG kernel and exchange launched eagerly)
+                "cg_graph_launches": s.get("cg_graph_launches"),
             }
             if ev.num_depth == 0:
                 cgb = cg_bytes(ev.num_residuals, int(L["num_points"]), ev.num_frames, int(L["cam_grad_size"]),
@@ -1066,7 +1078,7 @@ def main():
                                   "SQ_INSTS_VALU per kernel, median of non-gated launches)",
                     })
                 line["ba"]["roofline"] = roof
-            if world > 1:
+            if world > 1 or comm is not None:
                 # the per-CG-iteration exchange alone: one all-reduce of the
                 # camera-side product vector (cam_grad_size doubles), on the solver's
                 # stream, HIP events around K of them
@@ -1082,7 +1094,8 @@ def main():
                 for _ in range(args.warmup):
                     xchg()
                 torch.cuda.synchronize()
-                dist.barrier()
+                if world > 1:
+                    dist.barrier()
                 xe = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 t0 = time.perf_counter()
                 xe[0].record(stream)

@@ -597,7 +597,8 @@ typedef struct mvba_solver_summary {
   int32_t num_unsuccessful_steps;
   int32_t num_linear_iterations;       /* total CG iterations */
   int32_t termination_type;            /* MVBA_CONVERGENCE / NO_CONVERGENCE / FAILURE */
-  int32_t pad;
+  int32_t cg_graph_launches;           /* captured CG runs replayed (hipGraphLaunch); 0: every CG kernel
+                                          launched eagerly (was padding: same layout) */
   double total_time_s;
   double linearize_time_s;             /* Jacobian / normal equations (incl. exchange) */
   double linear_solver_time_s;         /* CG + back-substitution */

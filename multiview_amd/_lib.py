@@ -163,7 +163,7 @@ class SolverSummary(C.Structure):
         ("num_unsuccessful_steps", C.c_int32),
         ("num_linear_iterations", C.c_int32),
         ("termination_type", C.c_int32),
-        ("pad", C.c_int32),
+        ("cg_graph_launches", C.c_int32),
         ("total_time_s", C.c_double),
         ("linearize_time_s", C.c_double),
         ("linear_solver_time_s", C.c_double),

@@ -350,6 +350,7 @@ void mvba_comm_destroy(mvba_comm* c) {
 }
 
 int32_t mvba_comm_rank(const mvba_comm* c) { return c ? c->rank : -1; }
+int32_t mvba_comm_capturable(const mvba_comm* c) { return c && c->kind == 0 && c->nccl ? 1 : 0; }
 int32_t mvba_comm_size(const mvba_comm* c) { return c ? c->nranks : 0; }
 
 int32_t mvba_comm_allreduce(double* device_buf, int64_t count, int32_t op, void* hip_stream, void* comm) {

@@ -88,6 +88,10 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
                                   const double4* dmeas, const double* frec, const double* params, const double4* pts,
                                   int32_t flags, double cauchy_c, double* partial, hipStream_t s,
                                   int64_t* nblocks_out);
+// 1 when the communicator's exchange is a plain stream enqueue (RCCL: no host
+// rendezvous, no event waits across streams), so a hipGraph capture of the
+// solver's stream can hold it (mvba_comm.hip)
+int32_t mvba_comm_capturable(const mvba_comm* comm);
 }
 
 // Row layout of a host hand-over (mvba_transfer.hip): residual rows per block,

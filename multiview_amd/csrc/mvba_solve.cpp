@@ -308,6 +308,11 @@ class Solver {
     static const bool no_fold = std::getenv("MVBA_CG_FOLD") && std::getenv("MVBA_CG_FOLD")[0] == '0';
     if (o.allreduce == &mvba_comm_allreduce && !no_fold)
       exch_rank_ = mvba_comm_rank((const mvba_comm*)o.allreduce_user);
+    // an RCCL communicator's exchange is one ncclAllReduce on s_: a CG run
+    // holding it can be captured like a single-rank one (the local
+    // communicator meets its peer threads on the host: eager)
+    exch_capturable_ = !o.allreduce || (o.allreduce == &mvba_comm_allreduce &&
+                                        mvba_comm_capturable((const mvba_comm*)o.allreduce_user));
   }
 
   void run(mvba_solver_summary* sum);
@@ -324,6 +329,7 @@ class Solver {
   bool single_model_;
   bool bounded_ = false;
   int last_cg_iters_ = 0;  // CG iterations of the previous linear solve (batch sizing only)
+  int graph_launches_ = 0;  // captured CG runs replayed in this solve (summary)
   // MVBA_CG_TIMING=1: host-side split of the linear-solver wall time, printed
   // at the end of the solve (where a CG iteration's wall time goes)
   struct CgTiming {
@@ -335,6 +341,7 @@ class Solver {
     return on;
   }
   int32_t exch_rank_ = -1;  // this rank, when the exchange is a library communicator
+  bool exch_capturable_ = true;  // no exchange, or one a stream capture can hold (RCCL)
   // Single-rank, non-deterministic CG: the replica reduction adds p.q into
   // scal[kPqSlot + par] with one atomic per block (no finalising block) and the
   // update kernel takes the step length from it; par = the CG iteration's
@@ -437,14 +444,19 @@ class Solver {
   // One host read of scal[0..n) and the device error word (K0's alpha range
   // check); throws on a device error. The merged LM step below reads every
   // scalar a decision needs with one of these instead of one sync per quantity.
-  const double* fetch_checked(int n) {
+  // deferred: the device error is returned there instead of thrown (the merged
+  // step's candidate evaluation, whose error counts only for a valid step)
+  const double* fetch_checked(int n, mvba_status* deferred = nullptr) {
     HCHK(hipMemcpyAsync(S_->hscal, S_->scal, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, s_));
     HCHK(hipMemcpyAsync(S_->hscal + kErrSlot, h_->d_err, 2 * sizeof(int), hipMemcpyDeviceToHost, s_));
     HCHK(hipStreamSynchronize(s_));
     int err[2];
     std::memcpy(err, S_->hscal + kErrSlot, sizeof(err));
     const mvba_status st = device_error(err, h_->gen);
-    if (st != MVBA_OK) throw StatusErr{st, device_error_text(st)};
+    if (deferred)
+      *deferred = st;
+    else if (st != MVBA_OK)
+      throw StatusErr{st, device_error_text(st)};
     return S_->hscal;
   }
   static constexpr int kErrSlot = 30;  // hscal[30]: the device error word (2 ints)
@@ -707,12 +719,20 @@ class Solver {
   // only while all of them are unchanged.
   std::vector<uintptr_t> cg_signature(bool fused_dir) const {
     auto u = [](const void* p) { return (uintptr_t)p; };
+    // the launch-shaping switches read at enqueue time, by their first character
+    auto env0 = [](const char* name) {
+      const char* e = std::getenv(name);
+      return (uintptr_t)(e ? (unsigned char)e[0] : 0u);
+    };
+    uint64_t cauchy_bits = 0;  // the exact value (bit pattern), not a rounding of it
+    static_assert(sizeof(cauchy_bits) == sizeof(cauchy_c_), "fp64 bit pattern");
+    std::memcpy(&cauchy_bits, &cauchy_c_, sizeof(cauchy_bits));
     const char* co = std::getenv("MVBA_CO_ORDER");
-    const char* pa = std::getenv("MVBA_PASS_A_CHUNKS");
     std::vector<uintptr_t> v = {
-        (uintptr_t)fused_dir, (uintptr_t)pq_atomic(), (uintptr_t)co_slot_order(co), (uintptr_t)(pa ? pa[0] : 0),
-        (uintptr_t)point_w_tiles(), u(h_->d_wtiles), u(h_->d_wlane_pid), u(h_->d_wlane_slot), u(h_->d_wlane_pos),
-        (uintptr_t)flags_, (uintptr_t)std::llround(cauchy_c_ * 1e15), (uintptr_t)S_->ng, (uintptr_t)h_->nframes,
+        (uintptr_t)fused_dir, (uintptr_t)pq_atomic(), (uintptr_t)co_slot_order(co), env0("MVBA_PASS_A_CHUNKS"),
+        env0("MVBA_PASSB_WAVES"), (uintptr_t)point_w_tiles(), u(h_->d_wtiles), u(h_->d_wlane_pid),
+        u(h_->d_wlane_slot), u(h_->d_wlane_pos), (uintptr_t)flags_, (uintptr_t)cauchy_bits, (uintptr_t)S_->ng,
+        (uintptr_t)h_->nframes, u((const void*)o_.allreduce), u(o_.allreduce_user), (uintptr_t)(intptr_t)exch_rank_,
         u(obsx()), u(h_->d_params), u(h_->d_pts), u(h_->d_frec), u(h_->d_fd), u(h_->d_frame_lin), u(h_->d_segs),
         u(h_->d_chunks), u(h_->d_segchunks), u(h_->d_achunks), u(h_->d_obs_pid), u(h_->d_obs_meas), u(h_->d_slot_po),
         u(h_->d_po_slot), u(h_->d_pt_begin), u(h_->d_pt_off), u(h_->d_pt_free), u(h_->d_dep_segs),
@@ -732,6 +752,8 @@ class Solver {
       v.push_back((uintptr_t)G.chunk_count);
       v.push_back((uintptr_t)G.seg_begin);
       v.push_back((uintptr_t)G.seg_count);
+      v.push_back((uintptr_t)G.achunk_begin);
+      v.push_back((uintptr_t)G.achunk_count);
     }
     return v;
   }
@@ -746,7 +768,8 @@ class Solver {
   // double-buffered p, r, direction records and p.q accumulator by the parity
   // of i, the residual reset at i % 10 == 0; the iteration number itself is
   // counted on the device, CgCtl::it), so single-rank solves capture runs of
-  // iterations as hipGraphs once per handle and replay them: a batch of k
+  // iterations as hipGraphs once per handle and replay them (RCCL-sharded
+  // solves too, with the exchange inside the graph): a batch of k
   // iterations costs a few graph launches instead of 5 k kernel launches, whose
   // host time (≈ 25 us per iteration, 5-6 us per hipLaunchKernel) bound the
   // CG iteration of small problems (profiles/r05/r05b/s8_timing_r05b.log:
@@ -810,11 +833,15 @@ class Solver {
         upd(1 | 2 | 8, S_->q, P[i & 1], r_in, r_out);
       }
     };
-    // graphs: single rank (a library exchange or a callback inside the iteration
-    // is not captured), a capturable (non-null) stream; deterministic mode once
-    // its slab plan is recorded (schur_rhs's product records it, so always here)
+    // graphs: single rank, or a sharded solve exchanging through an RCCL
+    // communicator (the per-iteration ncclAllReduce is captured with the
+    // kernels around it: every rank replays the same runs, since the replicated
+    // camera-side CG state gives every rank the same batches); a caller's
+    // callback or the local communicator (host rendezvous) stays eager; a
+    // capturable (non-null) stream; deterministic mode once its slab plan is
+    // recorded (schur_rhs's product records it, so always here)
     const char* g_env = std::getenv("MVBA_CG_GRAPH");  // read per call: tests switch it
-    const bool use_graphs = !(g_env && g_env[0] == '0') && !o_.allreduce && s_ != nullptr &&
+    const bool use_graphs = !(g_env && g_env[0] == '0') && exch_capturable_ && s_ != nullptr &&
                             (!o_.deterministic || S_->b_det.ready) && !S_->graphs_broken;
     if (use_graphs) {
       std::vector<uintptr_t> sig = cg_signature(fused_dir);
@@ -830,13 +857,23 @@ class Solver {
       for (const SolverState::CgGraph& g : S_->graphs)
         if (g.o == o && g.L == L) {
           HCHK(hipGraphLaunch(g.exec, s_));
+          graph_launches_++;
           return;
         }
       hipGraph_t graph = nullptr;
       hipGraphExec_t exec = nullptr;
-      if (hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      // a refused capture is reported once per handle (stderr) and the solve
+      // goes on eagerly: the launches and exchanges of a failed capture never
+      // ran, so every rank (which fails the same way) re-enqueues them
+      auto broken = [&](const char* what, hipError_t e) {
         (void)hipGetLastError();
         S_->graphs_broken = true;
+        std::fprintf(stderr, "mvba_solve: CG graph capture refused at %s (%s)%s; eager launches from here\n", what,
+                     hipGetErrorString(e), o_.allreduce ? " with the RCCL exchange inside" : "");
+      };
+      const hipError_t eb = hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal);
+      if (eb != hipSuccess) {
+        broken("hipStreamBeginCapture", eb);
         for (int k = 0; k < L; k++) body(i + k);
         return;
       }
@@ -847,18 +884,20 @@ class Solver {
         ok = false;
       }
       const hipError_t ec = hipStreamEndCapture(s_, &graph);
-      ok = ok && ec == hipSuccess && graph;
-      if (ok && hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) ok = false;
+      hipError_t ei = hipSuccess;
+      if (ok && ec == hipSuccess && graph) ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
       if (graph) (void)hipGraphDestroy(graph);
-      if (!ok) {
-        (void)hipGetLastError();
+      if (!ok || ec != hipSuccess || !graph || ei != hipSuccess) {
         if (exec) (void)hipGraphExecDestroy(exec);
-        S_->graphs_broken = true;
+        broken(!ok ? "an enqueue inside the capture" : ec != hipSuccess || !graph ? "hipStreamEndCapture"
+                                                                                  : "hipGraphInstantiate",
+               !ok ? hipErrorStreamCaptureInvalidated : ec != hipSuccess ? ec : ei);
         for (int k = 0; k < L; k++) body(i + k);  // this run eagerly; later ones too
         return;
       }
       S_->graphs.push_back(SolverState::CgGraph{o, L, exec});
       HCHK(hipGraphLaunch(exec, s_));
+      graph_launches_++;
     };
     int i = 1;
     // Batch sizes only decide where the host looks at the control block (gated
@@ -1357,8 +1396,14 @@ void Solver::run(mvba_solver_summary* sum) {
     // four. An invalid step then restores the parameters it moved.
     const bool merged = !bounded_ && merged_reads();
     double m_cand = 0.0, m_step2 = 0.0, m_eval_gpu_s = 0.0;
+    // test hook (read per call): the first N steps of the solve are declared
+    // invalid after their model change is known, as a non-positive or NaN model
+    // change would be (both read paths must then end the same way)
+    const char* fi_env = std::getenv("MVBA_TEST_INVALID_STEPS");
+    const bool forced_invalid = fi_env && iteration <= std::atoi(fi_env);
     if (valid) {
       const double tbs = now_s();
+      mvba_status cand_err = MVBA_OK;
       if (merged) {
         back_substitute(false);
         HCHK(hipEventRecord(S_->ev[0], s_));
@@ -1368,7 +1413,10 @@ void Solver::run(mvba_solver_summary* sum) {
         HCHK(mvba_launch_axpby(S_->nc, 1.0, S_->xn, -1.0, S_->x, S_->scr, s_));
         norm2_enqueue(S_->scr, 3, 4);
         HCHK(hipEventRecord(S_->ev[1], s_));
-        const double* hs = fetch_checked(17);
+        // the candidate's device error (K0's alpha range check,
+        // rig_calibrator.cc:346) is raised only for a valid step: Ceres rejects
+        // an invalid step without evaluating its candidate
+        const double* hs = fetch_checked(17, &cand_err);
         mcc = model_change(hs);
         m_cand = hs[16];
         m_step2 = hs[3] + hs[4];
@@ -1379,8 +1427,11 @@ void Solver::run(mvba_solver_summary* sum) {
         mcc = back_substitute();
       }
       if (cg_timing()) tm_.backsub += now_s() - tbs - m_eval_gpu_s;
-      valid = std::isfinite(mcc) && mcc > 0.0;
+      valid = std::isfinite(mcc) && mcc > 0.0 && !forced_invalid;
+      if (merged && valid && cand_err != MVBA_OK) throw StatusErr{cand_err, device_error_text(cand_err)};
       if (merged && !valid) {  // the speculative candidate moved the parameters
+        // prep() starts a new evaluation generation: the candidate's error
+        // word (stamped with the old one) is stale from here on
         set_params_from(S_->x);
         prep();
       }
@@ -1492,6 +1543,7 @@ void Solver::run(mvba_solver_summary* sum) {
   }
   HCHK(hipStreamSynchronize(s_));
   sum->num_iterations = iteration;
+  sum->cg_graph_launches = graph_launches_;
   sum->final_cost = x_cost;
   sum->total_time_s = now_s() - t0;
   if (cg_timing() && tm_.solves)
@@ -1559,6 +1611,15 @@ mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver
   if (o->max_num_iterations < 0 || o->max_linear_solver_iterations < 1 || !(o->initial_trust_region_radius > 0.0))
     return h->fail(MVBA_E_INVALID, "invalid solver options");
   if (hipSetDevice(h->device) != hipSuccess) return h->fail(MVBA_E_HIP, "hipSetDevice failed");
+  // the library's own stream (a null-stream caller): a failed solve drains it
+  // before returning, so no kernel queued before the failure still writes the
+  // parameters or solver buffers behind the caller's next null-stream call
+  // (a non-blocking stream does not order against the null stream)
+  hipStream_t lib_stream = nullptr;
+  auto drain = [&]() {
+    if (lib_stream) (void)hipStreamSynchronize(lib_stream);
+    (void)hipGetLastError();
+  };
   try {
     if (!h->solver) h->solver = alloc_state(h);
     // A caller on the null stream gets the handle's own stream: the CG loop's
@@ -1572,6 +1633,7 @@ mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver
     if (!st && !o->allreduce && own) {
       HCHK(hipDeviceSynchronize());
       st = solver_stream(h->device);
+      lib_stream = st;
     }
     Solver sv(h, *o, st);
     // K2 writes the CG passes' per-slot records for the duration of the solve
@@ -1582,14 +1644,17 @@ mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver
     h->lin_obsx = sv.obsx_records();
     sv.run(summary);
   } catch (const HipErr& e) {
+    drain();
     std::snprintf(summary->message, sizeof(summary->message), "HIP error");
     summary->termination_type = MVBA_FAILURE;
     return h->hip_fail(e.e, e.where);
   } catch (const StatusErr& e) {
+    drain();
     summary->termination_type = MVBA_FAILURE;
     std::snprintf(summary->message, sizeof(summary->message), "%s", e.msg.c_str());
     return h->fail(e.st, e.msg);
   } catch (const std::bad_alloc&) {
+    drain();
     return h->fail(MVBA_E_INVALID, "host allocation failed");
   }
   return MVBA_OK;

@@ -199,6 +199,27 @@ class Comm:
         return cls(h)
 
     @classmethod
+    def rccl_world1(cls, device: int, timeout_s: float = 0.0):
+        """A one-rank RCCL communicator without torch.distributed (the unique
+        id stays in this process): the exchange path of a sharded solve
+        (ncclAllReduce on the solver's stream, the fold-mode CG tail, captured
+        CG runs) rehearsed on one GPU; the all-reduce is an identity there."""
+        import ctypes as C
+
+        import numpy as np
+
+        from . import _lib
+
+        lib = _lib.load()
+        ident = np.zeros(_lib.COMM_ID_BYTES, dtype=np.uint8)
+        _lib.check(lib.mvba_comm_unique_id(ident.ctypes.data))
+        h = C.c_void_p()
+        st = lib.mvba_comm_init_rccl_deadline(ident.ctypes.data, 1, 0, device, float(timeout_s), C.byref(h))
+        if st != 0:
+            raise _lib.MvbaError(st, lib.mvba_comm_error().decode())
+        return cls(h)
+
+    @classmethod
     def local(cls, devices):
         import ctypes as C
 

@@ -399,6 +399,7 @@ def summary_dict(s: _lib.SolverSummary) -> dict:
     return dict(initial_cost=s.initial_cost, final_cost=s.final_cost, num_iterations=s.num_iterations,
                 num_successful_steps=s.num_successful_steps, num_unsuccessful_steps=s.num_unsuccessful_steps,
                 num_linear_iterations=s.num_linear_iterations, termination_type=s.termination_type,
+                cg_graph_launches=s.cg_graph_launches,
                 total_time_s=s.total_time_s, linearize_time_s=s.linearize_time_s,
                 linear_solver_time_s=s.linear_solver_time_s, eval_time_s=s.eval_time_s,
                 message=s.message.decode(errors="replace"))

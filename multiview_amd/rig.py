@@ -256,7 +256,7 @@ def _sensor_yaw_deg(s: int, n_s: int) -> float:
 
 def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, models=None,
              seed=1001, point_range=None, window=20, noise_px=0.5, depth_sensors=(),
-             depth_noise=0.01, affine_depth=False, surface=None) -> Rig:
+             depth_noise=0.01, affine_depth=False, surface=None, alpha_shift=0.0) -> Rig:
     """Build a synthetic rig. ``point_range=(lo, hi)`` generates only points
     [lo, hi) of a larger problem (landmark-range sharding): the
     cameras are identical on every shard, points use a per-shard stream.
@@ -265,7 +265,12 @@ def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, mode
     depth_to_image^-1 (X_cam) + N(0, depth_noise^2), rounded to float32 (clouds
     are float32, dense_map_utils.cc:1382). ``surface="sphere"``: landmarks on the
     sphere of radius SPHERE_RADIUS (the surface ``sphere_mesh`` triangulates, for
-    the --mesh constraints), observed only by cameras on their outer side."""
+    the --mesh constraints), observed only by cameras on their outer side.
+    ``alpha_shift``: the bracketed images' true poses are interpolated at
+    alpha + alpha_shift (extrapolated past the bracket when the sum leaves
+    [0, 1]) while their timestamps stay put, so the offset that explains the
+    data lies outside the bracket (a test rig for the interpolation range check,
+    rig_calibrator.cc:346)."""
     models = list(models or ["radtan"] * num_sensors)
     assert len(models) == num_sensors
     rng = np.random.default_rng(seed)
@@ -315,6 +320,7 @@ def make_rig(num_sensors=3, num_ref=50, num_points=1000, obs_per_point=5.0, mode
     alpha = np.where(cam_beg == cam_end, 0.0,
                      ((cam_stamp - ref_stamps[cam_beg]) - offsets[cam_type]) /
                      np.where(cam_beg == cam_end, 1.0, ref_stamps[cam_end] - ref_stamps[cam_beg]))
+    alpha = np.where(cam_beg == cam_end, alpha, alpha + alpha_shift)
     q0, q1 = world_to_ref[cam_beg, 3:], world_to_ref[cam_end, 3:]
     qi = slerp(q0, q1, alpha)
     Ri = quat_to_mat(qi)

@@ -586,3 +586,50 @@ def test_rccl_comm_world1_solve(tmp_path):
     # same tolerances as the sharded tests (normalised poses: |q| is a gauge direction)
     assert _close(cam_r, cam, 1e-6)
     assert _close(pts_r, pts, 1e-6)
+
+
+def test_invalid_step_skips_candidate_range_check(monkeypatch):
+    """Ceres rejects an invalid step (non-positive or NaN model change, CG
+    failure) without evaluating its candidate, so the reference's
+    interpolation check (LOG(FATAL), rig_calibrator.cc:346) never sees that
+    candidate. The merged LM step evaluates the candidate speculatively; its
+    device error must count only for a valid step, so both read paths
+    (MVBA_LM_MERGED=1 / 0) end the same way.
+
+    Rig: sensor 1's images are generated at alpha + 1 (extrapolated past their
+    brackets; make_rig alpha_shift), so the offset that explains the data lies
+    outside the bracket and the first LM step's candidate leaves [0, 1] (the
+    floated offset carries no bounds here). (1) A valid first step raises
+    MVBA_E_ALPHA_RANGE in both modes. (2) With the first step declared invalid
+    (MVBA_TEST_INVALID_STEPS=1, after its model change is known) and one LM
+    iteration, both modes return the same summary: no error, the step counted
+    unsuccessful, the parameters unchanged."""
+    from multiview_amd import _lib
+
+    R = rig.make_rig(num_sensors=2, num_ref=10, num_points=200, obs_per_point=5, models=["radtan", "fov"], seed=61,
+                     alpha_shift=1.0)
+    P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=()))
+    kw = dict(max_num_iterations=1, use_loss=1, robust_threshold=3.0, deterministic=1, **TOL)
+    for merged in ("1", "0"):
+        monkeypatch.setenv("MVBA_LM_MERGED", merged)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            with pytest.raises(_lib.MvbaError) as e:
+                ev.solve(**kw)
+            assert e.value.status == _lib.MVBA_E_ALPHA_RANGE, (merged, e.value)
+    out = {}
+    monkeypatch.setenv("MVBA_TEST_INVALID_STEPS", "1")
+    for merged in ("1", "0"):
+        monkeypatch.setenv("MVBA_LM_MERGED", merged)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(**kw)
+            x = ev.get_params()
+        assert s["termination_type"] == 1, (merged, s["message"])  # NO_CONVERGENCE: iteration cap
+        assert s["num_unsuccessful_steps"] == 1 and s["num_successful_steps"] == 1, (merged, s)
+        assert s["final_cost"] == s["initial_cost"]
+        assert np.array_equal(x, P.params), merged
+        out[merged] = s
+    for k in ("termination_type", "num_iterations", "num_successful_steps", "num_unsuccessful_steps",
+              "num_linear_iterations", "initial_cost", "final_cost"):
+        assert out["1"][k] == out["0"][k], (k, out["1"][k], out["0"][k])

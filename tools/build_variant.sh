@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build another libmvba.so with extra compile definitions for a same-box A/B
-# (tools/gpu_ab.sh loads it through MVBA_LIB): tools/build_variant.sh NAME "-DX=1 ..."
+# (tools/gpu_session.sh's ab step loads it through MVBA_LIB): tools/build_variant.sh NAME "-DX=1 ..."
 set -eu
 cd "$(dirname "$0")/.."
 NAME=$1; shift

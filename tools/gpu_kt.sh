@@ -1,7 +1,7 @@
 #!/bin/bash
 # kernel traces of the CG iteration (median span + per-kernel medians over the
 # non-gated iterations, tools/cg_iter_med.py) for the listed configs and env
-# variants: usage gpu_kt_r05.sh TAG "cfg ..." "NAME=ENV,ENV NAME=ENV ..."
+# variants: usage gpu_kt.sh TAG "cfg ..." "NAME=ENV,ENV NAME=ENV ..."
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -11,7 +11,8 @@ CFGS=${2:-"s8 c2"}
 VARS=${3:-"cur=MVBA_CG_GRAPH=1"}
 for k in ${REPS:-1}; do
 for cfg in $CFGS; do
-  case $cfg in s8) A="--shard-of 8 --ba-iters 5";; c2) A="--ba-iters 5";; c3) A="--config c3 --ba-iters 2";; esac
+  case $cfg in s8) A="--shard-of 8 --ba-iters 5";; c2) A="--ba-iters 5";; c3) A="--config c3 --ba-iters 2";;
+    r8) A="--shard-of 8 --ba-exchange rccl --ba-iters 5";; esac
   for v in $VARS; do
     name=${v%%=*}; envs=${v#*=}
     D=$OUT/kt_$TAG/${cfg}_${name}_$k
