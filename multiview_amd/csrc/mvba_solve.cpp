@@ -104,8 +104,8 @@ hipError_t mvba_launch_extract_diag(int32_t nblocks, const int64_t* goff, const 
                                     const double* hess, int64_t npts, const double* V, int64_t ng, double* c,
                                     hipStream_t s);
 hipError_t mvba_launch_jacobi_scale(int64_t n, const double* c, double* sc, hipStream_t s);
-hipError_t mvba_launch_lm_diag(int64_t n, const double* c, const double* sc, double inv_radius, double dmin,
-                               double dmax, double* d, hipStream_t s);
+hipError_t mvba_launch_lm_diag(int64_t n, const double* c, const double* sc, double inv_radius,
+                               const double* inv_radius_dev, double dmin, double dmax, double* d, hipStream_t s);
 hipError_t mvba_launch_gather(int64_t ncam, const int64_t* cam_poff, int64_t npts, const int64_t* pt_off,
                               const uint8_t* pt_free, const double* params, double* out, hipStream_t s);
 hipError_t mvba_launch_scatter(int64_t ncam, const int64_t* cam_poff, int64_t npts, const int64_t* pt_off,
@@ -154,6 +154,7 @@ struct SolverState {
   unsigned* cnt = nullptr;    // [8] grid-reduction counters (kept zero between kernels)
   double* hscal = nullptr;    // [32] pinned host mirror
   mvba::CgCtl* ctl = nullptr; // device CG control (single-rank solves)
+  mvba::CgCtl* ctl0 = nullptr; // the solve's initial control block (options only; copied to ctl per linear solve)
   double* prec = nullptr;     // [nframes * kProjDoubles] projection records
   mvba::CgCtl* hctl = nullptr; // pinned host mirror
   int64_t npartial = 0;
@@ -171,6 +172,14 @@ struct SolverState {
     hipGraphExec_t exec = nullptr;
   };
   std::vector<CgGraph> graphs;
+  // Captured per-LM-step sequences (same signature as the CG runs): kind 0 the
+  // step prologue (damping, preconditioner, Schur right-hand side, CG start),
+  // kind 1 the back-substitution
+  struct SeqGraph {
+    int kind = 0;
+    hipGraphExec_t exec = nullptr;
+  };
+  std::vector<SeqGraph> seq_graphs;
   std::vector<uintptr_t> graph_sig;
   bool graphs_broken = false;  // a capture failed: eager launches from then on
   hipEvent_t ev[2] = {nullptr, nullptr};  // the merged LM step's candidate-evaluation span
@@ -179,6 +188,9 @@ struct SolverState {
     for (CgGraph& g : graphs)
       if (g.exec) (void)hipGraphExecDestroy(g.exec);
     graphs.clear();
+    for (SeqGraph& g : seq_graphs)
+      if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    seq_graphs.clear();
   }
 };
 
@@ -186,7 +198,7 @@ void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
                   S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->dirz, S->dirp[0], S->dirp[1], S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du, S->dcbuf,
-                  S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->prec};
+                  S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->ctl0, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (S->hscal) (void)hipHostFree(S->hscal);
@@ -266,6 +278,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->scal, 32));
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hscal), 32 * sizeof(double)));
     HCHK(hipMalloc(reinterpret_cast<void**>(&S->ctl), sizeof(mvba::CgCtl)));
+    HCHK(hipMalloc(reinterpret_cast<void**>(&S->ctl0), sizeof(mvba::CgCtl)));
     // [0]: the solve's initial control block (H2D source); [1], [2]: the
     // pipelined batches' read-backs
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hctl), 3 * sizeof(mvba::CgCtl)));
@@ -609,7 +622,8 @@ class Solver {
   // directions of x, dr.dz null for x = 0). Depth blocks need the point-lane kernel
   // (it also forms their u_d); otherwise the frame-order sweep + point solve.
   void pass_a_w(const mvba::DirPair& dr, const double* tinit, const double* xv, const int32_t* gate) {
-    const double* dir = dr.dz;
+    // x != 0: frame records given (dz), or formed by pass A from z (frec)
+    const double* dir = dr.dz ? dr.dz : dr.frec;
     if (h_->ndep > 0 && !dir) {
       // right-hand side (x = 0): the point-order kernel also forms u_d = -P w_p
       HCHK(mvba_launch_pass_a(pa_model(), pa_deg(), h_->d_pt_begin, h_->npts, h_->d_po_frame, h_->d_po_meas,
@@ -644,10 +658,11 @@ class Solver {
                                       h_->d_pts, h_->d_obs_pid, h_->d_obs_meas, co_slot ? nullptr : h_->d_slot_po, dr,
                                       (double4*)S_->cbuf, flags_, cauchy_c_, gate, S_->prec, obsx(), s_));
     // depth blocks in frame order (z_d into du, P z_d per block for the point solve)
-    const bool dep = dir && h_->ndep > 0;
+    // (depth problems never take the pass-A-formed records: fused_dir is off)
+    const bool dep = dr.dz && h_->ndep > 0;
     if (dep)
       HCHK(mvba_launch_depth_pa(h_->d_dep_segs, h_->ndep_segs, h_->d_dep_desc, h_->d_dep_pid, h_->d_dep_meas,
-                                h_->d_frec, h_->d_params, h_->d_pts, dir, xv, S_->du, h_->d_dslot_po,
+                                h_->d_frec, h_->d_params, h_->d_pts, dr.dz, xv, S_->du, h_->d_dslot_po,
                                 (double4*)S_->dcbuf, flags_, cauchy_c_, gate, s_));
     if (dir && !dep && point_w_tiles())
       HCHK(mvba_launch_point_w_seg(h_->nwtiles, h_->d_wtiles, h_->d_wlane_pid,
@@ -693,12 +708,6 @@ class Solver {
   // records for pass A are built here (parameters fixed until the next step).
   void schur_rhs() {
     HCHK(mvba_launch_frame_proj((int32_t)h_->nframes, h_->d_fd, h_->d_frec, h_->d_params, S_->prec, s_));
-    // the per-slot records (landmark + Cauchy weight sqrt(rho')) were written
-    // by K2 at this linearization point (h_->lin_obsx). A landmark-only copy
-    // would carry the prep kernel's free flag in .w, which the frame-order
-    // passes would take as the Cauchy weight: never fall back to one.
-    if (obsx() && h_->lin_obsx != obsx())
-      throw StatusErr{MVBA_E_INVALID, "internal: CG slot records were not written by the linearization"};
     pass_a_w(plain_dir(nullptr), S_->G + S_->ng, nullptr, nullptr);
     reduce_frames(S_->tmp, nullptr, 0, nullptr);  // = -W w
     HCHK(mvba_launch_axpby(S_->ng, -1.0, S_->G, -1.0, S_->tmp, S_->b, s_));
@@ -724,21 +733,29 @@ class Solver {
       const char* e = std::getenv(name);
       return (uintptr_t)(e ? (unsigned char)e[0] : 0u);
     };
-    uint64_t cauchy_bits = 0;  // the exact value (bit pattern), not a rounding of it
-    static_assert(sizeof(cauchy_bits) == sizeof(cauchy_c_), "fp64 bit pattern");
-    std::memcpy(&cauchy_bits, &cauchy_c_, sizeof(cauchy_bits));
+    // an fp64 host value by its exact bit pattern, not a rounding of it
+    auto bits = [](double v) {
+      uint64_t b = 0;
+      static_assert(sizeof(b) == sizeof(v), "fp64 bit pattern");
+      std::memcpy(&b, &v, sizeof(b));
+      return (uintptr_t)b;
+    };
     const char* co = std::getenv("MVBA_CO_ORDER");
     std::vector<uintptr_t> v = {
         (uintptr_t)fused_dir, (uintptr_t)pq_atomic(), (uintptr_t)co_slot_order(co), env0("MVBA_PASS_A_CHUNKS"),
         env0("MVBA_PASSB_WAVES"), (uintptr_t)point_w_tiles(), u(h_->d_wtiles), u(h_->d_wlane_pid),
-        u(h_->d_wlane_slot), u(h_->d_wlane_pos), (uintptr_t)flags_, (uintptr_t)cauchy_bits, (uintptr_t)S_->ng,
+        u(h_->d_wlane_slot), u(h_->d_wlane_pos), (uintptr_t)flags_, bits(cauchy_c_), (uintptr_t)S_->ng,
         (uintptr_t)h_->nframes, u((const void*)o_.allreduce), u(o_.allreduce_user), (uintptr_t)(intptr_t)exch_rank_,
         u(obsx()), u(h_->d_params), u(h_->d_pts), u(h_->d_frec), u(h_->d_fd), u(h_->d_frame_lin), u(h_->d_segs),
         u(h_->d_chunks), u(h_->d_segchunks), u(h_->d_achunks), u(h_->d_obs_pid), u(h_->d_obs_meas), u(h_->d_slot_po),
         u(h_->d_po_slot), u(h_->d_pt_begin), u(h_->d_pt_off), u(h_->d_pt_free), u(h_->d_dep_segs),
         u(h_->d_dep_desc), u(h_->d_dep_pid), u(h_->d_dep_meas), u(h_->d_dslot_po), u(h_->d_dpt_begin),
         u(h_->d_po_frame), u(h_->d_po_meas), (uintptr_t)h_->npts, (uintptr_t)h_->nchunks,
-        (uintptr_t)h_->ndep_segs, (uintptr_t)o_.deterministic};
+        (uintptr_t)h_->ndep_segs, (uintptr_t)o_.deterministic,
+        // the step prologue and back-substitution graphs (enqueue_seq)
+        bits(o_.min_lm_diagonal), bits(o_.max_lm_diagonal), (uintptr_t)o_.jacobi_scaling, env0("MVBA_BACKSUB"), env0("MVBA_CG_DZ"),
+        (uintptr_t)h_->ndep, (uintptr_t)h_->nxyz, u(h_->d_dpo_slot), u(h_->d_xpt_begin), u(h_->d_xref), u(h_->d_xcc),
+        u(h_->d_dep_order)};
     if (o_.deterministic) {
       const DetPlan& D = S_->b_det;
       for (uintptr_t x : {u(D.val), u(D.begin), u(D.pos), u(D.tiers), (uintptr_t)D.nheavy, (uintptr_t)D.nmedium,
@@ -775,34 +792,190 @@ class Solver {
   // CG iteration of small problems (profiles/r05/r05b/s8_timing_r05b.log:
   // enqueue 27.6 us vs 16.1 us of wait per iteration on the 1/8 c2 shard).
   // MVBA_CG_GRAPH=0: eager launches (A/B timing).
-  CgResult cg_device() {
-    CgResult R;
+  // Reprojection-only problems: the CG update's frame blocks form W z and the
+  // products combine it with the previous product's records (no direction
+  // kernel per iteration). Depth blocks read the direction in more kernels:
+  // they keep the direction kernel (MVBA_CG_DIR_KERNEL=1 forces it, for A/B).
+  bool fused_dir() const {
+    const char* dk_env = std::getenv("MVBA_CG_DIR_KERNEL");  // read per call: tests switch it
+    return h_->ndep == 0 && !(dk_env && dk_env[0] == '1');
+  }
+  // With fused_dir: pass A forms the pose sums W_f z of its frame from z
+  // (stage_dir, DirPair::frec), so the CG update launches its entry blocks
+  // only (no frame blocks; one grid-wide phase of the update's latency less).
+  // MVBA_CG_DZ=update keeps the update's frame blocks (dz), for A/B timing.
+  bool dz_in_pass_a() const {
+    const char* e = std::getenv("MVBA_CG_DZ");  // read per call: tests switch it
+    return fused_dir() && !(e && !std::strcmp(e, "update"));
+  }
+
+  // Graphs: single rank, or a sharded solve exchanging through an RCCL
+  // communicator (the ncclAllReduce is captured with the kernels around it:
+  // every rank replays the same runs, since the replicated camera-side CG state
+  // gives every rank the same batches); a caller's callback or the local
+  // communicator (host rendezvous) stays eager; a capturable (non-null)
+  // stream; deterministic mode once its slab plan is recorded (the first
+  // product records it). MVBA_CG_GRAPH=0: eager launches (A/B timing).
+  bool graphs_enabled() const {
+    const char* g_env = std::getenv("MVBA_CG_GRAPH");  // read per call: tests switch it
+    return !(g_env && g_env[0] == '0') && exch_capturable_ && s_ != nullptr &&
+           (!o_.deterministic || S_->b_det.ready) && !S_->graphs_broken;
+  }
+  // drops every captured graph whose launches no longer match (signature)
+  void refresh_graph_sig() {
+    if (!graphs_enabled()) return;
+    std::vector<uintptr_t> sig = cg_signature(fused_dir());
+    if (sig != S_->graph_sig) {
+      S_->drop_graphs();
+      S_->graph_sig = std::move(sig);
+    }
+  }
+
+  // Captures fn's enqueues on s_ into *exec. A refused capture is reported once
+  // per handle (stderr), graphs are off for the handle from then on, and the
+  // caller runs fn eagerly: the launches and exchanges of a failed capture
+  // never ran, so every rank (which fails the same way) re-enqueues them.
+  template <class F>
+  bool capture(F&& fn, hipGraphExec_t* exec) {
+    *exec = nullptr;
+    hipGraph_t graph = nullptr;
+    auto broken = [&](const char* what, hipError_t e) {
+      (void)hipGetLastError();
+      S_->graphs_broken = true;
+      std::fprintf(stderr, "mvba_solve: graph capture refused at %s (%s)%s; eager launches from here\n", what,
+                   hipGetErrorString(e), o_.allreduce ? " with the RCCL exchange inside" : "");
+    };
+    const hipError_t eb = hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal);
+    if (eb != hipSuccess) {
+      broken("hipStreamBeginCapture", eb);
+      return false;
+    }
+    bool ok = true;
+    try {
+      fn();
+    } catch (...) {
+      ok = false;
+    }
+    const hipError_t ec = hipStreamEndCapture(s_, &graph);
+    hipError_t ei = hipSuccess;
+    if (ok && ec == hipSuccess && graph) ei = hipGraphInstantiate(exec, graph, nullptr, nullptr, 0);
+    if (graph) (void)hipGraphDestroy(graph);
+    if (!ok || ec != hipSuccess || !graph || ei != hipSuccess) {
+      if (*exec) (void)hipGraphExecDestroy(*exec);
+      *exec = nullptr;
+      broken(!ok ? "an enqueue inside the capture" : ec != hipSuccess || !graph ? "hipStreamEndCapture"
+                                                                                : "hipGraphInstantiate",
+             !ok ? hipErrorStreamCaptureInvalidated : ec != hipSuccess ? ec : ei);
+      return false;
+    }
+    return true;
+  }
+
+  // A per-LM-step sequence (kind: SolverState::SeqGraph): replayed from its
+  // captured graph (captured at first use), or enqueued eagerly when graphs are
+  // off. fn's launch arguments must be fixed for the signature (the damping's
+  // 1/radius is read from device memory for that reason).
+  template <class F>
+  void enqueue_seq(int kind, F&& fn) {
+    if (!graphs_enabled()) {
+      fn();
+      return;
+    }
+    for (const SolverState::SeqGraph& g : S_->seq_graphs)
+      if (g.kind == kind) {
+        HCHK(hipGraphLaunch(g.exec, s_));
+        graph_launches_++;
+        return;
+      }
+    hipGraphExec_t exec = nullptr;
+    if (!capture(fn, &exec)) {
+      fn();
+      return;
+    }
+    S_->seq_graphs.push_back(SolverState::SeqGraph{kind, exec});
+    HCHK(hipGraphLaunch(exec, s_));
+    graph_launches_++;
+  }
+
+  // Start of a linear solve, enqueue only (part of the step prologue): x = 0,
+  // the control block from the solve's template, b.b, r = b, z = M^-1 r, rho.
+  void cg_start() {
     const int64_t n = S_->ng;
-    double* xv = S_->delta;
-    const double tc0 = now_s();
-    HCHK(hipMemsetAsync(xv, 0, (size_t)std::max<int64_t>(n, 1) * sizeof(double), s_));
-    if (n == 0) return R;
+    HCHK(hipMemsetAsync(S_->delta, 0, (size_t)std::max<int64_t>(n, 1) * sizeof(double), s_));
+    if (n == 0) return;
+    HCHK(hipMemcpyAsync(S_->ctl, S_->ctl0, sizeof(mvba::CgCtl), hipMemcpyDeviceToDevice, s_));
+    if (pq_atomic()) HCHK(hipMemsetAsync(S_->scal + kPqSlot, 0, 2 * sizeof(double), s_));
+    // b.b straight into the control block: the first update's finalisation stops
+    // the solve at |b| = 0 (Ceres: "Convergence. |b| = 0.", x = 0), so the host
+    // does not wait for it (one stream sync per linear solve less)
+    HCHK(mvba_launch_dot(n, S_->b, S_->b, S_->partial, S_->cnt + 6, &S_->ctl->bb, s_));
+    const mvba::FrameDirZ fz{h_->d_frame_lin, h_->d_fd, h_->d_frec, S_->dirz, (int32_t)h_->nframes, 0};
+    HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, 4 | 8, 0.0, S_->p, nullptr, S_->b, S_->delta, S_->r, S_->r2,
+                               S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl, mvba::kIterFromCtl,
+                               fused_dir() && !dz_in_pass_a() ? &fz : nullptr, nullptr, s_));
+  }
+
+  // The template control block of this solve's linear solves (options only)
+  void upload_ctl0() {
     mvba::CgCtl c{};
     c.eta = o_.eta;
     c.min_iter = o_.min_linear_solver_iterations;
     c.max_iter = o_.max_linear_solver_iterations;
     c.it = 0;
     *S_->hctl = c;
-    HCHK(hipMemcpyAsync(S_->ctl, S_->hctl, sizeof(mvba::CgCtl), hipMemcpyHostToDevice, s_));
-    if (pq_atomic()) HCHK(hipMemsetAsync(S_->scal + kPqSlot, 0, 2 * sizeof(double), s_));
-    // b.b straight into the control block: the first update's finalisation stops
-    // the solve at |b| = 0 (Ceres: "Convergence. |b| = 0.", x = 0), so the host
-    // does not wait for it (one stream sync per linear solve less)
-    HCHK(mvba_launch_dot(n, S_->b, S_->b, S_->partial, S_->cnt + 6, &S_->ctl->bb, s_));
-    if (cg_timing()) tm_.start += now_s() - tc0;
+    HCHK(hipMemcpyAsync(S_->ctl0, S_->hctl, sizeof(mvba::CgCtl), hipMemcpyHostToDevice, s_));
+    HCHK(hipStreamSynchronize(s_));  // hctl[0] is reused for the solves' results
+  }
+
+  // Everything a step computes before its CG iterations, enqueue only: LM
+  // damping (1/radius from scal[kRadSlot]), block-Jacobi preconditioner, Schur
+  // right-hand side, CG start. One captured graph per handle when graphs are on.
+  void step_prologue(double radius) {
+    S_->hscal[kRadSlot] = 1.0 / radius;  // the previous step's copy completed (its fetch synchronised)
+    HCHK(hipMemcpyAsync(S_->scal + kRadSlot, S_->hscal + kRadSlot, sizeof(double), hipMemcpyHostToDevice, s_));
+    // the per-slot records (landmark + Cauchy weight sqrt(rho')) were written
+    // by K2 at this linearization point (h_->lin_obsx). A landmark-only copy
+    // would carry the prep kernel's free flag in .w, which the frame-order
+    // passes would take as the Cauchy weight: never fall back to one.
+    if (obsx() && h_->lin_obsx != obsx())
+      throw StatusErr{MVBA_E_INVALID, "internal: CG slot records were not written by the linearization"};
+    refresh_graph_sig();
+    enqueue_seq(0, [&] {
+      HCHK(mvba_launch_lm_diag(S_->nc, S_->cdiag, o_.jacobi_scaling ? S_->sc : nullptr, 0.0, S_->scal + kRadSlot,
+                               o_.min_lm_diagonal, o_.max_lm_diagonal, S_->dmp, s_));
+      HCHK(mvba_launch_block_prec(S_->nblocks, S_->max_bsize, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng,
+                                  S_->dmp, S_->fac, s_));
+      schur_rhs();
+      cg_start();
+    });
+  }
+  static constexpr int kRadSlot = 20;  // scal[20]: 1/radius of the current step
+
+  // PCG on S delta_c = b (conjugate_gradients_solver.cc [ext]) with every
+  // scalar step on the device (CgCtl): iterations are enqueued in batches and
+  // gated by ctl->done, one host read per batch. Sharded solves run the same
+  // loop: the per-iteration exchange of the product is stream-ordered and the
+  // replicated camera-side state gives every rank the same stopping decisions.
+  // The start (cg_start) is part of the step prologue.
+  //
+  // Every launch argument of iteration i is a function of i mod 10 (the
+  // double-buffered p, r, direction records and p.q accumulator by the parity
+  // of i, the residual reset at i % 10 == 0; the iteration number itself is
+  // counted on the device, CgCtl::it), so solves capture runs of iterations as
+  // hipGraphs once per handle and replay them (RCCL-sharded solves too, with
+  // the exchange inside the graph): a batch of k iterations costs a few graph
+  // launches instead of 5 k kernel launches, whose host time (≈ 25 us per
+  // iteration, 5-6 us per hipLaunchKernel) bound the CG iteration of small
+  // problems (profiles/r05/r05b/s8_timing_r05b.log: enqueue 27.6 us vs 16.1 us
+  // of wait per iteration on the 1/8 c2 shard).
+  CgResult cg_device() {
+    CgResult R;
+    const int64_t n = S_->ng;
+    double* xv = S_->delta;
+    if (n == 0) return R;
     const int32_t* gate = &S_->ctl->done;
-    // Reprojection-only problems: the CG update's frame blocks form W z and the
-    // products combine it with the previous product's records (no direction
-    // kernel per iteration). Depth blocks read the direction in more kernels:
-    // they keep the direction kernel (MVBA_CG_DIR_KERNEL=1 forces it, for A/B).
-    const char* dk_env = std::getenv("MVBA_CG_DIR_KERNEL");  // read per call: tests switch it
-    const bool dir_kernel = dk_env && dk_env[0] == '1';
-    const bool fused_dir = h_->ndep == 0 && !dir_kernel;
+    const bool fused_dir = this->fused_dir();
+    const bool dz_pa = dz_in_pass_a();
     const mvba::FrameDirZ fz{h_->d_frame_lin, h_->d_fd, h_->d_frec, S_->dirz, (int32_t)h_->nframes, 0};
     // p[i & 1] = the direction of iteration i (p[(i - 1) & 1] the previous
     // one), r[i & 1] = the residual iteration i starts from, dirp likewise
@@ -810,17 +983,16 @@ class Solver {
     double* const Rv[2] = {S_->r, S_->r2};
     auto upd = [&](int32_t mode, const double* q, const double* p, const double* r_in, double* r_out) {
       HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, 0.0, p, q, S_->b, xv, r_in, r_out, S_->z, S_->partial,
-                                 S_->cnt, S_->scal + 8, S_->ctl, mvba::kIterFromCtl, fused_dir ? &fz : nullptr,
-                                 (mode & 1) && q ? pq_of(q) : nullptr, s_));
+                                 S_->cnt, S_->scal + 8, S_->ctl, mvba::kIterFromCtl,
+                                 fused_dir && !dz_pa ? &fz : nullptr, (mode & 1) && q ? pq_of(q) : nullptr, s_));
     };
-    upd(4 | 8, nullptr, P[0], Rv[0], Rv[1]);  // r = b, z = M^-1 r, rho
     auto body = [&](int i) {
       const mvba::LazyDir lz{S_->z, P[(i - 1) & 1], P[i & 1], n, S_->ctl, 0, 0.0};
       cg_par_ = i & 1;
       if (fused_dir)
         apply_schur_cg(S_->q, gate, S_->ctl, lz,
-                       mvba::DirPair{S_->dirz, S_->dirp[(i - 1) & 1], S_->dirp[i & 1], S_->ctl, lz.z, lz.p_old,
-                                     h_->d_frame_lin});
+                       mvba::DirPair{dz_pa ? nullptr : S_->dirz, S_->dirp[(i - 1) & 1], S_->dirp[i & 1], S_->ctl,
+                                     lz.z, lz.p_old, h_->d_frame_lin, dz_pa ? h_->d_frec : nullptr});
       else
         apply_schur(P[i & 1], S_->q, 0, gate, S_->ctl, &lz);
       double* r_in = Rv[i & 1];
@@ -833,23 +1005,8 @@ class Solver {
         upd(1 | 2 | 8, S_->q, P[i & 1], r_in, r_out);
       }
     };
-    // graphs: single rank, or a sharded solve exchanging through an RCCL
-    // communicator (the per-iteration ncclAllReduce is captured with the
-    // kernels around it: every rank replays the same runs, since the replicated
-    // camera-side CG state gives every rank the same batches); a caller's
-    // callback or the local communicator (host rendezvous) stays eager; a
-    // capturable (non-null) stream; deterministic mode once its slab plan is
-    // recorded (schur_rhs's product records it, so always here)
-    const char* g_env = std::getenv("MVBA_CG_GRAPH");  // read per call: tests switch it
-    const bool use_graphs = !(g_env && g_env[0] == '0') && exch_capturable_ && s_ != nullptr &&
-                            (!o_.deterministic || S_->b_det.ready) && !S_->graphs_broken;
-    if (use_graphs) {
-      std::vector<uintptr_t> sig = cg_signature(fused_dir);
-      if (sig != S_->graph_sig) {
-        S_->drop_graphs();
-        S_->graph_sig = std::move(sig);
-      }
-    }
+    refresh_graph_sig();
+    const bool use_graphs = graphs_enabled();
     // iterations [i, i + L) with i's offset o = (i - 1) % 10 and L <= 10 - o:
     // one replay of the captured run (captured on first use)
     auto run_chunk = [&](int i, int L) {
@@ -860,38 +1017,10 @@ class Solver {
           graph_launches_++;
           return;
         }
-      hipGraph_t graph = nullptr;
       hipGraphExec_t exec = nullptr;
-      // a refused capture is reported once per handle (stderr) and the solve
-      // goes on eagerly: the launches and exchanges of a failed capture never
-      // ran, so every rank (which fails the same way) re-enqueues them
-      auto broken = [&](const char* what, hipError_t e) {
-        (void)hipGetLastError();
-        S_->graphs_broken = true;
-        std::fprintf(stderr, "mvba_solve: CG graph capture refused at %s (%s)%s; eager launches from here\n", what,
-                     hipGetErrorString(e), o_.allreduce ? " with the RCCL exchange inside" : "");
-      };
-      const hipError_t eb = hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal);
-      if (eb != hipSuccess) {
-        broken("hipStreamBeginCapture", eb);
-        for (int k = 0; k < L; k++) body(i + k);
-        return;
-      }
-      bool ok = true;
-      try {
-        for (int k = 0; k < L; k++) body(i + k);
-      } catch (...) {
-        ok = false;
-      }
-      const hipError_t ec = hipStreamEndCapture(s_, &graph);
-      hipError_t ei = hipSuccess;
-      if (ok && ec == hipSuccess && graph) ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      if (graph) (void)hipGraphDestroy(graph);
-      if (!ok || ec != hipSuccess || !graph || ei != hipSuccess) {
-        if (exec) (void)hipGraphExecDestroy(exec);
-        broken(!ok ? "an enqueue inside the capture" : ec != hipSuccess || !graph ? "hipStreamEndCapture"
-                                                                                  : "hipGraphInstantiate",
-               !ok ? hipErrorStreamCaptureInvalidated : ec != hipSuccess ? ec : ei);
+      if (!capture([&] {
+            for (int k = 0; k < L; k++) body(i + k);
+          }, &exec)) {
         for (int k = 0; k < L; k++) body(i + k);  // this run eagerly; later ones too
         return;
       }
@@ -992,7 +1121,14 @@ class Solver {
   }
 
   // delta_p = -(V+D)^-1 (g_p + W' delta_c); returns model cost change -(g'delta + |J delta|^2 / 2)
+  // (fetch_now false: enqueue only, the three terms land in scal[0..2]). The
+  // enqueues are one captured graph per handle when graphs are on.
   double back_substitute(bool fetch_now = true) {
+    enqueue_seq(1, [&] { back_substitute_enqueue(); });
+    if (!fetch_now) return 0.0;
+    return model_change(fetch(3));
+  }
+  void back_substitute_enqueue() {
     HCHK(mvba_launch_frame_dir(h_->d_frame_lin, (int32_t)h_->nframes, h_->d_fd, h_->d_frec, S_->delta, S_->dir,
                                nullptr, nullptr, s_));
     // |J delta|^2 over the local reprojection and depth blocks -> scal[0].
@@ -1036,8 +1172,6 @@ class Solver {
     dot(3 * S_->np, S_->G + S_->ng, S_->delta + S_->ng, 1);  // g_p' delta_p (local points)
     exchange(S_->scal, 2, MVBA_REDUCE_SUM);
     dot(S_->ng, S_->G, S_->delta, 2);  // g_c' delta_c (global already)
-    if (!fetch_now) return 0.0;
-    return model_change(fetch(3));
   }
   // the model cost change from the back-substitution's scal[0..2]
   double model_change(const double* hs) {
@@ -1321,15 +1455,12 @@ void Solver::run(mvba_solver_summary* sum) {
     }
   }
   HCHK(mvba_launch_gather(S_->ng, S_->cam_poff, S_->np, h_->d_pt_off, h_->d_pt_free, h_->d_params, S_->x, s_));
+  upload_ctl0();
   double tl = now_s();
   double x_cost = linearize();
   sum->linearize_time_s += now_s() - tl;
   sum->initial_cost = x_cost;
-  const double* scale = nullptr;
-  if (o_.jacobi_scaling) {
-    HCHK(mvba_launch_jacobi_scale(nc, S_->cdiag, S_->sc, s_));
-    scale = S_->sc;
-  }
+  if (o_.jacobi_scaling) HCHK(mvba_launch_jacobi_scale(nc, S_->cdiag, S_->sc, s_));
   double gmax = grad_max_norm();
   double x_norm = std::sqrt(norm2_compact(S_->x));
   double radius = o_.initial_trust_region_radius, decrease = 2.0;
@@ -1374,11 +1505,7 @@ void Solver::run(mvba_solver_summary* sum) {
     const double it0 = now_s();
     // ComputeTrustRegionStep (LevenbergMarquardtStrategy::ComputeStep)
     const double ts = now_s();
-    HCHK(mvba_launch_lm_diag(nc, S_->cdiag, scale, 1.0 / radius, o_.min_lm_diagonal, o_.max_lm_diagonal, S_->dmp,
-                             s_));
-    HCHK(mvba_launch_block_prec(S_->nblocks, S_->max_bsize, S_->goff, S_->hoff, S_->bsize, S_->lin + S_->ng, S_->dmp,
-                                S_->fac, s_));
-    schur_rhs();
+    step_prologue(radius);  // damping, preconditioner, right-hand side, CG start
     if (cg_timing()) {
       HCHK(hipStreamSynchronize(s_));
       tm_.rhs += now_s() - ts;
@@ -1548,13 +1675,12 @@ void Solver::run(mvba_solver_summary* sum) {
   sum->total_time_s = now_s() - t0;
   if (cg_timing() && tm_.solves)
     std::fprintf(stderr,
-                 "mvba cg timing: %d solves, %d CG iterations (%d enqueued, %d batches) | us per solve: rhs+prec %.1f, "
-                 "cg start (|b| read) %.1f, back-substitution %.1f | us per enqueued iteration: enqueue %.1f, "
-                 "wait %.1f | loop us per CG iteration %.1f\n",
-                 tm_.solves, tm_.iters, tm_.enqueued, tm_.batches, 1e6 * tm_.rhs / tm_.solves,
-                 1e6 * tm_.start / tm_.solves, 1e6 * tm_.backsub / tm_.solves,
+                 "mvba cg timing: %d solves, %d CG iterations (%d enqueued, %d batches) | us per solve: prologue "
+                 "(damping, prec, rhs, cg start) %.1f, back-substitution %.1f | us per enqueued iteration: "
+                 "enqueue %.1f, wait %.1f | loop us per CG iteration %.1f | graph launches %d\n",
+                 tm_.solves, tm_.iters, tm_.enqueued, tm_.batches, 1e6 * tm_.rhs / tm_.solves, 1e6 * tm_.backsub / tm_.solves,
                  1e6 * tm_.enqueue / std::max(tm_.enqueued, 1), 1e6 * tm_.wait / std::max(tm_.enqueued, 1),
-                 1e6 * (tm_.enqueue + tm_.wait) / std::max(tm_.iters, 1));
+                 1e6 * (tm_.enqueue + tm_.wait) / std::max(tm_.iters, 1), graph_launches_);
 }
 
 }  // namespace

@@ -141,11 +141,41 @@ __device__ __forceinline__ void stage_dir(const DirPair& D, int frame, double* s
     beta = D.ctl->beta;
   }
   const int nrec = D.z ? 6 : N;  // entries taken from the frame records
-  for (int m = lane; m < nrec; m += 64) {
-    double v = D.dz[base + m];
-    if (!first) v = __fma_rn(beta, D.dp[base + m], v);
-    sd[m] = v;
-    if (writer) D.dp_out[base + m] = v;
+  if (D.frec) {
+    // the 6 pose sums W_f z of the frame from z itself (frame_dir_body's
+    // arithmetic): lane k < 22 takes pose column k, a butterfly over 32 lanes
+    const FrameLin& L = ((const FrameLin*)D.fl)[frame];
+    double u[6] = {0, 0, 0, 0, 0, 0};
+    if (lane < kPoseCols) {
+      const int blk = lane / 7;  // 0 beg, 1 end, 2 ref_to_cam, 3 offset (lane 21)
+      const int64_t g = L.goff[(blk == 3) ? MVBA_BLK_OFFSET : blk];
+      if (g >= 0) {
+        const double zv = D.z[g + (lane - 7 * blk)];
+        const double* wk = D.frec + (int64_t)frame * kFrameRecDoubles + 12 + 6 * lane;
+#pragma unroll
+        for (int a = 0; a < 6; a++) u[a] = wk[a] * zv;
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) u[a] += __shfl_xor(u[a], off, 64);
+    if (lane < 6) {
+      double v = u[0];
+#pragma unroll
+      for (int a = 1; a < 6; a++)
+        if (lane == a) v = u[a];
+      if (!first) v = __fma_rn(beta, D.dp[base + lane], v);
+      sd[lane] = v;
+      if (writer) D.dp_out[base + lane] = v;
+    }
+  } else {
+    for (int m = lane; m < nrec; m += 64) {
+      double v = D.dz[base + m];
+      if (!first) v = __fma_rn(beta, D.dp[base + m], v);
+      sd[m] = v;
+      if (writer) D.dp_out[base + m] = v;
+    }
   }
   if (D.z) {
     // intrinsic entries 0 focal, 1..2 centre, 3.. distortion: p_new's own
@@ -1753,12 +1783,16 @@ __global__ void k_jacobi_scale(int64_t n, const double* __restrict__ c, double* 
 
 // LevenbergMarquardtStrategy::ComputeStep [ext] on the scaled Jacobian J S:
 // D~^2 = clamp(s^2 c, min, max) / radius; unscaled damping = D~^2 / s^2.
+// 1/radius from device memory when inv_radius_dev is set (the solver's step
+// prologue is a captured graph: its launch arguments cannot change per step)
 __global__ void k_lm_diag(int64_t n, const double* __restrict__ c, const double* __restrict__ sc,
-                          double inv_radius, double dmin, double dmax, double* __restrict__ d) {
+                          double inv_radius, const double* __restrict__ inv_radius_dev, double dmin, double dmax,
+                          double* __restrict__ d) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
+  const double ir = inv_radius_dev ? *inv_radius_dev : inv_radius;
   const double s2 = sc ? sc[e] * sc[e] : 1.0;
-  d[e] = fmin(fmax(s2 * c[e], dmin), dmax) * inv_radius / s2;
+  d[e] = fmin(fmax(s2 * c[e], dmin), dmax) * ir / s2;
 }
 
 // compact <- packed parameters (constant points read as 0)
@@ -2176,10 +2210,11 @@ hipError_t mvba_launch_jacobi_scale(int64_t n, const double* c, double* sc, hipS
   return hipGetLastError();
 }
 
-hipError_t mvba_launch_lm_diag(int64_t n, const double* c, const double* sc, double inv_radius, double dmin,
-                               double dmax, double* d, hipStream_t s) {
+hipError_t mvba_launch_lm_diag(int64_t n, const double* c, const double* sc, double inv_radius,
+                               const double* inv_radius_dev, double dmin, double dmax, double* d, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_lm_diag, grid1(n), dim3(256), 0, s, n, c, sc, inv_radius, dmin, dmax, d);
+  hipLaunchKernelGGL(mvba::k_lm_diag, grid1(n), dim3(256), 0, s, n, c, sc, inv_radius, inv_radius_dev, dmin, dmax,
+                     d);
   return hipGetLastError();
 }
 

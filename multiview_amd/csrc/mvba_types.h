@@ -204,6 +204,10 @@ struct DirPair {
   const double* z = nullptr;      // intrinsic entries from z / p_old (null: from dz / dp)
   const double* p_old = nullptr;
   const void* fl = nullptr;       // FrameLin
+  // set (with dz null): the pose sums W_f z are formed here from z and the
+  // frame records (w_k per pose column) instead of read from dz, so the CG
+  // update needs no frame blocks
+  const double* frec = nullptr;
 };
 
 // Frame blocks of the CG update kernel: dz = W z for every frame, z = M^-1 r_new

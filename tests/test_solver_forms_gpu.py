@@ -150,11 +150,13 @@ def test_point_solve_forms_agree(monkeypatch, long_tracks):
 
 @pytest.mark.gpu
 def test_cg_direction_forms_agree(monkeypatch):
-    """The CG direction records (MVBA_CG_DIR_KERNEL, read per call): the
-    default forms W p as W z + beta W p_old (the update kernel's FrameDirZ
-    blocks + pass A's DirPair writer), the direction-kernel form computes
-    W (z + beta p_old) in k_frame_dir. The problem is sized so linear solves
-    run past 10 CG iterations, i.e. through Ceres' residual reset.
+    """The CG direction records (MVBA_CG_DIR_KERNEL, MVBA_CG_DZ, read per
+    call): the default forms W p as W z + beta W p_old with pass A forming the
+    pose sums W z of its frame from z (DirPair::frec) and keeping W p for the
+    next product (DirPair writer); "update" takes W z from the CG update
+    kernel's frame blocks (FrameDirZ) instead; the direction-kernel form
+    computes W (z + beta p_old) in k_frame_dir. The problem is sized so linear
+    solves run past 10 CG iterations, i.e. through Ceres' residual reset.
 
     Each form is checked against the CPU's exact step, not against the other
     form: oracle/lm_reference.first_step_system builds the first LM
@@ -187,8 +189,9 @@ def test_cg_direction_forms_agree(monkeypatch):
     tol = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
     sysm = _exact_step_system(P)
     conv = []
-    for form in ("0", "1"):
-        monkeypatch.setenv("MVBA_CG_DIR_KERNEL", form)
+    for form in ("0", "update", "1"):
+        monkeypatch.setenv("MVBA_CG_DIR_KERNEL", "1" if form == "1" else "0")
+        monkeypatch.setenv("MVBA_CG_DZ", form if form == "update" else "passa")
         with Evaluator(P) as ev:
             ev.set_params()
             s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=4000, use_loss=1,
@@ -200,6 +203,7 @@ def test_cg_direction_forms_agree(monkeypatch):
             ev.set_params()
             s = ev.solve(max_num_iterations=200, use_loss=1, robust_threshold=3.0, **tol)
             conv.append(s)
-    sa, sb = conv
-    assert sa["termination_type"] == 0 and sb["termination_type"] == 0, (sa["message"], sb["message"])
-    assert np.isclose(sa["final_cost"], sb["final_cost"], rtol=1e-9), (sa["final_cost"], sb["final_cost"])
+    sa = conv[0]
+    for sb in conv:
+        assert sb["termination_type"] == 0, sb["message"]
+        assert np.isclose(sa["final_cost"], sb["final_cost"], rtol=1e-9), (sa["final_cost"], sb["final_cost"])
