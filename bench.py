@@ -522,6 +522,11 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        # the LM phase captures its CG runs with the ncclAllReduce inside
+        # (mvba_solve.cpp cg_device): no user-buffer registration of captured
+        # collectives (56 KB exchanges gain nothing from zero-copy, and the
+        # registration would map the solver's buffers to every peer)
+        os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
         local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
         from datetime import timedelta

@@ -612,8 +612,9 @@ void mvba_solver_default_options(mvba_solver_options* o);
  * solve runs on. NULL with a single-rank solve (allreduce NULL): the library
  * waits for all earlier device work (hipDeviceSynchronize) and runs on its own
  * per-device stream, whose CG iterations it can capture and replay as graphs
- * (the null stream cannot be captured). NULL with a sharded solve: the null
- * stream itself. */
+ * (the null stream cannot be captured); likewise a solve sharded over an
+ * RCCL communicator (mvba_comm_init_rccl: one process per device). NULL with
+ * any other sharded solve: the null stream itself. */
 mvba_status mvba_solve(struct mvba_handle* h, const mvba_solver_options* o, mvba_solver_summary* summary,
                        void* hip_stream);
 /* Copy the handle's current packed parameter vector to host memory. */

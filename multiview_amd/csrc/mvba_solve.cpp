@@ -52,7 +52,14 @@ hipError_t mvba_launch_pass_sq(int model, int deg, const int4* chunks, int32_t n
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
                                const double* tinit, const double* V, const double* dp, const double4* pts,
                                double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
-                               const double4* dcbuf, hipStream_t s);
+                               const double4* dcbuf, const mvba::FusedStep* fs, hipStream_t s);
+hipError_t mvba_launch_upd_pass_a(int model, int deg, int64_t n, const mvba::CgEntry* ent, const double* minv,
+                                  const double* p, const double* q, const double* b, double* x, const double* r_in,
+                                  double* r_out, double* z, double* partial, unsigned* counters, double* out,
+                                  mvba::CgCtl* ctl, const double* pq_in, const int4* chunks, int32_t nchunks,
+                                  const void* fl, const mvba::FrameDesc* fd, const double* frec, const double* dp,
+                                  double* dz_out, const int32_t* slot_po, double4* cbuf, double* cbuf2,
+                                  const double* prec, const double4* obsX, hipStream_t s);
 hipError_t mvba_launch_point_w_seg(int32_t ntiles, const int4* tiles, const int32_t* wlane_pid,
                                    const int32_t* wlane_idx, const int64_t* pt_begin, const int32_t* po_idx,
                                    const double4* cbuf, const double* tinit, const double* V, const double* dp,
@@ -146,6 +153,7 @@ struct SolverState {
   double* zbuf = nullptr;     // [8 N] point-order z_o | J_pt rows
   double* wbuf = nullptr;     // [4 np] w_p of the last pass A (double4 per point)
   double* cbuf = nullptr;     // [4 slots] frame-order pass A: J_pt^T z per slot
+  double* cbuf2 = nullptr;    // [2 slots] the fused CG step's second product (c_p.y, c_p.z)
   double* obsX = nullptr;     // [4 slots] landmark of each slot (fixed during a linear solve)
   double* du = nullptr;       // [3 depth slots] u_d (point-order pass A) or z_d (k_depth_pa) -> k_depth_sb
   double* dcbuf = nullptr;    // [4 depth blocks] P z_d at the point-order position (k_depth_pa -> k_point_w)
@@ -197,7 +205,7 @@ struct SolverState {
 void solver_state_free(SolverState* S) {
   if (!S) return;
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
-                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->dirz, S->dirp[0], S->dirp[1], S->zbuf, S->wbuf, S->cbuf, S->obsX, S->du, S->dcbuf,
+                  S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->dirz, S->dirp[0], S->dirp[1], S->zbuf, S->wbuf, S->cbuf, S->cbuf2, S->obsX, S->du, S->dcbuf,
                   S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->ctl0, S->prec};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -262,6 +270,7 @@ SolverState* alloc_state(mvba_handle* h) {
     HCHK(dalloc(&S->zbuf, (size_t)(8 * N)));
     HCHK(dalloc(&S->wbuf, (size_t)(4 * std::max<int64_t>(S->np, 1))));
     HCHK(dalloc(&S->cbuf, (size_t)(4 * std::max<int64_t>(std::max<int64_t>(N, h->nslots), 1))));
+    HCHK(dalloc(&S->cbuf2, (size_t)(2 * std::max<int64_t>(std::max<int64_t>(N, h->nslots), 1))));
     HCHK(dalloc(&S->obsX, (size_t)(4 * std::max<int64_t>(h->nslots, 1))));
     HCHK(dalloc(&S->du, (size_t)(3 * h->ndep_slots)));
     HCHK(dalloc(&S->dcbuf, (size_t)(4 * std::max<int64_t>(h->ndep, 1))));
@@ -640,10 +649,7 @@ class Solver {
     // 132-144 us; c2, 3k chunks: equal; a 1/8 c2 shard, 470 chunks: 6.0 -> 10.3
     // us, so it keeps one segment per wave; profiles/r04/r04t/, r04w/).
     // MVBA_PASS_A_CHUNKS=0|1 forces one (read per call, for A/B timing)
-    const char* pa_env = std::getenv("MVBA_PASS_A_CHUNKS");
-    int32_t nchunks_all = 0;
-    for (const Group& G : h_->groups) nchunks_all += G.achunk_count;
-    const bool chunked = pa_env ? pa_env[0] == '1' : nchunks_all >= 4096;
+    const bool chunked = pass_a_chunked();
     // where pass A leaves c_o = J_pt^T z_o: at the observation's point-order
     // position (scattered 32-B stores, k_point_w reads its run) or in slot order
     // (coalesced stores, k_point_w gathers through po_slot). MVBA_CO_ORDER=
@@ -673,7 +679,32 @@ class Solver {
       HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
                                dir ? (const double4*)S_->cbuf : nullptr,
                                tinit, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf, 4, gate,
-                               dep ? h_->d_dpt_begin : nullptr, dep ? (const double4*)S_->dcbuf : nullptr, s_));
+                               dep ? h_->d_dpt_begin : nullptr, dep ? (const double4*)S_->dcbuf : nullptr, nullptr,
+                               s_));
+  }
+
+  bool pass_a_chunked() const {
+    const char* pa_env = std::getenv("MVBA_PASS_A_CHUNKS");
+    int32_t nchunks_all = 0;
+    for (const Group& G : h_->groups) nchunks_all += G.achunk_count;
+    return pa_env ? pa_env[0] == '1' : nchunks_all >= 4096;
+  }
+
+  // The fused CG step (k_upd_pass_a, mvba::FusedStep): the update of
+  // iteration i - 1 runs in the launch of iteration i's pass A, one grid-wide
+  // phase per CG iteration less; pass A then stores two products (+16 B per
+  // observation each way through k_point_w), which pays where the phases'
+  // fixed latency dominates: thin shards. Reprojection-only problems of one
+  // model group with the frame records from the update (fused_dir, not
+  // MVBA_CG_DZ=passa), per-slot records and the lane point solve.
+  // MVBA_CG_FUSE=0|1 forces it off / on (read per call); by default it runs
+  // below kFuseMaxObs observations.
+  static constexpr int64_t kFuseMaxObs = 400000;
+  bool fused_step() const {
+    if (!fused_dir() || dz_in_pass_a() || h_->groups.size() != 1 || !obsx() || point_w_tiles()) return false;
+    const char* e = std::getenv("MVBA_CG_FUSE");
+    if (e) return e[0] == '1';
+    return h_->nres <= kFuseMaxObs;
   }
 
   // k_point_w_seg (wave tiles of whole tracks, one lane per residual) when
@@ -753,7 +784,7 @@ class Solver {
         u(h_->d_po_frame), u(h_->d_po_meas), (uintptr_t)h_->npts, (uintptr_t)h_->nchunks,
         (uintptr_t)h_->ndep_segs, (uintptr_t)o_.deterministic,
         // the step prologue and back-substitution graphs (enqueue_seq)
-        bits(o_.min_lm_diagonal), bits(o_.max_lm_diagonal), (uintptr_t)o_.jacobi_scaling, env0("MVBA_BACKSUB"), env0("MVBA_CG_DZ"),
+        bits(o_.min_lm_diagonal), bits(o_.max_lm_diagonal), (uintptr_t)o_.jacobi_scaling, env0("MVBA_BACKSUB"), env0("MVBA_CG_DZ"), env0("MVBA_CG_FUSE"),
         (uintptr_t)h_->ndep, (uintptr_t)h_->nxyz, u(h_->d_dpo_slot), u(h_->d_xpt_begin), u(h_->d_xref), u(h_->d_xcc),
         u(h_->d_dep_order)};
     if (o_.deterministic) {
@@ -800,13 +831,17 @@ class Solver {
     const char* dk_env = std::getenv("MVBA_CG_DIR_KERNEL");  // read per call: tests switch it
     return h_->ndep == 0 && !(dk_env && dk_env[0] == '1');
   }
-  // With fused_dir: pass A forms the pose sums W_f z of its frame from z
-  // (stage_dir, DirPair::frec), so the CG update launches its entry blocks
-  // only (no frame blocks; one grid-wide phase of the update's latency less).
-  // MVBA_CG_DZ=update keeps the update's frame blocks (dz), for A/B timing.
+  // With fused_dir, MVBA_CG_DZ=passa: pass A forms the pose sums W_f z of its
+  // frame from z (stage_dir, DirPair::frec), so the CG update launches its
+  // entry blocks only. Measured slower, not the default (kernel traces,
+  // profiles/r06/r06a/cg_iter_r06a.txt): the update's time is its entry
+  // blocks' grid reduction (1/8 c2 shard 7.28 vs 7.52 us without / with the
+  // frame blocks; c2 8.32 vs 9.76), while every pass-A wave pays the frame's
+  // W z (a FrameLin load, then the z gathers: pass A 7.36 vs 5.60 us, c2 20.9
+  // vs 16.5). Default: the update's frame blocks write dz (read per call).
   bool dz_in_pass_a() const {
     const char* e = std::getenv("MVBA_CG_DZ");  // read per call: tests switch it
-    return fused_dir() && !(e && !std::strcmp(e, "update"));
+    return fused_dir() && e && !std::strcmp(e, "passa");
   }
 
   // Graphs: single rank, or a sharded solve exchanging through an RCCL
@@ -986,21 +1021,61 @@ class Solver {
                                  S_->cnt, S_->scal + 8, S_->ctl, mvba::kIterFromCtl,
                                  fused_dir && !dz_pa ? &fz : nullptr, (mode & 1) && q ? pq_of(q) : nullptr, s_));
     };
-    auto body = [&](int i) {
+    const int imax = std::max(o_.max_linear_solver_iterations, 1);
+    // the fused CG step: iteration i's pass A carries the update of iteration
+    // i - 1 (deferred by body(i - 1)), except at the start of a run of
+    // iterations (a graph run or an eager batch ends with its update, so the
+    // host's control-block read sees it) and after a residual reset
+    const bool fuse = fused_step();
+    const double* pending_pq = nullptr;  // the deferred update's p.q (its iteration's parity)
+    bool pending = false;
+    const Group& G0 = h_->groups[0];
+    const bool chunked = pass_a_chunked();
+    const bool co_slot = co_slot_order(std::getenv("MVBA_CO_ORDER"));
+    auto body = [&](int i, bool run_end) {
       const mvba::LazyDir lz{S_->z, P[(i - 1) & 1], P[i & 1], n, S_->ctl, 0, 0.0};
       cg_par_ = i & 1;
-      if (fused_dir)
+      if (pending) {
+        // update of iteration i - 1 (mode 1|2|8) + pass A of iteration i
+        HCHK(mvba_launch_upd_pass_a(G0.model, G0.deg, n, S_->ent, S_->fac, P[(i - 1) & 1], S_->q, S_->b, xv,
+                                    Rv[(i - 1) & 1], Rv[i & 1], S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl,
+                                    pending_pq, chunked ? h_->d_achunks + G0.achunk_begin
+                                                        : h_->d_segchunks + G0.seg_begin,
+                                    chunked ? G0.achunk_count : G0.seg_count, h_->d_frame_lin, h_->d_fd, h_->d_frec,
+                                    S_->dirp[(i - 1) & 1], S_->dirz, co_slot ? nullptr : h_->d_slot_po,
+                                    (double4*)S_->cbuf, S_->cbuf2, S_->prec, obsx(), s_));
+        // w_p from c_z + beta c_p; its frame blocks form this iteration's
+        // direction records d = d_z + beta d_p
+        mvba::FusedStep fs;
+        fs.dz = S_->dirz;
+        fs.dp = S_->dirp[(i - 1) & 1];
+        fs.dp_out = S_->dirp[i & 1];
+        fs.fd = h_->d_fd;
+        fs.fl = h_->d_frame_lin;
+        fs.ctl = S_->ctl;
+        fs.cbuf2 = S_->cbuf2;
+        fs.nframes = (int32_t)h_->nframes;
+        HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
+                                 (const double4*)S_->cbuf, nullptr, S_->phess, S_->dmp + S_->ng, h_->d_pts, S_->wbuf,
+                                 4, gate, nullptr, nullptr, &fs, s_));
+        reduce_frames(S_->q, lz.p_new, 0, S_->dirp[i & 1], gate, S_->ctl, &lz);
+        pending = false;
+      } else if (fused_dir) {
         apply_schur_cg(S_->q, gate, S_->ctl, lz,
                        mvba::DirPair{dz_pa ? nullptr : S_->dirz, S_->dirp[(i - 1) & 1], S_->dirp[i & 1], S_->ctl,
                                      lz.z, lz.p_old, h_->d_frame_lin, dz_pa ? h_->d_frec : nullptr});
-      else
+      } else {
         apply_schur(P[i & 1], S_->q, 0, gate, S_->ctl, &lz);
+      }
       double* r_in = Rv[i & 1];
       double* r_out = Rv[(i + 1) & 1];
       if (i % 10 == 0) {  // residual reset: r = b - A x
         upd(1, S_->q, P[i & 1], r_in, nullptr);
         apply_schur(xv, S_->tmp, 1, gate, nullptr);
         upd(4 | 8, S_->tmp, P[i & 1], r_in, r_out);
+      } else if (fuse && !run_end && i < imax) {
+        pending = true;  // into the next iteration's pass A
+        pending_pq = pq_of(S_->q);
       } else {
         upd(1 | 2 | 8, S_->q, P[i & 1], r_in, r_out);
       }
@@ -1019,9 +1094,10 @@ class Solver {
         }
       hipGraphExec_t exec = nullptr;
       if (!capture([&] {
-            for (int k = 0; k < L; k++) body(i + k);
+            for (int k = 0; k < L; k++) body(i + k, k == L - 1);
           }, &exec)) {
-        for (int k = 0; k < L; k++) body(i + k);  // this run eagerly; later ones too
+        pending = false;  // the failed capture's deferred update never ran: the run again, eagerly
+        for (int k = 0; k < L; k++) body(i + k, k == L - 1);  // this run eagerly; later ones too
         return;
       }
       S_->graphs.push_back(SolverState::CgGraph{o, L, exec});
@@ -1038,7 +1114,6 @@ class Solver {
     // ≈ 20 us at c2 and ≈ 36 us at c3 (a gated pass B alone is 10 us there).
     static const int second = std::getenv("MVBA_CG_BATCH2") ? std::max(1, std::atoi(std::getenv("MVBA_CG_BATCH2"))) : 2;
     int first = std::max(4, last_cg_iters_ - 2);
-    const int imax = std::max(o_.max_linear_solver_iterations, 1);
     // graph run length: 10 (one run per reset period) for long solves, shorter
     // runs (aligned to the period: 5, 2, 1) when the previous solve was short,
     // so rounding a batch up to whole runs adds few gated iterations (a gated
@@ -1082,7 +1157,7 @@ class Solver {
           i += L;
         }
       } else {
-        for (; i < iend; i++) body(i);
+        for (; i < iend; i++) body(i, i == iend - 1);
       }
       HCHK(hipMemcpyAsync(S_->hctl + slot, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
       HCHK(hipEventRecord(S_->ev_cg[slot - 1], s_));
@@ -1157,7 +1232,7 @@ class Solver {
       else
         HCHK(mvba_launch_point_w(h_->npts, h_->d_pt_begin, co_slot ? h_->d_po_slot : nullptr,
                                  (const double4*)S_->cbuf, S_->G + S_->ng, S_->phess, S_->dmp + S_->ng, h_->d_pts,
-                                 S_->delta + S_->ng, 3, nullptr, nullptr, nullptr, s_));
+                                 S_->delta + S_->ng, 3, nullptr, nullptr, nullptr, nullptr, s_));
       HCHK(mvba_launch_pass_sq(G.model, G.deg, h_->d_segchunks + G.seg_begin, G.seg_count, h_->d_obs_pid,
                                plain_dir(S_->dir), S_->delta + S_->ng, 3, S_->prec, obsx(), S_->partial,
                                S_->cnt + 5, S_->scal + 0, s_));
@@ -1752,11 +1827,18 @@ mvba_status mvba_solve(mvba_handle* h, const mvba_solver_options* o, mvba_solver
     // graphs cannot be captured on the null stream. The solve is host-
     // synchronous anyway (it ends with a stream sync); it starts after all
     // earlier device work, so it sees the caller's null-stream writes.
-    // (single-rank solves only: sharded ones keep the caller's stream, and a
-    // device-wide sync could wait on a peer shard's pending exchange)
+    // (single-rank and RCCL-sharded solves: shards of one process on the
+    // local communicator keep the caller's stream, where a device-wide sync
+    // could wait on a peer shard's pending exchange)
     hipStream_t st = (hipStream_t)stream;
     static const bool own = !(std::getenv("MVBA_OWN_STREAM") && std::getenv("MVBA_OWN_STREAM")[0] == '0');
-    if (!st && !o->allreduce && own) {
+    // (an RCCL-sharded solve too: one process per device, so the device-wide
+    // sync waits only for this rank's work, and its CG runs can be captured
+    // with the exchange inside; r06a: on the null stream every sharded CG
+    // kernel was launched eagerly)
+    const bool rccl = o->allreduce == &mvba_comm_allreduce &&
+                      mvba_comm_capturable((const mvba_comm*)o->allreduce_user);
+    if (!st && (!o->allreduce || rccl) && own) {
       HCHK(hipDeviceSynchronize());
       st = solver_stream(h->device);
       lib_stream = st;

@@ -339,6 +339,59 @@ __device__ __forceinline__ void pass_a_obs(const double* __restrict__ rec, const
   z[1] = z1;
 }
 
+// pass_a_obs for two frame directions at once (the fused CG step: the z record
+// and the previous direction's record), one projection: z1 = J_cam d1,
+// z2 = J_cam d2 and the point rows.
+template <int MODEL, int DEG>
+__device__ __forceinline__ void pass_a_obs2(const double* __restrict__ rec, const double* d1, const double* d2,
+                                            double4 X, double sr, double* z1, double* z2, double* P0, double* P1) {
+  const double f = rec[12];
+  const int K = (int)rec[17];
+  Proj o;
+  project<MODEL, DEG, kFastProj>(rec, X.x, X.y, X.z, f, rec[13], rec[14], rec + 18, K, rec[15], rec[16], o);
+  const double fz = fz_of<kFastProj>(f, o, sr);
+  const double G0[3] = {fz * o.A00, fz * o.A01, -fz * (o.A00 * o.nx + o.A01 * o.ny)};
+  const double G1[3] = {fz * o.A10, fz * o.A11, -fz * (o.A10 * o.nx + o.A11 * o.ny)};
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    P0[q] = G0[0] * rec[q] + G0[1] * rec[3 + q] + G0[2] * rec[6 + q];
+    P1[q] = G1[0] * rec[q] + G1[1] * rec[3 + q] + G1[2] * rec[6 + q];
+  }
+  double v[3], w[3];
+  cross(d1, o.Xc, v);
+  cross(d2, o.Xc, w);
+#pragma unroll
+  for (int q = 0; q < 3; q++) {
+    v[q] += d1[3 + q];
+    w[q] += d2[3 + q];
+  }
+  double a0 = G0[0] * v[0] + G0[1] * v[1] + G0[2] * v[2];
+  double a1 = G1[0] * v[0] + G1[1] * v[1] + G1[2] * v[2];
+  double b0 = G0[0] * w[0] + G0[1] * w[1] + G0[2] * w[2];
+  double b1 = G1[0] * w[0] + G1[1] * w[1] + G1[2] * w[2];
+  const double fx = o.df0 * sr, fy = o.df1 * sr;
+  a0 += fx * d1[6];
+  a1 += fy * d1[6];
+  b0 += fx * d2[6];
+  b1 += fy * d2[6];
+  if constexpr (MODEL != kModelRpc) {  // centre columns (RPC: structurally zero)
+    a0 += sr * d1[7];
+    a1 += sr * d1[8];
+    b0 += sr * d2[7];
+    b1 += sr * d2[8];
+  }
+  dist_columns<MODEL, DEG>(o, f, K, sr, [&](int q, double c0, double c1) {
+    a0 += c0 * d1[9 + q];
+    a1 += c1 * d1[9 + q];
+    b0 += c0 * d2[9 + q];
+    b1 += c1 * d2[9 + q];
+  });
+  z1[0] = a0;
+  z1[1] = a1;
+  z2[0] = b0;
+  z2[1] = b1;
+}
+
 // kLanesA lanes per point; each lane keeps its first kCacheA observations' rows
 // (z_o and the two J_pt rows: 8 doubles) in registers, later ones go through zbuf.
 constexpr int kLanesA = 4;
@@ -708,8 +761,19 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
                                                  const double* __restrict__ dp, const double4* __restrict__ pts,
                                                  double* __restrict__ wout, int32_t wstride,
                                                  const int32_t* __restrict__ gate, const int64_t* __restrict__ dbegin,
-                                                 const double4* __restrict__ dcbuf) {
+                                                 const double4* __restrict__ dcbuf, FusedStep fs) {
   if (gate && *gate) return;
+  if (fs.dz && (int32_t)blockIdx.x >= fs.point_blocks) {
+    // fused CG step: the frame direction d = d_z + beta d_p of this iteration
+    // (pass B's records and the next step's d_p), one wave per frame
+    const int f = ((int32_t)blockIdx.x - fs.point_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+    if (f >= fs.nframes) return;
+    const int64_t base = (int64_t)f * kDirStride;
+    const int nrec = min(9 + fs.fd[f].K, kDirStride);
+    const double beta = fs.ctl->beta;
+    for (int m = (int)(threadIdx.x & 63); m < nrec; m += 64) fs.dp_out[base + m] = __fma_rn(beta, fs.dp[base + m], fs.dz[base + m]);
+    return;
+  }
   const int64_t blk = xcd_block_solver((npts * kLanesW + 255) / 256);
   if (blk < 0) return;
   const int64_t t0 = blk * 256 + threadIdx.x;
@@ -733,7 +797,25 @@ __global__ void __launch_bounds__(256) k_point_w(int64_t npts, const int64_t* __
       for (int q = 0; q < 3; q++) ti[q] = tinit[3 * p + q];
   }
   double t[3] = {0.0, 0.0, 0.0};
-  if (valid && cbuf)
+  if (valid && cbuf && fs.cbuf2) {
+    // fused CG step: t = sum c_z + beta sum c_p (pass A could not know beta)
+    double tp[3] = {0.0, 0.0, 0.0};
+    const double2* __restrict__ c2 = (const double2*)fs.cbuf2;
+    for (int64_t j = pt_begin[p] + sub; j < pt_begin[p + 1]; j += kLanesW) {
+      const int64_t o = po_slot ? (int64_t)po_slot[j] : j;
+      const double4 cv = cbuf[o];
+      const double2 cw = c2[o];
+      t[0] += cv.x;
+      t[1] += cv.y;
+      t[2] += cv.z;
+      tp[0] += cv.w;
+      tp[1] += cw.x;
+      tp[2] += cw.y;
+    }
+    const double beta = fs.ctl->beta;
+#pragma unroll
+    for (int q = 0; q < 3; q++) t[q] = __fma_rn(beta, tp[q], t[q]);
+  } else if (valid && cbuf)
     for (int64_t j = pt_begin[p] + sub; j < pt_begin[p + 1]; j += kLanesW) {
       // po_slot set: pass A stored c_o in slot order; gather it
       const double4 cv = po_slot ? cbuf[po_slot[j]] : cbuf[j];
@@ -1433,57 +1515,45 @@ __device__ __forceinline__ double cg_zentry(const CgEntry& E, const double* __re
 // wave per frame: dz_f = W_f z from z recomputed for the frame's camera entries
 // (the next product's direction is then dz + beta dp, DirPair): the separate
 // direction kernel between this update and pass A is gone.
-__global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __restrict__ ent,
-                                                   const double* __restrict__ minv,
-                                                   int32_t mode, double alpha, const double* __restrict__ p,
-                                                   const double* __restrict__ q, const double* __restrict__ b,
-                                                   double* __restrict__ x, const double* __restrict__ r_in,
-                                                   double* __restrict__ r_out, double* __restrict__ z,
-                                                   double* __restrict__ partial, unsigned* __restrict__ counters,
-                                                   double* __restrict__ out, CgCtl* __restrict__ ctl, int32_t iter,
-                                                   FrameDirZ fz, const double* __restrict__ pq_in) {
-  if (ctl) {
-    if (ctl->done) return;
-    if (pq_in) {
-      // sharded solve: the step length from the exchanged p.q (every block
-      // computes the same value from the same inputs; block 0 records it)
-      const double pq = *pq_in;
-      const double a = ctl->rho_step / pq;
-      const bool indefinite = pq <= 0.0 || isinf(pq) || isnan(pq);
-      const bool bad = indefinite || isinf(a);
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctl->first = 0;
-        if (bad) {
-          ctl->status = indefinite ? 1 : 2;
-          ctl->done = 1;
-        } else {
-          ctl->alpha = a;
-        }
-      }
-      if (bad) return;
-      alpha = a;
+// The step length of the CG update: from the exchanged (sharded) or
+// atomically summed (single rank) p.q, pq_in, and rho_step (every block
+// computes the same value; `record`: this thread writes it to ctl), else the
+// reduction's ctl->alpha. False: the iteration stops here (indefinite / non-
+// finite step; ctl->done set by the recording thread).
+__device__ __forceinline__ bool cg_alpha(CgCtl* __restrict__ ctl, const double* __restrict__ pq_in, bool record,
+                                         double* alpha) {
+  if (!pq_in) {
+    *alpha = ctl->alpha;
+    return true;
+  }
+  const double pq = *pq_in;
+  const double a = ctl->rho_step / pq;
+  const bool indefinite = pq <= 0.0 || isinf(pq) || isnan(pq);
+  const bool bad = indefinite || isinf(a);
+  if (record) {
+    ctl->first = 0;
+    if (bad) {
+      ctl->status = indefinite ? 1 : 2;
+      ctl->done = 1;
     } else {
-      alpha = ctl->alpha;
+      ctl->alpha = a;
     }
   }
-  if (fz.dz && (int32_t)blockIdx.x >= fz.owner_blocks) {
-    const int f = ((int32_t)blockIdx.x - fz.owner_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
-    if (f >= fz.nframes) return;
-    const FrameLin& L = ((const FrameLin*)fz.fl)[f];
-    const int32_t K = fz.fd[f].K;
-    // z_j of camera block b straight from the frame's block offsets (the same
-    // entries and block-inverse row the entry threads use, without their
-    // CgEntry descriptor load)
-    auto Z = [&](int blk, int j) {
-      const int nb = blk <= MVBA_BLK_REF_TO_CAM ? 7 : blk == MVBA_BLK_CENTER ? 2 : blk == MVBA_BLK_DIST ? K : 1;
-      return cg_zentry(CgEntry{(int32_t)L.goff[blk], nb, L.hoff[blk] + (int64_t)j * nb}, minv, mode, alpha, q, b,
-                       r_in);
-    };
-    frame_dir_body<true>(L, K, fz.frec + (int64_t)f * kFrameRecDoubles, (int)(threadIdx.x & 63), Z,
-                         fz.dz + (int64_t)f * kDirStride);
-    return;
-  }
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  *alpha = a;
+  return !bad;
+}
+
+// The camera-entry part of a CG update (thread i of blocks [0, nb)): x, r, z
+// and, with mode & 8, the [x.b, x.r, r.z] grid sums whose last block takes the
+// step control (q-criterion, rho, beta) in ctl.
+__device__ __forceinline__ void cg_update_entries(int64_t i, int64_t n, const CgEntry* __restrict__ ent,
+                                                  const double* __restrict__ minv, int32_t mode, double alpha,
+                                                  const double* __restrict__ p, const double* __restrict__ q,
+                                                  const double* __restrict__ b, double* __restrict__ x,
+                                                  const double* __restrict__ r_in, double* __restrict__ r_out,
+                                                  double* __restrict__ z, double* __restrict__ partial,
+                                                  unsigned* __restrict__ counters, double* __restrict__ out,
+                                                  CgCtl* __restrict__ ctl, int32_t iter, unsigned nb) {
   double xb = 0.0, xr = 0.0, rz = 0.0;
   if (i < n) {
     const CgEntry E = ent[i];
@@ -1504,7 +1574,6 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
   }
   if (mode & 8) {
     double sums[3];
-    const unsigned nb = fz.dz ? (unsigned)fz.owner_blocks : 0u;
     if (grid_sum3_finalize(xb, xr, rz, partial, counters, out, sums, nb) && ctl && threadIdx.x == 0) {
       const double sxb = sums[0], sxr = sums[1];
       const double rho_next = sums[2];
@@ -1557,6 +1626,135 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
         ctl->iters = iter + 1;
         ctl->done = 1;
       }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __restrict__ ent,
+                                                   const double* __restrict__ minv,
+                                                   int32_t mode, double alpha, const double* __restrict__ p,
+                                                   const double* __restrict__ q, const double* __restrict__ b,
+                                                   double* __restrict__ x, const double* __restrict__ r_in,
+                                                   double* __restrict__ r_out, double* __restrict__ z,
+                                                   double* __restrict__ partial, unsigned* __restrict__ counters,
+                                                   double* __restrict__ out, CgCtl* __restrict__ ctl, int32_t iter,
+                                                   FrameDirZ fz, const double* __restrict__ pq_in) {
+  if (ctl) {
+    if (ctl->done) return;
+    // sharded / atomic p.q: the step length from the summed p.q (block 0 records it)
+    if (!cg_alpha(ctl, pq_in, blockIdx.x == 0 && threadIdx.x == 0, &alpha)) return;
+  }
+  if (fz.dz && (int32_t)blockIdx.x >= fz.owner_blocks) {
+    const int f = ((int32_t)blockIdx.x - fz.owner_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+    if (f >= fz.nframes) return;
+    const FrameLin& L = ((const FrameLin*)fz.fl)[f];
+    const int32_t K = fz.fd[f].K;
+    // z_j of camera block b straight from the frame's block offsets (the same
+    // entries and block-inverse row the entry threads use, without their
+    // CgEntry descriptor load)
+    auto Z = [&](int blk, int j) {
+      const int nb = blk <= MVBA_BLK_REF_TO_CAM ? 7 : blk == MVBA_BLK_CENTER ? 2 : blk == MVBA_BLK_DIST ? K : 1;
+      return cg_zentry(CgEntry{(int32_t)L.goff[blk], nb, L.hoff[blk] + (int64_t)j * nb}, minv, mode, alpha, q, b,
+                       r_in);
+    };
+    frame_dir_body<true>(L, K, fz.frec + (int64_t)f * kFrameRecDoubles, (int)(threadIdx.x & 63), Z,
+                         fz.dz + (int64_t)f * kDirStride);
+    return;
+  }
+  cg_update_entries((int64_t)blockIdx.x * blockDim.x + threadIdx.x, n, ent, minv, mode, alpha, p, q, b, x, r_in,
+                    r_out, z, partial, counters, out, ctl, iter, fz.dz ? (unsigned)fz.owner_blocks : 0u);
+}
+
+// The fused CG step (FusedStep): blocks [0, eb) run the update of iteration
+// i - 1 (k_cg_update's entry blocks, mode 1|2|8: x, r, z, the grid sums and
+// the step control), blocks from eb on run pass A of iteration i on its frame
+// chunks, one wave per chunk. A pass-A wave recomputes z = M^-1 (r - alpha q)
+// for its frame's camera entries (the entry blocks' arithmetic, the update's
+// frame blocks' form), stages the frame's z record and the previous
+// direction's record, and stores both products per slot (c_z | c_p.x in cbuf,
+// c_p.y, c_p.z in cbuf2): beta is known only once the entry blocks' grid
+// reduction has finished, i.e. in the next launch (k_point_w combines). The
+// wave of the frame's first chunk stores the z record (full: pose sums and
+// intrinsic entries) for k_point_w's frame blocks. eb is a multiple of 8, so
+// the pass-A blocks keep the XCD mapping of k_pass_a_frame. Reprojection-only,
+// one model group, obsX records (the host checks).
+template <int MODEL, int DEG>
+__global__ void __launch_bounds__(256) k_upd_pass_a(
+    int64_t n, const CgEntry* __restrict__ ent, const double* __restrict__ minv, const double* __restrict__ p,
+    const double* __restrict__ q, const double* __restrict__ b, double* __restrict__ x,
+    const double* __restrict__ r_in, double* __restrict__ r_out, double* __restrict__ z,
+    double* __restrict__ partial, unsigned* __restrict__ counters, double* __restrict__ out,
+    CgCtl* __restrict__ ctl, const double* __restrict__ pq_in, int32_t eb, const int4* __restrict__ chunks,
+    int32_t nchunks, const FrameLin* __restrict__ fl, const FrameDesc* __restrict__ fd,
+    const double* __restrict__ frec, const double* __restrict__ dp, double* __restrict__ dz_out,
+    const int32_t* __restrict__ slot_po, double4* __restrict__ cbuf, double2* __restrict__ cbuf2,
+    const double* __restrict__ prec, const double4* __restrict__ obsX) {
+  if (ctl->done) return;
+  double alpha = 0.0;
+  const bool entry = (int32_t)blockIdx.x < eb;
+  if (!cg_alpha(ctl, pq_in, entry && blockIdx.x == 0 && threadIdx.x == 0, &alpha)) return;
+  if (entry) {
+    cg_update_entries((int64_t)blockIdx.x * blockDim.x + threadIdx.x, n, ent, minv, 1 | 2 | 8, alpha, p, q, b, x,
+                      r_in, r_out, z, partial, counters, out, ctl, kIterFromCtl, (unsigned)eb);
+    return;
+  }
+  constexpr int ND = 6 + RowShape<MODEL, DEG>::kIntr;
+  __shared__ double sz[kPassAWaves][ND];
+  __shared__ double sp[kPassAWaves][ND];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t nb = (nchunks + kPassAWaves - 1) / kPassAWaves;
+  int64_t blk = -1;
+  {
+    // xcd_block_solver on the block index past the entry blocks
+    const int64_t bb = (int64_t)blockIdx.x - eb;
+    if (!MVBA_XCD_SOLVER) {
+      blk = bb < nb ? bb : -1;
+    } else {
+      const int64_t per = (nb + kXcds - 1) / kXcds;
+      const int64_t l = (bb % kXcds) * per + bb / kXcds;
+      blk = l < nb ? l : -1;
+    }
+  }
+  const int ch = (int)blk * kPassAWaves + wv;
+  if (blk < 0 || ch >= nchunks) return;
+  const int4 c = chunks[ch];
+  const int frame = __builtin_amdgcn_readfirstlane(c.z);
+  const int nobs = __builtin_amdgcn_readfirstlane(c.y);
+  const double* __restrict__ rec = prec + (int64_t)frame * kProjDoubles;
+  const int64_t base = (int64_t)frame * kDirStride;
+  double* d1 = sz[wv];
+  double* d2 = sp[wv];
+  for (int m = lane; m < ND; m += 64) {
+    d1[m] = 0.0;  // entries frame_dir_body leaves (past the live distortion columns)
+    d2[m] = dp[base + m];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  {
+    const FrameLin& L = fl[frame];
+    const int32_t K = fd[frame].K;
+    auto Z = [&](int bk, int j) {
+      const int nbk = bk <= MVBA_BLK_REF_TO_CAM ? 7 : bk == MVBA_BLK_CENTER ? 2 : bk == MVBA_BLK_DIST ? K : 1;
+      return cg_zentry(CgEntry{(int32_t)L.goff[bk], nbk, L.hoff[bk] + (int64_t)j * nbk}, minv, 1 | 2 | 8, alpha, q,
+                       b, r_in);
+    };
+    frame_dir_body<false>(L, K, frec + (int64_t)frame * kFrameRecDoubles, lane, Z, d1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (c.w)
+    for (int m = lane; m < ND; m += 64) dz_out[base + m] = d1[m];
+  for (int s0 = 0; s0 < nobs; s0 += 64) {
+    if (lane < nobs - s0) {
+      const int64_t i = (int64_t)c.x + s0 + lane;
+      const double4 X = obsX[i];
+      double za[2], zb[2], P0[3], P1[3];
+      pass_a_obs2<MODEL, DEG>(rec, d1, d2, X, X.w, za, zb, P0, P1);
+      const int64_t o = slot_po ? (int64_t)slot_po[i] : i;
+      cbuf[o] = make_double4(P0[0] * za[0] + P1[0] * za[1], P0[1] * za[0] + P1[1] * za[1],
+                             P0[2] * za[0] + P1[2] * za[1], P0[0] * zb[0] + P1[0] * zb[1]);
+      cbuf2[o] = make_double2(P0[1] * zb[0] + P1[1] * zb[1], P0[2] * zb[0] + P1[2] * zb[1]);
     }
   }
 }
@@ -2014,15 +2212,46 @@ hipError_t mvba_launch_pass_sq(int model, int deg, const int4* chunks, int32_t n
   return hipGetLastError();
 }
 
+// fs (nullable): the fused CG step's combination (mvba::FusedStep), with one
+// frame wave per frame after the point blocks
 hipError_t mvba_launch_point_w(int64_t npts, const int64_t* pt_begin, const int32_t* po_slot, const double4* cbuf,
                                const double* tinit, const double* V, const double* dp, const double4* pts,
                                double* wout, int32_t wstride, const int32_t* gate, const int64_t* dbegin,
-                               const double4* dcbuf, hipStream_t s) {
-  if (npts <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mvba::k_point_w, dim3(mvba::xcd_grid_solver((npts * mvba::kLanesW + 255) / 256)), dim3(256), 0, s,
-                     npts,
-                     pt_begin, po_slot,
-                     cbuf, tinit, V, dp, pts, wout, wstride, gate, dbegin, dcbuf);
+                               const double4* dcbuf, const mvba::FusedStep* fs, hipStream_t s) {
+  mvba::FusedStep f{};
+  const unsigned pb = npts > 0 ? mvba::xcd_grid_solver((npts * mvba::kLanesW + 255) / 256) : 0u;
+  unsigned fb = 0;
+  if (fs && fs->dz) {
+    f = *fs;
+    f.point_blocks = (int32_t)pb;
+    fb = (unsigned)((fs->nframes + 3) / 4);  // 4 frame waves per 256-thread block
+  }
+  if (pb + fb == 0) return hipSuccess;
+  hipLaunchKernelGGL(mvba::k_point_w, dim3(pb + fb), dim3(256), 0, s, npts, pt_begin, po_slot, cbuf, tinit, V, dp, pts,
+                     wout, wstride, gate, dbegin, dcbuf, f);
+  return hipGetLastError();
+}
+
+// The fused CG step (k_upd_pass_a): the update of the previous iteration (mode
+// 1|2|8, n camera entries) and this iteration's pass A in one launch.
+hipError_t mvba_launch_upd_pass_a(int model, int deg, int64_t n, const mvba::CgEntry* ent, const double* minv,
+                                  const double* p, const double* q, const double* b, double* x, const double* r_in,
+                                  double* r_out, double* z, double* partial, unsigned* counters, double* out,
+                                  mvba::CgCtl* ctl, const double* pq_in, const int4* chunks, int32_t nchunks,
+                                  const void* fl, const mvba::FrameDesc* fd, const double* frec, const double* dp,
+                                  double* dz_out, const int32_t* slot_po, double4* cbuf, double* cbuf2,
+                                  const double* prec, const double4* obsX, hipStream_t s) {
+  if (n <= 0 || !obsX || !ctl) return hipErrorInvalidValue;
+  // entry blocks rounded up to a multiple of 8: the pass-A blocks after them keep
+  // k_pass_a_frame's XCD mapping
+  const unsigned eb = (unsigned)(((n + 255) / 256 + 7) / 8 * 8);
+  const unsigned ab = nchunks > 0 ? mvba::xcd_grid_solver((nchunks + mvba::kPassAWaves - 1) / mvba::kPassAWaves) : 0u;
+#define MVBA_UPA(M, D)                                                                                        \
+  hipLaunchKernelGGL((mvba::k_upd_pass_a<M, D>), dim3(eb + ab), dim3(64 * mvba::kPassAWaves), 0, s, n, ent, minv, p, \
+                     q, b, x, r_in, r_out, z, partial, counters, out, ctl, pq_in, (int32_t)eb, chunks, nchunks,   \
+                     (const mvba::FrameLin*)fl, fd, frec, dp, dz_out, slot_po, cbuf, (double2*)cbuf2, prec, obsX)
+  MVBA_SOLVER_SWITCH(model, deg, MVBA_UPA)
+#undef MVBA_UPA
   return hipGetLastError();
 }
 

@@ -210,6 +210,26 @@ struct DirPair {
   const double* frec = nullptr;
 };
 
+// The fused CG step (k_upd_pass_a: the update of iteration i-1 and pass A of
+// iteration i in one launch). Pass A cannot know beta (the update's grid
+// reduction finishes inside the same launch), so it forms both products
+// c_z = J_pt^T J_cam d_z and c_p = J_pt^T J_cam d_p (d_z: the frame record of
+// z = M^-1 r_new, recomputed by each wave from r, q and alpha; d_p: the
+// previous direction's record) and the next launch combines them with beta:
+// k_point_w sums c_z + beta c_p (cbuf: c_z | c_p.x, cbuf2: c_p.y, c_p.z) and its
+// frame blocks store d = d_z + beta d_p for pass B and the next step.
+struct FusedStep {
+  const double* dz = nullptr;    // [frames * dir stride] z records (the fused pass A's writers)
+  const double* dp = nullptr;    // previous direction records
+  double* dp_out = nullptr;      // this iteration's direction records
+  const FrameDesc* fd = nullptr;
+  const void* fl = nullptr;      // FrameLin
+  const CgCtl* ctl = nullptr;    // beta
+  const double* cbuf2 = nullptr;  // [2 per slot] c_p.y, c_p.z
+  int32_t nframes = 0;
+  int32_t point_blocks = 0;      // k_point_w: blocks from here on are frame blocks
+};
+
 // Frame blocks of the CG update kernel: dz = W z for every frame, z = M^-1 r_new
 // recomputed from the same inputs as the entry blocks (owner_blocks of them);
 // the 6 pose sums only (pass A forms the intrinsic entries, DirPair::z).

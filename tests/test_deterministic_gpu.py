@@ -139,13 +139,16 @@ def test_graph_replayed_cg_equals_eager(monkeypatch, depth):
     assert np.array_equal(xa, xb)
 
 
-def test_rccl_captured_cg_equals_eager(monkeypatch):
+@pytest.mark.parametrize("null_stream", [False, True])
+def test_rccl_captured_cg_equals_eager(monkeypatch, null_stream):
     """The sharded solve's CG runs are captured with the exchange inside
     (mvba_solve.cpp cg_device: an RCCL communicator's ncclAllReduce is a plain
     enqueue on the solver's stream). Through a one-rank RCCL communicator
     (dist.Comm.rccl_world1: the fold-mode CG tail, p.q exchanged with the
     product), deterministic mode, captured == eager bit for bit, and the
-    captured solve did replay graphs (cg_graph_launches > 0)."""
+    captured solve did replay graphs (cg_graph_launches > 0). null_stream:
+    the caller passes the null stream (as bench.py's LM phase does), and the
+    library runs the RCCL-sharded solve on its own capturable stream."""
     from multiview_amd.dist import Comm
 
     P = _rig_problem(False)
@@ -158,7 +161,7 @@ def test_rccl_captured_cg_equals_eager(monkeypatch):
             with Evaluator(P) as ev:
                 ev.set_params()
                 s = ev.solve(max_num_iterations=6, use_loss=1, robust_threshold=3.0, deterministic=1, comm=comm,
-                             stream=st.cuda_stream, **TOL)
+                             stream=None if null_stream else st.cuda_stream, **TOL)
                 runs.append((s, ev.get_params()))
     finally:
         comm.close()

@@ -151,10 +151,13 @@ def test_point_solve_forms_agree(monkeypatch, long_tracks):
 @pytest.mark.gpu
 def test_cg_direction_forms_agree(monkeypatch):
     """The CG direction records (MVBA_CG_DIR_KERNEL, MVBA_CG_DZ, read per
-    call): the default forms W p as W z + beta W p_old with pass A forming the
-    pose sums W z of its frame from z (DirPair::frec) and keeping W p for the
-    next product (DirPair writer); "update" takes W z from the CG update
-    kernel's frame blocks (FrameDirZ) instead; the direction-kernel form
+    call): the default forms W p as W z + beta W p_old with W z from the CG
+    update kernel's frame blocks (FrameDirZ) and pass A keeping W p for the
+    next product (DirPair writer); the fused CG step (MVBA_CG_FUSE,
+    k_upd_pass_a) runs the update inside the next pass A, which forms W z
+    itself and both products (c_z, c_p) for k_point_w to combine with beta,
+    whose frame blocks store W p; MVBA_CG_DZ=passa has pass A form the pose
+    sums W z of its frame from z (DirPair::frec) instead; the direction-kernel form
     computes W (z + beta p_old) in k_frame_dir. The problem is sized so linear
     solves run past 10 CG iterations, i.e. through Ceres' residual reset.
 
@@ -189,9 +192,13 @@ def test_cg_direction_forms_agree(monkeypatch):
     tol = dict(function_tolerance=1e-16, gradient_tolerance=1e-16, parameter_tolerance=1e-12)
     sysm = _exact_step_system(P)
     conv = []
-    for form in ("0", "update", "1"):
+    # "0": W z formed by pass A (MVBA_CG_DZ=passa); "update": the default (W z
+    # from the update's frame blocks, the fused CG step at this size);
+    # "nofuse": the same without the fused step; "1": the direction kernel
+    for form in ("0", "update", "nofuse", "1"):
         monkeypatch.setenv("MVBA_CG_DIR_KERNEL", "1" if form == "1" else "0")
-        monkeypatch.setenv("MVBA_CG_DZ", form if form == "update" else "passa")
+        monkeypatch.setenv("MVBA_CG_DZ", "passa" if form == "0" else "update")
+        monkeypatch.setenv("MVBA_CG_FUSE", "0" if form == "nofuse" else "1")
         with Evaluator(P) as ev:
             ev.set_params()
             s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=4000, use_loss=1,

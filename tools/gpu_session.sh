@@ -16,6 +16,8 @@
 #   kt         kernel traces of the CG iteration (tools/gpu_kt.sh; KT_CFGS, KT_VARS)
 #   ab         same-box A/B of bench lines against other builds (BASE="tools/ab/X/libmvba.so ...",
 #              AB_CFGS="c2 s8 c3"); the in-tree library is "cur"
+#   envab      same-box A/B of bench lines under env variants, with MVBA_CG_TIMING=1
+#              (ENV_VARS="name=VAR=V,VAR=V name2=..." ; ENV_CFGS="s8 r8 c2"), twice each
 #   pmc        PMC passes per config (tools/gpu_pmc.sh; PMC_CFGS)
 #   baroof     BA roofline of one CG iteration (tools/gpu_ba_roofline.sh; BA_CFGS)
 #
@@ -84,6 +86,25 @@ for step in ${STEPS//,/ }; do
       done
       unset MVBA_LIB
       python3 tools/bench_summary.py $OUT/ab_*_$TAG.log || true ;;
+    envab)
+      for k in 1 2; do
+        for v in ${ENV_VARS:-cur=MVBA_CG_GRAPH=1}; do
+          name=${v%%=*}; envs=${v#*=}
+          for c in ${ENV_CFGS:-s8 r8 c2}; do
+            case $c in
+              c2) A="--steps 500 --ba-iters 5" ;;
+              s8) A="--shard-of 8 --steps 200 --ba-iters 5" ;;
+              r8) A="--shard-of 8 --ba-exchange rccl --steps 200 --ba-iters 5" ;;
+              c3) A="--config c3 --steps 30 --ba-iters 2" ;;
+            esac
+            env ${envs//,/ } MVBA_CG_TIMING=1 timeout -k 10 300 python3 bench.py $A $NB > $OUT/envab_${c}_${name}_${k}_$TAG.log 2>&1
+            rc=$?
+            if [ $rc -ne 0 ]; then echo "envab $c $name failed (rc=$rc)"; tail -3 $OUT/envab_${c}_${name}_${k}_$TAG.log; exit $rc; fi
+            echo "$c $name $k: $(grep 'cg timing' $OUT/envab_${c}_${name}_${k}_$TAG.log | sed -n 2p | sed 's/.*| us per solve/us per solve/')"
+          done
+        done
+      done
+      python3 tools/bench_summary.py $OUT/envab_*_$TAG.log || true ;;
     pmc)
       PMC_CFGS=${PMC_CFGS:-c2} bash tools/gpu_pmc.sh $TAG || exit 1 ;;
     baroof)
