@@ -784,7 +784,7 @@ class Solver {
         u(h_->d_po_frame), u(h_->d_po_meas), (uintptr_t)h_->npts, (uintptr_t)h_->nchunks,
         (uintptr_t)h_->ndep_segs, (uintptr_t)o_.deterministic,
         // the step prologue and back-substitution graphs (enqueue_seq)
-        bits(o_.min_lm_diagonal), bits(o_.max_lm_diagonal), (uintptr_t)o_.jacobi_scaling, env0("MVBA_BACKSUB"), env0("MVBA_CG_DZ"), env0("MVBA_CG_FUSE"),
+        bits(o_.min_lm_diagonal), bits(o_.max_lm_diagonal), (uintptr_t)o_.jacobi_scaling, env0("MVBA_BACKSUB"), env0("MVBA_CG_DZ"), env0("MVBA_CG_FUSE"), env0("MVBA_REP_THREADS"),
         (uintptr_t)h_->ndep, (uintptr_t)h_->nxyz, u(h_->d_dpo_slot), u(h_->d_xpt_begin), u(h_->d_xref), u(h_->d_xcc),
         u(h_->d_dep_order)};
     if (o_.deterministic) {

@@ -2332,8 +2332,13 @@ hipError_t mvba_launch_rep_reduce_vec(double* yrep, int64_t ng, const double* di
   if (ng <= 0) return hipSuccess;
   if (local_dot == 2 && (!dot_out || !dot_zero || !ctl)) return hipErrorInvalidValue;
   const mvba::LazyDir l = lz ? *lz : mvba::LazyDir{};
-  hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + 255) / 256)), dim3(256), 0, s, yrep, ng, diag, x,
-                     y, partial, counter, dot_out, gate, ctl, l, local_dot, dot_zero);
+  // threads per block (MVBA_REP_THREADS=64|128|256, read per call; A/B timing):
+  // smaller blocks spread the replica reads (32 per entry) over more CUs
+  const char* te = std::getenv("MVBA_REP_THREADS");
+  const int nt = te ? std::atoi(te) : 256;
+  const unsigned threads = nt == 64 || nt == 128 ? (unsigned)nt : 256u;
+  hipLaunchKernelGGL(mvba::k_vec_rep_reduce, dim3((unsigned)((ng + threads - 1) / threads)), dim3(threads), 0, s, yrep,
+                     ng, diag, x, y, partial, counter, dot_out, gate, ctl, l, local_dot, dot_zero);
   return hipGetLastError();
 }
 
