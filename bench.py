@@ -300,7 +300,7 @@ def _stream_copy_gbs(torch, stream, nbytes=1 << 30, reps=10):
     return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02", "r01")  # newest first: committed PMC summaries are read from here
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02", "r01")  # newest first: committed PMC summaries are read from here
 
 
 def _profile_path(name):
@@ -1067,8 +1067,13 @@ def main():
                         "frac_wall": cgb / (wall_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                         "wall_note": "algorithmic bytes / (linear-solver wall time / CG iterations): includes the "
                                      "residual-reset products (every 10th), the per-solve setup and host reads"}
-                summ = _ba_summary(args.config)
-                if summ and whole_cfg:
+                # the whole config's summary, or the one-GPU shard rehearsal's own
+                # (ba_<cfg>_s<N>[_rccl].json: the rank-0 shard through the same exchange)
+                ba_key = (args.config if whole_cfg else
+                          f"{args.config}_s{args.shard_of}{'_rccl' if comm is not None else ''}"
+                          if world == 1 and args.shard_of > 1 else None)
+                summ = _ba_summary(ba_key) if ba_key else {}
+                if summ:
                     kus = summ["kernel_us_per_cg_iteration"]
                     roof.update({
                         "kernel_us": kus,
@@ -1079,8 +1084,9 @@ def main():
                         "valu_floor_us": summ["valu_floor_us"],
                         "valu_frac": summ["valu_floor_us"] / kus,
                         "source": summ["path"] + " (rocprofv3 kernel trace: median span of non-gated iterations "
-                                  "pass A -> update, boundaries included; FETCH_SIZE x2 + WRITE_SIZE and "
-                                  "SQ_INSTS_VALU per kernel, median of non-gated launches)",
+                                  "pass A -> update, or the fused step's period, boundaries included; FETCH_SIZE x2 "
+                                  "+ WRITE_SIZE and SQ_INSTS_VALU per kernel, median of non-gated launches)",
+                        "cg_form": summ.get("cg_form", "separate update"),
                     })
                 line["ba"]["roofline"] = roof
             if world > 1 or comm is not None:

@@ -7,9 +7,13 @@ usage: ba_roofline.py OUT.json CONFIG kernel_trace.csv fetch.csv write.csv sq.cs
 A CG iteration of a reprojection-only problem is the launch sequence
     k_pass_a_frame -> k_point_w -> k_pass_b -> k_vec_rep_reduce -> k_cg_update
 (the fused-direction CG; a k_frame_dir in front marks a residual-reset or
-right-hand-side product, which is skipped). Iterations whose pass B ran
-(> 8 us: gated launches past the CG stop take ~2-5 us) give
-  kernel_us      median over iterations of end(k_cg_update) - start(k_pass_a_frame)
+right-hand-side product, which is skipped), or, with the fused CG step (the
+default below 400k observations: thin shards),
+    k_upd_pass_a -> k_point_w -> k_pass_b -> k_vec_rep_reduce (-> k_upd_pass_a)
+whichever the trace holds more of. Iterations whose pass B ran (gated
+launches past the CG stop take ~2-5 us) give
+  kernel_us      median over iterations of end(k_cg_update) - start(k_pass_a_frame),
+                 or for the fused step start(next k_upd_pass_a) - start(k_upd_pass_a)
                  (kernel boundaries included), and the per-kernel medians;
 from the PMC passes, per kernel, the median over its launches in the upper
 half (the non-gated ones):
@@ -27,6 +31,7 @@ import sys
 from collections import defaultdict
 
 SEQ = ["k_pass_a_frame", "k_point_w", "k_pass_b", "k_vec_rep_reduce", "k_cg_update"]
+SEQ_FUSED = ["k_upd_pass_a", "k_point_w", "k_pass_b", "k_vec_rep_reduce"]
 
 
 def short(name):
@@ -35,39 +40,48 @@ def short(name):
     return {"k_point_w_seg": "k_point_w"}.get(name, name)  # the point solve's tile form
 
 
-def trace_iterations(path):
+def trace_iterations(path, seq=None):
+    """Non-gated CG iterations of the trace: (iterations, launch sequence).
+    seq None: the form the trace holds more iterations of."""
+    if seq is None:
+        a, b = trace_iterations(path, SEQ), trace_iterations(path, SEQ_FUSED)
+        return b if len(b[0]) > len(a[0]) else a
     ev = []
     with open(path) as f:
         for r in csv.DictReader(f):
             ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     ev.sort()
+    fused = seq[0] == "k_upd_pass_a"
     groups = []
-    for i in range(1, len(ev) - len(SEQ) + 1):
-        if [e[2] for e in ev[i:i + len(SEQ)]] != SEQ or ev[i - 1][2] == "k_frame_dir":
+    for i in range(1, len(ev) - len(seq)):
+        if [e[2] for e in ev[i:i + len(seq)]] != seq or ev[i - 1][2] == "k_frame_dir":
             continue
-        groups.append(ev[i:i + len(SEQ)])
+        if fused and ev[i + len(seq)][2] != "k_upd_pass_a":
+            continue  # the fused step's period ends at the next fused launch
+        groups.append((ev[i:i + len(seq)], ev[i + len(seq)]))
     if not groups:
-        return []
+        return [], seq
     # gated iterations (past the CG stop) return at once: their pass B is a
     # small fraction of a working one's (any chunking, any problem size)
-    pb_max = max((g[2][1] - g[2][0]) for g in groups)
+    pbs = sorted(g[0][2][1] - g[0][2][0] for g in groups)
+    pb_ref = pbs[len(pbs) // 2]
     its = []
-    for grp in groups:
-        if (grp[2][1] - grp[2][0]) < 0.4 * pb_max:
+    for grp, nxt in groups:
+        if (grp[2][1] - grp[2][0]) < 0.4 * pb_ref:
             continue
-        its.append({"span_us": (grp[-1][1] - grp[0][0]) / 1e3,
-                    **{k: (e[1] - e[0]) / 1e3 for k, e in zip(SEQ, grp)}})
-    return its
+        span = (nxt[0] - grp[0][0]) if fused else (grp[-1][1] - grp[0][0])
+        its.append({"span_us": span / 1e3, **{k: (e[1] - e[0]) / 1e3 for k, e in zip(seq, grp)}})
+    return its, seq
 
 
-def pmc(paths):
+def pmc(paths, seq=SEQ):
     d = defaultdict(lambda: defaultdict(list))
     for p in paths:
         with open(p) as f:
             for r in csv.DictReader(f):
                 d[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
-    for k in SEQ:
+    for k in seq:
         row = {}
         for c, v in d[k].items():
             v = sorted(v)[len(v) // 2:]
@@ -79,13 +93,13 @@ def pmc(paths):
 def main():
     out, cfg, trace, fetch, write, sq = sys.argv[1:7]
     extra = [a for a in sys.argv[7:8] if a]
-    its = trace_iterations(trace)
+    its, seq = trace_iterations(trace)
     if not its:
         raise SystemExit("no non-gated CG iterations in the trace")
-    counters = pmc([fetch, write, sq] + extra)
+    counters = pmc([fetch, write, sq] + extra, seq)
     per_k = {}
     traffic = valu = 0.0
-    for k in SEQ:
+    for k in seq:
         c = counters[k]
         fb = 2e3 * c.get("FETCH_SIZE", 0.0)  # KB -> bytes, x2 (gfx950 FETCH_SIZE)
         wb = 1e3 * c.get("WRITE_SIZE", 0.0)
@@ -103,6 +117,7 @@ def main():
         "config": cfg,
         "generator": "tools/ba_roofline.py",
         "iterations_used": len(its),
+        "cg_form": "fused step" if seq[0] == "k_upd_pass_a" else "separate update",
         "kernel_us_per_cg_iteration": st.median(i["span_us"] for i in its),
         "traffic_bytes_per_cg_iteration": traffic,
         "valu_insts_per_cg_iteration": valu,
