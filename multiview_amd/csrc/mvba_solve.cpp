@@ -98,7 +98,8 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
-                                 int32_t iter, const mvba::FrameDirZ* fz, const double* pq_in, hipStream_t s);
+                                 int32_t iter, const mvba::FrameDirZ* fz, const double* pq_in, mvba::CgMirror* mir,
+                                 hipStream_t s);
 hipError_t mvba_launch_axpby(int64_t n, double a, const double* x, double b, const double* y, double* out,
                              hipStream_t s);
 hipError_t mvba_launch_dot(int64_t n, const double* x, const double* y, double* partial, unsigned* counter, double* out,
@@ -165,6 +166,10 @@ struct SolverState {
   mvba::CgCtl* ctl0 = nullptr; // the solve's initial control block (options only; copied to ctl per linear solve)
   double* prec = nullptr;     // [nframes * kProjDoubles] projection records
   mvba::CgCtl* hctl = nullptr; // pinned host mirror
+  // host-coherent mapped CgMirror the batches' last update launches write
+  // (hmir: host address, dmir: its device address)
+  mvba::CgMirror* hmir = nullptr;
+  mvba::CgMirror* dmir = nullptr;
   int64_t npartial = 0;
   int32_t* bsize = nullptr;
   mvba::CgEntry* ent = nullptr;  // per camera entry: block start, size, inverse row
@@ -211,6 +216,7 @@ void solver_state_free(SolverState* S) {
     if (p) (void)hipFree(p);
   if (S->hscal) (void)hipHostFree(S->hscal);
   if (S->hctl) (void)hipHostFree(S->hctl);
+  if (S->hmir) (void)hipHostFree(S->hmir);
   S->b_det.release();
   S->drop_graphs();
   for (hipEvent_t e : S->ev)
@@ -291,6 +297,9 @@ SolverState* alloc_state(mvba_handle* h) {
     // [0]: the solve's initial control block (H2D source); [1], [2]: the
     // pipelined batches' read-backs
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hctl), 3 * sizeof(mvba::CgCtl)));
+    HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hmir), sizeof(mvba::CgMirror),
+                       hipHostMallocCoherent | hipHostMallocMapped));
+    HCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&S->dmir), S->hmir, 0));
     std::vector<int32_t> bs(S->nblocks);
     for (int32_t k = 0; k < S->nblocks; k++) {
       const int32_t bid = h->cam_block_ids[k];
@@ -785,6 +794,7 @@ class Solver {
         (uintptr_t)h_->ndep_segs, (uintptr_t)o_.deterministic,
         // the step prologue and back-substitution graphs (enqueue_seq)
         bits(o_.min_lm_diagonal), bits(o_.max_lm_diagonal), (uintptr_t)o_.jacobi_scaling, env0("MVBA_BACKSUB"), env0("MVBA_CG_DZ"), env0("MVBA_CG_FUSE"), env0("MVBA_REP_THREADS"),
+        (uintptr_t)mirror_on(), u(S_->dmir),
         (uintptr_t)h_->ndep, (uintptr_t)h_->nxyz, u(h_->d_dpo_slot), u(h_->d_xpt_begin), u(h_->d_xref), u(h_->d_xcc),
         u(h_->d_dep_order)};
     if (o_.deterministic) {
@@ -855,6 +865,13 @@ class Solver {
     const char* g_env = std::getenv("MVBA_CG_GRAPH");  // read per call: tests switch it
     return !(g_env && g_env[0] == '0') && exch_capturable_ && s_ != nullptr &&
            (!o_.deterministic || S_->b_det.ready) && !S_->graphs_broken;
+  }
+  // CG batches end in a host-coherent CgMirror (cg_device); MVBA_CG_MIRROR=0
+  // or pipelined batches (MVBA_CG_PIPE=1): a copy launch and an event
+  bool mirror_on() const {
+    const char* m = std::getenv("MVBA_CG_MIRROR");  // read per call: tests switch it
+    const char* pp = std::getenv("MVBA_CG_PIPE");
+    return !(m && m[0] == '0') && !(pp && pp[0] == '1');
   }
   // drops every captured graph whose launches no longer match (signature)
   void refresh_graph_sig() {
@@ -947,7 +964,7 @@ class Solver {
     const mvba::FrameDirZ fz{h_->d_frame_lin, h_->d_fd, h_->d_frec, S_->dirz, (int32_t)h_->nframes, 0};
     HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, 4 | 8, 0.0, S_->p, nullptr, S_->b, S_->delta, S_->r, S_->r2,
                                S_->z, S_->partial, S_->cnt, S_->scal + 8, S_->ctl, mvba::kIterFromCtl,
-                               fused_dir() && !dz_in_pass_a() ? &fz : nullptr, nullptr, s_));
+                               fused_dir() && !dz_in_pass_a() ? &fz : nullptr, nullptr, nullptr, s_));
   }
 
   // The template control block of this solve's linear solves (options only)
@@ -1016,10 +1033,23 @@ class Solver {
     // one), r[i & 1] = the residual iteration i starts from, dirp likewise
     double* const P[2] = {S_->p, S_->p2};
     double* const Rv[2] = {S_->r, S_->r2};
-    auto upd = [&](int32_t mode, const double* q, const double* p, const double* r_in, double* r_out) {
+    // The host learns where a batch ended from the CgMirror its last update
+    // launch writes into host-coherent memory (one spin on a pinned word), not
+    // from a device-to-host copy launch and an event after it. Every run of
+    // iterations (graph) or eager batch ends with one such launch; the host
+    // counts them. MVBA_CG_MIRROR=0 (read per call): the copy and the event.
+    // Pipelined batches keep the copies (two batches in flight).
+    const char* pipe_env = std::getenv("MVBA_CG_PIPE");  // read per call
+    const bool pipelined = pipe_env && pipe_env[0] == '1';
+    const bool mirror = mirror_on();
+    mvba::CgMirror* const mir = mirror ? S_->dmir : nullptr;
+    uint32_t mir_expected = 0;
+    if (mirror) __atomic_store_n(&S_->hmir->seq, 0u, __ATOMIC_RELEASE);  // ctl->mseq restarts with cg_start
+    auto upd = [&](int32_t mode, const double* q, const double* p, const double* r_in, double* r_out,
+                   mvba::CgMirror* m = nullptr) {
       HCHK(mvba_launch_cg_update(n, S_->ent, S_->fac, mode, 0.0, p, q, S_->b, xv, r_in, r_out, S_->z, S_->partial,
                                  S_->cnt, S_->scal + 8, S_->ctl, mvba::kIterFromCtl,
-                                 fused_dir && !dz_pa ? &fz : nullptr, (mode & 1) && q ? pq_of(q) : nullptr, s_));
+                                 fused_dir && !dz_pa ? &fz : nullptr, (mode & 1) && q ? pq_of(q) : nullptr, m, s_));
     };
     const int imax = std::max(o_.max_linear_solver_iterations, 1);
     // the fused CG step: iteration i's pass A carries the update of iteration
@@ -1072,12 +1102,12 @@ class Solver {
       if (i % 10 == 0) {  // residual reset: r = b - A x
         upd(1, S_->q, P[i & 1], r_in, nullptr);
         apply_schur(xv, S_->tmp, 1, gate, nullptr);
-        upd(4 | 8, S_->tmp, P[i & 1], r_in, r_out);
+        upd(4 | 8, S_->tmp, P[i & 1], r_in, r_out, run_end ? mir : nullptr);
       } else if (fuse && !run_end && i < imax) {
         pending = true;  // into the next iteration's pass A
         pending_pq = pq_of(S_->q);
       } else {
-        upd(1 | 2 | 8, S_->q, P[i & 1], r_in, r_out);
+        upd(1 | 2 | 8, S_->q, P[i & 1], r_in, r_out, run_end ? mir : nullptr);
       }
     };
     refresh_graph_sig();
@@ -1134,8 +1164,6 @@ class Solver {
     // (profiles/r05/r05k/): CG loop 42.5 vs 42.2 us per iteration (1/8 c2
     // shard), 73.6 vs 74.0 (c2), back-substitution +46 / +64 us per solve
     // behind the gated batch: not the default.
-    const char* pipe_env = std::getenv("MVBA_CG_PIPE");  // read per call
-    const bool pipelined = pipe_env && pipe_env[0] == '1';
     auto enqueue_batch = [&](int batch, int slot) {
       if (use_graphs) batch = (batch + kGraphRun - 1) / kGraphRun * kGraphRun;
       const double tb0 = now_s();
@@ -1155,17 +1183,40 @@ class Solver {
           const int L = std::min({kGraphRun - o % kGraphRun, 10 - o, imax + 1 - i});
           run_chunk(i, L);
           i += L;
+          mir_expected++;  // the run's last update mirrors
         }
       } else {
         for (; i < iend; i++) body(i, i == iend - 1);
+        mir_expected++;
       }
-      HCHK(hipMemcpyAsync(S_->hctl + slot, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
-      HCHK(hipEventRecord(S_->ev_cg[slot - 1], s_));
+      if (!mirror) {
+        HCHK(hipMemcpyAsync(S_->hctl + slot, S_->ctl, sizeof(mvba::CgCtl), hipMemcpyDeviceToHost, s_));
+        HCHK(hipEventRecord(S_->ev_cg[slot - 1], s_));
+      }
       if (cg_timing()) tm_.enqueue += now_s() - tb0;
     };
     auto wait_batch = [&](int slot) -> const mvba::CgCtl& {
       const double tw = now_s();
-      HCHK(hipEventSynchronize(S_->ev_cg[slot - 1]));
+      if (mirror) {
+        // spin on the pinned seq word; every 4096 polls ask the stream, so a
+        // failed launch (which never writes the mirror) surfaces as its error
+        const uint32_t want = mir_expected;
+        for (unsigned k = 1; __atomic_load_n(&S_->hmir->seq, __ATOMIC_ACQUIRE) != want; k++) {
+          if (k % 4096 == 0) {
+            const hipError_t e = hipStreamQuery(s_);
+            if (e == hipSuccess && __atomic_load_n(&S_->hmir->seq, __ATOMIC_ACQUIRE) != want)
+              throw StatusErr{MVBA_E_INVALID, "internal: CG batch ended without its control mirror"};
+            if (e != hipSuccess && e != hipErrorNotReady) HCHK(e);
+          }
+          __builtin_ia32_pause();
+        }
+        mvba::CgCtl& c = S_->hctl[slot];
+        c.done = S_->hmir->done;
+        c.status = S_->hmir->status;
+        c.iters = S_->hmir->iters;
+      } else {
+        HCHK(hipEventSynchronize(S_->ev_cg[slot - 1]));
+      }
       if (cg_timing()) tm_.wait += now_s() - tw;
       return S_->hctl[slot];
     };

@@ -1543,9 +1543,75 @@ __device__ __forceinline__ bool cg_alpha(CgCtl* __restrict__ ctl, const double* 
   return !bad;
 }
 
+// One thread: the control block's outcome into the host mirror (CgMirror).
+__device__ __forceinline__ void cg_mirror(CgCtl* __restrict__ ctl, CgMirror* __restrict__ mir) {
+  const uint32_t q = ++ctl->mseq;
+  mir->done = ctl->done;
+  mir->status = ctl->status;
+  mir->iters = ctl->iters;
+  __hip_atomic_store(&mir->seq, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The finalising thread of a CG update: the q-criterion, rho and beta of the
+// next iteration (conjugate_gradients_solver.cc [ext]) into ctl, from the
+// grid sums [x.b, x.r, r.z].
+__device__ __forceinline__ void cg_finalize(CgCtl* __restrict__ ctl, const double* sums, int32_t iter) {
+  const double sxb = sums[0], sxr = sums[1];
+  const double rho_next = sums[2];
+  if (iter == kIterFromCtl) iter = ctl->it++;
+  auto bad = [](double v) { return v == 0.0 || isinf(v) || isnan(v); };
+  if (iter == 0) {  // r = b, z = M^-1 r: initial rho, Q0 = 0
+    if (ctl->bb == 0.0) {  // "Convergence. |b| = 0." (x stays 0)
+      ctl->status = 0;
+      ctl->iters = 0;
+      ctl->done = 1;
+      return;
+    }
+    ctl->Q0 = 0.0;
+    ctl->first = 1;
+    if (bad(rho_next)) {
+      ctl->status = 2;
+      ctl->iters = 1;
+      ctl->done = 1;
+    }
+    ctl->rho = rho_next;
+    return;
+  }
+  ctl->iters = iter;
+  const double Q1 = -(sxb + sxr);
+  const double zeta = iter * (Q1 - ctl->Q0) / Q1;
+  if (zeta < ctl->eta && iter >= ctl->min_iter) {
+    ctl->status = 0;
+    ctl->done = 1;
+    return;
+  }
+  ctl->Q0 = Q1;
+  if (iter >= ctl->max_iter) {
+    ctl->status = 1;
+    ctl->done = 1;
+    return;
+  }
+  // top of the next iteration: rho, beta
+  const double last_rho = ctl->rho;
+  if (bad(rho_next)) {
+    ctl->status = 2;
+    ctl->iters = iter + 1;
+    ctl->done = 1;
+    return;
+  }
+  const double beta = rho_next / last_rho;
+  ctl->rho = rho_next;
+  ctl->beta = beta;
+  if (bad(beta)) {
+    ctl->status = 2;
+    ctl->iters = iter + 1;
+    ctl->done = 1;
+  }
+}
+
 // The camera-entry part of a CG update (thread i of blocks [0, nb)): x, r, z
 // and, with mode & 8, the [x.b, x.r, r.z] grid sums whose last block takes the
-// step control (q-criterion, rho, beta) in ctl.
+// step control (q-criterion, rho, beta) in ctl and, with mir, mirrors it.
 __device__ __forceinline__ void cg_update_entries(int64_t i, int64_t n, const CgEntry* __restrict__ ent,
                                                   const double* __restrict__ minv, int32_t mode, double alpha,
                                                   const double* __restrict__ p, const double* __restrict__ q,
@@ -1553,7 +1619,8 @@ __device__ __forceinline__ void cg_update_entries(int64_t i, int64_t n, const Cg
                                                   const double* __restrict__ r_in, double* __restrict__ r_out,
                                                   double* __restrict__ z, double* __restrict__ partial,
                                                   unsigned* __restrict__ counters, double* __restrict__ out,
-                                                  CgCtl* __restrict__ ctl, int32_t iter, unsigned nb) {
+                                                  CgCtl* __restrict__ ctl, int32_t iter, unsigned nb,
+                                                  CgMirror* __restrict__ mir = nullptr) {
   double xb = 0.0, xr = 0.0, rz = 0.0;
   if (i < n) {
     const CgEntry E = ent[i];
@@ -1575,57 +1642,8 @@ __device__ __forceinline__ void cg_update_entries(int64_t i, int64_t n, const Cg
   if (mode & 8) {
     double sums[3];
     if (grid_sum3_finalize(xb, xr, rz, partial, counters, out, sums, nb) && ctl && threadIdx.x == 0) {
-      const double sxb = sums[0], sxr = sums[1];
-      const double rho_next = sums[2];
-      if (iter == kIterFromCtl) iter = ctl->it++;
-      auto bad = [](double v) { return v == 0.0 || isinf(v) || isnan(v); };
-      if (iter == 0) {  // r = b, z = M^-1 r: initial rho, Q0 = 0
-        if (ctl->bb == 0.0) {  // "Convergence. |b| = 0." (x stays 0)
-          ctl->status = 0;
-          ctl->iters = 0;
-          ctl->done = 1;
-          return;
-        }
-        ctl->Q0 = 0.0;
-        ctl->first = 1;
-        if (bad(rho_next)) {
-          ctl->status = 2;
-          ctl->iters = 1;
-          ctl->done = 1;
-        }
-        ctl->rho = rho_next;
-        return;
-      }
-      ctl->iters = iter;
-      const double Q1 = -(sxb + sxr);
-      const double zeta = iter * (Q1 - ctl->Q0) / Q1;
-      if (zeta < ctl->eta && iter >= ctl->min_iter) {
-        ctl->status = 0;
-        ctl->done = 1;
-        return;
-      }
-      ctl->Q0 = Q1;
-      if (iter >= ctl->max_iter) {
-        ctl->status = 1;
-        ctl->done = 1;
-        return;
-      }
-      // top of the next iteration: rho, beta
-      const double last_rho = ctl->rho;
-      if (bad(rho_next)) {
-        ctl->status = 2;
-        ctl->iters = iter + 1;
-        ctl->done = 1;
-        return;
-      }
-      const double beta = rho_next / last_rho;
-      ctl->rho = rho_next;
-      ctl->beta = beta;
-      if (bad(beta)) {
-        ctl->status = 2;
-        ctl->iters = iter + 1;
-        ctl->done = 1;
-      }
+      cg_finalize(ctl, sums, iter);
+      if (mir) cg_mirror(ctl, mir);
     }
   }
 }
@@ -1638,11 +1656,20 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
                                                    double* __restrict__ r_out, double* __restrict__ z,
                                                    double* __restrict__ partial, unsigned* __restrict__ counters,
                                                    double* __restrict__ out, CgCtl* __restrict__ ctl, int32_t iter,
-                                                   FrameDirZ fz, const double* __restrict__ pq_in) {
+                                                   FrameDirZ fz, const double* __restrict__ pq_in,
+                                                   CgMirror* __restrict__ mir) {
   if (ctl) {
-    if (ctl->done) return;
+    // (a stopped or failed step still mirrors its state: block 0, thread 0)
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (ctl->done) {
+      if (mir && lead) cg_mirror(ctl, mir);
+      return;
+    }
     // sharded / atomic p.q: the step length from the summed p.q (block 0 records it)
-    if (!cg_alpha(ctl, pq_in, blockIdx.x == 0 && threadIdx.x == 0, &alpha)) return;
+    if (!cg_alpha(ctl, pq_in, lead, &alpha)) {
+      if (mir && lead) cg_mirror(ctl, mir);
+      return;
+    }
   }
   if (fz.dz && (int32_t)blockIdx.x >= fz.owner_blocks) {
     const int f = ((int32_t)blockIdx.x - fz.owner_blocks) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
@@ -1662,7 +1689,7 @@ __global__ void __launch_bounds__(256) k_cg_update(int64_t n, const CgEntry* __r
     return;
   }
   cg_update_entries((int64_t)blockIdx.x * blockDim.x + threadIdx.x, n, ent, minv, mode, alpha, p, q, b, x, r_in,
-                    r_out, z, partial, counters, out, ctl, iter, fz.dz ? (unsigned)fz.owner_blocks : 0u);
+                    r_out, z, partial, counters, out, ctl, iter, fz.dz ? (unsigned)fz.owner_blocks : 0u, mir);
 }
 
 // The fused CG step (FusedStep): blocks [0, eb) run the update of iteration
@@ -2357,7 +2384,8 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
                                  const double* p,
                                  const double* q, const double* b, double* x, const double* r_in, double* r_out,
                                  double* z, double* partial, unsigned* counters, double* out, mvba::CgCtl* ctl,
-                                 int32_t iter, const mvba::FrameDirZ* fz, const double* pq_in, hipStream_t s) {
+                                 int32_t iter, const mvba::FrameDirZ* fz, const double* pq_in, mvba::CgMirror* mir,
+                                 hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 255) / 256);
   mvba::FrameDirZ f{};
@@ -2368,7 +2396,7 @@ hipError_t mvba_launch_cg_update(int64_t n, const mvba::CgEntry* ent, const doub
     fblocks = (unsigned)((fz->nframes + 3) / 4);  // 4 frame waves per 256-thread block
   }
   hipLaunchKernelGGL(mvba::k_cg_update, dim3(blocks + fblocks), dim3(256), 0, s, n, ent, minv, mode, alpha,
-                     p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter, f, pq_in);
+                     p, q, b, x, r_in, r_out, z, partial, counters, out, ctl, iter, f, pq_in, mir);
   return hipGetLastError();
 }
 

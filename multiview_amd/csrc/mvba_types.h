@@ -161,6 +161,18 @@ struct CgCtl {
   double bb;        // b.b of the linear solve (|b| = 0: converged at iteration 0, x = 0)
   int32_t it;       // next CG iteration number (the update kernel's finalisation counts on the device,
                     // so a captured iteration's launch arguments do not depend on its number)
+  uint32_t mseq;    // mirror writes of this linear solve (CgMirror::seq)
+};
+
+// The CG state a batch of iterations ends in, written by the batch's last
+// update launch straight into host-coherent pinned memory (no copy launch, no
+// event): seq last, with a system-scope release, so the host that sees the seq
+// it waits for sees the fields written before it.
+struct CgMirror {
+  int32_t done;
+  int32_t status;
+  int32_t iters;
+  uint32_t seq;
 };
 constexpr int32_t kIterFromCtl = -2;  // k_cg_update iter argument: take it from CgCtl::it
 

@@ -139,6 +139,36 @@ def test_graph_replayed_cg_equals_eager(monkeypatch, depth):
     assert np.array_equal(xa, xb)
 
 
+def test_cg_control_mirror_equals_copy(monkeypatch):
+    """Where a batch of CG iterations ended reaches the host through the
+    CgMirror the batch's last update launch writes into host-coherent memory
+    (mvba_solve.cpp cg_device), or, with MVBA_CG_MIRROR=0 / pipelined batches,
+    through a device-to-host copy and an event. The host only decides where
+    the next batch starts, so every form gives the same deterministic solve,
+    bit for bit, eager and captured; solves whose CG stops inside a batch
+    mirror from gated launches too (the stop is not the batch's last
+    iteration)."""
+    P = _rig_problem(False)
+    runs = []
+    for env in ({"MVBA_CG_MIRROR": "0"}, {"MVBA_CG_MIRROR": "1"}, {"MVBA_CG_MIRROR": "1", "MVBA_CG_GRAPH": "0"},
+                {"MVBA_CG_PIPE": "1"}):
+        for k in ("MVBA_CG_MIRROR", "MVBA_CG_GRAPH", "MVBA_CG_PIPE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(max_num_iterations=6, use_loss=1, robust_threshold=3.0, deterministic=1, **TOL)
+            runs.append((env, s, ev.get_params()))
+    _, s0, x0 = runs[0]
+    assert s0["num_linear_iterations"] > 20, s0["num_linear_iterations"]
+    for env, s, x in runs[1:]:
+        for k in ("termination_type", "num_iterations", "num_successful_steps", "num_linear_iterations",
+                  "final_cost"):
+            assert s[k] == s0[k], (env, k, s[k], s0[k])
+        assert np.array_equal(x, x0), env
+
+
 @pytest.mark.parametrize("null_stream", [False, True])
 def test_rccl_captured_cg_equals_eager(monkeypatch, null_stream):
     """The sharded solve's CG runs are captured with the exchange inside
