@@ -37,6 +37,9 @@
 #include <string>
 #include <vector>
 
+// mvba_solve.cpp: drops the captured graphs that hold a communicator's collectives
+extern "C" void mvba_drop_comm_graphs(const void* comm);
+
 #include "../../include/mvba/mvba.h"
 
 namespace {
@@ -323,6 +326,7 @@ mvba_status mvba_comm_abort(mvba_comm* c) {
 
 void mvba_comm_destroy(mvba_comm* c) {
   if (!c) return;
+  mvba_drop_comm_graphs(c);  // graphs holding this communicator's collectives go first
   if (c->kind == 0) {
     std::lock_guard<std::mutex> lk(c->nccl_m);
     if (c->nccl && !c->aborted.exchange(true)) (void)ncclCommDestroy(c->nccl);

@@ -92,6 +92,11 @@ hipError_t mvba_launch_depth_cost(int64_t nslots, const mvba::DepthDesc* dd, con
 // rendezvous, no event waits across streams), so a hipGraph capture of the
 // solver's stream can hold it (mvba_comm.hip)
 int32_t mvba_comm_capturable(const mvba_comm* comm);
+// Drops every captured graph (CG runs, step sequences) recorded with this
+// communicator's collectives inside, before the communicator goes
+// (mvba_comm_destroy; RCCL keeps per-graph resources of a captured
+// collective until its graph is destroyed) (mvba_solve.cpp)
+void mvba_drop_comm_graphs(const void* comm);
 }
 
 // Row layout of a host hand-over (mvba_transfer.hip): residual rows per block,

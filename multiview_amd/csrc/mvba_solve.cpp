@@ -195,6 +195,7 @@ struct SolverState {
   std::vector<SeqGraph> seq_graphs;
   std::vector<uintptr_t> graph_sig;
   bool graphs_broken = false;  // a capture failed: eager launches from then on
+  const void* graph_comm = nullptr;  // the library communicator whose collectives the graphs hold
   hipEvent_t ev[2] = {nullptr, nullptr};  // the merged LM step's candidate-evaluation span
   hipEvent_t ev_cg[2] = {nullptr, nullptr};  // the CG's pipelined batches
   void drop_graphs() {
@@ -207,8 +208,34 @@ struct SolverState {
   }
 };
 
+// Solver states whose captured graphs hold a library communicator's
+// collectives, by communicator (mvba_drop_comm_graphs)
+static std::mutex g_comm_graphs_m;
+static std::vector<SolverState*> g_comm_graphs;
+
+static void comm_graphs_forget(SolverState* S) {
+  std::lock_guard<std::mutex> lk(g_comm_graphs_m);
+  g_comm_graphs.erase(std::remove(g_comm_graphs.begin(), g_comm_graphs.end(), S), g_comm_graphs.end());
+  S->graph_comm = nullptr;
+}
+
+void mvba_drop_comm_graphs(const void* comm) {
+  std::lock_guard<std::mutex> lk(g_comm_graphs_m);
+  for (SolverState* S : g_comm_graphs)
+    if (S->graph_comm == comm) {
+      S->drop_graphs();
+      S->graph_sig.clear();  // the next solve captures afresh
+      S->graph_comm = nullptr;
+    }
+  g_comm_graphs.erase(std::remove_if(g_comm_graphs.begin(), g_comm_graphs.end(),
+                                     [](SolverState* S) { return S->graph_comm == nullptr; }),
+                      g_comm_graphs.end());
+}
+
 void solver_state_free(SolverState* S) {
   if (!S) return;
+  comm_graphs_forget(S);
+  S->drop_graphs();  // before the buffers their launches name
   void* ptrs[] = {S->lin, S->phess, S->G, S->cdiag, S->sc, S->dmp, S->fac, S->x, S->xn, S->delta, S->scr, S->lo,
                   S->hi, S->b, S->r, S->r2, S->z, S->p, S->p2, S->q, S->tmp, S->yrep, S->dir, S->dirz, S->dirp[0], S->dirp[1], S->zbuf, S->wbuf, S->cbuf, S->cbuf2, S->obsX, S->du, S->dcbuf,
                   S->cnt, S->partial, S->scal, S->bsize, S->ent, S->goff, S->hoff, S->cam_poff, S->ctl, S->ctl0, S->prec};
@@ -919,6 +946,12 @@ class Solver {
                                                                                 : "hipGraphInstantiate",
              !ok ? hipErrorStreamCaptureInvalidated : ec != hipSuccess ? ec : ei);
       return false;
+    }
+    if (o_.allreduce == &mvba_comm_allreduce && S_->graph_comm != o_.allreduce_user) {
+      // the graph holds this communicator's collectives: mvba_comm_destroy drops it first
+      std::lock_guard<std::mutex> lk(g_comm_graphs_m);
+      if (!S_->graph_comm) g_comm_graphs.push_back(S_);
+      S_->graph_comm = o_.allreduce_user;
     }
     return true;
   }
@@ -1838,8 +1871,16 @@ void mvba_solver_default_options(mvba_solver_options* o) {
 // One non-blocking stream per device for solves called on the null stream,
 // created on first use and kept for the process's lifetime (handles come and go
 // per pass in the CLI; a stream per handle would be created and destroyed with
-// each, and the sanitizer build's runtime teardown trips over the freed queue
-// memory it still holds: profiles/r05/r05h/san_cli_g0_r05h.log).
+// each). The sanitizer build's failure with per-handle streams
+// (profiles/r05/r05h/san_cli_g0_r05h.log:124-153): at exit, libamdhip64's own
+// static destructors (__cxa_finalize) free HSA runtime objects; ASan's
+// quarantine, taking that free, recycles older quarantined chunks, and among
+// them were device allocations made through ASan's device allocator and
+// released earlier by hipStreamDestroy (a stream's queue memory). ASan had by
+// then marked the device runtime unloaded, so DeviceAllocator::Deallocate
+// failed its CHECK. No object of ours frees anything after the runtime
+// unloads; what matters is that no destroyed stream's device memory sits in
+// the quarantine when HIP tears down, which one stream per process ensures.
 hipStream_t solver_stream(int device) {
   static std::mutex m;
   static std::vector<hipStream_t> streams;

@@ -202,3 +202,31 @@ def test_rccl_captured_cg_equals_eager(monkeypatch, null_stream):
     for k in ("termination_type", "num_iterations", "num_successful_steps", "num_linear_iterations", "final_cost"):
         assert sa[k] == sb[k], (k, sa[k], sb[k])
     assert np.array_equal(xa, xb)
+
+
+def test_comm_destroy_drops_its_graphs():
+    """A captured CG run holds the RCCL communicator's collective (RCCL keeps
+    per-graph resources until the graph is destroyed), so mvba_comm_destroy
+    first drops every graph recorded with it (mvba_drop_comm_graphs). The
+    handle then solves again through a new communicator, capturing afresh, and
+    the deterministic solve is the same bit for bit."""
+    from multiview_amd.dist import Comm
+
+    P = _rig_problem(False)
+    st = torch.cuda.Stream()
+    runs = []
+    with Evaluator(P) as ev:
+        for _ in range(2):
+            comm = Comm.rccl_world1(0)
+            try:
+                ev.set_params()
+                s = ev.solve(max_num_iterations=4, use_loss=1, robust_threshold=3.0, deterministic=1, comm=comm,
+                             stream=st.cuda_stream, **TOL)
+                runs.append((s, ev.get_params()))
+            finally:
+                comm.close()  # drops the handle's graphs before the communicator
+    (sa, xa), (sb, xb) = runs
+    assert sa["cg_graph_launches"] > 0 and sb["cg_graph_launches"] > 0, (sa, sb)
+    for k in ("termination_type", "num_iterations", "num_linear_iterations", "final_cost"):
+        assert sa[k] == sb[k], (k, sa[k], sb[k])
+    assert np.array_equal(xa, xb)
