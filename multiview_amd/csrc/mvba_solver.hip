@@ -24,12 +24,14 @@ constexpr bool kFastProj = MVBA_FAST_PROJ;
 
 constexpr int kDirStride = 128;    // per-frame direction record: u (6) | x_intr (<= 122: RPC degree 6 has 113)
 // pass-B vector replicas (chunk mod R): 32 since round 2 (8 contended then).
-// Round 5 re-measured 16 with 8-segment chunks: c2 CG iteration 60.4 / 60.5 vs
-// 61.3 / 61.8 us of kernels, c3 452.7 / 455.8 vs 456.1 / 455.9, 1/8 shard
-// equal (profiles/r05/r05aa/), but the full GPU suite on that build sent the
-// atomic and deterministic depth solves of test_deterministic_solve_is_
-// reproducible[True] to different Cauchy minima within 50 iterations (6896.5
-// vs 6893.7, r05zz): 32 kept (-DMVBA_VEC_REPLICAS=16 for A/B builds)
+// Round 6 re-decided 16 vs 32 on timing alone, with the solver tests that once
+// decided it re-grounded (each solve against the CPU LM; the 16-replica build
+// passes the whole GPU suite, profiles/r06/r06i/pytest_gpu_r06i.log). Kernel
+// traces, same box, two runs each (r06i/cg_iter_r06i.txt): c2 61.5 / 61.4 vs
+// 62.3 / 61.8 us per CG iteration, c3 447.3 / 448.9 vs 450.9 / 445.5, the 1/8
+// shard 27.7 / 28.8 vs 27.2 / 27.2 (its pass B 7.4-7.6 vs 6.8-6.9: 16 replicas
+// contend on a thin shard's shared entries). 32 kept: the thin shard is the
+// 8-GPU path. -DMVBA_VEC_REPLICAS=16 for A/B builds.
 #ifndef MVBA_VEC_REPLICAS
 #define MVBA_VEC_REPLICAS 32
 #endif
