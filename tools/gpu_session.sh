@@ -7,6 +7,7 @@
 #   tests      pytest -m gpu (TESTS=... narrows it, PYTEST_ARGS adds options)
 #   smoke      __graft_entry__.smoke()
 #   bench      the default bench line (c2, CPU baseline) + c1 and c3 lines
+#   bench45    the c4 (50M observations) and c5 (depth) bench lines
 #   prof       rocprofv3 --kernel-trace --stats of the c2 bench (roofline.kernel_ms check)
 #   shard      rank 0's shard of an N-way landmark split of c2, N = 1 2 4 8
 #              (bench.py --shard-of N): the per-rank step of the strong-scaling headline
@@ -53,6 +54,10 @@ for step in ${STEPS//,/ }; do
       run bench_c1_$TAG 300 python bench.py --config c1 --mesh-subdiv 0
       run bench_c3_$TAG 600 python bench.py --config c3 --steps 50 --mesh-subdiv 0 --cpu-sample 200000
       python3 tools/bench_summary.py $OUT/bench_$TAG.log $OUT/bench_c1_$TAG.log $OUT/bench_c3_$TAG.log || true ;;
+    bench45)
+      run bench_c4_$TAG 400 python3 bench.py --config c4 --steps 20 --ba-iters 2 --mesh-subdiv 0 --cpu-sample 1000000
+      run bench_c5_$TAG 400 python3 bench.py --config c5 --mesh-subdiv 0
+      python3 tools/bench_summary.py $OUT/bench_c4_$TAG.log $OUT/bench_c5_$TAG.log || true ;;
     prof)
       run prof_c2_$TAG 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c2_$TAG -o run --output-format csv -- \
         python3 bench.py --steps 200 $NB ;;
