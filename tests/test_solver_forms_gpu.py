@@ -214,3 +214,40 @@ def test_cg_direction_forms_agree(monkeypatch):
     for sb in conv:
         assert sb["termination_type"] == 0, sb["message"]
         assert np.isclose(sa["final_cost"], sb["final_cost"], rtol=1e-9), (sa["final_cost"], sb["final_cost"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["none", "rccl"])
+def test_atomic_exact_step_through_resets(exchange):
+    """Atomic (non-deterministic) sums, CG to eta = 1e-14: dozens of
+    iterations and several of Ceres' residual resets (r = b - A x every 10th
+    iteration, a product in line), on one rank and through a one-rank RCCL
+    communicator (fold-mode tail, the exchanged p.q, graphs with the
+    all-reduce inside): the step against the CPU's exact step of the same
+    system. (A side-stream form of the reset product measured slower,
+    profiles/r06/r06l/.)"""
+    import torch
+
+    # reference poses fixed: a unique minimum (test_point_solve_forms_agree)
+    R = rig.make_rig(num_sensors=3, num_ref=10, num_points=400, obs_per_point=4, seed=11)
+    P = rig.build_problem(R, rig.FloatFlags(camera_poses_to_float=()))
+    sysm = _exact_step_system(P)
+    st = torch.cuda.Stream()
+    comm = None
+    if exchange == "rccl":
+        from multiview_amd.dist import Comm
+
+        comm = Comm.rccl_world1(0)
+    try:
+        with Evaluator(P) as ev:
+            ev.set_params()
+            s = ev.solve(max_num_iterations=1, eta=1e-14, max_linear_solver_iterations=2000, use_loss=1,
+                         robust_threshold=3.0, deterministic=0, function_tolerance=1e-16, gradient_tolerance=1e-16,
+                         parameter_tolerance=1e-16, comm=comm, stream=st.cuda_stream)
+            x = ev.get_params()
+    finally:
+        if comm is not None:
+            comm.close()
+    assert s["num_linear_iterations"] > 20, s["num_linear_iterations"]
+    assert s["final_cost"] < s["initial_cost"]
+    _check_against_exact_step(sysm, x, f"atomic {exchange} ({s['num_linear_iterations']} CG iterations)")
