@@ -324,9 +324,15 @@ SolverState* alloc_state(mvba_handle* h) {
     // [0]: the solve's initial control block (H2D source); [1], [2]: the
     // pipelined batches' read-backs
     HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hctl), 3 * sizeof(mvba::CgCtl)));
-    HCHK(hipHostMalloc(reinterpret_cast<void**>(&S->hmir), sizeof(mvba::CgMirror),
-                       hipHostMallocCoherent | hipHostMallocMapped));
-    HCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&S->dmir), S->hmir, 0));
+    // (no host-coherent mapped memory: the CG batches end with the copy and the event)
+    if (hipHostMalloc(reinterpret_cast<void**>(&S->hmir), sizeof(mvba::CgMirror),
+                      hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&S->dmir), S->hmir, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      if (S->hmir) (void)hipHostFree(S->hmir);
+      S->hmir = nullptr;
+      S->dmir = nullptr;
+    }
     std::vector<int32_t> bs(S->nblocks);
     for (int32_t k = 0; k < S->nblocks; k++) {
       const int32_t bid = h->cam_block_ids[k];
@@ -898,7 +904,7 @@ class Solver {
   bool mirror_on() const {
     const char* m = std::getenv("MVBA_CG_MIRROR");  // read per call: tests switch it
     const char* pp = std::getenv("MVBA_CG_PIPE");
-    return !(m && m[0] == '0') && !(pp && pp[0] == '1');
+    return S_->dmir && !(m && m[0] == '0') && !(pp && pp[0] == '1');
   }
   // drops every captured graph whose launches no longer match (signature)
   void refresh_graph_sig() {
