@@ -107,14 +107,24 @@ __device__ __forceinline__ void rot_to_quat(const double* m, double* q) {
 
 // array_to_rigid_transform (dense_map_utils.cc:171-178): normalised quaternion,
 // its rotation and 1/|q| (for the derivative through normalize()).
+// (MVBA_K0_FAST: one reciprocal and four products instead of four divisions:
+// the frame record is K0's dependent chain on thin shards, within an ulp of
+// Eigen's q / |q|)
+#ifndef MVBA_K0_FAST
+#define MVBA_K0_FAST 1
+#endif
 __device__ __forceinline__ void rigid(const double* p, double* R, double* qh, double* inv_norm) {
   double x = p[3], y = p[4], z = p[5], w = p[6];
   const double n2 = x * x + y * y + z * z + w * w;
   double in = 1.0;
   if (n2 > 0.0) {
     const double n = sqrt(n2);
-    x /= n; y /= n; z /= n; w /= n;
     in = 1.0 / n;
+    if (MVBA_K0_FAST) {
+      x *= in; y *= in; z *= in; w *= in;
+    } else {
+      x /= n; y /= n; z /= n; w /= n;
+    }
   }
   qh[0] = x; qh[1] = y; qh[2] = z; qh[3] = w;
   *inv_norm = in;

@@ -108,12 +108,28 @@ __device__ __forceinline__ void frame_columns(const FrameDesc& F, const double* 
     dw1_da = 1.0;
   } else {
     const double th = acos(absD);
-    const double S = sin(th), C = cos(th);
-    const double s0 = sin((1.0 - alpha) * th), c0 = cos((1.0 - alpha) * th);
-    const double s1 = sin(alpha * th), c1 = cos(alpha * th);
-    w0 = s0 / S;  // Eigen's slerp weights, divided as Eigen does
-    w1 = s1 / S;
-    const double iS = 1.0 / S;  // derivative terms: one reciprocal
+    double S, C, s0, c0, s1, c1;
+    double iS;
+    if (MVBA_K0_FAST) {
+      // one range reduction per angle (sincos), the weights through the
+      // derivative terms' reciprocal: within an ulp of Eigen's divisions
+      sincos(th, &S, &C);
+      sincos((1.0 - alpha) * th, &s0, &c0);
+      sincos(alpha * th, &s1, &c1);
+      iS = 1.0 / S;
+      w0 = s0 * iS;
+      w1 = s1 * iS;
+    } else {
+      S = sin(th);
+      C = cos(th);
+      s0 = sin((1.0 - alpha) * th);
+      c0 = cos((1.0 - alpha) * th);
+      s1 = sin(alpha * th);
+      c1 = cos(alpha * th);
+      w0 = s0 / S;  // Eigen's slerp weights, divided as Eigen does
+      w1 = s1 / S;
+      iS = 1.0 / S;  // derivative terms: one reciprocal
+    }
     dw0_dth = ((1.0 - alpha) * c0 * S - s0 * C) * (iS * iS);
     dw1_dth = (alpha * c1 * S - s1 * C) * (iS * iS);
     dw0_da = -th * c0 * iS;
@@ -271,6 +287,23 @@ struct FusedIn {
 // about one segment per frame, where a hand-off costs more than the K0 work).
 enum { kRecGlobal = 0, kRecFused = 1, kRecLocal = 2 };
 
+// -DMVBA_EVAL_STAMPS builds (timing probes, tools/eval_stamps.py): lane 0 of
+// each k_eval_local wave records the real-time counter (100 MHz) at its phase
+// boundaries; mvba_debug_eval_stamps reads them back.
+#ifdef MVBA_EVAL_STAMPS
+constexpr int kStampWaves = 16384, kStamps = 5;
+__device__ unsigned long long g_eval_stamps[kStampWaves * kStamps];
+#define MVBA_STAMP(k)                                                                          \
+  do {                                                                                         \
+    if (RECM == kRecLocal && lane == 0 && wave < kStampWaves)                                  \
+      g_eval_stamps[wave * kStamps + (k)] = __builtin_amdgcn_s_memrealtime();                  \
+  } while (0)
+#else
+#define MVBA_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
+
 template <int MODEL, int DEG, class OT, bool JAC, int RECM = kRecGlobal>
 __device__ __forceinline__ void obs_body(
     const Segment* __restrict__ segs, int32_t nseg, const FrameDesc* __restrict__ fd,
@@ -285,6 +318,7 @@ __device__ __forceinline__ void obs_body(
   const int wave = (int)((blk * blockDim.x + threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   if (wave >= nseg) return;
+  MVBA_STAMP(0);
   const Segment sg = segs[wave];
   const int begin = __builtin_amdgcn_readfirstlane(sg.begin);
   const int count = __builtin_amdgcn_readfirstlane(sg.count);
@@ -371,6 +405,7 @@ __device__ __forceinline__ void obs_body(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     rec = sr;
+    MVBA_STAMP(1);
     // the wave of the frame's first segment stores the record for later
     // launches (solver, SKIP_PREP evaluations): in a one-group problem every
     // frame has a segment (frames are the reprojection residuals' images)
@@ -386,6 +421,7 @@ __device__ __forceinline__ void obs_body(
   const double2 meas = obs_meas[isrc];
   Proj o;
   project<MODEL, DEG>(rec, P.x, P.y, P.z, f, c0, c1, kd, K, F.h0, F.h1, o);
+  MVBA_STAMP(2);
 
   double r0 = o.d0 - meas.x;  // rig_calibrator.cc:478-479
   double r1 = o.d1 - meas.y;
@@ -544,6 +580,19 @@ __global__ void __launch_bounds__(256, 3) k_eval_local(
   if ((int64_t)bid >= fu.k1_block0) {
     obs_body<MODEL, DEG, OT, JAC, kRecLocal>(segs, nseg, fd, frec, params, pts, obs_pid, obs_meas, res, J, ld,
                                              flags, cauchy_c, fu);
+#ifdef MVBA_EVAL_STAMPS
+    {
+      constexpr int RECM = kRecLocal;
+      const int64_t blk = xcd_block_of((int64_t)blockIdx.x - fu.k1_block0, (nseg + 3) / 4);
+      const int wave = (int)((blk * blockDim.x + threadIdx.x) >> 6);
+      const int lane = threadIdx.x & 63;
+      if (blk >= 0 && wave < nseg) {
+        MVBA_STAMP(3);  // every store issued
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        MVBA_STAMP(4);  // every store acknowledged
+      }
+    }
+#endif
     return;
   }
   const int64_t p = (int64_t)bid * kPrepBlock + threadIdx.x;
@@ -1288,3 +1337,10 @@ hipError_t mvba_launch_points_lin(int model, int deg, const int64_t* pt_begin, i
 size_t mvba_frame_lin_size(void) { return sizeof(mvba::FrameLin); }
 
 }  // extern "C"
+
+#ifdef MVBA_EVAL_STAMPS
+extern "C" int mvba_debug_eval_stamps(unsigned long long* out, int n) {
+  const int m = n < mvba::kStampWaves * mvba::kStamps ? n : mvba::kStampWaves * mvba::kStamps;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(mvba::g_eval_stamps), (size_t)m * sizeof(unsigned long long));
+}
+#endif
