@@ -28,6 +28,9 @@ namespace mvba {
 // frame (each lane recomputes the frame's common part and emits a subset of the
 // 22 pose columns); the remaining blocks gather the points.
 constexpr int kThreadsPerFrame = 16;
+#ifndef MVBA_K0_LANES
+#define MVBA_K0_LANES 32  // lanes of a k_eval_local wave running its frame's K0 (22 pose columns: one pass)
+#endif
 constexpr int kPrepBlock = 256;
 #ifndef MVBA_PREP_POINTS
 #define MVBA_PREP_POINTS 4
@@ -51,21 +54,47 @@ __device__ __forceinline__ void put_col_wt(double* rec, int k, const double* om,
   wr<WT>(o + 3, dt[0] - c[0]); wr<WT>(o + 4, dt[1] - c[1]); wr<WT>(o + 5, dt[2] - c[2]);
 }
 
-template <bool WT>
+// K0's common part split over the frame's lanes (MVBA_K0_SPLIT, default on):
+// lane sub % 3 of the group builds the rigid transform (and quaternion) of the
+// beg / end / ref_to_cam block and the sine and cosine of one of the three
+// slerp angles, and the group takes each from its lane: one dependent chain
+// instead of three, and (readlane) the common part's values in SGPRs:
+// k_eval_local 148 -> 95 VGPRs, 3 -> 5 waves per SIMD. The same operations on
+// the same values; the compiler's fp64 contractions around them differ, so the
+// record moves by roundoff against the unsplit build (tools/k0_split_check.py)
+// while every form, all built on frame_columns, still agrees bit for bit.
+// BC: 0 every lane computes everything, 1 ds_bpermute within NT-lane groups
+// (k_prep: 16 lanes per frame), 2 readlane (k_eval_local: one frame per wave,
+// its lanes from lane 0). (profiles/r06/r06y: the c2 evaluation 121 -> 115 us
+// with the Jacobian, 45 -> 37 us without; 32 K0 lanes: 114 / 35 us.)
+#ifndef MVBA_K0_SPLIT
+#define MVBA_K0_SPLIT 1
+#endif
+template <int BC, int NT>
+__device__ __forceinline__ double from_lane(double v, int src) {
+  if constexpr (BC == 2) return readlane_f64(v, src);
+  else return __shfl(v, src, NT);
+}
+
+// NT: the lanes sharing the frame (lane sub takes columns sub, sub + NT, ...);
+// BC: the common part's broadcast (above); stamp (probe builds): where lane 0
+// records the end of the common part
+template <bool WT, int NT = kThreadsPerFrame, int BC = (MVBA_K0_SPLIT ? 1 : 0)>
 __device__ __forceinline__ void frame_columns(const FrameDesc& F, const double* __restrict__ params, double* rec,
-                              int sub, int gen, int* err) {
+                              int sub, int gen, int* err, unsigned long long* stamp = nullptr) {
+  static_assert(BC == 0 || NT >= 3, "the split common part takes three lanes");
   const double* p0 = params + F.off[MVBA_BLK_BEG];
-  double R0[9], qh0[4], in0;
-  rigid(p0, R0, qh0, &in0);
   const double t0[3] = {p0[0], p0[1], p0[2]};
 
   if (F.sb == F.se) {
+    double R0[9], qh0[4], in0;
+    rigid(p0, R0, qh0, &in0);
     // rig_calibrator.cc:371-374 — reference camera or --no_rig: T = rigid(p0).
     if (sub == 0) {
       for (int k = 0; k < 9; k++) wr<WT>(rec + k, R0[k]);
       wr<WT>(rec + 9, t0[0]); wr<WT>(rec + 10, t0[1]); wr<WT>(rec + 11, t0[2]);
     }
-    for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
+    for (int k = sub; k < kPoseCols; k += NT) {
       double om[3] = {0.0, 0.0, 0.0};
       // unit translation column by value (a dynamic index into dt would put the
       // array in scratch memory)
@@ -82,20 +111,43 @@ __device__ __forceinline__ void frame_columns(const FrameDesc& F, const double* 
   const double* p1 = params + F.off[MVBA_BLK_END];
   const double* p2 = params + F.off[MVBA_BLK_REF_TO_CAM];
   const double off = params[F.off[MVBA_BLK_OFFSET]];
-  double R1[9], qh1[4], in1, R2[9], qh2[4], in2;
-  rigid(p1, R1, qh1, &in1);
-  rigid(p2, R2, qh2, &in2);
   const double t1[3] = {p1[0], p1[1], p1[2]};
   const double t2[3] = {p2[0], p2[1], p2[2]};
+  // linearInterp's quaternions of the beg / end rotations (Eigen slerp [ext])
+  double qh0[4], in0, q0[4], qh1[4], in1, q1[4], R2[9], qh2[4], in2;
+  if constexpr (BC == 0) {
+    double R0[9], R1[9];
+    rigid(p0, R0, qh0, &in0);
+    rigid(p1, R1, qh1, &in1);
+    rigid(p2, R2, qh2, &in2);
+    rot_to_quat(R0, q0);
+    rot_to_quat(R1, q1);
+  } else {
+    const int b = sub % 3;
+    const double* pb = b == 0 ? p0 : b == 1 ? p1 : p2;
+    double Rb[9], qhb[4], inb, qb[4];
+    rigid(pb, Rb, qhb, &inb);
+    rot_to_quat(Rb, qb);  // (ref_to_cam's lane: unused)
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      qh0[m] = from_lane<BC, NT>(qhb[m], 0);
+      q0[m] = from_lane<BC, NT>(qb[m], 0);
+      qh1[m] = from_lane<BC, NT>(qhb[m], 1);
+      q1[m] = from_lane<BC, NT>(qb[m], 1);
+      qh2[m] = from_lane<BC, NT>(qhb[m], 2);
+    }
+#pragma unroll
+    for (int m = 0; m < 9; m++) R2[m] = from_lane<BC, NT>(Rb[m], 2);
+    in0 = from_lane<BC, NT>(inb, 0);
+    in1 = from_lane<BC, NT>(inb, 1);
+    in2 = from_lane<BC, NT>(inb, 2);
+  }
 
   // rig_calibrator.cc:343-346 (big stamps subtracted first).
   const double alpha = ((F.sc - F.sb) - off) / (F.se - F.sb);
   if (sub == 0 && (alpha < 0.0 || alpha > 1.0)) atomicMax(err, gen);
 
   // linearInterp with Eigen slerp [ext] (dense_map_utils.cc:315-329).
-  double q0[4], q1[4];
-  rot_to_quat(R0, q0);
-  rot_to_quat(R1, q1);
   const double sig0 = (q0[0] * qh0[0] + q0[1] * qh0[1] + q0[2] * qh0[2] + q0[3] * qh0[3]) >= 0.0 ? 1.0 : -1.0;
   const double sig1 = (q1[0] * qh1[0] + q1[1] * qh1[1] + q1[2] * qh1[2] + q1[3] * qh1[3]) >= 0.0 ? 1.0 : -1.0;
   const double d = q0[0] * q1[0] + q0[1] * q1[1] + q0[2] * q1[2] + q0[3] * q1[3];
@@ -110,7 +162,27 @@ __device__ __forceinline__ void frame_columns(const FrameDesc& F, const double* 
     const double th = acos(absD);
     double S, C, s0, c0, s1, c1;
     double iS;
-    if (MVBA_K0_FAST) {
+    if constexpr (BC != 0) {
+      // the three angles' sines and cosines on lanes 0 / 1 / 2 of the group
+      const int b = sub % 3;
+      const double x = b == 0 ? th : b == 1 ? (1.0 - alpha) * th : alpha * th;
+      double sx, cx;
+      if (MVBA_K0_FAST) {
+        sincos(x, &sx, &cx);
+      } else {
+        sx = sin(x);
+        cx = cos(x);
+      }
+      S = from_lane<BC, NT>(sx, 0);
+      C = from_lane<BC, NT>(cx, 0);
+      s0 = from_lane<BC, NT>(sx, 1);
+      c0 = from_lane<BC, NT>(cx, 1);
+      s1 = from_lane<BC, NT>(sx, 2);
+      c1 = from_lane<BC, NT>(cx, 2);
+      iS = 1.0 / S;
+      w0 = MVBA_K0_FAST ? s0 * iS : s0 / S;
+      w1 = MVBA_K0_FAST ? s1 * iS : s1 / S;
+    } else if (MVBA_K0_FAST) {
       // one range reduction per angle (sincos), the weights through the
       // derivative terms' reciprocal: within an ulp of Eigen's divisions
       sincos(th, &S, &C);
@@ -161,7 +233,12 @@ __device__ __forceinline__ void frame_columns(const FrameDesc& F, const double* 
     wr<WT>(rec + 9, tw[0]); wr<WT>(rec + 10, tw[1]); wr<WT>(rec + 11, tw[2]);
   }
 
-  for (int k = sub; k < kPoseCols; k += kThreadsPerFrame) {
+#ifdef MVBA_EVAL_STAMPS
+  if (stamp && sub == 0) *stamp = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)stamp;
+#endif
+  for (int k = sub; k < kPoseCols; k += NT) {
     // Every per-column choice below is made by value (selects), never by a
     // dynamic index into a register array or a pointer to one of two arrays:
     // either would move the arrays to scratch memory (80 B per lane before).
@@ -291,7 +368,7 @@ enum { kRecGlobal = 0, kRecFused = 1, kRecLocal = 2 };
 // each k_eval_local wave records the real-time counter (100 MHz) at its phase
 // boundaries; mvba_debug_eval_stamps reads them back.
 #ifdef MVBA_EVAL_STAMPS
-constexpr int kStampWaves = 16384, kStamps = 5;
+constexpr int kStampWaves = 16384, kStamps = 8;
 __device__ unsigned long long g_eval_stamps[kStampWaves * kStamps];
 #define MVBA_STAMP(k)                                                                          \
   do {                                                                                         \
@@ -323,6 +400,7 @@ __device__ __forceinline__ void obs_body(
   const int begin = __builtin_amdgcn_readfirstlane(sg.begin);
   const int count = __builtin_amdgcn_readfirstlane(sg.count);
   const int frame = __builtin_amdgcn_readfirstlane(sg.frame);
+  MVBA_STAMP(5);  // (probes) the segment record arrived
   // Lanes past the frame's last observation up to the next 128-B line (16
   // fp64 / 32 fp32 slots; segments start on 16- or 32-slot boundaries) recompute the
   // last observation and store it into their padding slots, inside the same
@@ -345,6 +423,10 @@ __device__ __forceinline__ void obs_body(
   const double* __restrict__ kd = params + F.off[MVBA_BLK_DIST];
   const int free_mask = F.free_mask;
   const int K = F.K;
+#ifdef MVBA_EVAL_STAMPS
+  asm volatile("" ::"v"(f));  // (probes) the frame descriptor and a parameter through it arrived
+  MVBA_STAMP(6);
+#endif
 
   double4 P;
   const double* rec;
@@ -389,7 +471,7 @@ __device__ __forceinline__ void obs_body(
     if (!active) return;
     rec = sr;
   } else if constexpr (RECM == kRecLocal) {
-    // lanes 0..15 (always active: count >= 1) run K0 for this wave's frame
+    // lanes 0..MVBA_K0_LANES-1 (present whatever the segment's count) run K0 for this wave's frame
     // into the wave's LDS area; then the landmark straight from the parameter
     // vector (no prep launch; loaded after K0 so the two register sets are
     // never live together: 3 waves per SIMD without spills)
@@ -397,7 +479,14 @@ __device__ __forceinline__ void obs_body(
     // 20.0 vs 18.4-20.6 us on the 8-way shard, profiles/r03/ab_eval_local/)
     __shared__ double srec[4][kFrameRecDoubles];
     double* sr = srec[threadIdx.x >> 6];
-    if (lane < kThreadsPerFrame) frame_columns<false>(F, params, sr, lane, (int)fu.epoch, fu.err);
+#ifdef MVBA_EVAL_STAMPS
+    unsigned long long* k0stamp = wave < kStampWaves ? g_eval_stamps + wave * kStamps + 7 : nullptr;
+#else
+    unsigned long long* k0stamp = nullptr;
+#endif
+    if (lane < MVBA_K0_LANES)
+      frame_columns<false, MVBA_K0_LANES, (MVBA_K0_SPLIT ? 2 : 0)>(F, params, sr, lane, (int)fu.epoch, fu.err,
+                                                                  k0stamp);
     const int32_t pid = obs_pid[isrc];
     const int64_t po = fu.pt_off[pid];
     P = make_double4(params[po], params[po + 1], params[po + 2], fu.pt_free[pid] ? 1.0 : 0.0);

@@ -2,11 +2,12 @@
 """Where a k_eval_local wave spends its time: run rank 0's shard of an N-way
 split of a config (default c2, N = 8) through a -DMVBA_EVAL_STAMPS build
 (tools/build_variant.sh stamps -DMVBA_EVAL_STAMPS; loaded through MVBA_LIB),
-evaluate a few times, read the per-wave real-time stamps (100 MHz) of the last
-launch and print the phase durations: 0 entry -> 1 K0 done -> 2 projection
-done (landmark / measurement loads consumed) -> 3 every store issued -> 4
-every store acknowledged; plus the spread of wave start and end times over
-the launch.
+evaluate a few times, read the per-wave real-time stamps (100 MHz) of the
+last launch and print the phase durations: entry -> segment record -> frame
+descriptor and a parameter through it -> K0's common part -> K0's pose
+columns -> projection done (landmark
+/ measurement loads consumed) -> every store issued -> every store
+acknowledged; plus the spread of wave start and end times over the launch.
 
 usage: MVBA_LIB=tools/ab/stamps/libmvba.so python3 tools/eval_stamps.py [--config c2] [--shard-of 8]
 """
@@ -46,7 +47,7 @@ def main():
         ev.evaluate_device(True, residuals=res, jac=jac, ld=ld)
     torch.cuda.synchronize()
     ev.sync(0)
-    nst = 5
+    nst = 8
     nw = 16384
     buf = (C.c_ulonglong * (nw * nst))()
     ev.lib.mvba_debug_eval_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
@@ -58,14 +59,19 @@ def main():
     ok = (t > 0).all(axis=1)
     t = t[ok]
     us = 0.01  # 100 MHz ticks
+    # columns: 0 entry, 5 segment record, 6 frame descriptor + a parameter,
+    # 7 K0's common part done (lane 0), 1 K0 done, 2 projection done,
+    # 3 stores issued, 4 stores acknowledged
+    t = t[:, [0, 5, 6, 7, 1, 2, 3, 4]]
     d = np.diff(t, axis=1) * us
-    names = ["K0 + barrier", "loads + projection", "stores issued", "stores acknowledged"]
+    names = ["segment record load", "frame descriptor + parameter loads", "K0 common part",
+             "K0 pose columns + barrier", "loads + projection", "stores issued", "stores acknowledged"]
     out = {"config": a.config, "shard_of": a.shard_of, "waves": int(len(t)), "form": ev.eval_form(),
-           "launch_span_us": float((t[:, 4].max() - t[:, 0].min()) * us),
+           "launch_span_us": float((t[:, -1].max() - t[:, 0].min()) * us),
            "wave_start_spread_us": float((t[:, 0].max() - t[:, 0].min()) * us),
-           "wave_life_us": {"median": float(np.median((t[:, 4] - t[:, 0]) * us)),
-                            "p90": float(np.percentile((t[:, 4] - t[:, 0]) * us, 90)),
-                            "max": float(((t[:, 4] - t[:, 0]) * us).max())},
+           "wave_life_us": {"median": float(np.median((t[:, -1] - t[:, 0]) * us)),
+                            "p90": float(np.percentile((t[:, -1] - t[:, 0]) * us, 90)),
+                            "max": float(((t[:, -1] - t[:, 0]) * us).max())},
            "phases_us": {n: {"median": float(np.median(d[:, k])), "p90": float(np.percentile(d[:, k], 90))}
                          for k, n in enumerate(names)}}
     print(json.dumps(out, indent=1))
