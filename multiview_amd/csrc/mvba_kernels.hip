@@ -28,6 +28,9 @@ namespace mvba {
 // frame (each lane recomputes the frame's common part and emits a subset of the
 // 22 pose columns); the remaining blocks gather the points.
 constexpr int kThreadsPerFrame = 16;
+#ifndef MVBA_K0_SHARE
+#define MVBA_K0_SHARE 1  // k_eval_local: one K0 per frame and block (obs_body)
+#endif
 #ifndef MVBA_K0_LANES
 #define MVBA_K0_LANES 32  // lanes of a k_eval_local wave running its frame's K0 (22 pose columns: one pass)
 #endif
@@ -477,22 +480,36 @@ __device__ __forceinline__ void obs_body(
     // never live together: 3 waves per SIMD without spills)
     // (loading the landmark's offset and free flag before K0 measured no gain:
     // 20.0 vs 18.4-20.6 us on the 8-way shard, profiles/r03/ab_eval_local/)
+    // MVBA_K0_SHARE (default on): a wave whose block predecessors hold the same
+    // frame skips K0 and reads the record of the block's first wave of that
+    // frame (a frame spans ~5 segment waves at c2 and its shards): K0 runs once
+    // per frame and block instead of once per wave, the waves meet at one block
+    // barrier. (Waves past nseg returned above: a finished wave leaves the
+    // barrier's count.)
     __shared__ double srec[4][kFrameRecDoubles];
-    double* sr = srec[threadIdx.x >> 6];
+    const int wb = (int)(threadIdx.x >> 6);
+    int lead = wb;
+    if (MVBA_K0_SHARE)
+      while (lead > 0 && __builtin_amdgcn_readfirstlane(segs[wave - (wb - lead) - 1].frame) == frame) lead--;
+    double* sr = srec[lead];
 #ifdef MVBA_EVAL_STAMPS
     unsigned long long* k0stamp = wave < kStampWaves ? g_eval_stamps + wave * kStamps + 7 : nullptr;
 #else
     unsigned long long* k0stamp = nullptr;
 #endif
-    if (lane < MVBA_K0_LANES)
+    if (lead == wb && lane < MVBA_K0_LANES)
       frame_columns<false, MVBA_K0_LANES, (MVBA_K0_SPLIT ? 2 : 0)>(F, params, sr, lane, (int)fu.epoch, fu.err,
                                                                   k0stamp);
     const int32_t pid = obs_pid[isrc];
     const int64_t po = fu.pt_off[pid];
     P = make_double4(params[po], params[po + 1], params[po + 2], fu.pt_free[pid] ? 1.0 : 0.0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (MVBA_K0_SHARE) {
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     rec = sr;
     MVBA_STAMP(1);
     // the wave of the frame's first segment stores the record for later

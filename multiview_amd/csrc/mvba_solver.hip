@@ -1182,7 +1182,10 @@ __device__ __forceinline__ void pass_b_rpc_obs(const FrameDesc& F, const double*
 template <int MODEL, int DEG>
 // (min waves per EU: keeps radtan / none within 128 VGPRs under the 128-thread
 // bound, as under the old 64-thread one; FOV needs ~155, RPC more)
-__global__ void __launch_bounds__(128, MODEL == kModelRpc ? (DEG <= 2 ? MVBA_RPC_PB_WAVES : 1) : MODEL == kModelFov ? 3 : 4) k_pass_b(
+#ifndef MVBA_PB_WAVES
+#define MVBA_PB_WAVES 4  // radtan / none
+#endif
+__global__ void __launch_bounds__(128, MODEL == kModelRpc ? (DEG <= 2 ? MVBA_RPC_PB_WAVES : 1) : MODEL == kModelFov ? 3 : MVBA_PB_WAVES) k_pass_b(
     const int4* __restrict__ chunks, int32_t nchunks, int32_t chunk_base,
     const Segment* __restrict__ segs, const FrameDesc* __restrict__ fd, const FrameLin* __restrict__ fl,
     const double* __restrict__ frec, const double* __restrict__ params,

@@ -56,6 +56,8 @@ def main():
     t = np.frombuffer(buf, dtype=np.uint64).reshape(nw, nst).astype(np.int64)
     nseg = int((t[:, 0] > 0).sum())
     t = t[:nseg]
+    follower = t[:, 7] == 0  # (MVBA_K0_SHARE) waves that took the record of their block's first wave of the frame
+    t[follower, 7] = t[follower, 6]
     ok = (t > 0).all(axis=1)
     t = t[ok]
     us = 0.01  # 100 MHz ticks
@@ -67,6 +69,7 @@ def main():
     names = ["segment record load", "frame descriptor + parameter loads", "K0 common part",
              "K0 pose columns + barrier", "loads + projection", "stores issued", "stores acknowledged"]
     out = {"config": a.config, "shard_of": a.shard_of, "waves": int(len(t)), "form": ev.eval_form(),
+           "k0_waves": int((~follower[ok]).sum()),
            "launch_span_us": float((t[:, -1].max() - t[:, 0].min()) * us),
            "wave_start_spread_us": float((t[:, 0].max() - t[:, 0].min()) * us),
            "wave_life_us": {"median": float(np.median((t[:, -1] - t[:, 0]) * us)),
