@@ -1018,7 +1018,10 @@ double mvba_eval_bytes(const mvba_handle* h, int32_t flags) {
 // 95.7 vs 107.2 us, c3 2.14 vs 2.20 ms (profiles/r05/r05m/). Past that every
 // frame's K0 runs in too many waves: c4 (~39 segments per frame) split 6.66 /
 // 6.67 ms per step, local 7.58 / 7.62, fused 7.78 / 7.79 (same box,
-// profiles/r05/r05w/), so the split form takes over there (c3: ~17).
+// profiles/r05/r05w/), so the split form takes over there (c3: ~17). With the
+// round-6 K0 (split common part, one K0 per frame and block) the gap narrowed
+// and held: c4 local 6.35 / 6.37 vs split 6.02 / 6.03 ms, c3 local 2.19 / 2.19
+// vs split 2.24 / 2.22 ms (same box, profiles/r06/r06zg/).
 static constexpr double kLocalSegsPerFrame = 24.0;
 static int eval_form(const mvba_handle* h) {
   const char* sp = std::getenv("MVBA_SPLIT_PREP");
