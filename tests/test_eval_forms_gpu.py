@@ -1,7 +1,9 @@
 """The one-launch forms of mvba_evaluate_device against the two-launch form.
 
 mvba_evaluate_device runs one launch for a one-group problem: k_eval_local by
-default (each K1 wave computes its own frame's K0 record in LDS) or, forced by
+default (each block computes the K0 record of each of its frames once in LDS,
+its waves of one frame sharing it; npts 120: one segment per frame, 2500:
+~5, frames spanning blocks) or, forced by
 MVBA_EVAL_MODE=fused, k_eval (K0 blocks hand the records to the K1 waves of the
 same grid). Both must write bit-identical planes to the two-launch form (the
 prep kernel, MVBA_EVAL_PREP_ONLY, then K1 with MVBA_EVAL_SKIP_PREP: the same
